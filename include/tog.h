@@ -1,0 +1,288 @@
+/*
+ * tog.h — C ABI of the MI355X-native batched iLQR / AL-iLQR hot path.
+ *
+ * This is the drop-in boundary for TrajectoryOptimization.jl's inner loop
+ * (reference at /root/reference, cited as file:line). Everything here is
+ * plain C: fp64 column-major arrays, int32/int64 sizes, int status codes,
+ * no exceptions, no torch types. Every entry point is ccall/ctypes friendly.
+ *
+ * Layout of batched buffers (host side and device side are identical):
+ *   x0 : (n, B)            x0[i + n*b]
+ *   X  : (n, N, B)         X[i + n*(k + N*b)]          k = 0..N-1 (knot k+1 in Julia)
+ *   U  : (m, N-1, B)       U[i + m*(k + (N-1)*b)]
+ *   K  : (m, n, N-1, B)    column-major m x n block per knot
+ *   d  : (m, N-1, B)
+ *   A  : (n, n, N-1, B)    = ∇F[k].xx   (src/model.jl:341 partition :xx)
+ *   Bm : (n, m, N-1, B)    = ∇F[k].xu
+ *   S  : (n, n, N, B)      cost-to-go Hessian (std) or its upper-triangular
+ *                          square-root factor (sqrt), src/solvers/ilqr/ilqr_solver.jl:104
+ *   s  : (n, N, B)         cost-to-go gradient S[k].x
+ *   lambda, mu, C : (pmax, N, B)  AL multipliers / penalties / constraint values
+ */
+#ifndef TOG_H
+#define TOG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TOG_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+enum tog_status_code {
+  TOG_OK = 0,
+  TOG_ERR_ARG = -1,        /* invalid argument (reference: ArgumentError, src/problem.jl:66-68,169-219) */
+  TOG_ERR_DEVICE = -2,     /* HIP runtime failure                                                   */
+  TOG_ERR_NOMEM = -3,
+  TOG_ERR_UNSUPPORTED = -4 /* model / option combination not built                                  */
+};
+
+/* per-trajectory status bits (tog_status). Replace the reference's exceptions and @warn. */
+enum tog_traj_flag {
+  TOG_TRAJ_ACTIVE = 1 << 0,          /* still iterating                                         */
+  TOG_TRAJ_CONVERGED = 1 << 1,       /* evaluate_convergence true (ilqr_methods.jl:139-162)     */
+  TOG_TRAJ_MAX_ITERS = 1 << 2,       /* stats[:iterations] >= iterations                        */
+  TOG_TRAJ_COST_INCREASED = 1 << 3,  /* error("Cost increased") forward_pass.jl:80-82           */
+  TOG_TRAJ_COST_BLOWUP = 1 << 4,     /* J > max_cost_value, ilqr_methods.jl:25-28              */
+  TOG_TRAJ_MAX_REG = 1 << 5,         /* @warn "Max regularization exceeded" ilqr_methods.jl:169 */
+  TOG_TRAJ_SQRT_PD_FAIL = 1 << 6,    /* lowrankdowndate!/cholesky PosDefException (sqrt BP)     */
+  TOG_TRAJ_AL_CONVERGED = 1 << 7,    /* c_max < constraint_tolerance                            */
+  TOG_TRAJ_AL_MAX_ITERS = 1 << 8,    /* AL outer loop exhausted                                 */
+  TOG_TRAJ_SINGULAR = 1 << 9         /* SingularException path (pinv fallback) hit in sqrt BP   */
+};
+
+/* ---------------------------------------------------------------- models */
+enum tog_model_id {
+  TOG_MODEL_DOUBLE_INTEGRATOR = 0, /* dynamics/double_integrator.jl:1-4   n=2  m=1 */
+  TOG_MODEL_CARTPOLE = 1,          /* dynamics/cartpole.jl:9-36           n=4  m=1 */
+  TOG_MODEL_QUADROTOR = 2,         /* dynamics/quadrotor.jl:10-71         n=13 m=4 */
+  TOG_MODEL_CAR = 3,               /* dynamics/car.jl:3-8                 n=3  m=2 */
+  TOG_MODEL_PENDULUM = 4,          /* dynamics/pendulum.jl:3-12           n=2  m=1 */
+  TOG_MODEL_COUNT = 5
+};
+
+enum tog_integrator {
+  TOG_RK3 = 0, /* src/integration.jl:149-158 */
+  TOG_RK4 = 1  /* src/integration.jl:115-125 */
+};
+
+/* ---------------------------------------------------------------- constraints */
+enum tog_constraint_type {
+  /* BoundConstraint(n,m; x_min,x_max,u_min,u_max, trim=true), src/constraints.jl:155-188.
+     data = [x_max(n), x_min(n), u_max(m), u_min(m)]; ±INFINITY entries are trimmed. */
+  TOG_CON_BOUND = 0,
+  /* goal_constraint(xf), src/constraints.jl:299-304. Terminal equality. data = xf(n) */
+  TOG_CON_GOAL = 1,
+  /* `count` circle_constraint rows (src/utils.jl:140-144) on x[1],x[2]:
+     c = -((x1-x0)^2 + (x2-y0)^2 - r^2). data = [x0,y0,r]*count. Stage inequality. */
+  TOG_CON_CIRCLES = 2,
+  /* `count` sphere_constraint rows (src/utils.jl:150-156) on x[1..3]:
+     c = -((x1-x0)^2 + (x2-y0)^2 + (x3-z0)^2 - r^2). data = [x0,y0,z0,r]*count. */
+  TOG_CON_SPHERES = 3
+};
+
+typedef struct tog_constraint {
+  int32_t type;       /* tog_constraint_type */
+  int32_t count;      /* number of circles / spheres (ignored for BOUND/GOAL) */
+  const double* data; /* see tog_constraint_type */
+} tog_constraint;
+
+/* An ordered ConstraintSet (src/constraint_sets.jl:1). Order = order of the
+   constraint vector C[k] (labels in insertion order, constraint_sets.jl:64-94). */
+typedef struct tog_constraint_set {
+  int32_t n_con;
+  const tog_constraint* con;
+} tog_constraint_set;
+
+/* ---------------------------------------------------------------- problem */
+/* Problem{T,Discrete} (src/problem.jl:37-72) with LQR/Quadratic objective
+   (src/cost.jl:112-157, src/objective.jl:102-114) and per-knot constraint sets
+   (src/constraint_sets.jl:157-206). One problem, B independent trajectories
+   that differ in x0 and the initial controls U0. */
+typedef struct tog_problem_desc {
+  int32_t model;      /* tog_model_id                       */
+  int32_t integrator; /* tog_integrator                     */
+  int32_t n, m, N;    /* must match the model's n, m        */
+  int32_t reserved0;
+  int64_t batch;      /* B                                  */
+  double dt;          /* prob.dt (tf > 0; min-time is out of scope) */
+  /* stage QuadraticCost: 1/2 x'Qx + 1/2 u'Ru + q'x + r'u + c + u'Hx, times dt */
+  const double* Q; /* n*n */
+  const double* R; /* m*m */
+  const double* H; /* m*n */
+  const double* q; /* n   */
+  const double* r; /* m   */
+  double c;
+  /* terminal QuadraticCost: 1/2 x'Qf x + qf'x + cf */
+  const double* Qf; /* n*n */
+  const double* qf; /* n   */
+  double cf;
+  /* constraints: sets[] table and knot_set[N] (-1 = empty set at that knot).
+     knot_set[N-1] is the terminal set (evaluated with the terminal methods). */
+  int32_t n_sets;
+  int32_t reserved1;
+  const tog_constraint_set* sets;
+  const int32_t* knot_set;
+} tog_problem_desc;
+
+/* ---------------------------------------------------------------- options */
+/* Live fields of iLQRSolverOptions (src/solvers/ilqr/ilqr_solver.jl:7-81) and
+   AugmentedLagrangianSolverOptions (src/solvers/augmented_lagrangian/augmented_lagrangian_solver.jl:8-66).
+   tog_default_options() fills the reference defaults. */
+typedef struct tog_options {
+  double cost_tolerance;          /* 1e-4 */
+  double gradient_norm_tolerance; /* 1e-5 */
+  int32_t iterations;             /* 300  */
+  int32_t dJ_counter_limit;       /* 10   */
+  int32_t square_root;            /* 0    */
+  int32_t bp_reg_type;            /* 0 = :control, 1 = :state */
+  int32_t gradient_type;          /* 0 = :todorov, 1 = :feedforward */
+  int32_t iterations_linesearch;  /* 20   */
+  double line_search_lower_bound; /* 1e-8 */
+  double line_search_upper_bound; /* 10   */
+  double bp_reg_increase_factor;  /* 1.6  */
+  double bp_reg_max;              /* 1e8  */
+  double bp_reg_min;              /* 1e-8 */
+  double bp_reg_fp;               /* 10   */
+  double max_cost_value;          /* 1e8  */
+  double max_state_value;         /* 1e8  */
+  double max_control_value;       /* 1e8  */
+  /* augmented Lagrangian */
+  double al_cost_tolerance;                       /* 1e-4 */
+  double al_cost_tolerance_intermediate;          /* 1e-3 */
+  double al_gradient_norm_tolerance;              /* 1e-5 */
+  double al_gradient_norm_tolerance_intermediate; /* 1e-5 */
+  double constraint_tolerance;                    /* 1e-3 */
+  double dual_min;                                /* -1e8 */
+  double dual_max;                                /* 1e8  */
+  double penalty_max;                             /* 1e8  */
+  double penalty_initial;                         /* 1    */
+  double penalty_scaling;                         /* 10   */
+  int32_t al_iterations;                          /* 30   */
+  int32_t kickout_max_penalty;                    /* 0    */
+} tog_options;
+
+/* solve modes */
+enum tog_mode {
+  TOG_MODE_ILQR = 0, /* solve!(prob, iLQRSolverOptions): objective only (ilqr_methods.jl:3-45)   */
+  TOG_MODE_AL = 1    /* solve!(prob, AugmentedLagrangianSolverOptions) (augmented_lagrangian_methods.jl:2-31) */
+};
+
+/* fields for tog_get / tog_set */
+enum tog_field {
+  TOG_FIELD_X = 0,      /* (n,N,B)        prob.X                               */
+  TOG_FIELD_U = 1,      /* (m,N-1,B)      prob.U                               */
+  TOG_FIELD_XBAR = 2,   /* (n,N,B)        solver.X̄                            */
+  TOG_FIELD_UBAR = 3,   /* (m,N-1,B)      solver.Ū                            */
+  TOG_FIELD_K = 4,      /* (m,n,N-1,B)    solver.K                             */
+  TOG_FIELD_D = 5,      /* (m,N-1,B)      solver.d                             */
+  TOG_FIELD_A = 6,      /* (n,n,N-1,B)    solver.∇F[k].xx                      */
+  TOG_FIELD_B = 7,      /* (n,m,N-1,B)    solver.∇F[k].xu                      */
+  TOG_FIELD_S = 8,      /* (n,n,N,B)      solver.S[k].xx (needs TOG_BP_STORE_S) */
+  TOG_FIELD_SX = 9,     /* (n,N,B)        solver.S[k].x  (needs TOG_BP_STORE_S) */
+  TOG_FIELD_DV = 10,    /* (2,B)          last ΔV                              */
+  TOG_FIELD_LAMBDA = 11,/* (pmax,N,B)                                          */
+  TOG_FIELD_MU = 12,    /* (pmax,N,B)                                          */
+  TOG_FIELD_C = 13,     /* (pmax,N,B)     constraint values at (X,U)           */
+  TOG_FIELD_X0 = 14,    /* (n,B)                                               */
+  TOG_FIELD_STATS = 15, /* (TOG_NSTATS,B) see tog_stat                         */
+  TOG_FIELD_RHO = 16    /* (2,B)          [ρ, dρ]                              */
+};
+
+/* per-trajectory statistics row (TOG_FIELD_STATS), all stored as double */
+enum tog_stat {
+  TOG_STAT_J = 0,           /* current cost (J_prev of the inner loop)              */
+  TOG_STAT_DJ = 1,          /* last dJ                                              */
+  TOG_STAT_GRADIENT = 2,    /* last gradient (todorov / feedforward)                */
+  TOG_STAT_ITERATIONS = 3,  /* iLQR stats[:iterations] (includes initial record)    */
+  TOG_STAT_ZERO_COUNT = 4,  /* dJ_zero_counter                                      */
+  TOG_STAT_ALPHA = 5,       /* last accepted step (logged 2*alpha)                  */
+  TOG_STAT_Z = 6,           /* last line-search ratio                               */
+  TOG_STAT_C_MAX = 7,       /* max_violation(solver)                                */
+  TOG_STAT_AL_ITER = 8,     /* AL outer iteration counter                           */
+  TOG_STAT_TOTAL_STEPS = 9, /* iLQR step!s executed in total                        */
+  TOG_STAT_LS_TRIALS = 10,  /* rollouts evaluated in the last forward pass          */
+  TOG_STAT_BP_RESTARTS = 11,/* regularisation restarts in the last backward pass    */
+  TOG_STAT_FLAGS = 12,      /* tog_traj_flag bits                                   */
+  TOG_STAT_PENALTY_MAX = 13,/* max μ                                                */
+  TOG_NSTATS = 14
+};
+
+/* backward-pass flags */
+enum tog_bp_flag {
+  TOG_BP_STORE_S = 1 /* write S[k].xx, S[k].x for every knot (test/inspection only) */
+};
+
+typedef struct tog_handle tog_handle;
+
+/* ---------------------------------------------------------------- API */
+int32_t tog_version(void);
+int32_t tog_device_count(void);
+void tog_default_options(tog_options* opts);
+
+/* AbstractSolver(prob, opts) — src/solvers.jl:47-94, ilqr_solver.jl:118-144,
+   augmented_lagrangian_solver.jl:120-140. Allocates every device buffer. */
+int32_t tog_create(const tog_problem_desc* desc, const tog_options* opts, int32_t device,
+                   tog_handle** out);
+int32_t tog_destroy(tog_handle* h);
+/* use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream */
+int32_t tog_set_stream(tog_handle* h, void* hip_stream);
+int32_t tog_synchronize(tog_handle* h);
+
+/* initial_controls!/set_x0!/initial_states! (src/problem.jl:149-160).
+   X may be NULL: then X is set to NaN (empty_state, src/problem.jl:232). Host pointers. */
+int32_t tog_set_state(tog_handle* h, const double* x0, const double* U, const double* X);
+/* copy a field host->device / device->host (host pointers, sizes per tog_field) */
+int32_t tog_set(tog_handle* h, int32_t field, const double* in);
+int32_t tog_get(tog_handle* h, int32_t field, double* out);
+/* same, device pointers (no host staging) — for torch / RCCL interop */
+int32_t tog_get_device_ptr(tog_handle* h, int32_t field, void** dptr);
+int32_t tog_dims(tog_handle* h, int64_t* out6); /* [n, m, N, B, pmax, mode] */
+
+/* ---- step level (exported because tests and callers use them:
+        src/TrajectoryOptimization.jl:82-95, test/sqrt_bp_tests.jl:27-37) ---- */
+/* rollout!(prob) src/rollout.jl:25-31: open-loop rollout of trajectories whose X is non-finite */
+int32_t tog_rollout_open_loop(tog_handle* h);
+/* jacobian!(prob, solver) src/solvers.jl:126 -> src/model.jl:301-306 */
+int32_t tog_jacobians(tog_handle* h);
+/* update_constraints! + update_active_set! (constraint_sets.jl:221-260) at (X,U) */
+int32_t tog_update_constraints(tog_handle* h);
+/* cost(obj, X, U, dt) (objective.jl:40-48) or AL cost (augmented_lagrangian_methods.jl:298-313);
+   al != 0 selects the AL objective. J_out: (B) host pointer */
+int32_t tog_cost(tog_handle* h, int32_t al, double* J_out);
+/* cost_expansion! + backwardpass! (ilqr_methods.jl:55-62, backward_pass.jl:1-169).
+   sqrt selects _backwardpass_sqrt!; al selects the AL objective; flags = tog_bp_flag.
+   Uses and updates the per-trajectory ρ, dρ. dV_out: (2,B) host or NULL. */
+int32_t tog_backward_pass(tog_handle* h, int32_t sqrt, int32_t al, int32_t flags, double* dV_out);
+/* forwardpass! (forward_pass.jl:5-85) from the stored ΔV; J_prev (B) host pointer;
+   J_out (B) host or NULL. Writes X̄, Ū. */
+int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double* J_out);
+/* rollout!(prob, solver, α) (src/rollout.jl:2-23) for every trajectory; ok_out (B) int32 or NULL */
+int32_t tog_rollout(tog_handle* h, double alpha, int32_t* ok_out);
+
+/* ---- solve level ---- */
+/* initialise the per-trajectory solve state machine (reset!, λ=0, μ=μ0, initial rollout, J) */
+int32_t tog_solve_init(tog_handle* h, int32_t mode);
+/* advance every active trajectory by `nsteps` iLQR step!s (AL outer updates happen in between
+   on the trajectories whose inner loop converged). Asynchronous: no host sync. */
+int32_t tog_solve_step(tog_handle* h, int32_t nsteps);
+/* number of trajectories still active + batch sums; blocking. out3 = [n_active, Σ J, max c_max] */
+int32_t tog_batch_stats(tog_handle* h, double* out3);
+/* batch stats into a device buffer of 3 doubles (stream-ordered, no host sync) */
+int32_t tog_batch_stats_device(tog_handle* h, void* dptr3);
+/* counter of step!s executed since tog_solve_init (device side, read blocking) */
+int32_t tog_total_steps(tog_handle* h, int64_t* out);
+/* full solves: run until no trajectory is active (or max_steps) */
+int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps);
+/* per-trajectory tog_traj_flag bits; flags_out: (B) int32 */
+int32_t tog_status(tog_handle* h, int32_t* flags_out);
+
+/* human readable message for the last error on this thread */
+const char* tog_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TOG_H */

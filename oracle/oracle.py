@@ -1,0 +1,214 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the C oracle (oracle/tog_oracle.c).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's cpu_baseline leg import this module,
+as the checker; the product path (libtog.so) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import pathlib
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+
+_pkg = sys.modules.get("trajopt_amd")
+if _pkg is None:  # pragma: no cover
+    sys.path.insert(0, str(HERE.parent))
+    import __graft_entry__  # noqa: E402
+
+    _pkg = __graft_entry__.load_package()
+abi = _pkg.abi
+
+_lib = None
+
+FIELDS = {"X": abi.FIELD_X, "U": abi.FIELD_U, "Xbar": abi.FIELD_XBAR, "Ubar": abi.FIELD_UBAR, "K": abi.FIELD_K,
+          "d": abi.FIELD_D, "A": abi.FIELD_A, "B": abi.FIELD_B, "S": abi.FIELD_S, "Sx": abi.FIELD_SX,
+          "dV": abi.FIELD_DV, "lambda": abi.FIELD_LAMBDA, "mu": abi.FIELD_MU, "C": abi.FIELD_C,
+          "x0": abi.FIELD_X0, "stats": abi.FIELD_STATS, "rho": abi.FIELD_RHO}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            subprocess.run(["make"], cwd=HERE, check=True, capture_output=True)
+        L = C.CDLL(str(LIB))
+        vp, dp = C.c_void_p, C.POINTER(C.c_double)
+        L.oc_create.restype = vp
+        L.oc_create.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options)]
+        L.oc_destroy.argtypes = [vp]
+        L.oc_set_state.argtypes = [vp, dp, dp, dp]
+        L.oc_get.argtypes = [vp, C.c_int, dp]
+        L.oc_set.argtypes = [vp, C.c_int, dp]
+        L.oc_pmax.argtypes = [vp]
+        L.oc_rollout_open_loop.argtypes = [vp]
+        L.oc_rollout.argtypes = [vp, C.c_double]
+        L.oc_jacobians.argtypes = [vp]
+        L.oc_cost_expansion.argtypes = [vp, C.c_int, C.c_int]
+        L.oc_backward.argtypes = [vp, C.c_int, dp]
+        L.oc_forward.argtypes = [vp, C.c_int, C.c_double]
+        L.oc_forward.restype = C.c_double
+        L.oc_cost.argtypes = [vp, C.c_int]
+        L.oc_cost.restype = C.c_double
+        L.oc_cost_bar.argtypes = [vp, C.c_int]
+        L.oc_cost_bar.restype = C.c_double
+        L.oc_solve_ilqr.argtypes = [vp]
+        L.oc_solve_al.argtypes = [vp]
+        L.oc_update_constraints.argtypes = [vp]
+        L.oc_max_violation.argtypes = [vp]
+        L.oc_max_violation.restype = C.c_double
+        L.oc_get_trace.argtypes = [vp, dp]
+        L.oc_discrete_f.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
+        L.oc_continuous_f.argtypes = [C.c_int, dp, dp, dp]
+        L.oc_discrete_jacobian.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
+        L.oc_cond2.argtypes = [dp, C.c_int]
+        L.oc_cond2.restype = C.c_double
+        L.oc_qr_R.argtypes = [dp, dp, C.c_int, C.c_int]
+        L.oc_solve_batch.restype = C.c_int64
+        L.oc_solve_batch.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp, dp,
+                                     C.c_int64, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def discrete_f(model, integ, x, u, dt):
+    n = len(x)
+    out = np.empty(n)
+    lib().oc_discrete_f(model, integ, _dp(out), _dp(np.ascontiguousarray(x, float)),
+                        _dp(np.ascontiguousarray(u, float)), dt)
+    return out
+
+
+def continuous_f(model, x, u):
+    out = np.empty(len(x))
+    lib().oc_continuous_f(model, _dp(out), _dp(np.ascontiguousarray(x, float)), _dp(np.ascontiguousarray(u, float)))
+    return out
+
+
+def discrete_jacobian(model, integ, x, u, dt):
+    """n x (n+m+1) ForwardDiff Jacobian of the discrete map w.r.t. [x; u; dt]."""
+    n, m = len(x), len(u)
+    S = np.empty((n + m + 1, n))  # column-major n x L
+    lib().oc_discrete_jacobian(model, integ, _dp(S), _dp(np.ascontiguousarray(x, float)),
+                               _dp(np.ascontiguousarray(u, float)), dt)
+    return S.T.copy()
+
+
+def cond2(A):
+    A = np.asfortranarray(A, dtype=float)
+    return lib().oc_cond2(A.ctypes.data_as(C.POINTER(C.c_double)), A.shape[0])
+
+
+def qr_R(P):
+    P = np.asfortranarray(P, dtype=float).copy(order="F")
+    rows, cols = P.shape
+    R = np.zeros((cols, cols), order="F")
+    lib().oc_qr_R(R.ctypes.data_as(C.POINTER(C.c_double)), P.ctypes.data_as(C.POINTER(C.c_double)), rows, cols)
+    return np.array(R)
+
+
+class OracleSolver:
+    """Single-trajectory oracle solver for trajectory ``b`` of a (possibly batched) Problem."""
+
+    def __init__(self, prob, opts, b=0):
+        self.prob = prob
+        self.n, self.m, self.N = prob.model.n, prob.model.m, prob.N
+        self.desc = prob.build_desc()
+        self.opts = _pkg.to_tog_options(opts)
+        self.al_requested = isinstance(opts, (_pkg.AugmentedLagrangianSolverOptions, _pkg.ALTROSolverOptions))
+        self.mode = abi.MODE_AL if (self.al_requested and prob.is_constrained()) else abi.MODE_ILQR
+        if self.al_requested and not prob.is_constrained():
+            self.opts = _pkg.to_tog_options(opts.opts_uncon if hasattr(opts, "opts_uncon") else opts.opts_al.opts_uncon)
+        self.s = lib().oc_create(C.byref(self.desc.desc), C.byref(self.opts))
+        self.pmax = lib().oc_pmax(self.s)
+        X = prob._X[b]
+        lib().oc_set_state(self.s, _dp(np.ascontiguousarray(prob.x0[b])), _dp(np.ascontiguousarray(prob._U[b])),
+                           _dp(np.ascontiguousarray(X)) if np.isfinite(X).all() else C.cast(None, C.POINTER(C.c_double)))
+
+    def __del__(self):
+        try:
+            lib().oc_destroy(self.s)
+        except Exception:
+            pass
+
+    def shape(self, name):
+        n, m, N, P = self.n, self.m, self.N, max(self.pmax, 1)
+        return {"X": (N, n), "U": (N - 1, m), "Xbar": (N, n), "Ubar": (N - 1, m), "K": (N - 1, n, m),
+                "d": (N - 1, m), "A": (N - 1, n, n), "B": (N - 1, m, n), "S": (N, n, n), "Sx": (N, n),
+                "dV": (2,), "lambda": (N, P), "mu": (N, P), "C": (N, P), "x0": (n,), "stats": (abi.NSTATS,),
+                "rho": (2,)}[name]
+
+    def get(self, name):
+        out = np.empty(self.shape(name))
+        lib().oc_get(self.s, FIELDS[name], _dp(out))
+        if name in ("K", "A", "B", "S"):
+            out = np.ascontiguousarray(np.swapaxes(out, -1, -2))
+        return out
+
+    def set(self, name, v):
+        v = np.asarray(v, dtype=float)
+        if name in ("K", "A", "B", "S"):
+            v = np.swapaxes(v, -1, -2)
+        v = np.ascontiguousarray(v.reshape(self.shape(name)))
+        lib().oc_set(self.s, FIELDS[name], _dp(v))
+
+    # step level
+    def rollout_open_loop(self):
+        lib().oc_rollout_open_loop(self.s)
+
+    def rollout(self, alpha):
+        return bool(lib().oc_rollout(self.s, alpha))
+
+    def jacobians(self):
+        lib().oc_jacobians(self.s)
+
+    def update_constraints(self):
+        lib().oc_update_constraints(self.s)
+
+    def cost_expansion(self, sqrt=False, al=False):
+        return lib().oc_cost_expansion(self.s, int(sqrt), int(al))
+
+    def backward(self, sqrt=False):
+        dV = np.empty(2)
+        restarts = lib().oc_backward(self.s, int(sqrt), _dp(dV))
+        return dV, restarts
+
+    def forward(self, J_prev, al=False):
+        return lib().oc_forward(self.s, int(al), float(J_prev))
+
+    def cost(self, al=False):
+        return lib().oc_cost(self.s, int(al))
+
+    def solve(self):
+        if self.mode == abi.MODE_AL:
+            return lib().oc_solve_al(self.s)
+        return lib().oc_solve_ilqr(self.s)
+
+    def max_violation(self):
+        return lib().oc_max_violation(self.s)
+
+    def trace(self):
+        out = np.empty((4096, 6))
+        n = lib().oc_get_trace(self.s, _dp(out))
+        return out[:n]
+
+
+def solve_batch(prob, opts, nthreads=1, B=None):
+    """CPU baseline: solve ``B`` trajectories of ``prob`` with ``nthreads`` OpenMP threads.
+    Returns the total number of iLQR step!s."""
+    desc = prob.build_desc()
+    o = _pkg.to_tog_options(opts)
+    al = isinstance(opts, (_pkg.AugmentedLagrangianSolverOptions, _pkg.ALTROSolverOptions)) and prob.is_constrained()
+    B = prob.B if B is None else B
+    x0 = np.ascontiguousarray(prob.x0[:B])
+    U0 = np.ascontiguousarray(prob._U[:B])
+    return int(lib().oc_solve_batch(C.byref(desc.desc), C.byref(o), abi.MODE_AL if al else abi.MODE_ILQR,
+                                    _dp(x0), _dp(U0), B, nthreads))

@@ -1,0 +1,1831 @@
+/*
+ * tog_oracle.c — TEST INFRASTRUCTURE ONLY (parity oracle + CPU baseline "port").
+ *
+ * A plain-C, fp64, single-trajectory restatement of TrajectoryOptimization.jl's
+ * iLQR / augmented-Lagrangian hot path (reference mounted read-only at
+ * /root/reference; every function cites the file:line it follows). It is NOT
+ * part of the product: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load it, as the checker. The product (libtog.so, HIP) never
+ * links or calls it.
+ *
+ * Parity pinning: the reference cannot run here (no Julia toolchain; SURVEY.md
+ * §8c). This restatement is pinned by re-running the reference's own test
+ * assertions (tests/test_oracle.py: test/sqrt_bp_tests.jl, test/cost_tests.jl,
+ * test/constraint_tests.jl, test/model_tests.jl, test/test_utils.jl,
+ * test/quadrotor_tests.jl convergence thresholds) and by LAPACK cross-checks
+ * of its linear algebra (numpy.linalg). Rounding-level differences from Julia
+ * (BLAS summation order, ForwardDiff op order, LAPACK blocking) are expected;
+ * the parity bar is 1e-6 relative.
+ *
+ * Third-party arithmetic restated here: ForwardDiff v0.10.3 forward-mode duals
+ * (Manifest.toml:164-168) and the Julia 1.1 LinearAlgebra/LAPACK routines used
+ * by backward_pass.jl (geqrf Householder, potrf, getrf/getrs, lowrankdowndate!,
+ * cond via singular values).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/tog.h"
+
+#define DMAX 24 /* max partials: n+m+1 */
+#define OC_EXPORT __attribute__((visibility("default")))
+
+/* =====================================================================
+ * Dual numbers — ForwardDiff.Dual semantics (value + partials)
+ * ===================================================================== */
+typedef struct {
+  double v;
+  double p[DMAX];
+} dual;
+
+static int g_nd = 0; /* number of active partials (0 => primal evaluation) */
+
+static inline dual dc(double v) {
+  dual r;
+  r.v = v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = 0.0;
+  return r;
+}
+static inline dual dadd(dual a, dual b) {
+  dual r;
+  r.v = a.v + b.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = a.p[i] + b.p[i];
+  return r;
+}
+static inline dual dsub(dual a, dual b) {
+  dual r;
+  r.v = a.v - b.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = a.p[i] - b.p[i];
+  return r;
+}
+static inline dual dneg(dual a) {
+  dual r;
+  r.v = -a.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = -a.p[i];
+  return r;
+}
+/* ForwardDiff: x*y -> Dual(xv*yv, yv*x.p + xv*y.p) (dual.jl _mul_partials) */
+static inline dual dmul(dual a, dual b) {
+  dual r;
+  r.v = a.v * b.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = b.v * a.p[i] + a.v * b.p[i];
+  return r;
+}
+static inline dual dscale(dual a, double s) { /* Real * Dual */
+  dual r;
+  r.v = s * a.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = s * a.p[i];
+  return r;
+}
+static inline dual ddivc(dual a, double s) { /* Dual / Real */
+  dual r;
+  r.v = a.v / s;
+  for (int i = 0; i < g_nd; i++) r.p[i] = a.p[i] / s;
+  return r;
+}
+/* ForwardDiff: x/y -> Dual(xv/yv, x.p*inv(yv) + y.p*(-(xv/(yv*yv)))) */
+static inline dual ddiv(dual a, dual b) {
+  dual r;
+  double iy = 1.0 / b.v, c2 = -(a.v / (b.v * b.v));
+  r.v = a.v / b.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = a.p[i] * iy + b.p[i] * c2;
+  return r;
+}
+static inline dual dinv(dual a) { /* inv(x): 1/v, -p/v^2 */
+  dual r;
+  r.v = 1.0 / a.v;
+  double c = -(1.0 / (a.v * a.v));
+  for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
+  return r;
+}
+static inline dual dsin(dual a) {
+  dual r;
+  r.v = sin(a.v);
+  double c = cos(a.v);
+  for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
+  return r;
+}
+static inline dual dcos(dual a) {
+  dual r;
+  r.v = cos(a.v);
+  double c = -sin(a.v);
+  for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
+  return r;
+}
+static inline dual dsqrt(dual a) {
+  dual r;
+  r.v = sqrt(a.v);
+  double c = 1.0 / (2.0 * r.v);
+  for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
+  return r;
+}
+static inline dual dsq(dual a) { /* x^2 (literal_pow -> ^(Dual,2)): v^2, 2v*p */
+  dual r;
+  r.v = a.v * a.v;
+  double c = 2.0 * a.v;
+  for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
+  return r;
+}
+
+/* =====================================================================
+ * Continuous dynamics f!(xdot, x, u) on duals
+ * ===================================================================== */
+static const int model_n[TOG_MODEL_COUNT] = {2, 4, 13, 3, 2};
+static const int model_m[TOG_MODEL_COUNT] = {1, 1, 4, 2, 1};
+
+/* dynamics/double_integrator.jl:1-4 */
+static void f_double_integrator(dual* xd, const dual* x, const dual* u) {
+  xd[0] = x[1];
+  xd[1] = u[0];
+}
+
+/* dynamics/pendulum.jl:3-12 */
+static void f_pendulum(dual* xd, const dual* x, const dual* u) {
+  const double m = 1.0, b = 0.1, lc = 0.5, I = 0.25, g = 9.81;
+  xd[0] = x[1];
+  /* (u - m*g*lc*sin(x1) - b*x2)/I */
+  dual t = dsub(dsub(u[0], dscale(dsin(x[0]), m * g * lc)), dscale(x[1], b));
+  xd[1] = ddivc(t, I);
+}
+
+/* dynamics/car.jl:3-8 */
+static void f_car(dual* xd, const dual* x, const dual* u) {
+  xd[0] = dmul(u[0], dcos(x[2]));
+  xd[1] = dmul(u[0], dsin(x[2]));
+  xd[2] = u[1];
+}
+
+/* dynamics/cartpole.jl:9-36:  qdd = -H \ (C*qd + G - B*u), Julia generic LU (generic_lufact!,
+   partial pivoting; |H11|=1.2 > |H21| so never swaps for finite q2) */
+static void f_cartpole(dual* xd, const dual* x, const dual* u) {
+  const double mc = 1.0, mp = 0.2, l = 0.5, g = 9.81;
+  dual s, c;
+  if (isfinite(x[1].v)) {
+    s = dsin(x[1]);
+    c = dcos(x[1]);
+  } else { /* cartpole.jl:18-24 */
+    s = dc(INFINITY);
+    c = dc(INFINITY);
+  }
+  /* H = [mc+mp, mp*l*c; mp*l*c, mp*l^2] */
+  dual H11 = dc(mc + mp);
+  dual H12 = dscale(c, mp * l);
+  dual H21 = H12;
+  dual H22 = dc(mp * (l * l));
+  /* C*qd + G - B*u : C = [0 -mp*qd2*l*s; 0 0], G = [0; mp*g*l*s], B=[1;0] */
+  /* row 1: 0*qd1 + C12*qd2 + 0 - u ; C12 = -mp*qd[2]*l*s = ((-mp*qd2)*l)*s */
+  dual C12 = dmul(dscale(dscale(x[3], -mp), l), s);
+  dual r1 = dadd(dmul(dc(0.0), x[2]), dmul(C12, x[3]));
+  r1 = dsub(dadd(r1, dc(0.0)), u[0]);
+  /* row 2: 0*qd1 + 0*qd2 + mp*g*l*s - 0*u */
+  dual r2 = dadd(dmul(dc(0.0), x[2]), dmul(dc(0.0), x[3]));
+  r2 = dsub(dadd(r2, dscale(s, mp * g * l)), dscale(u[0], 0.0));
+  /* generic LU (no pivot swap when |H11| >= |H21|) */
+  dual a11 = H11, a12 = H12, a21 = H21, a22 = H22, b1 = r1, b2 = r2;
+  if (fabs(a21.v) > fabs(a11.v)) { /* partial pivoting swap */
+    dual t;
+    t = a11; a11 = a21; a21 = t;
+    t = a12; a12 = a22; a22 = t;
+    t = b1; b1 = b2; b2 = t;
+  }
+  dual l21 = dmul(a21, dinv(a11));
+  dual u22 = dsub(a22, dmul(l21, a12));
+  dual y2 = dsub(b2, dmul(l21, b1));
+  dual q2 = ddiv(y2, u22);
+  dual q1 = ddiv(dsub(b1, dmul(a12, q2)), a11);
+  xd[0] = x[2];
+  xd[1] = x[3];
+  xd[2] = dneg(q1);
+  xd[3] = dneg(q2);
+}
+
+/* dynamics/quadrotor.jl:10-71 with dynamics/quaternions.jl:23-40.
+   Hamilton product a⊗b = (aw*bw - av·bv, aw*bv + bw*av + av×bv); quaternions.jl:23-27 computes
+   w = s1*s2 - v1'v2, v = s1*v2 + s2*v1 + v2×v1 with (q2,q1) = (a,b). */
+static void qmul(dual* r, const dual* a, const dual* b) {
+  /* q1 = b, q2 = a */
+  dual s1 = b[0], s2 = a[0];
+  const dual* v1 = b + 1;
+  const dual* v2 = a + 1;
+  dual dot = dadd(dadd(dmul(v1[0], v2[0]), dmul(v1[1], v2[1])), dmul(v1[2], v2[2]));
+  r[0] = dsub(dmul(s1, s2), dot);
+  /* cross(v2, v1) */
+  dual cx = dsub(dmul(v2[1], v1[2]), dmul(v2[2], v1[1]));
+  dual cy = dsub(dmul(v2[2], v1[0]), dmul(v2[0], v1[2]));
+  dual cz = dsub(dmul(v2[0], v1[1]), dmul(v2[1], v1[0]));
+  r[1] = dadd(dadd(dmul(s1, v2[0]), dmul(s2, v1[0])), cx);
+  r[2] = dadd(dadd(dmul(s1, v2[1]), dmul(s2, v1[1])), cy);
+  r[3] = dadd(dadd(dmul(s1, v2[2]), dmul(s2, v1[2])), cz);
+}
+
+static void f_quadrotor(dual* xd, const dual* x, const dual* u) {
+  const double mass = 0.5, L = 0.175, kf = 1.0, km = 0.0245;
+  const double Jd[3] = {0.0023, 0.0023, 0.004};
+  const double Jinv[3] = {1.0 / 0.0023, 1.0 / 0.0023, 1.0 / 0.004};
+  const double grav[3] = {0.0, 0.0, -9.81};
+  /* q = normalize(Quaternion(x[4:7])) : StaticArrays normalize = inv(norm(a))*a */
+  dual nrm2 = dadd(dadd(dadd(dmul(x[3], x[3]), dmul(x[4], x[4])), dmul(x[5], x[5])), dmul(x[6], x[6]));
+  dual inrm = dinv(dsqrt(nrm2));
+  dual q[4];
+  for (int i = 0; i < 4; i++) q[i] = dmul(inrm, x[3 + i]);
+  const dual* v = x + 7;
+  const dual* om = x + 10;
+  dual F1 = dscale(u[0], kf), F2 = dscale(u[1], kf), F3 = dscale(u[2], kf), F4 = dscale(u[3], kf);
+  dual Fz = dadd(dadd(dadd(F1, F2), F3), F4);
+  dual M1 = dscale(u[0], km), M2 = dscale(u[1], km), M3 = dscale(u[2], km), M4 = dscale(u[3], km);
+  dual tau[3];
+  tau[0] = dscale(dsub(F2, F4), L);
+  tau[1] = dscale(dsub(F3, F1), L);
+  tau[2] = dsub(dadd(dsub(M1, M2), M3), M4);
+  /* xd[1:3] = v */
+  xd[0] = v[0];
+  xd[1] = v[1];
+  xd[2] = v[2];
+  /* xd[4:7] = 0.5*q*Quaternion(0, omega) */
+  dual hq[4], w4[4], qd[4];
+  for (int i = 0; i < 4; i++) hq[i] = dscale(q[i], 0.5);
+  w4[0] = dc(0.0);
+  w4[1] = om[0];
+  w4[2] = om[1];
+  w4[3] = om[2];
+  qmul(qd, hq, w4);
+  for (int i = 0; i < 4; i++) xd[3 + i] = qd[i];
+  /* xd[8:10] = g + (1/m)*(q*F),  q*F = vec(q*Quaternion(0,F)*inv(q)) */
+  dual F4q[4], t1[4], qinv[4], t2[4];
+  F4q[0] = dc(0.0);
+  F4q[1] = dc(0.0);
+  F4q[2] = dc(0.0);
+  F4q[3] = Fz;
+  qmul(t1, q, F4q);
+  qinv[0] = q[0];
+  qinv[1] = dneg(q[1]);
+  qinv[2] = dneg(q[2]);
+  qinv[3] = dneg(q[3]);
+  qmul(t2, t1, qinv);
+  for (int i = 0; i < 3; i++) xd[7 + i] = dadd(dc(grav[i]), dscale(t2[1 + i], 1.0 / mass));
+  /* xd[11:13] = Jinv*(tau - cross(omega, J*omega)) (diagonal J, Jinv) */
+  dual Jw[3];
+  for (int i = 0; i < 3; i++) Jw[i] = dscale(om[i], Jd[i]);
+  dual cr[3];
+  cr[0] = dsub(dmul(om[1], Jw[2]), dmul(om[2], Jw[1]));
+  cr[1] = dsub(dmul(om[2], Jw[0]), dmul(om[0], Jw[2]));
+  cr[2] = dsub(dmul(om[0], Jw[1]), dmul(om[1], Jw[0]));
+  for (int i = 0; i < 3; i++) xd[10 + i] = dscale(dsub(tau[i], cr[i]), Jinv[i]);
+}
+
+static void model_f(int model, dual* xd, const dual* x, const dual* u) {
+  switch (model) {
+    case TOG_MODEL_DOUBLE_INTEGRATOR: f_double_integrator(xd, x, u); break;
+    case TOG_MODEL_CARTPOLE: f_cartpole(xd, x, u); break;
+    case TOG_MODEL_QUADROTOR: f_quadrotor(xd, x, u); break;
+    case TOG_MODEL_CAR: f_car(xd, x, u); break;
+    case TOG_MODEL_PENDULUM: f_pendulum(xd, x, u); break;
+  }
+}
+
+/* rk4: src/integration.jl:115-125 ; rk3: src/integration.jl:149-158 (dt is a Dual input) */
+static void discrete_f_dual(int model, int integ, int n, dual* xn, const dual* x, const dual* u, dual dt) {
+  dual k1[16], k2[16], k3[16], k4[16], t[16];
+  model_f(model, k1, x, u);
+  for (int i = 0; i < n; i++) k1[i] = dmul(k1[i], dt);
+  for (int i = 0; i < n; i++) t[i] = dadd(x[i], ddivc(k1[i], 2.0));
+  model_f(model, k2, t, u);
+  for (int i = 0; i < n; i++) k2[i] = dmul(k2[i], dt);
+  if (integ == TOG_RK4) {
+    for (int i = 0; i < n; i++) t[i] = dadd(x[i], ddivc(k2[i], 2.0));
+    model_f(model, k3, t, u);
+    for (int i = 0; i < n; i++) k3[i] = dmul(k3[i], dt);
+    for (int i = 0; i < n; i++) t[i] = dadd(x[i], k3[i]);
+    model_f(model, k4, t, u);
+    for (int i = 0; i < n; i++) k4[i] = dmul(k4[i], dt);
+    /* x + (k1 + 2*k2 + 2*k3 + k4)/6 */
+    for (int i = 0; i < n; i++) {
+      dual s = dadd(dadd(dadd(k1[i], dscale(k2[i], 2.0)), dscale(k3[i], 2.0)), k4[i]);
+      xn[i] = dadd(x[i], ddivc(s, 6.0));
+    }
+  } else {
+    /* k3 = f(x - k1 + 2*k2) */
+    for (int i = 0; i < n; i++) t[i] = dadd(dsub(x[i], k1[i]), dscale(k2[i], 2.0));
+    model_f(model, k3, t, u);
+    for (int i = 0; i < n; i++) k3[i] = dmul(k3[i], dt);
+    /* x + (k1 + 4*k2 + k3)/6 */
+    for (int i = 0; i < n; i++) {
+      dual s = dadd(dadd(k1[i], dscale(k2[i], 4.0)), k3[i]);
+      xn[i] = dadd(x[i], ddivc(s, 6.0));
+    }
+  }
+}
+
+/* evaluate!(ẋ, model::Model{M,Discrete}, x, u, dt)  src/model.jl:171-174 */
+OC_EXPORT void oc_discrete_f(int model, int integ, double* xn, const double* x, const double* u, double dt) {
+  int n = model_n[model], m = model_m[model];
+  int save = g_nd;
+  g_nd = 0;
+  dual X[16], U[8], XN[16];
+  for (int i = 0; i < n; i++) X[i].v = x[i];
+  for (int i = 0; i < m; i++) U[i].v = u[i];
+  dual DT;
+  DT.v = dt;
+  discrete_f_dual(model, integ, n, XN, X, U, DT);
+  for (int i = 0; i < n; i++) xn[i] = XN[i].v;
+  g_nd = save;
+}
+
+/* continuous dynamics (for tests) */
+OC_EXPORT void oc_continuous_f(int model, double* xd, const double* x, const double* u) {
+  int n = model_n[model], m = model_m[model];
+  g_nd = 0;
+  dual X[16], U[8], XD[16];
+  for (int i = 0; i < n; i++) X[i].v = x[i];
+  for (int i = 0; i < m; i++) U[i].v = u[i];
+  model_f(model, XD, X, U);
+  for (int i = 0; i < n; i++) xd[i] = XD[i].v;
+}
+
+/* ∇fd!(S, x, u, dt): ForwardDiff.jacobian!(S, fd_aug!, ẋ, [x;u;dt])  src/model.jl:491-512.
+   S is n x (n+m+1) column-major, partitioned xx | xu | xdt (src/model.jl:341). */
+OC_EXPORT void oc_discrete_jacobian(int model, int integ, double* S, const double* x, const double* u, double dt) {
+  int n = model_n[model], m = model_m[model];
+  int L = n + m + 1;
+  g_nd = L;
+  dual X[16], U[8], XN[16], DT;
+  for (int i = 0; i < n; i++) {
+    X[i] = dc(x[i]);
+    X[i].p[i] = 1.0;
+  }
+  for (int i = 0; i < m; i++) {
+    U[i] = dc(u[i]);
+    U[i].p[n + i] = 1.0;
+  }
+  DT = dc(dt);
+  DT.p[n + m] = 1.0;
+  discrete_f_dual(model, integ, n, XN, X, U, DT);
+  for (int j = 0; j < L; j++)
+    for (int i = 0; i < n; i++) S[i + n * j] = XN[i].p[j];
+  g_nd = 0;
+}
+
+OC_EXPORT int oc_model_n(int model) { return model_n[model]; }
+OC_EXPORT int oc_model_m(int model) { return model_m[model]; }
+
+/* =====================================================================
+ * Small dense linear algebra (column-major), restating Julia 1.1 / LAPACK
+ * ===================================================================== */
+#define IDX(i, j, ld) ((i) + (size_t)(j) * (ld))
+
+/* C(r x c) = A^T(r x k) * B(k x c) where A is k x r */
+static void matTmul(double* C, const double* A, int k, int r, const double* B, int c) {
+  for (int j = 0; j < c; j++)
+    for (int i = 0; i < r; i++) {
+      double s = 0.0;
+      for (int l = 0; l < k; l++) s += A[IDX(l, i, k)] * B[IDX(l, j, k)];
+      C[IDX(i, j, r)] = s;
+    }
+}
+/* C(r x c) = A(r x k) * B(k x c) */
+static void matmul(double* C, const double* A, int r, int k, const double* B, int c) {
+  for (int j = 0; j < c; j++)
+    for (int i = 0; i < r; i++) {
+      double s = 0.0;
+      for (int l = 0; l < k; l++) s += A[IDX(i, l, r)] * B[IDX(l, j, k)];
+      C[IDX(i, j, r)] = s;
+    }
+}
+
+/* dlapy2 */
+static double lapy2(double x, double y) {
+  double xa = fabs(x), ya = fabs(y);
+  double w = xa > ya ? xa : ya, z = xa < ya ? xa : ya;
+  if (z == 0.0 || w > 1.79e308) return w;
+  double t = z / w;
+  return w * sqrt(1.0 + t * t);
+}
+
+/* R factor of qr(P) for P (rows x cols), rows >= cols, LAPACK dgeqr2/dlarfg Householder.
+   Julia: qr(P).R (chol_plus, backward_pass.jl:172-183). Writes the cols x cols upper triangle to R. */
+static void qr_R(double* R, double* P, int rows, int cols) {
+  int kmax = rows < cols ? rows : cols;
+  for (int j = 0; j < kmax; j++) {
+    double alpha = P[IDX(j, j, rows)];
+    double xnorm = 0.0;
+    {
+      /* dnrm2 with scaling */
+      double scale = 0.0, ssq = 1.0;
+      for (int i = j + 1; i < rows; i++) {
+        double a = P[IDX(i, j, rows)];
+        if (a != 0.0) {
+          double absxi = fabs(a);
+          if (scale < absxi) {
+            ssq = 1.0 + ssq * (scale / absxi) * (scale / absxi);
+            scale = absxi;
+          } else {
+            ssq += (absxi / scale) * (absxi / scale);
+          }
+        }
+      }
+      xnorm = scale * sqrt(ssq);
+    }
+    if (xnorm == 0.0) continue; /* tau = 0, H = I */
+    double beta = -copysign(lapy2(alpha, xnorm), alpha);
+    double tau = (beta - alpha) / beta;
+    double sc = 1.0 / (alpha - beta);
+    for (int i = j + 1; i < rows; i++) P[IDX(i, j, rows)] *= sc;
+    P[IDX(j, j, rows)] = beta;
+    /* apply H = I - tau v v' to P[j:rows, j+1:cols], v = [1; P[j+1:rows, j]] */
+    for (int c = j + 1; c < cols; c++) {
+      double w = P[IDX(j, c, rows)];
+      for (int i = j + 1; i < rows; i++) w += P[IDX(i, j, rows)] * P[IDX(i, c, rows)];
+      w *= tau;
+      P[IDX(j, c, rows)] -= w;
+      for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] -= P[IDX(i, j, rows)] * w;
+    }
+  }
+  for (int j = 0; j < cols; j++)
+    for (int i = 0; i < cols; i++) R[IDX(i, j, cols)] = (i <= j && i < rows) ? P[IDX(i, j, rows)] : 0.0;
+}
+
+/* chol_plus(A, B) = qr([A; B]).R, A n1 x c, B n2 x c (backward_pass.jl:172-179) */
+static void chol_plus(double* R, const double* A, int n1, const double* B, int n2, int c) {
+  int rows = n1 + n2;
+  double* P = (double*)malloc(sizeof(double) * rows * c);
+  for (int j = 0; j < c; j++) {
+    for (int i = 0; i < n1; i++) P[IDX(i, j, rows)] = A[IDX(i, j, n1)];
+    for (int i = 0; i < n2; i++) P[IDX(n1 + i, j, rows)] = B[IDX(i, j, n2)];
+  }
+  qr_R(R, P, rows, c);
+  free(P);
+}
+
+/* upper Cholesky (dpotrf uplo=U) reading only the upper triangle; returns 0 on success
+   (isposdef(Hermitian(A)), cholesky(A).U).  U written with zeros below the diagonal. */
+static int chol_upper(double* Uo, const double* A, int n) {
+  double* U = (double*)calloc((size_t)n * n, sizeof(double));
+  int info = 0;
+  for (int j = 0; j < n && !info; j++) {
+    double s = A[IDX(j, j, n)];
+    for (int k = 0; k < j; k++) s -= U[IDX(k, j, n)] * U[IDX(k, j, n)];
+    if (!(s > 0.0)) {
+      info = j + 1;
+      break;
+    }
+    double ujj = sqrt(s);
+    U[IDX(j, j, n)] = ujj;
+    for (int c = j + 1; c < n; c++) {
+      double t = A[IDX(j, c, n)];
+      for (int k = 0; k < j; k++) t -= U[IDX(k, j, n)] * U[IDX(k, c, n)];
+      U[IDX(j, c, n)] = t / ujj;
+    }
+  }
+  if (!info && Uo) memcpy(Uo, U, sizeof(double) * n * n);
+  free(U);
+  return info;
+}
+
+/* X = A \ B with A n x n general (LU with partial pivoting, dgetrf/dgetrs; Julia `\`).
+   Julia's `\` first checks istriu/istril and uses triangular substitution when applicable. */
+static int is_triu(const double* A, int n) {
+  for (int j = 0; j < n; j++)
+    for (int i = j + 1; i < n; i++)
+      if (A[IDX(i, j, n)] != 0.0) return 0;
+  return 1;
+}
+static int is_tril(const double* A, int n) {
+  for (int j = 0; j < n; j++)
+    for (int i = 0; i < j; i++)
+      if (A[IDX(i, j, n)] != 0.0) return 0;
+  return 1;
+}
+static void solve_upper(const double* A, int n, double* B, int nrhs) {
+  for (int c = 0; c < nrhs; c++)
+    for (int j = n - 1; j >= 0; j--) {
+      double xj = B[IDX(j, c, n)] / A[IDX(j, j, n)];
+      B[IDX(j, c, n)] = xj;
+      for (int i = j - 1; i >= 0; i--) B[IDX(i, c, n)] -= A[IDX(i, j, n)] * xj;
+    }
+}
+static void solve_lower(const double* A, int n, double* B, int nrhs) {
+  for (int c = 0; c < nrhs; c++)
+    for (int j = 0; j < n; j++) {
+      double xj = B[IDX(j, c, n)] / A[IDX(j, j, n)];
+      B[IDX(j, c, n)] = xj;
+      for (int i = j + 1; i < n; i++) B[IDX(i, c, n)] -= A[IDX(i, j, n)] * xj;
+    }
+}
+static void lu_solve(const double* Ain, int n, double* B, int nrhs) {
+  if (is_triu(Ain, n)) {
+    solve_upper(Ain, n, B, nrhs);
+    return;
+  }
+  if (is_tril(Ain, n)) {
+    solve_lower(Ain, n, B, nrhs);
+    return;
+  }
+  double* A = (double*)malloc(sizeof(double) * n * n);
+  memcpy(A, Ain, sizeof(double) * n * n);
+  int piv[32];
+  for (int k = 0; k < n; k++) {
+    int p = k;
+    double amax = fabs(A[IDX(k, k, n)]);
+    for (int i = k + 1; i < n; i++)
+      if (fabs(A[IDX(i, k, n)]) > amax) {
+        amax = fabs(A[IDX(i, k, n)]);
+        p = i;
+      }
+    piv[k] = p;
+    if (p != k)
+      for (int j = 0; j < n; j++) {
+        double t = A[IDX(k, j, n)];
+        A[IDX(k, j, n)] = A[IDX(p, j, n)];
+        A[IDX(p, j, n)] = t;
+      }
+    double akk = A[IDX(k, k, n)];
+    if (akk != 0.0) {
+      double r = 1.0 / akk;
+      for (int i = k + 1; i < n; i++) A[IDX(i, k, n)] *= r;
+    }
+    for (int j = k + 1; j < n; j++)
+      for (int i = k + 1; i < n; i++) A[IDX(i, j, n)] -= A[IDX(i, k, n)] * A[IDX(k, j, n)];
+  }
+  for (int c = 0; c < nrhs; c++) {
+    double* b = B + (size_t)c * n;
+    for (int k = 0; k < n; k++)
+      if (piv[k] != k) {
+        double t = b[k];
+        b[k] = b[piv[k]];
+        b[piv[k]] = t;
+      }
+    for (int j = 0; j < n; j++)
+      for (int i = j + 1; i < n; i++) b[i] -= A[IDX(i, j, n)] * b[j];
+    for (int j = n - 1; j >= 0; j--) {
+      b[j] /= A[IDX(j, j, n)];
+      for (int i = 0; i < j; i++) b[i] -= A[IDX(i, j, n)] * b[j];
+    }
+  }
+  free(A);
+}
+
+/* singular values of a small n x n matrix by one-sided Jacobi; returns cond = smax/smin (cond(A)) */
+static double cond2(const double* Ain, int n) {
+  double A[64], V[64];
+  memcpy(A, Ain, sizeof(double) * n * n);
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double off = 0.0;
+    for (int p = 0; p < n - 1; p++)
+      for (int q = p + 1; q < n; q++) {
+        double alpha = 0, beta = 0, gamma = 0;
+        for (int i = 0; i < n; i++) {
+          alpha += A[IDX(i, p, n)] * A[IDX(i, p, n)];
+          beta += A[IDX(i, q, n)] * A[IDX(i, q, n)];
+          gamma += A[IDX(i, p, n)] * A[IDX(i, q, n)];
+        }
+        if (gamma == 0.0) continue;
+        double c0 = fabs(gamma) / sqrt(alpha * beta);
+        if (c0 > off) off = c0;
+        if (c0 < 1e-15) continue;
+        double zeta = (beta - alpha) / (2.0 * gamma);
+        double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+        for (int i = 0; i < n; i++) {
+          double ap = A[IDX(i, p, n)], aq = A[IDX(i, q, n)];
+          A[IDX(i, p, n)] = c * ap - s * aq;
+          A[IDX(i, q, n)] = s * ap + c * aq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  (void)V;
+  double smax = 0.0, smin = INFINITY;
+  for (int j = 0; j < n; j++) {
+    double s = 0;
+    for (int i = 0; i < n; i++) s += A[IDX(i, j, n)] * A[IDX(i, j, n)];
+    s = sqrt(s);
+    if (s > smax) smax = s;
+    if (s < smin) smin = s;
+  }
+  if (isnan(smax) || isnan(smin)) return NAN;
+  return smax / smin;
+}
+
+OC_EXPORT double oc_cond2(const double* A, int n) { return cond2(A, n); }
+OC_EXPORT void oc_qr_R(double* R, double* P, int rows, int cols) { qr_R(R, P, rows, cols); }
+
+/* chol_minus(A, B) (backward_pass.jl:186-192): Cholesky(copy(A), :U, 0) then
+   lowrankdowndate!(C, B[i,:]) per row (Julia 1.1 LinearAlgebra cholesky.jl). Returns 0 or
+   PosDefException index. */
+static int chol_minus(double* Uo, const double* A, int n, const double* B, int nb) {
+  double U[64], v[8];
+  memcpy(U, A, sizeof(double) * n * n);
+  for (int r = 0; r < nb; r++) {
+    for (int j = 0; j < n; j++) v[j] = B[IDX(r, j, nb)];
+    for (int i = 0; i < n; i++) {
+      double Aii = U[IDX(i, i, n)];
+      double s = v[i] / Aii;
+      double s2 = s * s;
+      if (s2 > 1.0) return i + 1;
+      double c = sqrt(1.0 - s2);
+      U[IDX(i, i, n)] = c * Aii;
+      for (int j = i + 1; j < n; j++) {
+        double tmp = (U[IDX(i, j, n)] - s * v[j]) / c;
+        v[j] = c * v[j] - s * tmp;
+        U[IDX(i, j, n)] = tmp;
+      }
+    }
+  }
+  memcpy(Uo, U, sizeof(double) * n * n);
+  return 0;
+}
+
+/* =====================================================================
+ * Problem (single trajectory view of tog_problem_desc)
+ * ===================================================================== */
+typedef struct {
+  int type;     /* tog_constraint_type */
+  int inequality;
+  int p_stage, p_term;
+  /* bound */
+  double x_max[16], x_min[16], u_max[8], u_min[8];
+  int ax_max[16], ax_min[16], au_max[8], au_min[8];
+  /* goal */
+  double xf[16];
+  /* obstacles */
+  int count;
+  double obs[64 * 4];
+} oc_con;
+
+typedef struct {
+  int ncon;
+  oc_con con[8];
+  int p_stage, p_term;
+} oc_cset;
+
+typedef struct oc_solver {
+  int model, integ, n, m, N;
+  double dt;
+  double *Q, *R, *H, *q, *r, c, *Qf, *qf, cf;
+  int nsets;
+  oc_cset* sets;
+  int* knot_set;
+  int* p;   /* p[k] constraints at knot k */
+  int pmax;
+  tog_options opts;
+  /* iLQR solver buffers (ilqr_solver.jl:93-144) */
+  double *x0, *X, *U, *Xb, *Ub, *K, *d, *F; /* F: n x (n+m+1) per knot */
+  double *Sxx, *Sx;                         /* S[k].xx, S[k].x */
+  double *Qx, *Qu, *Qxx, *Quu, *Qux;        /* Q expansion per knot */
+  double rho, drho;
+  double dV[2];
+  /* AL (augmented_lagrangian_solver.jl:111-118) */
+  double *C, *lam, *mu;
+  int* active;
+  int* ineq; /* ineq[k*pmax+i] 1 if inequality */
+  /* stats */
+  int iterations, zero_count, bp_restarts, ls_trials, al_iter, total_steps, flags;
+  double J, dJ, gradient, alpha, z, c_max, expected;
+  /* per-iteration trace (for localisation) */
+  int trace_len;
+  double* trace; /* [J, alpha, rho, restarts, trials, z] per step */
+} oc_solver;
+
+static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
+  memset(oc, 0, sizeof(*oc));
+  oc->type = tc->type;
+  switch (tc->type) {
+    case TOG_CON_BOUND: {
+      /* src/constraints.jl:155-188, trim=true: active = isfinite.(bound) */
+      const double* D = tc->data;
+      int cx = 0, cu = 0, cxn = 0, cun = 0;
+      for (int i = 0; i < n; i++) {
+        oc->x_max[i] = D[i];
+        oc->x_min[i] = D[n + i];
+        oc->ax_max[i] = isfinite(D[i]);
+        oc->ax_min[i] = isfinite(D[n + i]);
+        cx += oc->ax_max[i];
+        cxn += oc->ax_min[i];
+      }
+      for (int i = 0; i < m; i++) {
+        oc->u_max[i] = D[2 * n + i];
+        oc->u_min[i] = D[2 * n + m + i];
+        oc->au_max[i] = isfinite(D[2 * n + i]);
+        oc->au_min[i] = isfinite(D[2 * n + m + i]);
+        cu += oc->au_max[i];
+        cun += oc->au_min[i];
+      }
+      oc->inequality = 1;
+      oc->p_stage = cx + cu + cxn + cun;
+      oc->p_term = cx + cxn; /* length(bnd, :terminal) constraints.jl:244-252 */
+      break;
+    }
+    case TOG_CON_GOAL:
+      for (int i = 0; i < n; i++) oc->xf[i] = tc->data[i];
+      oc->inequality = 0;
+      oc->p_stage = 0; /* terminal-only (term=:terminal) */
+      oc->p_term = n;
+      break;
+    case TOG_CON_CIRCLES:
+      oc->count = tc->count;
+      memcpy(oc->obs, tc->data, sizeof(double) * 3 * tc->count);
+      oc->inequality = 1;
+      oc->p_stage = tc->count;
+      oc->p_term = 0; /* stage-only: c(v,x,u) method only */
+      break;
+    case TOG_CON_SPHERES:
+      oc->count = tc->count;
+      memcpy(oc->obs, tc->data, sizeof(double) * 4 * tc->count);
+      oc->inequality = 1;
+      oc->p_stage = tc->count;
+      oc->p_term = 0;
+      break;
+  }
+}
+
+/* evaluate constraint `oc` into v (stage: x,u; terminal: u == NULL), and its Jacobian rows
+   into Jx (p x n, ld = ldj) and Ju (p x m) if non-NULL. src/constraints.jl:212-237,299-304,
+   src/utils.jl:140-156 (ForwardDiff of the generic primitives = the analytic derivative). */
+static int con_eval(const oc_con* oc, int n, int m, const double* x, const double* u, double* v,
+                    double* Jx, double* Ju, int ldj) {
+  int term = (u == NULL);
+  int r = 0;
+  switch (oc->type) {
+    case TOG_CON_BOUND:
+      if (!term) {
+        for (int i = 0; i < n; i++)
+          if (oc->ax_max[i]) {
+            v[r] = x[i] - oc->x_max[i];
+            if (Jx) Jx[r + ldj * i] = 1.0;
+            r++;
+          }
+        for (int i = 0; i < m; i++)
+          if (oc->au_max[i]) {
+            v[r] = u[i] - oc->u_max[i];
+            if (Ju) Ju[r + ldj * i] = 1.0;
+            r++;
+          }
+        for (int i = 0; i < n; i++)
+          if (oc->ax_min[i]) {
+            v[r] = oc->x_min[i] - x[i];
+            if (Jx) Jx[r + ldj * i] = -1.0;
+            r++;
+          }
+        for (int i = 0; i < m; i++)
+          if (oc->au_min[i]) {
+            v[r] = oc->u_min[i] - u[i];
+            if (Ju) Ju[r + ldj * i] = -1.0;
+            r++;
+          }
+      } else {
+        for (int i = 0; i < n; i++)
+          if (oc->ax_max[i]) {
+            v[r] = x[i] - oc->x_max[i];
+            if (Jx) Jx[r + ldj * i] = 1.0;
+            r++;
+          }
+        for (int i = 0; i < n; i++)
+          if (oc->ax_min[i]) {
+            v[r] = oc->x_min[i] - x[i];
+            if (Jx) Jx[r + ldj * i] = -1.0;
+            r++;
+          }
+      }
+      break;
+    case TOG_CON_GOAL:
+      if (term) {
+        for (int i = 0; i < n; i++) {
+          v[r] = x[i] - oc->xf[i];
+          if (Jx) Jx[r + ldj * i] = 1.0;
+          r++;
+        }
+      }
+      break;
+    case TOG_CON_CIRCLES:
+      if (!term) {
+        for (int o = 0; o < oc->count; o++) {
+          double x0 = oc->obs[3 * o], y0 = oc->obs[3 * o + 1], rr = oc->obs[3 * o + 2];
+          double dx = x[0] - x0, dy = x[1] - y0;
+          v[r] = -((dx * dx + dy * dy) - rr * rr);
+          if (Jx) {
+            Jx[r + ldj * 0] = -(2.0 * dx);
+            Jx[r + ldj * 1] = -(2.0 * dy);
+          }
+          r++;
+        }
+      }
+      break;
+    case TOG_CON_SPHERES:
+      if (!term) {
+        for (int o = 0; o < oc->count; o++) {
+          double x0 = oc->obs[4 * o], y0 = oc->obs[4 * o + 1], z0 = oc->obs[4 * o + 2], rr = oc->obs[4 * o + 3];
+          double dx = x[0] - x0, dy = x[1] - y0, dz = x[2] - z0;
+          v[r] = -(((dx * dx + dy * dy) + dz * dz) - rr * rr);
+          if (Jx) {
+            Jx[r + ldj * 0] = -(2.0 * dx);
+            Jx[r + ldj * 1] = -(2.0 * dy);
+            Jx[r + ldj * 2] = -(2.0 * dz);
+          }
+          r++;
+        }
+      }
+      break;
+  }
+  return r;
+}
+
+/* evaluate!(c, C::ConstraintSet, x[, u]) (constraint_sets.jl:106-118) + jacobian
+   (constraint_sets.jl:121-131). Jx: p x n (ld p), Ju: p x m. Returns p. */
+static int set_eval(const oc_solver* s, int k, const double* x, const double* u, double* c, double* Jx, double* Ju,
+                    int* ineq) {
+  int si = s->knot_set[k];
+  if (si < 0) return 0;
+  const oc_cset* set = &s->sets[si];
+  int term = (k == s->N - 1);
+  int p = term ? set->p_term : set->p_stage;
+  if (Jx) memset(Jx, 0, sizeof(double) * p * s->n);
+  if (Ju) memset(Ju, 0, sizeof(double) * p * s->m);
+  int r = 0;
+  for (int i = 0; i < set->ncon; i++) {
+    const oc_con* oc = &set->con[i];
+    int pr = term ? oc->p_term : oc->p_stage;
+    if (pr == 0) continue;
+    con_eval(oc, s->n, s->m, x, term ? NULL : u, c + r, Jx ? Jx + r : NULL, Ju ? Ju + r : NULL, p);
+    if (ineq)
+      for (int j = 0; j < pr; j++) ineq[r + j] = oc->inequality;
+    r += pr;
+  }
+  return p;
+}
+
+static void desc_load(oc_solver* s, const tog_problem_desc* d) {
+  s->model = d->model;
+  s->integ = d->integrator;
+  s->n = d->n;
+  s->m = d->m;
+  s->N = d->N;
+  s->dt = d->dt;
+  int n = s->n, m = s->m, N = s->N;
+  s->Q = malloc(sizeof(double) * n * n);
+  memcpy(s->Q, d->Q, sizeof(double) * n * n);
+  s->R = malloc(sizeof(double) * m * m);
+  memcpy(s->R, d->R, sizeof(double) * m * m);
+  s->H = malloc(sizeof(double) * m * n);
+  memcpy(s->H, d->H, sizeof(double) * m * n);
+  s->q = malloc(sizeof(double) * n);
+  memcpy(s->q, d->q, sizeof(double) * n);
+  s->r = malloc(sizeof(double) * m);
+  memcpy(s->r, d->r, sizeof(double) * m);
+  s->c = d->c;
+  s->Qf = malloc(sizeof(double) * n * n);
+  memcpy(s->Qf, d->Qf, sizeof(double) * n * n);
+  s->qf = malloc(sizeof(double) * n);
+  memcpy(s->qf, d->qf, sizeof(double) * n);
+  s->cf = d->cf;
+  s->nsets = d->n_sets;
+  s->sets = calloc(d->n_sets > 0 ? d->n_sets : 1, sizeof(oc_cset));
+  for (int i = 0; i < d->n_sets; i++) {
+    oc_cset* os = &s->sets[i];
+    os->ncon = d->sets[i].n_con;
+    for (int j = 0; j < os->ncon; j++) {
+      con_init(&os->con[j], &d->sets[i].con[j], n, m);
+      os->p_stage += os->con[j].p_stage;
+      os->p_term += os->con[j].p_term;
+    }
+  }
+  s->knot_set = malloc(sizeof(int) * N);
+  s->p = malloc(sizeof(int) * N);
+  s->pmax = 0;
+  for (int k = 0; k < N; k++) {
+    s->knot_set[k] = d->knot_set ? d->knot_set[k] : -1;
+    int si = s->knot_set[k];
+    s->p[k] = si < 0 ? 0 : (k == N - 1 ? s->sets[si].p_term : s->sets[si].p_stage);
+    if (s->p[k] > s->pmax) s->pmax = s->p[k];
+  }
+}
+
+#define Xk(s, k) ((s)->X + (size_t)(k) * (s)->n)
+#define Uk(s, k) ((s)->U + (size_t)(k) * (s)->m)
+
+OC_EXPORT oc_solver* oc_create(const tog_problem_desc* d, const tog_options* o) {
+  oc_solver* s = calloc(1, sizeof(oc_solver));
+  desc_load(s, d);
+  s->opts = *o;
+  int n = s->n, m = s->m, N = s->N, P = s->pmax > 0 ? s->pmax : 1;
+  s->x0 = calloc(n, sizeof(double));
+  s->X = calloc((size_t)n * N, sizeof(double));
+  s->U = calloc((size_t)m * (N - 1), sizeof(double));
+  s->Xb = calloc((size_t)n * N, sizeof(double));
+  s->Ub = calloc((size_t)m * (N - 1), sizeof(double));
+  s->K = calloc((size_t)m * n * (N - 1), sizeof(double));
+  s->d = calloc((size_t)m * (N - 1), sizeof(double));
+  s->F = calloc((size_t)n * (n + m + 1) * (N - 1), sizeof(double));
+  s->Sxx = calloc((size_t)n * n * N, sizeof(double));
+  s->Sx = calloc((size_t)n * N, sizeof(double));
+  s->Qx = calloc((size_t)n * N, sizeof(double));
+  s->Qu = calloc((size_t)m * N, sizeof(double));
+  s->Qxx = calloc((size_t)n * n * N, sizeof(double));
+  s->Quu = calloc((size_t)m * m * N, sizeof(double));
+  s->Qux = calloc((size_t)m * n * N, sizeof(double));
+  s->C = calloc((size_t)P * N, sizeof(double));
+  s->lam = calloc((size_t)P * N, sizeof(double));
+  s->mu = calloc((size_t)P * N, sizeof(double));
+  s->active = calloc((size_t)P * N, sizeof(int));
+  for (int i = 0; i < P * N; i++) s->mu[i] = o->penalty_initial; /* init_constraint_trajectories μ_init */
+  s->ineq = calloc((size_t)P * N, sizeof(int));
+  for (int k = 0; k < N; k++) {
+    double cbuf[256];
+    double xz[16] = {0}, uz[8] = {0};
+    set_eval(s, k, xz, k < N - 1 ? uz : NULL, cbuf, NULL, NULL, s->ineq + (size_t)k * P);
+  }
+  s->trace = calloc(6 * 4096, sizeof(double));
+  return s;
+}
+
+OC_EXPORT void oc_destroy(oc_solver* s) {
+  if (!s) return;
+  free(s->Q); free(s->R); free(s->H); free(s->q); free(s->r); free(s->Qf); free(s->qf);
+  free(s->sets); free(s->knot_set); free(s->p);
+  free(s->x0); free(s->X); free(s->U); free(s->Xb); free(s->Ub); free(s->K); free(s->d); free(s->F);
+  free(s->Sxx); free(s->Sx); free(s->Qx); free(s->Qu); free(s->Qxx); free(s->Quu); free(s->Qux);
+  free(s->C); free(s->lam); free(s->mu); free(s->active); free(s->ineq); free(s->trace);
+  free(s);
+}
+
+OC_EXPORT int oc_pmax(oc_solver* s) { return s->pmax; }
+
+/* initial_controls!, set_x0!, X0 = NaN (src/problem.jl:149-160,232) */
+OC_EXPORT void oc_set_state(oc_solver* s, const double* x0, const double* U, const double* X) {
+  memcpy(s->x0, x0, sizeof(double) * s->n);
+  memcpy(s->U, U, sizeof(double) * s->m * (s->N - 1));
+  if (X)
+    memcpy(s->X, X, sizeof(double) * s->n * s->N);
+  else
+    for (int i = 0; i < s->n * s->N; i++) s->X[i] = NAN;
+}
+
+/* =====================================================================
+ * Cost (src/cost.jl:171-181, src/objective.jl:40-48)
+ * ===================================================================== */
+static double stage_cost(const oc_solver* s, const double* x, const double* u, double dt) {
+  int n = s->n, m = s->m;
+  /* 0.5*x'Q*x + 0.5*u'*R*u + q'x + r'u + c + u'*H*x, then *dt */
+  double xQx = 0, uRu = 0, qx = 0, ru = 0, uHx = 0;
+  for (int j = 0; j < n; j++) {
+    double t = 0;
+    for (int i = 0; i < n; i++) t += (0.5 * x[i]) * s->Q[IDX(i, j, n)];
+    xQx += t * x[j];
+  }
+  for (int j = 0; j < m; j++) {
+    double t = 0;
+    for (int i = 0; i < m; i++) t += (0.5 * u[i]) * s->R[IDX(i, j, m)];
+    uRu += t * u[j];
+  }
+  for (int i = 0; i < n; i++) qx += s->q[i] * x[i];
+  for (int i = 0; i < m; i++) ru += s->r[i] * u[i];
+  for (int j = 0; j < n; j++) {
+    double t = 0;
+    for (int i = 0; i < m; i++) t += u[i] * s->H[IDX(i, j, m)];
+    uHx += t * x[j];
+  }
+  return ((((xQx + uRu) + qx) + ru) + s->c + uHx) * dt;
+}
+static double terminal_cost(const oc_solver* s, const double* x) {
+  int n = s->n;
+  double xQx = 0, qx = 0;
+  for (int j = 0; j < n; j++) {
+    double t = 0;
+    for (int i = 0; i < n; i++) t += (0.5 * x[i]) * s->Qf[IDX(i, j, n)];
+    xQx += t * x[j];
+  }
+  for (int i = 0; i < n; i++) qx += s->qf[i] * x[i];
+  return (xQx + qx) + s->cf;
+}
+
+static double obj_cost(const oc_solver* s, const double* X, const double* U) {
+  int n = s->n, m = s->m, N = s->N;
+  double J = 0.0;
+  for (int k = 0; k < N - 1; k++) J += stage_cost(s, X + (size_t)k * n, U + (size_t)k * m, s->dt);
+  J += terminal_cost(s, X + (size_t)(N - 1) * n);
+  return J;
+}
+
+/* update_constraints! + update_active_set! (constraint_sets.jl:221-260) */
+static void update_constraints(oc_solver* s, const double* X, const double* U) {
+  int n = s->n, m = s->m, N = s->N, P = s->pmax;
+  for (int k = 0; k < N; k++) {
+    if (s->p[k] == 0) continue;
+    set_eval(s, k, X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : NULL, s->C + (size_t)k * P, NULL, NULL, NULL);
+  }
+}
+static void update_active_set(oc_solver* s) {
+  int N = s->N, P = s->pmax;
+  for (int k = 0; k < N; k++)
+    for (int i = 0; i < s->p[k]; i++) {
+      size_t j = (size_t)k * P + i;
+      s->active[j] = s->ineq[j] ? ((s->C[j] >= 0.0) || (s->lam[j] > 0.0)) : 1;
+    }
+}
+
+/* AL cost (augmented_lagrangian_methods.jl:298-313): mutates C and the active set (A.10) */
+static double al_cost(oc_solver* s, const double* X, const double* U) {
+  int N = s->N, P = s->pmax;
+  double J = obj_cost(s, X, U);
+  update_constraints(s, X, U);
+  update_active_set(s);
+  double Jc = 0.0;
+  for (int k = 0; k < N; k++) {
+    /* aula_cost: λ'c + 1/2*c'Diagonal(a .* μ)*c */
+    double lc = 0.0, cIc = 0.0;
+    for (int i = 0; i < s->p[k]; i++) {
+      size_t j = (size_t)k * P + i;
+      lc += s->lam[j] * s->C[j];
+    }
+    for (int i = 0; i < s->p[k]; i++) {
+      size_t j = (size_t)k * P + i;
+      double w = s->active[j] ? s->mu[j] : 0.0;
+      cIc += (s->C[j] * w) * s->C[j];
+    }
+    Jc += lc + 0.5 * cIc;
+  }
+  return J + Jc;
+}
+
+static double cost(oc_solver* s, int al, const double* X, const double* U) {
+  return al ? al_cost(s, X, U) : obj_cost(s, X, U);
+}
+
+OC_EXPORT double oc_cost(oc_solver* s, int al) { return cost(s, al, s->X, s->U); }
+OC_EXPORT double oc_cost_bar(oc_solver* s, int al) { return cost(s, al, s->Xb, s->Ub); }
+
+/* =====================================================================
+ * Rollouts (src/rollout.jl)
+ * ===================================================================== */
+/* rollout!(prob) src/rollout.jl:25-38: open loop only if any X non-finite */
+OC_EXPORT void oc_rollout_open_loop(oc_solver* s) {
+  int n = s->n, m = s->m, N = s->N;
+  int finite = 1;
+  for (int i = 0; i < n * N; i++)
+    if (!isfinite(s->X[i])) finite = 0;
+  if (finite) return;
+  memcpy(s->X, s->x0, sizeof(double) * n);
+  for (int k = 0; k < N - 1; k++)
+    oc_discrete_f(s->model, s->integ, s->X + (size_t)(k + 1) * n, s->X + (size_t)k * n, s->U + (size_t)k * m, s->dt);
+}
+
+/* rollout!(prob, solver, alpha) src/rollout.jl:2-23 */
+OC_EXPORT int oc_rollout(oc_solver* s, double alpha) {
+  int n = s->n, m = s->m, N = s->N;
+  memcpy(s->Xb, s->x0, sizeof(double) * n);
+  for (int k = 1; k < N; k++) {
+    const double* xb = s->Xb + (size_t)(k - 1) * n;
+    const double* x = s->X + (size_t)(k - 1) * n;
+    double dx[16];
+    for (int i = 0; i < n; i++) dx[i] = xb[i] - x[i]; /* state_diff */
+    double* ub = s->Ub + (size_t)(k - 1) * m;
+    const double* Kk = s->K + (size_t)(k - 1) * m * n;
+    const double* dk = s->d + (size_t)(k - 1) * m;
+    /* Ū = U + K*δx + alpha*d */
+    for (int i = 0; i < m; i++) {
+      double t = 0.0;
+      for (int j = 0; j < n; j++) t += Kk[IDX(i, j, m)] * dx[j];
+      ub[i] = (s->U[(size_t)(k - 1) * m + i] + t) + alpha * dk[i];
+    }
+    oc_discrete_f(s->model, s->integ, s->Xb + (size_t)k * n, xb, ub, s->dt);
+    double nx = 0, nu = 0;
+    int bad = 0;
+    for (int i = 0; i < n; i++) {
+      double a = fabs(s->Xb[(size_t)k * n + i]);
+      if (!(a <= nx)) nx = a;
+      if (isnan(a)) bad = 1;
+    }
+    for (int i = 0; i < m; i++) {
+      double a = fabs(ub[i]);
+      if (!(a <= nu)) nu = a;
+      if (isnan(a)) bad = 1;
+    }
+    if (bad || !(nx < s->opts.max_state_value && nu < s->opts.max_control_value)) return 0;
+  }
+  return 1;
+}
+
+/* =====================================================================
+ * Jacobians (src/solvers.jl:126 -> src/model.jl:301-306)
+ * ===================================================================== */
+OC_EXPORT void oc_jacobians(oc_solver* s) {
+  int n = s->n, m = s->m, N = s->N, L = n + m + 1;
+  for (int k = 0; k < N - 1; k++)
+    oc_discrete_jacobian(s->model, s->integ, s->F + (size_t)k * n * L, Xk(s, k), Uk(s, k), s->dt);
+}
+
+/* =====================================================================
+ * Cost expansion (ilqr_methods.jl:55-62 -> objective.jl:51-94, cost.jl:183-198,
+ * AL: augmented_lagrangian_methods.jl:186-276)
+ * ===================================================================== */
+static void expansion_stage(oc_solver* s, int k) {
+  int n = s->n, m = s->m;
+  const double* x = Xk(s, k);
+  const double* u = Uk(s, k);
+  double dt = s->dt;
+  double* Qx = s->Qx + (size_t)k * n;
+  double* Qu = s->Qu + (size_t)k * m;
+  /* Q.x .= cost.Q*x + cost.q + cost.H'*u ; Q.u .= cost.R*u + cost.r + cost.H*x ; then Q*dt */
+  for (int i = 0; i < n; i++) {
+    double a = 0, b = 0;
+    for (int j = 0; j < n; j++) a += s->Q[IDX(i, j, n)] * x[j];
+    for (int j = 0; j < m; j++) b += s->H[IDX(j, i, m)] * u[j];
+    Qx[i] = ((a + s->q[i]) + b) * dt;
+  }
+  for (int i = 0; i < m; i++) {
+    double a = 0, b = 0;
+    for (int j = 0; j < m; j++) a += s->R[IDX(i, j, m)] * u[j];
+    for (int j = 0; j < n; j++) b += s->H[IDX(i, j, m)] * x[j];
+    Qu[i] = ((a + s->r[i]) + b) * dt;
+  }
+  for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = s->Q[i] * dt;
+  for (int i = 0; i < m * m; i++) s->Quu[(size_t)k * m * m + i] = s->R[i] * dt;
+  for (int i = 0; i < m * n; i++) s->Qux[(size_t)k * m * n + i] = s->H[i] * dt;
+}
+static void expansion_terminal(oc_solver* s) {
+  int n = s->n, k = s->N - 1;
+  const double* x = Xk(s, k);
+  for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = s->Qf[i];
+  for (int i = 0; i < n; i++) {
+    double a = 0;
+    for (int j = 0; j < n; j++) a += s->Qf[IDX(i, j, n)] * x[j];
+    s->Qx[(size_t)k * n + i] = a + s->qf[i];
+  }
+}
+
+/* returns 0, or -1 on PosDefException in the sqrt expansion */
+OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
+  int n = s->n, m = s->m, N = s->N, P = s->pmax;
+  for (int k = 0; k < N - 1; k++) {
+    expansion_stage(s, k);
+    if (sq) { /* objective.jl:70-86 */
+      double U[256];
+      if (chol_upper(U, s->Qxx + (size_t)k * n * n, n)) return -1;
+      memcpy(s->Qxx + (size_t)k * n * n, U, sizeof(double) * n * n);
+      if (chol_upper(U, s->Quu + (size_t)k * m * m, m)) return -1;
+      memcpy(s->Quu + (size_t)k * m * m, U, sizeof(double) * m * m);
+    }
+  }
+  expansion_terminal(s);
+  if (sq) {
+    double U[256];
+    if (chol_upper(U, s->Qxx + (size_t)(N - 1) * n * n, n)) return -1;
+    memcpy(s->Qxx + (size_t)(N - 1) * n * n, U, sizeof(double) * n * n);
+  }
+  if (!al) return 0;
+  /* AL terms */
+  double cx[64 * 16], cu[64 * 8], cval[64];
+  for (int k = 0; k < N; k++) {
+    int p = s->p[k];
+    if (p == 0) continue;
+    int term = (k == N - 1);
+    set_eval(s, k, Xk(s, k), term ? NULL : Uk(s, k), cval, cx, term ? NULL : cu, NULL);
+    const double* c = s->C + (size_t)k * P; /* obj.C[k] (last evaluated, A.10) */
+    const double* lam = s->lam + (size_t)k * P;
+    const double* mu = s->mu + (size_t)k * P;
+    double w[64], g[64], ws[64];
+    for (int i = 0; i < p; i++) {
+      /* a = active_set(c, λ) */
+      int ineq = s->ineq[(size_t)k * P + i];
+      int a = ineq ? ((c[i] >= 0.0) || (lam[i] > 0.0)) : 1;
+      w[i] = a ? mu[i] : 0.0;
+      ws[i] = a ? sqrt(mu[i]) : 0.0;
+      g[i] = w[i] * c[i] + lam[i];
+    }
+    double* Qx = s->Qx + (size_t)k * n;
+    double* Qxx = s->Qxx + (size_t)k * n * n;
+    if (!sq) {
+      /* Q.xx .+= cx'Iμ*cx ; Q.uu .+= cu'Iμ*cu ; Q.ux .+= cu'Iμ*cx */
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < n; i++) {
+          double t = 0;
+          for (int r = 0; r < p; r++) t += (cx[r + p * i] * w[r]) * cx[r + p * j];
+          Qxx[IDX(i, j, n)] += t;
+        }
+      if (!term) {
+        double* Quu = s->Quu + (size_t)k * m * m;
+        double* Qux = s->Qux + (size_t)k * m * n;
+        for (int j = 0; j < m; j++)
+          for (int i = 0; i < m; i++) {
+            double t = 0;
+            for (int r = 0; r < p; r++) t += (cu[r + p * i] * w[r]) * cu[r + p * j];
+            Quu[IDX(i, j, m)] += t;
+          }
+        for (int j = 0; j < n; j++)
+          for (int i = 0; i < m; i++) {
+            double t = 0;
+            for (int r = 0; r < p; r++) t += (cu[r + p * i] * w[r]) * cx[r + p * j];
+            Qux[IDX(i, j, m)] += t;
+          }
+      }
+    } else {
+      /* chol_plus!(Q.xx, Iμ_sqrt*cx) ; chol_plus!(Q.uu, Iμ_sqrt*cu)  (no ux term, A.5) */
+      double M[64 * 16], R[256];
+      for (int j = 0; j < n; j++)
+        for (int r = 0; r < p; r++) M[r + p * j] = ws[r] * cx[r + p * j];
+      chol_plus(R, Qxx, n, M, p, n);
+      memcpy(Qxx, R, sizeof(double) * n * n);
+      if (!term) {
+        double* Quu = s->Quu + (size_t)k * m * m;
+        for (int j = 0; j < m; j++)
+          for (int r = 0; r < p; r++) M[r + p * j] = ws[r] * cu[r + p * j];
+        chol_plus(R, Quu, m, M, p, m);
+        memcpy(Quu, R, sizeof(double) * m * m);
+      }
+    }
+    /* Q.x .+= cx'g ; Q.u .+= cu'g */
+    for (int i = 0; i < n; i++) {
+      double t = 0;
+      for (int r = 0; r < p; r++) t += cx[r + p * i] * g[r];
+      Qx[i] += t;
+    }
+    if (!term) {
+      double* Qu = s->Qu + (size_t)k * m;
+      for (int i = 0; i < m; i++) {
+        double t = 0;
+        for (int r = 0; r < p; r++) t += cu[r + p * i] * g[r];
+        Qu[i] += t;
+      }
+    }
+  }
+  return 0;
+}
+
+/* =====================================================================
+ * Regularisation (ilqr_methods.jl:164-176)
+ * ===================================================================== */
+static void reg_update(oc_solver* s, int increase) {
+  const tog_options* o = &s->opts;
+  if (increase) {
+    s->drho = fmax(s->drho * o->bp_reg_increase_factor, o->bp_reg_increase_factor);
+    s->rho = fmax(s->rho * s->drho, o->bp_reg_min);
+    if (s->rho > o->bp_reg_max) s->flags |= TOG_TRAJ_MAX_REG;
+  } else {
+    s->drho = fmin(s->drho / o->bp_reg_increase_factor, 1.0 / o->bp_reg_increase_factor);
+    s->rho = s->rho * s->drho * (double)(s->rho * s->drho > o->bp_reg_min);
+  }
+}
+
+/* =====================================================================
+ * Backward passes (src/solvers/ilqr/backward_pass.jl)
+ * ===================================================================== */
+static void backward_std(oc_solver* s) {
+  int n = s->n, m = s->m, N = s->N, L = n + m + 1;
+  double* Sxx = s->Sxx;
+  double* Sx = s->Sx;
+  memcpy(Sxx + (size_t)(N - 1) * n * n, s->Qxx + (size_t)(N - 1) * n * n, sizeof(double) * n * n);
+  memcpy(Sx + (size_t)(N - 1) * n, s->Qx + (size_t)(N - 1) * n, sizeof(double) * n);
+  s->dV[0] = s->dV[1] = 0.0;
+  s->bp_restarts = 0;
+  double AtS[256], T[256], Quu_reg[64], Qux_reg[128], Kk[128], dk[8], tmp[256];
+  int k = N - 2;
+  while (k >= 0) {
+    const double* Fk = s->F + (size_t)k * n * L;
+    const double* A = Fk;         /* fdx n x n */
+    const double* B = Fk + n * n; /* fdu n x m */
+    const double* S1 = Sxx + (size_t)(k + 1) * n * n;
+    const double* s1 = Sx + (size_t)(k + 1) * n;
+    double* Qx = s->Qx + (size_t)k * n;
+    double* Qu = s->Qu + (size_t)k * m;
+    double* Qxx = s->Qxx + (size_t)k * n * n;
+    double* Quu = s->Quu + (size_t)k * m * m;
+    double* Qux = s->Qux + (size_t)k * m * n;
+    /* Q[k].x .+= fdx'*S[k+1].x ; Q[k].u .+= fdu'*S[k+1].x */
+    matTmul(tmp, A, n, n, s1, 1);
+    for (int i = 0; i < n; i++) Qx[i] += tmp[i];
+    matTmul(tmp, B, n, m, s1, 1);
+    for (int i = 0; i < m; i++) Qu[i] += tmp[i];
+    /* Q[k].xx .+= fdx'*S*fdx  ((fdx'S)fdx, A.16) */
+    matTmul(AtS, A, n, n, S1, n);
+    matmul(T, AtS, n, n, A, n);
+    for (int i = 0; i < n * n; i++) Qxx[i] += T[i];
+    /* Q[k].uu .+= fdu'*S*fdu */
+    double BtS[128];
+    matTmul(BtS, B, n, m, S1, n);
+    matmul(T, BtS, m, n, B, m);
+    for (int i = 0; i < m * m; i++) Quu[i] += T[i];
+    /* Q[k].ux .+= fdu'*S*fdx */
+    matmul(T, BtS, m, n, A, n);
+    for (int i = 0; i < m * n; i++) Qux[i] += T[i];
+
+    if (s->opts.bp_reg_type == 1) { /* :state */
+      double BtB[64], BtA[128];
+      matTmul(BtB, B, n, m, B, m);
+      matTmul(BtA, B, n, m, A, n);
+      for (int i = 0; i < m * m; i++) Quu_reg[i] = Quu[i] + s->rho * BtB[i];
+      for (int i = 0; i < m * n; i++) Qux_reg[i] = Qux[i] + s->rho * BtA[i];
+    } else { /* :control */
+      for (int i = 0; i < m * m; i++) Quu_reg[i] = Quu[i];
+      for (int i = 0; i < m; i++) Quu_reg[i + m * i] += s->rho;
+      memcpy(Qux_reg, Qux, sizeof(double) * m * n);
+    }
+    /* if !isposdef(Hermitian(Quu_reg)) -> increase ρ and restart at N-1 (A.1: Q not reset) */
+    if (chol_upper(NULL, Quu_reg, m)) {
+      reg_update(s, 1);
+      s->bp_restarts++;
+      k = N - 2;
+      s->dV[0] = s->dV[1] = 0.0;
+      if (s->bp_restarts > 2000) return;
+      continue;
+    }
+    /* K = -(Quu_reg\Qux_reg) ; d = -(Quu_reg\Q.u) */
+    memcpy(Kk, Qux_reg, sizeof(double) * m * n);
+    lu_solve(Quu_reg, m, Kk, n);
+    for (int i = 0; i < m * n; i++) Kk[i] = -1.0 * Kk[i];
+    memcpy(dk, Qu, sizeof(double) * m);
+    lu_solve(Quu_reg, m, dk, 1);
+    for (int i = 0; i < m; i++) dk[i] = -1.0 * dk[i];
+    memcpy(s->K + (size_t)k * m * n, Kk, sizeof(double) * m * n);
+    memcpy(s->d + (size_t)k * m, dk, sizeof(double) * m);
+    /* S[k].x = Q.x + K'*Q.uu*d + K'*Q.u + Q.ux'*d */
+    double KtQuu[128];
+    matTmul(KtQuu, Kk, m, n, Quu, m); /* n x m */
+    double* Sk = Sxx + (size_t)k * n * n;
+    double* sk = Sx + (size_t)k * n;
+    {
+      double a[16], b[16], c[16];
+      matmul(a, KtQuu, n, m, dk, 1);
+      matTmul(b, Kk, m, n, Qu, 1);
+      matTmul(c, Qux, m, n, dk, 1);
+      for (int i = 0; i < n; i++) sk[i] = ((Qx[i] + a[i]) + b[i]) + c[i];
+    }
+    /* S[k].xx = Q.xx + K'*Q.uu*K + K'*Q.ux + Q.ux'*K ; symmetrise */
+    {
+      double a[256], b[256], c[256];
+      matmul(a, KtQuu, n, m, Kk, n);
+      matTmul(b, Kk, m, n, Qux, n);
+      matTmul(c, Qux, m, n, Kk, n);
+      for (int i = 0; i < n * n; i++) Sk[i] = ((Qxx[i] + a[i]) + b[i]) + c[i];
+      double tS[256];
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < n; i++) tS[IDX(i, j, n)] = 0.5 * (Sk[IDX(i, j, n)] + Sk[IDX(j, i, n)]);
+      memcpy(Sk, tS, sizeof(double) * n * n);
+    }
+    /* ΔV[1] += d'*Q.u ; ΔV[2] += 0.5*d'*Q.uu*d */
+    {
+      double a = 0.0, b = 0.0;
+      for (int i = 0; i < m; i++) a += dk[i] * Qu[i];
+      for (int j = 0; j < m; j++) {
+        double t = 0.0;
+        for (int i = 0; i < m; i++) t += (0.5 * dk[i]) * Quu[IDX(i, j, m)];
+        b += t * dk[j];
+      }
+      s->dV[0] += a;
+      s->dV[1] += b;
+    }
+    k--;
+  }
+  reg_update(s, 0);
+}
+
+static void backward_sqrt(oc_solver* s) {
+  int n = s->n, m = s->m, N = s->N, L = n + m + 1;
+  double* Sxx = s->Sxx;
+  double* Sx = s->Sx;
+  memcpy(Sxx + (size_t)(N - 1) * n * n, s->Qxx + (size_t)(N - 1) * n * n, sizeof(double) * n * n);
+  memcpy(Sx + (size_t)(N - 1) * n, s->Qx + (size_t)(N - 1) * n, sizeof(double) * n);
+  s->dV[0] = s->dV[1] = 0.0;
+  s->bp_restarts = 0;
+  double tmp_x[256], tmp_u[128], R[256], Quu_reg[64], Qux_reg[128], Kk[128], dk[8], t[256];
+  int k = N - 2;
+  while (k >= 0) {
+    const double* Fk = s->F + (size_t)k * n * L;
+    const double* A = Fk;
+    const double* B = Fk + n * n;
+    const double* S1 = Sxx + (size_t)(k + 1) * n * n; /* factor */
+    const double* s1 = Sx + (size_t)(k + 1) * n;
+    double* Qx = s->Qx + (size_t)k * n;
+    double* Qu = s->Qu + (size_t)k * m;
+    double* Qxx = s->Qxx + (size_t)k * n * n;
+    double* Quu = s->Quu + (size_t)k * m * m;
+    double* Qux = s->Qux + (size_t)k * m * n;
+    matTmul(t, A, n, n, s1, 1);
+    for (int i = 0; i < n; i++) Qx[i] += t[i];
+    matTmul(t, B, n, m, s1, 1);
+    for (int i = 0; i < m; i++) Qu[i] += t[i];
+    matmul(tmp_x, S1, n, n, A, n); /* S*fdx */
+    matmul(tmp_u, S1, n, n, B, m); /* S*fdu */
+    chol_plus(R, Qxx, n, tmp_x, n, n);
+    memcpy(Qxx, R, sizeof(double) * n * n);
+    chol_plus(R, Quu, m, tmp_u, n, m);
+    memcpy(Quu, R, sizeof(double) * m * m);
+    matTmul(t, tmp_u, n, m, tmp_x, n); /* tmp_u'*tmp_x */
+    for (int i = 0; i < m * n; i++) Qux[i] += t[i];
+
+    if (s->opts.bp_reg_type == 1) { /* :state: chol_plus(Q.uu, sqrt(ρ)*fdu) */
+      double Bs[128], BtA[128];
+      for (int i = 0; i < n * m; i++) Bs[i] = sqrt(s->rho) * B[i];
+      chol_plus(Quu_reg, Quu, m, Bs, n, m);
+      matTmul(BtA, B, n, m, A, n);
+      for (int i = 0; i < m * n; i++) Qux_reg[i] = Qux[i] + s->rho * BtA[i];
+    } else {
+      double D[64];
+      memset(D, 0, sizeof(D));
+      for (int i = 0; i < m; i++) D[i + m * i] = sqrt(s->rho);
+      chol_plus(Quu_reg, Quu, m, D, m, m);
+      memcpy(Qux_reg, Qux, sizeof(double) * m * n);
+    }
+    /* if cond(Quu_reg) > 1e8: increase ρ, restart */
+    if (cond2(Quu_reg, m) > 1e8) {
+      reg_update(s, 1);
+      s->bp_restarts++;
+      k = N - 2;
+      s->dV[0] = s->dV[1] = 0.0;
+      if (s->bp_restarts > 2000) return;
+      continue;
+    }
+    /* K = -Quu_reg\(Quu_reg'\Qux_reg) ; d = -Quu_reg\(Quu_reg'\Q.u) */
+    double RT[64];
+    for (int j = 0; j < m; j++)
+      for (int i = 0; i < m; i++) RT[IDX(i, j, m)] = Quu_reg[IDX(j, i, m)];
+    memcpy(Kk, Qux_reg, sizeof(double) * m * n);
+    lu_solve(RT, m, Kk, n);
+    lu_solve(Quu_reg, m, Kk, n);
+    for (int i = 0; i < m * n; i++) Kk[i] = -Kk[i];
+    memcpy(dk, Qu, sizeof(double) * m);
+    lu_solve(RT, m, dk, 1);
+    lu_solve(Quu_reg, m, dk, 1);
+    for (int i = 0; i < m; i++) dk[i] = -dk[i];
+    memcpy(s->K + (size_t)k * m * n, Kk, sizeof(double) * m * n);
+    memcpy(s->d + (size_t)k * m, dk, sizeof(double) * m);
+    /* S[k].x = Q.x + (K'*Q.uu')*(Q.uu*d) + K'*Q.u + Q.ux'*d */
+    double* sk = Sx + (size_t)k * n;
+    {
+      double KtUt[128], Ud[8], a[16], b[16], c[16];
+      for (int j = 0; j < m; j++) /* K'*Quu' : n x m, (K'Quu')[i,j] = Σ_l K[l,i] Quu[j,l] */
+        for (int i = 0; i < n; i++) {
+          double acc = 0;
+          for (int l = 0; l < m; l++) acc += Kk[IDX(l, i, m)] * Quu[IDX(j, l, m)];
+          KtUt[IDX(i, j, n)] = acc;
+        }
+      matmul(Ud, Quu, m, m, dk, 1);
+      matmul(a, KtUt, n, m, Ud, 1);
+      matTmul(b, Kk, m, n, Qu, 1);
+      matTmul(c, Qux, m, n, dk, 1);
+      for (int i = 0; i < n; i++) sk[i] = ((Qx[i] + a[i]) + b[i]) + c[i];
+    }
+    /* tmp1 = (Q.xx')\Q.ux'  (n x m) */
+    double tmp1[128], QxxT[256];
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < n; i++) QxxT[IDX(i, j, n)] = Qxx[IDX(j, i, n)];
+    int singular = 0;
+    for (int i = 0; i < n; i++)
+      if (Qxx[IDX(i, i, n)] == 0.0) singular = 1;
+    for (int j = 0; j < m; j++)
+      for (int i = 0; i < n; i++) tmp1[IDX(i, j, n)] = Qux[IDX(j, i, m)];
+    if (singular) s->flags |= TOG_TRAJ_SINGULAR;
+    lu_solve(QxxT, n, tmp1, m);
+    /* tmp2 = chol_minus(Q.uu, tmp1) */
+    double tmp2[64];
+    if (chol_minus(tmp2, Quu, m, tmp1, n)) {
+      s->flags |= TOG_TRAJ_SQRT_PD_FAIL;
+      memcpy(tmp2, Quu, sizeof(double) * m * m); /* the reference throws here */
+    }
+    /* S[k].xx = chol_plus(Q.xx + tmp1*K, tmp2*K) */
+    {
+      double top[256], bot[128];
+      matmul(top, tmp1, n, m, Kk, n);
+      for (int i = 0; i < n * n; i++) top[i] = Qxx[i] + top[i];
+      matmul(bot, tmp2, m, m, Kk, n);
+      chol_plus(Sxx + (size_t)k * n * n, top, n, bot, m, n);
+    }
+    /* ΔV */
+    {
+      double a = 0.0, Ud[8], b = 0.0;
+      for (int i = 0; i < m; i++) a += dk[i] * Qu[i];
+      matmul(Ud, Quu, m, m, dk, 1);
+      for (int i = 0; i < m; i++) b += Ud[i] * Ud[i];
+      s->dV[0] += a;
+      s->dV[1] += 0.5 * b;
+    }
+    k--;
+  }
+  reg_update(s, 0);
+}
+
+OC_EXPORT int oc_backward(oc_solver* s, int sq, double* dV) {
+  if (sq)
+    backward_sqrt(s);
+  else
+    backward_std(s);
+  if (dV) {
+    dV[0] = s->dV[0];
+    dV[1] = s->dV[1];
+  }
+  return s->bp_restarts;
+}
+
+/* =====================================================================
+ * Forward pass (src/solvers/ilqr/forward_pass.jl:5-85)
+ * ===================================================================== */
+OC_EXPORT double oc_forward(oc_solver* s, int al, double J_prev) {
+  const tog_options* o = &s->opts;
+  int n = s->n, m = s->m, N = s->N;
+  double J = INFINITY, alpha = 1.0, z = -1.0, expected = 0.0;
+  int iter = 0;
+  s->ls_trials = 0;
+  while ((z <= o->line_search_lower_bound || z > o->line_search_upper_bound) && J >= J_prev) {
+    if (iter > o->iterations_linesearch) {
+      memcpy(s->Xb, s->X, sizeof(double) * n * N);
+      memcpy(s->Ub, s->U, sizeof(double) * m * (N - 1));
+      J = cost(s, al, s->Xb, s->Ub);
+      z = 0.0;
+      alpha = 0.0;
+      expected = 0.0;
+      reg_update(s, 1);
+      s->rho += o->bp_reg_fp;
+      break;
+    }
+    int ok = oc_rollout(s, alpha);
+    s->ls_trials++;
+    if (!ok) {
+      iter++;
+      alpha /= 2.0;
+      continue;
+    }
+    J = cost(s, al, s->Xb, s->Ub);
+    expected = -alpha * (s->dV[0] + alpha * s->dV[1]);
+    if (expected > 0.0)
+      z = (J_prev - J) / expected;
+    else
+      z = -1.0;
+    iter++;
+    alpha /= 2.0;
+  }
+  s->alpha = 2.0 * alpha;
+  s->z = z;
+  s->expected = expected;
+  if (J > J_prev) s->flags |= TOG_TRAJ_COST_INCREASED;
+  return J;
+}
+
+/* =====================================================================
+ * Solves
+ * ===================================================================== */
+/* gradient_todorov (ilqr_methods.jl:122-129) / gradient_feedforward (:135-137) */
+static double calc_gradient(oc_solver* s) {
+  int m = s->m, N = s->N;
+  if (s->opts.gradient_type == 1) {
+    double g = 0.0;
+    for (int k = 0; k < N - 1; k++) {
+      double t = 0;
+      for (int i = 0; i < m; i++) t += s->d[(size_t)k * m + i] * s->d[(size_t)k * m + i];
+      t = sqrt(t);
+      if (t > g) g = t;
+    }
+    return g;
+  }
+  double sum = 0.0;
+  for (int k = 0; k < N - 1; k++) {
+    double mx = -INFINITY;
+    for (int i = 0; i < m; i++) {
+      double v = fabs(s->d[(size_t)k * m + i]) / (fabs(s->U[(size_t)k * m + i]) + 1.0);
+      if (v > mx || isnan(v)) mx = v;
+    }
+    sum += mx;
+  }
+  return sum / N; /* mean over N entries, entry N = 0 (A.3) */
+}
+
+static void record_iteration(oc_solver* s, double J, double dJ) {
+  s->iterations++;
+  s->J = J;
+  s->dJ = dJ;
+  s->gradient = calc_gradient(s);
+  if (dJ == 0.0)
+    s->zero_count++;
+  else
+    s->zero_count = 0;
+}
+
+static int evaluate_convergence(oc_solver* s, double cost_tol, double grad_tol) {
+  if (0.0 < s->dJ && s->dJ < cost_tol) return 1;
+  if (s->gradient < grad_tol) return 1;
+  if (s->iterations >= s->opts.iterations) return 1;
+  if (s->zero_count > s->opts.dJ_counter_limit) return 1;
+  return 0;
+}
+
+/* one iLQR step! (ilqr_methods.jl:47-53) + the bookkeeping of solve! (:21-42).
+   returns 1 if the inner solve finished (converged or early exit). */
+static int ilqr_iterate(oc_solver* s, int al, double cost_tol, double grad_tol) {
+  oc_jacobians(s);
+  if (oc_cost_expansion(s, s->opts.square_root, al)) s->flags |= TOG_TRAJ_SQRT_PD_FAIL;
+  oc_backward(s, s->opts.square_root, NULL);
+  double J = oc_forward(s, al, s->J);
+  s->total_steps++;
+  if (s->trace_len < 4096) {
+    double* t = s->trace + 6 * s->trace_len++;
+    t[0] = J; t[1] = s->alpha; t[2] = s->rho; t[3] = s->bp_restarts; t[4] = s->ls_trials; t[5] = s->z;
+  }
+  if (J > s->opts.max_cost_value) {
+    s->flags |= TOG_TRAJ_COST_BLOWUP;
+    return 1;
+  }
+  memcpy(s->X, s->Xb, sizeof(double) * s->n * s->N);
+  memcpy(s->U, s->Ub, sizeof(double) * s->m * (s->N - 1));
+  double dJ = fabs(J - s->J);
+  record_iteration(s, J, dJ);
+  if (evaluate_convergence(s, cost_tol, grad_tol)) {
+    if (s->iterations >= s->opts.iterations) s->flags |= TOG_TRAJ_MAX_ITERS;
+    return 1;
+  }
+  return 0;
+}
+
+static void ilqr_reset(oc_solver* s) { /* reset!(solver) ilqr_solver.jl:146-154 */
+  s->iterations = 0;
+  s->zero_count = 0;
+  s->rho = 0.0;
+  s->drho = 0.0;
+}
+
+/* solve!(prob, iLQRSolver) ilqr_methods.jl:3-45 ; al selects the AL objective (inner solve) */
+static void ilqr_solve(oc_solver* s, int al, double cost_tol, double grad_tol) {
+  ilqr_reset(s);
+  oc_rollout_open_loop(s);
+  double J_prev = cost(s, al, s->X, s->U);
+  record_iteration(s, J_prev, INFINITY);
+  for (int i = 0; i < s->opts.iterations; i++) {
+    if (ilqr_iterate(s, al, cost_tol, grad_tol)) break;
+  }
+}
+
+OC_EXPORT int oc_solve_ilqr(oc_solver* s) {
+  s->flags = 0;
+  s->total_steps = 0;
+  s->trace_len = 0;
+  ilqr_solve(s, 0, s->opts.cost_tolerance, s->opts.gradient_norm_tolerance);
+  s->flags |= TOG_TRAJ_CONVERGED;
+  return s->total_steps;
+}
+
+/* max_violation(solver) augmented_lagrangian_methods.jl:171-184 */
+static double max_violation(oc_solver* s) {
+  int N = s->N, P = s->pmax;
+  double c_max = 0.0;
+  for (int k = 0; k < N; k++) {
+    if (s->p[k] == 0) continue;
+    double e = 0.0, im = -INFINITY;
+    int ni = 0;
+    for (int i = 0; i < s->p[k]; i++) {
+      size_t j = (size_t)k * P + i;
+      if (s->ineq[j]) {
+        ni++;
+        if (s->C[j] > im) im = s->C[j];
+      } else if (fabs(s->C[j]) > e)
+        e = fabs(s->C[j]);
+    }
+    c_max = fmax(e, c_max);
+    if (ni > 0) c_max = fmax(fmax(0.0, im), c_max);
+  }
+  return c_max;
+}
+
+/* solve!(prob, AugmentedLagrangianSolver) augmented_lagrangian_methods.jl:2-31 */
+OC_EXPORT int oc_solve_al(oc_solver* s) {
+  const tog_options* o = &s->opts;
+  int N = s->N, P = s->pmax;
+  s->flags = 0;
+  s->total_steps = 0;
+  s->trace_len = 0;
+  /* reset!(solver): λ = 0, μ = penalty_initial (augmented_lagrangian_solver.jl:173-187) */
+  for (int i = 0; i < P * N; i++) {
+    s->lam[i] = 0.0;
+    s->mu[i] = o->penalty_initial;
+  }
+  oc_rollout_open_loop(s);
+  (void)al_cost(s, s->X, s->U); /* record_iteration!(prob_al, solver, cost(prob_al)) */
+  s->c_max = max_violation(s);
+  for (int i = 1; i <= o->al_iterations; i++) {
+    s->al_iter = i;
+    /* set_tolerances! (:39-50) */
+    double ct = (i != o->al_iterations) ? o->al_cost_tolerance_intermediate : o->al_cost_tolerance;
+    double gt = (i != o->al_iterations) ? o->al_gradient_norm_tolerance_intermediate : o->al_gradient_norm_tolerance;
+    ilqr_solve(s, 1, ct, gt);
+    (void)al_cost(s, s->X, s->U); /* J = cost(prob) */
+    /* dual_update! (:107-118) */
+    for (int k = 0; k < N; k++)
+      for (int j = 0; j < s->p[k]; j++) {
+        size_t q = (size_t)k * P + j;
+        double l = s->lam[q] + s->mu[q] * s->C[q];
+        l = fmax(o->dual_min, fmin(o->dual_max, l));
+        if (s->ineq[q]) l = fmax(0.0, l);
+        s->lam[q] = l;
+      }
+    update_active_set(s);
+    /* penalty_update! (:121-126) */
+    double mumax = 0.0;
+    for (int k = 0; k < N; k++)
+      for (int j = 0; j < s->p[k]; j++) {
+        size_t q = (size_t)k * P + j;
+        s->mu[q] = fmax(0.0, fmin(o->penalty_max, o->penalty_scaling * s->mu[q]));
+        if (s->mu[q] > mumax) mumax = s->mu[q];
+      }
+    s->c_max = max_violation(s);
+    int conv = 0;
+    if (o->kickout_max_penalty && mumax == o->penalty_max) conv = 1;
+    if (s->c_max < o->constraint_tolerance) conv = 1;
+    if (conv) {
+      s->flags |= TOG_TRAJ_AL_CONVERGED;
+      break;
+    }
+    if (i == o->al_iterations) s->flags |= TOG_TRAJ_AL_MAX_ITERS;
+  }
+  return s->total_steps;
+}
+
+/* =====================================================================
+ * Field access
+ * ===================================================================== */
+OC_EXPORT void oc_get(oc_solver* s, int field, double* out) {
+  int n = s->n, m = s->m, N = s->N, P = s->pmax, L = n + m + 1;
+  switch (field) {
+    case TOG_FIELD_X: memcpy(out, s->X, sizeof(double) * n * N); break;
+    case TOG_FIELD_U: memcpy(out, s->U, sizeof(double) * m * (N - 1)); break;
+    case TOG_FIELD_XBAR: memcpy(out, s->Xb, sizeof(double) * n * N); break;
+    case TOG_FIELD_UBAR: memcpy(out, s->Ub, sizeof(double) * m * (N - 1)); break;
+    case TOG_FIELD_K: memcpy(out, s->K, sizeof(double) * m * n * (N - 1)); break;
+    case TOG_FIELD_D: memcpy(out, s->d, sizeof(double) * m * (N - 1)); break;
+    case TOG_FIELD_A:
+      for (int k = 0; k < N - 1; k++) memcpy(out + (size_t)k * n * n, s->F + (size_t)k * n * L, sizeof(double) * n * n);
+      break;
+    case TOG_FIELD_B:
+      for (int k = 0; k < N - 1; k++)
+        memcpy(out + (size_t)k * n * m, s->F + (size_t)k * n * L + n * n, sizeof(double) * n * m);
+      break;
+    case TOG_FIELD_S: memcpy(out, s->Sxx, sizeof(double) * n * n * N); break;
+    case TOG_FIELD_SX: memcpy(out, s->Sx, sizeof(double) * n * N); break;
+    case TOG_FIELD_DV: out[0] = s->dV[0]; out[1] = s->dV[1]; break;
+    case TOG_FIELD_LAMBDA: memcpy(out, s->lam, sizeof(double) * P * N); break;
+    case TOG_FIELD_MU: memcpy(out, s->mu, sizeof(double) * P * N); break;
+    case TOG_FIELD_C: memcpy(out, s->C, sizeof(double) * P * N); break;
+    case TOG_FIELD_X0: memcpy(out, s->x0, sizeof(double) * n); break;
+    case TOG_FIELD_RHO: out[0] = s->rho; out[1] = s->drho; break;
+    case TOG_FIELD_STATS:
+      memset(out, 0, sizeof(double) * TOG_NSTATS);
+      out[TOG_STAT_J] = s->J;
+      out[TOG_STAT_DJ] = s->dJ;
+      out[TOG_STAT_GRADIENT] = s->gradient;
+      out[TOG_STAT_ITERATIONS] = s->iterations;
+      out[TOG_STAT_ZERO_COUNT] = s->zero_count;
+      out[TOG_STAT_ALPHA] = s->alpha;
+      out[TOG_STAT_Z] = s->z;
+      out[TOG_STAT_C_MAX] = s->c_max;
+      out[TOG_STAT_AL_ITER] = s->al_iter;
+      out[TOG_STAT_TOTAL_STEPS] = s->total_steps;
+      out[TOG_STAT_LS_TRIALS] = s->ls_trials;
+      out[TOG_STAT_BP_RESTARTS] = s->bp_restarts;
+      out[TOG_STAT_FLAGS] = s->flags;
+      break;
+  }
+}
+
+OC_EXPORT void oc_set(oc_solver* s, int field, const double* in) {
+  int n = s->n, m = s->m, N = s->N, P = s->pmax;
+  switch (field) {
+    case TOG_FIELD_X: memcpy(s->X, in, sizeof(double) * n * N); break;
+    case TOG_FIELD_U: memcpy(s->U, in, sizeof(double) * m * (N - 1)); break;
+    case TOG_FIELD_K: memcpy(s->K, in, sizeof(double) * m * n * (N - 1)); break;
+    case TOG_FIELD_D: memcpy(s->d, in, sizeof(double) * m * (N - 1)); break;
+    case TOG_FIELD_LAMBDA: memcpy(s->lam, in, sizeof(double) * P * N); break;
+    case TOG_FIELD_MU: memcpy(s->mu, in, sizeof(double) * P * N); break;
+    case TOG_FIELD_DV: s->dV[0] = in[0]; s->dV[1] = in[1]; break;
+    case TOG_FIELD_RHO: s->rho = in[0]; s->drho = in[1]; break;
+    case TOG_FIELD_X0: memcpy(s->x0, in, sizeof(double) * n); break;
+  }
+}
+
+OC_EXPORT void oc_update_constraints(oc_solver* s) {
+  update_constraints(s, s->X, s->U);
+  update_active_set(s);
+}
+
+OC_EXPORT int oc_get_trace(oc_solver* s, double* out) {
+  memcpy(out, s->trace, sizeof(double) * 6 * s->trace_len);
+  return s->trace_len;
+}
+
+OC_EXPORT double oc_max_violation(oc_solver* s) { return max_violation(s); }
+
+/* =====================================================================
+ * Batched CPU baseline: B independent solves over `nthreads` OpenMP threads.
+ * Returns Σ iLQR step!s. (bench.py cpu_baseline leg)
+ * ===================================================================== */
+OC_EXPORT int64_t oc_solve_batch(const tog_problem_desc* d, const tog_options* o, int mode, const double* x0,
+                                 const double* U0, int64_t B, int nthreads) {
+  int n = d->n, m = d->m, N = d->N;
+  int64_t total = 0;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : total)
+#endif
+  for (int64_t b = 0; b < B; b++) {
+    oc_solver* s = oc_create(d, o);
+    oc_set_state(s, x0 + (size_t)b * n, U0 + (size_t)b * m * (N - 1), NULL);
+    total += mode == TOG_MODE_AL ? oc_solve_al(s) : oc_solve_ilqr(s);
+    oc_destroy(s);
+  }
+  (void)nthreads;
+  return total;
+}

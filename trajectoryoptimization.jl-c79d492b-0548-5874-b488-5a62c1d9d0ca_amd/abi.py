@@ -1,0 +1,245 @@
+"""ctypes mirror of ``include/tog.h`` (the C ABI of the HIP hot path) and the loader of
+``libtog.so``.
+
+No torch types cross this boundary: plain fp64 column-major buffers, int32/int64 sizes,
+int status codes. The library is built in-tree (``csrc/``) by ``__graft_entry__.build()``;
+loading fails loudly when it is missing -- there is no CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+import numpy as np
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "csrc" / "libtog.so"
+
+TOG_ABI_VERSION = 1
+
+# models (include/tog.h tog_model_id)
+MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM = range(5)
+MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1)}
+RK3, RK4 = 0, 1
+CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES = range(4)
+MODE_ILQR, MODE_AL = 0, 1
+
+(FIELD_X, FIELD_U, FIELD_XBAR, FIELD_UBAR, FIELD_K, FIELD_D, FIELD_A, FIELD_B, FIELD_S, FIELD_SX,
+ FIELD_DV, FIELD_LAMBDA, FIELD_MU, FIELD_C, FIELD_X0, FIELD_STATS, FIELD_RHO) = range(17)
+
+(STAT_J, STAT_DJ, STAT_GRADIENT, STAT_ITERATIONS, STAT_ZERO_COUNT, STAT_ALPHA, STAT_Z, STAT_C_MAX,
+ STAT_AL_ITER, STAT_TOTAL_STEPS, STAT_LS_TRIALS, STAT_BP_RESTARTS, STAT_FLAGS, STAT_PENALTY_MAX) = range(14)
+NSTATS = 14
+
+TRAJ_ACTIVE = 1 << 0
+TRAJ_CONVERGED = 1 << 1
+TRAJ_MAX_ITERS = 1 << 2
+TRAJ_COST_INCREASED = 1 << 3
+TRAJ_COST_BLOWUP = 1 << 4
+TRAJ_MAX_REG = 1 << 5
+TRAJ_SQRT_PD_FAIL = 1 << 6
+TRAJ_AL_CONVERGED = 1 << 7
+TRAJ_AL_MAX_ITERS = 1 << 8
+TRAJ_SINGULAR = 1 << 9
+
+BP_STORE_S = 1
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class tog_constraint(C.Structure):
+    _fields_ = [("type", C.c_int32), ("count", C.c_int32), ("data", _dp)]
+
+
+class tog_constraint_set(C.Structure):
+    _fields_ = [("n_con", C.c_int32), ("con", C.POINTER(tog_constraint))]
+
+
+class tog_problem_desc(C.Structure):
+    _fields_ = [
+        ("model", C.c_int32), ("integrator", C.c_int32), ("n", C.c_int32), ("m", C.c_int32),
+        ("N", C.c_int32), ("reserved0", C.c_int32), ("batch", C.c_int64), ("dt", C.c_double),
+        ("Q", _dp), ("R", _dp), ("H", _dp), ("q", _dp), ("r", _dp), ("c", C.c_double),
+        ("Qf", _dp), ("qf", _dp), ("cf", C.c_double),
+        ("n_sets", C.c_int32), ("reserved1", C.c_int32),
+        ("sets", C.POINTER(tog_constraint_set)), ("knot_set", _ip),
+    ]
+
+
+class tog_options(C.Structure):
+    _fields_ = [
+        ("cost_tolerance", C.c_double), ("gradient_norm_tolerance", C.c_double),
+        ("iterations", C.c_int32), ("dJ_counter_limit", C.c_int32), ("square_root", C.c_int32),
+        ("bp_reg_type", C.c_int32), ("gradient_type", C.c_int32), ("iterations_linesearch", C.c_int32),
+        ("line_search_lower_bound", C.c_double), ("line_search_upper_bound", C.c_double),
+        ("bp_reg_increase_factor", C.c_double), ("bp_reg_max", C.c_double), ("bp_reg_min", C.c_double),
+        ("bp_reg_fp", C.c_double), ("max_cost_value", C.c_double), ("max_state_value", C.c_double),
+        ("max_control_value", C.c_double),
+        ("al_cost_tolerance", C.c_double), ("al_cost_tolerance_intermediate", C.c_double),
+        ("al_gradient_norm_tolerance", C.c_double), ("al_gradient_norm_tolerance_intermediate", C.c_double),
+        ("constraint_tolerance", C.c_double), ("dual_min", C.c_double), ("dual_max", C.c_double),
+        ("penalty_max", C.c_double), ("penalty_initial", C.c_double), ("penalty_scaling", C.c_double),
+        ("al_iterations", C.c_int32), ("kickout_max_penalty", C.c_int32),
+    ]
+
+
+def default_options() -> tog_options:
+    """Reference defaults (ilqr_solver.jl:7-81, augmented_lagrangian_solver.jl:8-66)."""
+    o = tog_options()
+    o.cost_tolerance = 1e-4
+    o.gradient_norm_tolerance = 1e-5
+    o.iterations = 300
+    o.dJ_counter_limit = 10
+    o.square_root = 0
+    o.bp_reg_type = 0
+    o.gradient_type = 0
+    o.iterations_linesearch = 20
+    o.line_search_lower_bound = 1e-8
+    o.line_search_upper_bound = 10.0
+    o.bp_reg_increase_factor = 1.6
+    o.bp_reg_max = 1e8
+    o.bp_reg_min = 1e-8
+    o.bp_reg_fp = 10.0
+    o.max_cost_value = 1e8
+    o.max_state_value = 1e8
+    o.max_control_value = 1e8
+    o.al_cost_tolerance = 1e-4
+    o.al_cost_tolerance_intermediate = 1e-3
+    o.al_gradient_norm_tolerance = 1e-5
+    o.al_gradient_norm_tolerance_intermediate = 1e-5
+    o.constraint_tolerance = 1e-3
+    o.dual_min = -1e8
+    o.dual_max = 1e8
+    o.penalty_max = 1e8
+    o.penalty_initial = 1.0
+    o.penalty_scaling = 10.0
+    o.al_iterations = 30
+    o.kickout_max_penalty = 0
+    return o
+
+
+def as_dp(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["F_CONTIGUOUS"] or a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_dp)
+
+
+class DescBuilder:
+    """Builds a ``tog_problem_desc`` and keeps every backing numpy array alive.
+
+    ``sets`` is a list of ordered constraint sets; each set is a list of
+    ``(type, count, data ndarray)``; ``knot_set`` has N entries (-1 = none).
+    """
+
+    def __init__(self, model, integrator, n, m, N, dt, Q, R, H, q, r, c, Qf, qf, cf, sets, knot_set,
+                 batch=1):
+        self._keep = []
+
+        def arr(x, shape):
+            a = np.asfortranarray(np.asarray(x, dtype=np.float64).reshape(shape, order="F"))
+            self._keep.append(a)
+            return a
+
+        d = tog_problem_desc()
+        d.model, d.integrator, d.n, d.m, d.N = int(model), int(integrator), int(n), int(m), int(N)
+        d.batch = int(batch)
+        d.dt = float(dt)
+        d.Q = as_dp(arr(Q, (n, n)))
+        d.R = as_dp(arr(R, (m, m)))
+        d.H = as_dp(arr(H, (m, n)))
+        d.q = as_dp(arr(q, (n,)))
+        d.r = as_dp(arr(r, (m,)))
+        d.c = float(c)
+        d.Qf = as_dp(arr(Qf, (n, n)))
+        d.qf = as_dp(arr(qf, (n,)))
+        d.cf = float(cf)
+        cs_arr = (tog_constraint_set * max(1, len(sets)))()
+        for i, s in enumerate(sets):
+            carr = (tog_constraint * max(1, len(s)))()
+            for j, (t, cnt, data) in enumerate(s):
+                da = np.ascontiguousarray(np.asarray(data, dtype=np.float64).ravel())
+                self._keep.append(da)
+                carr[j].type = int(t)
+                carr[j].count = int(cnt)
+                carr[j].data = da.ctypes.data_as(_dp)
+            self._keep.append(carr)
+            cs_arr[i].n_con = len(s)
+            cs_arr[i].con = carr
+        self._keep.append(cs_arr)
+        d.n_sets = len(sets)
+        d.sets = cs_arr
+        ks = np.ascontiguousarray(np.asarray(knot_set, dtype=np.int32))
+        assert ks.shape == (N,)
+        self._keep.append(ks)
+        d.knot_set = ks.ctypes.data_as(_ip)
+        self.desc = d
+
+
+_LIB = None
+
+
+def load_library(path: os.PathLike | None = None):
+    """Load libtog.so (HIP). Raises if it has not been built -- no fallback."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = pathlib.Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f"libtog.so not found at {p}: run __graft_entry__.build() (hipcc, gfx950)")
+    lib = C.CDLL(str(p))
+    vp = C.c_void_p
+    lib.tog_version.restype = C.c_int32
+    lib.tog_device_count.restype = C.c_int32
+    lib.tog_default_options.argtypes = [C.POINTER(tog_options)]
+    lib.tog_create.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_options), C.c_int32, C.POINTER(vp)]
+    lib.tog_destroy.argtypes = [vp]
+    lib.tog_set_stream.argtypes = [vp, vp]
+    lib.tog_synchronize.argtypes = [vp]
+    lib.tog_set_state.argtypes = [vp, _dp, _dp, _dp]
+    lib.tog_set.argtypes = [vp, C.c_int32, _dp]
+    lib.tog_get.argtypes = [vp, C.c_int32, _dp]
+    lib.tog_get_device_ptr.argtypes = [vp, C.c_int32, C.POINTER(vp)]
+    lib.tog_dims.argtypes = [vp, C.POINTER(C.c_int64)]
+    lib.tog_rollout_open_loop.argtypes = [vp]
+    lib.tog_jacobians.argtypes = [vp]
+    lib.tog_update_constraints.argtypes = [vp]
+    lib.tog_cost.argtypes = [vp, C.c_int32, _dp]
+    lib.tog_backward_pass.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, _dp]
+    lib.tog_forward_pass.argtypes = [vp, C.c_int32, _dp, _dp]
+    lib.tog_rollout.argtypes = [vp, C.c_double, _ip]
+    lib.tog_solve_init.argtypes = [vp, C.c_int32]
+    lib.tog_solve_step.argtypes = [vp, C.c_int32]
+    lib.tog_batch_stats.argtypes = [vp, _dp]
+    lib.tog_batch_stats_device.argtypes = [vp, vp]
+    lib.tog_total_steps.argtypes = [vp, C.POINTER(C.c_int64)]
+    lib.tog_solve.argtypes = [vp, C.c_int32, C.c_int32]
+    lib.tog_status.argtypes = [vp, _ip]
+    lib.tog_last_error.restype = C.c_char_p
+    for name in ("tog_create", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
+                 "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
+                 "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
+                 "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
+                 "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status"):
+        getattr(lib, name).restype = C.c_int32
+    if lib.tog_version() != TOG_ABI_VERSION:
+        raise RuntimeError("libtog ABI version mismatch")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+EXPORTED_SYMBOLS = (
+    "tog_version", "tog_device_count", "tog_default_options", "tog_create", "tog_destroy", "tog_set_stream",
+    "tog_synchronize", "tog_set_state", "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims",
+    "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
+    "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
+    "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_last_error",
+)
+
+
+def check(lib, rc):
+    if rc != 0:
+        msg = lib.tog_last_error()
+        raise RuntimeError(f"libtog error {rc}: {msg.decode() if msg else ''}")
+    return rc

@@ -1,0 +1,158 @@
+"""``BatchHandle``: one ``tog_handle`` (include/tog.h) = one problem x B trajectories resident in
+HBM on one GPU. Thin ctypes plumbing; all compute happens in libtog.so (HIP, gfx950).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class BatchHandle:
+    def __init__(self, prob, opts: abi.tog_options, device: int = 0, stream=None):
+        self.lib = abi.load_library()
+        self.desc_builder = prob.build_desc()
+        self.opts = opts
+        h = C.c_void_p()
+        abi.check(self.lib, self.lib.tog_create(C.byref(self.desc_builder.desc), C.byref(opts), int(device),
+                                                C.byref(h)))
+        self.h = h
+        dims = (C.c_int64 * 6)()
+        abi.check(self.lib, self.lib.tog_dims(self.h, dims))
+        self.n, self.m, self.N, self.B, self.pmax, _ = [int(v) for v in dims]
+        if stream is not None:
+            abi.check(self.lib, self.lib.tog_set_stream(self.h, C.c_void_p(int(stream))))
+        self.upload_state(prob)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) is not None and self.h:
+                self.lib.tog_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ shapes per field
+    def shape(self, field):
+        n, m, N, B, P = self.n, self.m, self.N, self.B, max(self.pmax, 1)
+        return {
+            abi.FIELD_X: (B, N, n), abi.FIELD_U: (B, N - 1, m), abi.FIELD_XBAR: (B, N, n),
+            abi.FIELD_UBAR: (B, N - 1, m), abi.FIELD_K: (B, N - 1, n, m), abi.FIELD_D: (B, N - 1, m),
+            abi.FIELD_A: (B, N - 1, n, n), abi.FIELD_B: (B, N - 1, m, n), abi.FIELD_S: (B, N, n, n),
+            abi.FIELD_SX: (B, N, n), abi.FIELD_DV: (B, 2), abi.FIELD_LAMBDA: (B, N, P),
+            abi.FIELD_MU: (B, N, P), abi.FIELD_C: (B, N, P), abi.FIELD_X0: (B, n),
+            abi.FIELD_STATS: (B, abi.NSTATS), abi.FIELD_RHO: (B, 2),
+        }[field]
+
+    def get(self, field, raw=False):
+        """Copy a field to the host. Matrices come back as (…, rows, cols) (the raw buffer is
+        column-major per block, i.e. the transpose in numpy C order)."""
+        out = np.empty(self.shape(field), dtype=np.float64)
+        abi.check(self.lib, self.lib.tog_get(self.h, field, abi.as_dp(out)))
+        if raw:
+            return out
+        if field in (abi.FIELD_K, abi.FIELD_A, abi.FIELD_B, abi.FIELD_S):
+            return np.ascontiguousarray(np.swapaxes(out, -1, -2))
+        return out
+
+    def set(self, field, value):
+        v = np.asarray(value, dtype=np.float64)
+        if field in (abi.FIELD_K, abi.FIELD_A, abi.FIELD_B, abi.FIELD_S):
+            v = np.swapaxes(v, -1, -2)
+        v = np.ascontiguousarray(v.reshape(self.shape(field)))
+        abi.check(self.lib, self.lib.tog_set(self.h, field, abi.as_dp(v)))
+
+    def device_ptr(self, field) -> int:
+        p = C.c_void_p()
+        abi.check(self.lib, self.lib.tog_get_device_ptr(self.h, field, C.byref(p)))
+        return int(p.value or 0)
+
+    # ------------------------------------------------------------------ state
+    def upload_state(self, prob):
+        x0 = np.ascontiguousarray(prob.x0, dtype=np.float64)
+        U = np.ascontiguousarray(prob._U, dtype=np.float64)
+        X = np.ascontiguousarray(prob._X, dtype=np.float64)
+        Xp = abi.as_dp(X) if np.isfinite(X).all() else C.cast(None, C.POINTER(C.c_double))
+        if not np.isfinite(X).all() and not np.isnan(X).all():
+            # a partially finite X0: upload as given (rollout!(prob) will trigger on the NaNs)
+            Xp = abi.as_dp(X)
+        abi.check(self.lib, self.lib.tog_set_state(self.h, abi.as_dp(x0), abi.as_dp(U), Xp))
+
+    def download_state(self, prob):
+        prob._X[...] = self.get(abi.FIELD_X)
+        prob._U[...] = self.get(abi.FIELD_U)
+
+    # ------------------------------------------------------------------ step level
+    def rollout_open_loop(self):
+        abi.check(self.lib, self.lib.tog_rollout_open_loop(self.h))
+
+    def jacobians(self):
+        abi.check(self.lib, self.lib.tog_jacobians(self.h))
+
+    def update_constraints(self):
+        abi.check(self.lib, self.lib.tog_update_constraints(self.h))
+
+    def cost(self, al=False):
+        J = np.empty(self.B)
+        abi.check(self.lib, self.lib.tog_cost(self.h, int(al), abi.as_dp(J)))
+        return J
+
+    def backward_pass(self, sqrt=False, al=False, store_S=False):
+        dV = np.empty((self.B, 2))
+        abi.check(self.lib, self.lib.tog_backward_pass(self.h, int(sqrt), int(al),
+                                                       abi.BP_STORE_S if store_S else 0, abi.as_dp(dV)))
+        return dV
+
+    def forward_pass(self, J_prev, al=False):
+        Jp = np.ascontiguousarray(np.broadcast_to(np.asarray(J_prev, dtype=np.float64), (self.B,)))
+        J = np.empty(self.B)
+        abi.check(self.lib, self.lib.tog_forward_pass(self.h, int(al), abi.as_dp(Jp), abi.as_dp(J)))
+        return J
+
+    def rollout(self, alpha=1.0):
+        ok = np.empty(self.B, dtype=np.int32)
+        abi.check(self.lib, self.lib.tog_rollout(self.h, float(alpha), ok.ctypes.data_as(C.POINTER(C.c_int32))))
+        return ok.astype(bool)
+
+    # ------------------------------------------------------------------ solve level
+    def solve_init(self, mode):
+        abi.check(self.lib, self.lib.tog_solve_init(self.h, int(mode)))
+
+    def solve_step(self, nsteps=1):
+        abi.check(self.lib, self.lib.tog_solve_step(self.h, int(nsteps)))
+
+    def solve(self, mode, max_steps=10000):
+        abi.check(self.lib, self.lib.tog_solve(self.h, int(mode), int(max_steps)))
+
+    def batch_stats(self):
+        out = np.empty(3)
+        abi.check(self.lib, self.lib.tog_batch_stats(self.h, abi.as_dp(out)))
+        return out
+
+    def total_steps(self):
+        v = C.c_int64()
+        abi.check(self.lib, self.lib.tog_total_steps(self.h, C.byref(v)))
+        return int(v.value)
+
+    def synchronize(self):
+        abi.check(self.lib, self.lib.tog_synchronize(self.h))
+
+    def status(self):
+        f = np.empty(self.B, dtype=np.int32)
+        abi.check(self.lib, self.lib.tog_status(self.h, f.ctypes.data_as(C.POINTER(C.c_int32))))
+        return f
+
+    def stats_dict(self):
+        S = self.get(abi.FIELD_STATS)
+        return {
+            "cost": S[:, abi.STAT_J], "dJ": S[:, abi.STAT_DJ], "gradient": S[:, abi.STAT_GRADIENT],
+            "iterations": S[:, abi.STAT_ITERATIONS].astype(np.int64),
+            "dJ_zero_counter": S[:, abi.STAT_ZERO_COUNT].astype(np.int64),
+            "alpha": S[:, abi.STAT_ALPHA], "c_max": S[:, abi.STAT_C_MAX],
+            "iterations_outer": S[:, abi.STAT_AL_ITER].astype(np.int64),
+            "iterations_total": S[:, abi.STAT_TOTAL_STEPS].astype(np.int64),
+            "penalty_max": S[:, abi.STAT_PENALTY_MAX],
+            "flags": S[:, abi.STAT_FLAGS].astype(np.int64),
+        }

@@ -1,0 +1,583 @@
+"""Host-side mirror of the reference's problem definition layer (L0 in SURVEY.md §1):
+``Model``/``rk3``/``rk4`` (src/model.jl), ``QuadraticCost``/``LQRCost`` (src/cost.jl),
+``Objective``/``LQRObjective`` (src/objective.jl), ``BoundConstraint``/``goal_constraint``
+(src/constraints.jl), ``Constraints`` (src/constraint_sets.jl) and ``Problem``
+(src/problem.jl).
+
+These are plain data holders: they are marshalled into ``tog_problem_desc`` (include/tog.h)
+and every computation runs in libtog.so on the GPU. The small ``evaluate``/``jacobian``
+helpers on constraints exist for the reference's own unit assertions
+(test/constraint_tests.jl) and for ``max_violation(prob)``, which the reference evaluates
+on the host after a solve (src/problem.jl:242-267).
+
+Julia → Python naming: a trailing ``!`` becomes ``_b`` (``solve!`` → ``solve_b``), 1-based
+knot ``k`` becomes 0-based ``k-1``; trajectories are numpy arrays ``X[N, n]`` (one trajectory)
+or ``X[B, N, n]`` (a batch), which is exactly the C-ABI memory layout.
+"""
+from __future__ import annotations
+
+import copy as _copy
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+# ----------------------------------------------------------------------------- models
+
+
+@dataclass
+class Model:
+    """``AnalyticalModel{Nominal, Continuous|Discrete}`` (src/model.jl:36-74).
+
+    Only the canned dynamics built into the HIP kernels exist (``Dynamics.*``); a
+    discrete model carries its integrator (``rk3``/``rk4``, src/model.jl:642-644).
+    """
+
+    model_id: int
+    n: int
+    m: int
+    name: str
+    integration: int | None = None  # None = Continuous; abi.RK3 / abi.RK4 = Discrete
+
+    @property
+    def discrete(self) -> bool:
+        return self.integration is not None
+
+
+def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) -> Model:
+    """``discretize_model(model, :rk3|:rk4)`` (src/model.jl:607-615)."""
+    if model.discrete:
+        raise ValueError("model is already discrete")
+    key = discretizer.lstrip(":")
+    if key not in ("rk3", "rk4"):
+        raise ValueError(f"integration {discretizer!r} is not built (rk3, rk4 only; SURVEY.md §2)")
+    return Model(model.model_id, model.n, model.m, model.name, abi.RK3 if key == "rk3" else abi.RK4)
+
+
+def rk3(model: Model, dt: float = 1.0) -> Model:
+    return discretize_model(model, "rk3", dt)
+
+
+def rk4(model: Model, dt: float = 1.0) -> Model:
+    return discretize_model(model, "rk4", dt)
+
+
+class Dynamics:
+    """``TrajectoryOptimization.Dynamics`` canned models (src/dynamics.jl:23-32)."""
+
+    doubleintegrator = Model(abi.MODEL_DOUBLE_INTEGRATOR, 2, 1, "doubleintegrator")  # double_integrator.jl
+    cartpole = Model(abi.MODEL_CARTPOLE, 4, 1, "cartpole")  # dynamics/cartpole.jl:9-36
+    quadrotor = Model(abi.MODEL_QUADROTOR, 13, 4, "quadrotor")  # dynamics/quadrotor.jl:10-71
+    car = Model(abi.MODEL_CAR, 3, 2, "car")  # dynamics/car.jl:3-8
+    pendulum = Model(abi.MODEL_PENDULUM, 2, 1, "pendulum")  # dynamics/pendulum.jl:3-12
+
+
+# ----------------------------------------------------------------------------- costs
+
+
+def _mat(a, shape):
+    a = np.asarray(a, dtype=np.float64)
+    if a.ndim == 0:
+        a = a * np.eye(shape[0])
+    return np.array(a.reshape(shape), dtype=np.float64)
+
+
+class QuadraticCost:
+    """``QuadraticCost(Q, R, H, q, r, c)`` (src/cost.jl:112-131):
+    1/2 x'Qx + 1/2 u'Ru + u'Hx + q'x + r'u + c (times dt for stage costs)."""
+
+    def __init__(self, Q, R=None, H=None, q=None, r=None, c=0.0):
+        Q = np.asarray(Q, dtype=np.float64)
+        n = Q.shape[0]
+        if R is None:  # QuadraticCost(Q, q, c) terminal form
+            R = np.zeros((0, 0))
+        R = np.asarray(R, dtype=np.float64)
+        m = R.shape[0]
+        self.Q = _mat(Q, (n, n))
+        self.R = _mat(R, (m, m)) if m else np.zeros((0, 0))
+        self.H = np.zeros((m, n)) if H is None else _mat(H, (m, n))
+        self.q = np.zeros(n) if q is None else np.asarray(q, dtype=np.float64).reshape(n).copy()
+        self.r = np.zeros(m) if r is None else np.asarray(r, dtype=np.float64).reshape(m).copy()
+        self.c = float(c)
+        if m and not _isposdef(self.R):
+            import warnings
+
+            warnings.warn("R is not positive definite")
+        if not _ispossemidef(self.Q):
+            raise ValueError("Q must be positive semi-definite")
+
+    def sizes(self):
+        return self.Q.shape[0], self.R.shape[0]
+
+    # reference formulas (src/cost.jl:171-198), host side for the KAT tests only
+    def stage_cost(self, x, u=None, dt=None):
+        x = np.asarray(x, dtype=np.float64)
+        if u is None:
+            return 0.5 * x @ self.Q @ x + self.q @ x + self.c
+        u = np.asarray(u, dtype=np.float64)
+        J = 0.5 * x @ self.Q @ x + 0.5 * u @ self.R @ u + self.q @ x + self.r @ u + self.c + u @ self.H @ x
+        return J * (1.0 if dt is None else dt)
+
+    def copy(self):
+        return _copy.deepcopy(self)
+
+
+def _isposdef(A):
+    try:
+        np.linalg.cholesky(0.5 * (A + A.T))
+        return np.allclose(A, A.T)
+    except np.linalg.LinAlgError:
+        return False
+
+
+def _ispossemidef(A):
+    return bool(np.all(np.linalg.eigvalsh(0.5 * (A + A.T)) >= -1e-12 * max(1.0, np.abs(A).max())))
+
+
+def LQRCost(Q, R, xf) -> QuadraticCost:
+    """``LQRCost(Q, R, xf)`` (src/cost.jl:151-157)."""
+    Q = np.asarray(Q, dtype=np.float64)
+    xf = np.asarray(xf, dtype=np.float64)
+    R = np.asarray(R, dtype=np.float64)
+    return QuadraticCost(Q, R, np.zeros((R.shape[0], Q.shape[0])), -Q @ xf, np.zeros(R.shape[0]), 0.5 * xf @ Q @ xf)
+
+
+def LQRCostTerminal(Qf, xf) -> QuadraticCost:
+    """``LQRCostTerminal(Qf, xf)`` (src/cost.jl:165-169)."""
+    Qf = np.asarray(Qf, dtype=np.float64)
+    xf = np.asarray(xf, dtype=np.float64)
+    return QuadraticCost(Qf, None, None, -Qf @ xf, None, 0.5 * xf @ Qf @ xf)
+
+
+class Objective:
+    """``Objective(costs)`` (src/objective.jl:15-29). The HIP path requires one stage cost
+    shared by knots 1..N-1 and one terminal cost (the form every config uses)."""
+
+    def __init__(self, cost, cost_terminal=None, N=None):
+        if isinstance(cost, list):
+            costs = list(cost) + ([cost_terminal] if cost_terminal is not None else [])
+        else:
+            if N is None:
+                raise ValueError("N required")
+            term = cost if cost_terminal is None else cost_terminal
+            costs = [cost] * (N - 1) + [term]
+        self.cost = costs
+        stage = costs[0]
+        for c in costs[:-1]:
+            if c is not stage and not _same_cost(c, stage):
+                raise NotImplementedError("time-varying stage costs are not built (one stage cost per problem)")
+        self.stage = stage
+        self.terminal = costs[-1]
+
+    def __len__(self):
+        return len(self.cost)
+
+    def __getitem__(self, k):
+        return self.cost[k]
+
+
+def _same_cost(a, b):
+    return all(np.array_equal(getattr(a, f), getattr(b, f)) for f in ("Q", "R", "H", "q", "r")) and a.c == b.c
+
+
+def LQRObjective(Q, R, Qf, xf, N) -> Objective:
+    """``LQRObjective(Q, R, Qf, xf, N)`` (src/objective.jl:102-114)."""
+    Q = np.asarray(Q, dtype=np.float64)
+    R = np.asarray(R, dtype=np.float64)
+    Qf = np.asarray(Qf, dtype=np.float64)
+    xf = np.asarray(xf, dtype=np.float64)
+    ell = QuadraticCost(Q, R, np.zeros((R.shape[0], Q.shape[0])), -Q @ xf, np.zeros(R.shape[0]), 0.5 * xf @ Q @ xf)
+    ellN = QuadraticCost(Qf, None, None, -Qf @ xf, None, 0.5 * xf @ Qf @ xf)
+    return Objective([ell] * (N - 1) + [ellN])
+
+
+# ----------------------------------------------------------------------------- constraints
+
+
+class _Constraint:
+    inequality = True
+    label = "con"
+
+    def __add__(self, other):
+        return ConstraintSet([self]) + other
+
+    def __radd__(self, other):
+        return ConstraintSet(list(other)) + self
+
+
+class BoundConstraint(_Constraint):
+    """``BoundConstraint(n, m; x_min, x_max, u_min, u_max, trim=true)`` (src/constraints.jl:155-188).
+    Constraint vector order ``[x_max; u_max; x_min; u_min]`` with infinite bounds trimmed."""
+
+    label = "bound"
+
+    def __init__(self, n, m, x_min=-math.inf, x_max=math.inf, u_min=-math.inf, u_max=math.inf, trim=True):
+        self.n, self.m = n, m
+        self.u_max, self.u_min = _validate_bounds(u_max, u_min, m)
+        self.x_max, self.x_min = _validate_bounds(x_max, x_min, n)
+        if not trim:
+            raise NotImplementedError("trim=false bounds are not built")
+        self.active = dict(x_max=np.isfinite(self.x_max), u_max=np.isfinite(self.u_max),
+                           x_min=np.isfinite(self.x_min), u_min=np.isfinite(self.u_min))
+
+    def length(self, kind="stage"):
+        a = self.active
+        if kind == "stage":
+            return int(sum(v.sum() for v in a.values()))
+        return int(a["x_max"].sum() + a["x_min"].sum())
+
+    def evaluate(self, x, u=None):  # src/constraints.jl:212-227
+        a = self.active
+        x = np.asarray(x, dtype=np.float64)
+        if u is None:
+            return np.concatenate([(x - self.x_max)[a["x_max"]], (self.x_min - x)[a["x_min"]]])
+        u = np.asarray(u, dtype=np.float64)
+        return np.concatenate([(x - self.x_max)[a["x_max"]], (u - self.u_max)[a["u_max"]],
+                               (self.x_min - x)[a["x_min"]], (self.u_min - u)[a["u_min"]]])
+
+    def jacobian(self, x, u=None):  # src/constraints.jl:229-237
+        n, m = self.n, self.m
+        jac = np.vstack([np.eye(n + m), -np.eye(n + m)])
+        a = self.active
+        if u is None:
+            sel = np.concatenate([a["x_max"], np.zeros(m, bool), a["x_min"], np.zeros(m, bool)])
+            return jac[sel][:, :n]
+        sel = np.concatenate([a["x_max"], a["u_max"], a["x_min"], a["u_min"]])
+        return jac[sel]
+
+    def to_abi(self):
+        data = np.concatenate([self.x_max, self.x_min, self.u_max, self.u_min])
+        return (abi.CON_BOUND, 0, data)
+
+
+def _validate_bounds(mx, mn, n):  # src/constraints.jl:276-296
+    if np.isscalar(mn):
+        mn = np.ones(n) * mn
+    if np.isscalar(mx):
+        mx = np.ones(n) * mx
+    mx = np.asarray(mx, dtype=np.float64).copy()
+    mn = np.asarray(mn, dtype=np.float64).copy()
+    if len(mx) != len(mn):
+        raise ValueError("u_max and u_min must have equal length")
+    if not np.all(mx >= mn):
+        raise ValueError("u_max must be greater than u_min")
+    if len(mx) != n:
+        raise ValueError(f"limit of length {len(mx)} doesn't match expected length of {n}")
+    return mx, mn
+
+
+class GoalConstraint(_Constraint):
+    """``goal_constraint(xf)`` (src/constraints.jl:299-304): terminal equality x_N - xf."""
+
+    inequality = False
+    label = "goal"
+
+    def __init__(self, xf):
+        self.xf = np.asarray(xf, dtype=np.float64).copy()
+
+    def length(self, kind="stage"):
+        return 0 if kind == "stage" else len(self.xf)
+
+    def evaluate(self, x, u=None):
+        return np.asarray(x, dtype=np.float64) - self.xf if u is None else np.zeros(0)
+
+    def to_abi(self):
+        return (abi.CON_GOAL, 0, self.xf)
+
+
+def goal_constraint(xf):
+    return GoalConstraint(xf)
+
+
+def circle_constraint(x, x0, y0=None, r=None):
+    """``circle_constraint(x, x0, y0, r)`` / ``(x, c, r)`` (src/utils.jl:140-144); c <= 0 is feasible."""
+    if r is None:
+        c, r = x0, y0
+        x0, y0 = c[0], c[1]
+    return -((x[0] - x0) ** 2 + (x[1] - y0) ** 2 - r ** 2)
+
+
+def sphere_constraint(x, x0, y0, z0=None, r=None):
+    """``sphere_constraint`` (src/utils.jl:150-156)."""
+    if z0 is None:  # (x, c, r)
+        c, r = x0, y0
+        x0, y0, z0 = c[0], c[1], c[2]
+    return -((x[0] - x0) ** 2 + (x[1] - y0) ** 2 + (x[2] - z0) ** 2 - r ** 2)
+
+
+class CircleConstraints(_Constraint):
+    """A ``Constraint{Inequality}`` whose rows are ``circle_constraint(x, xc, yc, r)`` — the
+    reference's cylinder-obstacle idiom (problems/quad_obs.jl:53-62). Stage only."""
+
+    label = "circles"
+
+    def __init__(self, n, m, circles, label="circles"):
+        self.circles = np.asarray(circles, dtype=np.float64).reshape(-1, 3)
+        self.label = label
+
+    def length(self, kind="stage"):
+        return len(self.circles) if kind == "stage" else 0
+
+    def evaluate(self, x, u=None):
+        if u is None:
+            return np.zeros(0)
+        return np.array([circle_constraint(x, c[0], c[1], c[2]) for c in self.circles])
+
+    def to_abi(self):
+        return (abi.CON_CIRCLES, len(self.circles), self.circles.ravel())
+
+
+class SphereConstraints(_Constraint):
+    """Rows ``sphere_constraint(x, xc, yc, zc, r)`` (test/quadrotor_tests.jl:68-74,
+    problems/quad_obs.jl:64-69). Stage only."""
+
+    label = "spheres"
+
+    def __init__(self, n, m, spheres, label="spheres"):
+        self.spheres = np.asarray(spheres, dtype=np.float64).reshape(-1, 4)
+        self.label = label
+
+    def length(self, kind="stage"):
+        return len(self.spheres) if kind == "stage" else 0
+
+    def evaluate(self, x, u=None):
+        if u is None:
+            return np.zeros(0)
+        return np.array([sphere_constraint(x, s[0], s[1], s[2], s[3]) for s in self.spheres])
+
+    def to_abi(self):
+        return (abi.CON_SPHERES, len(self.spheres), self.spheres.ravel())
+
+
+class ConstraintSet(list):
+    """``ConstraintSet`` (src/constraint_sets.jl:1): an ordered list of constraints."""
+
+    def __add__(self, other):
+        out = ConstraintSet(self)
+        if isinstance(other, (list, tuple)):
+            out.extend(other)
+        else:
+            out.append(other)
+        return out
+
+    __iadd__ = __add__
+
+    def num_constraints(self, kind="stage"):
+        return sum(c.length(kind) for c in self)
+
+
+class Constraints:
+    """``Constraints`` per-knot constraint sets (src/constraint_sets.jl:157-206)."""
+
+    def __init__(self, C=None, N=None, C_term=None):
+        if isinstance(C, int) and N is None:  # Constraints(N)
+            N, C = C, None
+        if N is None:
+            raise ValueError("N required")
+        if C is None:
+            self.C = [ConstraintSet() for _ in range(N)]
+        elif C_term is None:
+            self.C = [ConstraintSet(C) for _ in range(N)]
+        else:
+            self.C = [ConstraintSet(C) for _ in range(N - 1)] + [ConstraintSet(C_term)]
+
+    def __len__(self):
+        return len(self.C)
+
+    def __getitem__(self, k):
+        return self.C[k]
+
+    def __setitem__(self, k, v):
+        self.C[k] = v if isinstance(v, ConstraintSet) else ConstraintSet(v if isinstance(v, list) else [v])
+
+    def is_constrained(self):
+        return any(len(c) > 0 for c in self.C)
+
+    def num_constraints(self):
+        N = len(self.C)
+        return [c.num_constraints("stage" if k < N - 1 else "terminal") for k, c in enumerate(self.C)]
+
+    def copy(self):
+        return Constraints([], N=len(self.C)) if not self.C else _copy_constraints(self)
+
+
+def _copy_constraints(cons):
+    out = Constraints(len(cons.C))
+    out.C = [ConstraintSet(c) for c in cons.C]
+    return out
+
+
+# ----------------------------------------------------------------------------- problem
+
+
+class Problem:
+    """``Problem{T,Discrete}`` (src/problem.jl:37-113).
+
+    ``x0`` may be a vector (one trajectory) or an array ``(B, n)``; ``U0`` a list of N-1
+    control vectors, an array ``(N-1, m)`` or a batch ``(B, N-1, m)``. ``X`` starts as NaN
+    (``empty_state``, src/problem.jl:232), which makes the solvers roll out first.
+    """
+
+    def __init__(self, model: Model, obj: Objective, U0=None, X0=None, *, constraints: Constraints | None = None,
+                 x0=None, xf=None, N=None, dt=None, tf=None, integration=None):
+        if not model.discrete:
+            if integration is None:
+                raise ValueError("a continuous model needs integration=:rk3/:rk4 (DIRCOL is out of scope)")
+            model = discretize_model(model, integration)
+        N = len(obj) if N is None else N
+        if len(obj) != N:
+            raise ValueError("objective length must equal N")
+        N, tf, dt = _validate_time(N, tf, dt)
+        self.model = model
+        self.obj = obj
+        self.constraints = constraints if constraints is not None else Constraints(N)
+        if len(self.constraints) != N:
+            raise ValueError("constraints length must equal N")
+        n, m = model.n, model.m
+        x0 = np.zeros(n) if x0 is None else np.asarray(x0, dtype=np.float64)
+        self.batched = x0.ndim == 2
+        B = x0.shape[0] if self.batched else 1
+        self.x0 = x0.reshape(B, n).copy()
+        self.xf = np.zeros(n) if xf is None else np.asarray(xf, dtype=np.float64).copy()
+        self.N, self.dt, self.tf = N, dt, tf
+        self._X = np.full((B, N, n), np.nan)
+        self._U = np.zeros((B, N - 1, m))
+        if U0 is not None:
+            initial_controls_b(self, U0)
+        if X0 is not None:
+            initial_states_b(self, X0)
+
+    # ---- shapes
+    @property
+    def B(self):
+        return self._X.shape[0]
+
+    def size(self):
+        return self.model.n, self.model.m, self.N
+
+    @property
+    def X(self):
+        return self._X if self.batched else self._X[0]
+
+    @X.setter
+    def X(self, v):
+        self._X[...] = np.asarray(v, dtype=np.float64).reshape(self._X.shape)
+
+    @property
+    def U(self):
+        return self._U if self.batched else self._U[0]
+
+    @U.setter
+    def U(self, v):
+        self._U[...] = np.asarray(v, dtype=np.float64).reshape(self._U.shape)
+
+    def copy(self):
+        p = _copy.copy(self)
+        p.constraints = _copy_constraints(self.constraints)
+        p.x0 = self.x0.copy()
+        p.xf = self.xf.copy()
+        p._X = self._X.copy()
+        p._U = self._U.copy()
+        return p
+
+    def is_constrained(self):
+        return self.constraints.is_constrained()
+
+    # ---- marshalling to the C ABI
+    def build_desc(self) -> abi.DescBuilder:
+        n, m, N = self.model.n, self.model.m, self.N
+        stage, term = self.obj.stage, self.obj.terminal
+        sets, knot_set, keys = [], [], {}
+        for k in range(N):
+            cs = self.constraints[k]
+            if len(cs) == 0:
+                knot_set.append(-1)
+                continue
+            key = tuple(id(c) for c in cs) + (k == N - 1,)
+            if key not in keys:
+                keys[key] = len(sets)
+                sets.append([c.to_abi() for c in cs])
+            knot_set.append(keys[key])
+        R = stage.R if stage.R.size else np.zeros((m, m))
+        return abi.DescBuilder(self.model.model_id, self.model.integration, n, m, N, self.dt, stage.Q, R, stage.H,
+                               stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B)
+
+
+def _validate_time(N, tf, dt):
+    """``_validate_time`` (src/problem.jl:169-220) for the fixed-time case."""
+    if N is None and dt is None and tf is None:
+        raise ValueError("Must specify at least 2: N, dt, or tf")
+    if tf == 0:
+        raise NotImplementedError("minimum-time problems are out of scope (SURVEY.md §8f)")
+    if tf is not None:
+        if dt is None and N is not None:
+            dt = tf / (N - 1)
+        elif dt is not None and N is None:
+            N = int(round(tf / dt)) + 1
+            dt = tf / (N - 1)
+        elif dt is not None and N is not None and dt != tf / (N - 1):
+            raise ValueError("Specified time step, number of knot points, and final time do not agree")
+    else:
+        if dt is None or not dt > 0:
+            raise ValueError("dt must be positive for a non-minimum-time problem")
+        if N is None:
+            N = 51
+        tf = dt * (N - 1)
+    if N < 0:
+        raise ValueError(f"{N} is not a valid entry for N")
+    if not dt > 0:
+        raise ValueError("dt must be strictly positive")
+    return N, tf, dt
+
+
+def initial_controls_b(prob: Problem, U0):
+    """``initial_controls!(prob, U0)`` (src/problem.jl:149-150)."""
+    U0 = np.asarray(U0, dtype=np.float64)
+    N, m = prob.N, prob.model.m
+    if U0.ndim == 2:
+        U0 = U0[: N - 1]
+        prob._U[...] = U0[None, :, :]
+    else:
+        prob._U[...] = U0[:, : N - 1, :]
+
+
+def initial_states_b(prob: Problem, X0):
+    """``initial_states!(prob, X0)`` (src/problem.jl:153-154)."""
+    X0 = np.asarray(X0, dtype=np.float64)
+    prob._X[...] = X0 if X0.ndim == 3 else X0[None]
+
+
+def set_x0_b(prob: Problem, x0):
+    prob.x0[...] = np.asarray(x0, dtype=np.float64)
+
+
+def max_violation(prob: Problem) -> float:
+    """``max_violation(prob)`` (src/problem.jl:242-267), host side, per trajectory max over
+    the batch (returns an array for a batched problem)."""
+    out = []
+    N = prob.N
+    for b in range(prob.B):
+        c_max = 0.0
+        if prob.is_constrained():
+            X, U = prob._X[b], prob._U[b]
+            for k in range(N):
+                cs = prob.constraints[k]
+                term = k == N - 1
+                vals_e, vals = [], []
+                for c in cs:
+                    v = c.evaluate(X[k]) if term else c.evaluate(X[k], U[k])
+                    if len(v) == 0:
+                        continue
+                    vals.append(v)
+                    if not c.inequality:
+                        vals_e.append(v)
+                if not vals:
+                    continue
+                allc = np.concatenate(vals)
+                max_e = np.max(np.abs(np.concatenate(vals_e))) if vals_e else 0.0
+                max_i = np.max(np.maximum(allc, 0.0))
+                c_max = max(c_max, max(max_e, max_i))
+        out.append(c_max)
+    return out[0] if not prob.batched else np.array(out)

@@ -1,0 +1,216 @@
+"""Canned problems (``TrajectoryOptimization.Problems``, src/problems.jl:14-24) and the
+BASELINE.json benchmark configurations with their synthetic batched inputs
+(SURVEY.md §8(d)). Every constructor cites the reference file it restates."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .problem import (BoundConstraint, CircleConstraints, Constraints, Dynamics, LQRObjective, Problem,
+                      SphereConstraints, goal_constraint, rk3, rk4)
+from .solvers import ALTROSolverOptions, AugmentedLagrangianSolverOptions, iLQRSolverOptions
+
+HOVER = 0.5 * 9.81 / 4.0
+
+
+def doubleintegrator(U0=None, seed=0):
+    """problems/doubleintegrator.jl:1-31 (config 1)."""
+    model_d = rk3(Dynamics.doubleintegrator)
+    n, m = 2, 1
+    Q, Qf, R = np.eye(n), np.eye(n), 0.1 * np.eye(m)
+    x0, xf = np.array([0.0, 0.0]), np.array([1.0, 0.0])
+    N, dt = 21, 0.1
+    if U0 is None:
+        U0 = 0.001 * np.random.default_rng(seed).random((N - 1, m))
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    bnd = BoundConstraint(n, m, u_max=1.5, u_min=-1.5, trim=True)
+    goal = goal_constraint(xf)
+    cons = Constraints(N)
+    for k in range(N - 1):
+        cons[k] += bnd
+    cons[N - 1] += goal
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+
+
+def cartpole(constrained=True, x0=None, U0=None):
+    """problems/cartpole.jl:1-28. ``constrained=False`` gives config 2's unconstrained problem."""
+    model_d = rk3(Dynamics.cartpole)
+    n, m = 4, 1
+    Q, Qf, R = 1e-2 * np.eye(n), 100.0 * np.eye(n), 1e-1 * np.eye(m)
+    xf = np.array([0.0, math.pi, 0.0, 0.0])
+    N, tf = 101, 5.0
+    dt = tf / (N - 1)
+    if x0 is None:
+        x0 = np.zeros(n)
+    if U0 is None:
+        U0 = 0.01 * np.ones((N - 1, m))
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    cons = Constraints(N)
+    if constrained:
+        bnd = BoundConstraint(n, m, u_min=-3.0, u_max=3.0)
+        goal = goal_constraint(xf)
+        for k in range(N - 1):
+            cons[k] += bnd
+        cons[N - 1] += goal
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+
+
+def quadrotor_test(constraints="goal+bounds", x0=None, U0=None, integration="rk4"):
+    """test/quadrotor_tests.jl:4-84: rk4, N=101, dt=0.05, Q=R=1e-2 I, Qf=1000 I.
+    constraints in {"none", "goal", "goal+bounds", "goal+bounds+obs"}."""
+    model_d = rk4(Dynamics.quadrotor) if integration == "rk4" else rk3(Dynamics.quadrotor)
+    n, m = 13, 4
+    Q, R, Qf = 1e-2 * np.eye(n), 1e-2 * np.eye(m), 1000.0 * np.eye(n)
+    q0 = np.array([1.0, 0.0, 0.0, 0.0])
+    if x0 is None:
+        x0 = np.zeros(n)
+        x0[3:7] = q0
+    xf = np.zeros(n)
+    xf[0:3] = [0.0, 50.0, 0.0]
+    xf[3:7] = q0
+    N, dt = 101, 0.05
+    if U0 is None:
+        U0 = HOVER * np.ones((N - 1, m))
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    goal = goal_constraint(xf)
+    bnd = BoundConstraint(n, m, u_min=0.0, u_max=15.0, trim=True)
+    if constraints == "none":
+        con = []
+    elif constraints == "goal":
+        con = [goal]
+    elif constraints == "goal+bounds":
+        con = [bnd, goal]
+    elif constraints == "goal+bounds+obs":
+        r_quad, r_sphere = 1.0, 3.0
+        spheres = [(0.0, 10.0, 0.0, r_sphere + r_quad), (0.0, 20.0, 0.0, r_sphere + r_quad),
+                   (0.0, 30.0, 0.0, r_sphere + r_quad)]
+        con = [bnd, SphereConstraints(n, m, spheres, "obs"), goal]
+    else:
+        raise ValueError(constraints)
+    cons = Constraints(con, N) if con else Constraints(N)
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+
+
+def quad_obs(N=101, x0=None, U0=None):
+    """problems/quad_obs.jl:1-89 "as written" (the sphere radius argument is
+    z+r_quad, and the file initialises the other problem's controls, so U starts at 0)."""
+    model_d = rk3(Dynamics.quadrotor)
+    n, m = 13, 4
+    q0 = np.array([1.0, 0.0, 0.0, 0.0])
+    if x0 is None:
+        x0 = np.zeros(n)
+        x0[0:3] = [0.0, 0.0, 10.0]
+        x0[3:7] = q0
+    xf = np.zeros(n)
+    xf[0:3] = [0.0, 60.0, 10.0]
+    xf[3:7] = q0
+    Q = 1e-3 * np.eye(n)
+    Q[3:7, 3:7] = 1e-3 * np.eye(4)
+    R = 1e-2 * np.eye(m)
+    Qf = 1.0 * np.eye(n)
+    u_min, u_max = 0.0, 50.0
+    x_max = np.full(n, np.inf)
+    x_min = np.full(n, -np.inf)
+    x_max[0:3] = [25.0, np.inf, 20.0]
+    x_min[0:3] = [-25.0, -np.inf, 0.0]
+    bnd_u = BoundConstraint(n, m, u_min=u_min, u_max=u_max)
+    bnd = BoundConstraint(n, m, u_min=u_min, u_max=u_max, x_min=x_min, x_max=x_max)
+    xf_U = xf.copy()
+    xf_L = xf.copy()
+    xf_U[3:7] = np.inf
+    xf_L[3:7] = -np.inf
+    xf_U[7:10] = 0.0
+    xf_L[7:10] = 0.0
+    bnd_xf = BoundConstraint(n, m, x_min=xf_L, x_max=xf_U)
+    tf = 5.0
+    dt = tf / (N - 1)
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    r_quad = 2.0
+    cyl = [(0.0, 10.0, 3.0), (10.0, 30.0, 3.0), (-13.0, 25.0, 2.0), (5.0, 50.0, 4.0)]
+    sph = [(0.0, 40.0, 5.0, 2.0), (-5.0, 15.0, 3.0, 1.0), (10.0, 20.0, 7.0, 2.0)]
+    cyl_con = CircleConstraints(n, m, [(c[0], c[1], c[2] + r_quad) for c in cyl], "cylinders")
+    sph_con = SphereConstraints(n, m, [(s[0], s[1], s[2], s[2] + r_quad) for s in sph], "spheres")  # A.6
+    cons = Constraints(N)
+    cons[0] += bnd_u
+    for k in range(1, N - 1):
+        cons[k] += bnd + cyl_con + sph_con
+    cons[N - 1] += bnd_xf
+    if U0 is None:
+        U0 = np.zeros((N - 1, m))
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+
+
+def car_sqrt_bp(constrained=False):
+    """test/sqrt_bp_tests.jl:1-16 / :46-56: car, rk4, N=31, dt=0.15, U=ones, Q=R=1e-3 I,
+    Qf=100 I, xf=[0,1,0]; constrained adds bounds ±5 and the goal."""
+    model_d = rk4(Dynamics.car)
+    n, m = 3, 2
+    Q, R, Qf = 1e-3 * np.eye(n), 1e-3 * np.eye(m), 100.0 * np.eye(n)
+    x0, xf = np.zeros(n), np.array([0.0, 1.0, 0.0])
+    N, dt = 31, 0.15
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    cons = Constraints(N)
+    if constrained:
+        bnd = BoundConstraint(n, m, u_min=-5.0, u_max=5.0, trim=True)
+        cons = Constraints([bnd, goal_constraint(xf)], N)
+    return Problem(model_d, obj, np.ones((N - 1, m)), constraints=cons, x0=x0, N=N, dt=dt)
+
+
+# ---------------------------------------------------------------------------- BASELINE configs
+
+def _per_traj_rng(seed0, B, fn):
+    return np.stack([fn(np.random.default_rng(seed0 + b)) for b in range(B)])
+
+
+def config_cartpole(B=1024, offset=0):
+    """Config 2: cartpole swing-up, unconstrained iLQR, U0[b] = 0.01 + 0.5 N(0,1) (seed 1000+b)."""
+    N, m = 101, 1
+    U0 = _per_traj_rng(1000 + offset, B, lambda r: 0.01 + 0.5 * r.standard_normal((N - 1, m)))
+    prob = cartpole(constrained=False, x0=np.zeros((B, 4)), U0=U0)
+    return prob, iLQRSolverOptions()
+
+
+def config_quadrotor(B=8192, offset=0):
+    """Config 3: quadrotor point-to-point, AL-iLQR with u in [0,15] + goal, square-root BP.
+    U0 = hover + 0.1 N(0,1), x0[1:3] += N(0,1) (seed 2000+b)."""
+    N, n, m = 101, 13, 4
+
+    def gen(r):
+        x0 = np.zeros(n)
+        x0[3] = 1.0
+        x0[0:3] += r.standard_normal(3)
+        U0 = HOVER + 0.1 * r.standard_normal((N - 1, m))
+        return np.concatenate([x0, U0.ravel()])
+
+    Z = _per_traj_rng(2000 + offset, B, gen)
+    x0 = Z[:, :n]
+    U0 = Z[:, n:].reshape(B, N - 1, m)
+    prob = quadrotor_test("goal+bounds", x0=x0, U0=U0)
+    opts_ilqr = iLQRSolverOptions(cost_tolerance=1e-5, square_root=True)
+    opts_al = AugmentedLagrangianSolverOptions(opts_uncon=opts_ilqr, constraint_tolerance=1e-3,
+                                               cost_tolerance=1e-5, cost_tolerance_intermediate=1e-4)
+    return prob, opts_al
+
+
+def config_quad_maze(B=8192, offset=0, N=201):
+    """Config 4 (per GPU shard): quad_obs with N=201, dt=0.025; x0[1:3] ~ U([-5,5]x[-3,0]x[8,12]),
+    U0 = hover + 0.1 N (seed 3000+b)."""
+    n, m = 13, 4
+
+    def gen(r):
+        x0 = np.zeros(n)
+        x0[3] = 1.0
+        x0[0:3] = [r.uniform(-5, 5), r.uniform(-3, 0), r.uniform(8, 12)]
+        U0 = HOVER + 0.1 * r.standard_normal((N - 1, m))
+        return np.concatenate([x0, U0.ravel()])
+
+    Z = _per_traj_rng(3000 + offset, B, gen)
+    prob = quad_obs(N=N, x0=Z[:, :n], U0=Z[:, n:].reshape(B, N - 1, m))
+    return prob, AugmentedLagrangianSolverOptions()
+
+
+def config_doubleintegrator(B=1):
+    """Config 1: double integrator block move, ALTRO defaults."""
+    prob = doubleintegrator()
+    return prob, ALTROSolverOptions()

@@ -1,0 +1,293 @@
+"""Solver plugin interface mirror (src/solvers.jl:7-126, docs/src/solvers.md:25-47).
+
+``iLQRSolverOptions`` / ``AugmentedLagrangianSolverOptions`` / ``ALTROSolverOptions`` mirror the
+reference's ``@with_kw`` option structs (same field names and defaults);
+``iLQRSolver`` / ``AugmentedLagrangianSolver`` / ``ALTROSolver`` are ``AbstractSolver``s whose
+buffers live on the GPU behind the C ABI (include/tog.h); ``solve_b(prob, opts)`` is the
+reference's ``solve!`` and ``solve(prob, opts)`` its copying variant (src/solvers.jl:91-123).
+
+Errors follow the reference: invalid arguments raise ``ValueError`` (ArgumentError),
+``Cost increased during Forward Pass`` raises ``RuntimeError`` when a trajectory reports it
+(forward_pass.jl:80-82); the ``@warn``s become per-trajectory status flags in ``solver.stats``.
+"""
+from __future__ import annotations
+
+import copy as _copy
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .device import BatchHandle
+
+
+# ----------------------------------------------------------------------------- options
+
+@dataclass
+class iLQRSolverOptions:
+    """src/solvers/ilqr/ilqr_solver.jl:7-81 (defaults identical)."""
+
+    verbose: bool = False
+    live_plotting: str = "off"
+    cost_tolerance: float = 1.0e-4
+    gradient_type: str = "todorov"
+    gradient_norm_tolerance: float = 1.0e-5
+    iterations: int = 300
+    dJ_counter_limit: int = 10
+    square_root: bool = False
+    line_search_lower_bound: float = 1.0e-8
+    line_search_upper_bound: float = 10.0
+    iterations_linesearch: int = 20
+    bp_reg_initial: float = 0.0
+    bp_reg_increase_factor: float = 1.6
+    bp_reg_max: float = 1.0e8
+    bp_reg_min: float = 1.0e-8
+    bp_reg_type: str = "control"
+    bp_reg_fp: float = 10.0
+    bp_sqrt_inv_type: str = "pseudo"
+    bp_reg_sqrt_initial: float = 1.0e-6
+    bp_reg_sqrt_increase_factor: float = 10.0
+    max_cost_value: float = 1.0e8
+    max_state_value: float = 1.0e8
+    max_control_value: float = 1.0e8
+
+    def copy(self):
+        return _copy.deepcopy(self)
+
+
+@dataclass
+class AugmentedLagrangianSolverOptions:
+    """src/solvers/augmented_lagrangian/augmented_lagrangian_solver.jl:8-66."""
+
+    verbose: bool = False
+    opts_uncon: iLQRSolverOptions = field(default_factory=iLQRSolverOptions)
+    cost_tolerance: float = 1.0e-4
+    cost_tolerance_intermediate: float = 1.0e-3
+    gradient_norm_tolerance: float = 1.0e-5
+    gradient_norm_tolerance_intermediate: float = 1.0e-5
+    constraint_tolerance: float = 1.0e-3
+    constraint_tolerance_intermediate: float = 1.0e-3
+    iterations: int = 30
+    dual_min: float = -1.0e8
+    dual_max: float = 1.0e8
+    penalty_max: float = 1.0e8
+    penalty_initial: float = 1.0
+    penalty_scaling: float = 10.0
+    penalty_scaling_no: float = 1.0
+    constraint_decrease_ratio: float = 0.25
+    outer_loop_update_type: str = "default"
+    active_constraint_tolerance: float = 0.0
+    kickout_max_penalty: bool = False
+
+    def copy(self):
+        return _copy.deepcopy(self)
+
+
+@dataclass
+class ALTROSolverOptions:
+    """src/solvers/altro/altro_solver.jl:6-65. With ``projected_newton=false`` (default), a NaN
+    initial state trajectory and ``tf > 0`` ALTRO reduces to the AL solve (altro_methods.jl:98-124);
+    the infeasible-start, minimum-time and projected-Newton phases are SURVEY.md §8(f) "next"."""
+
+    verbose: bool = False
+    opts_al: AugmentedLagrangianSolverOptions = field(default_factory=AugmentedLagrangianSolverOptions)
+    constraint_tolerance_infeasible: float = 1.0e-5
+    R_inf: float = 1.0
+    dynamically_feasible_projection: bool = True
+    resolve_feasible_problem: bool = True
+    penalty_initial_infeasible: float = 1.0
+    penalty_scaling_infeasible: float = 10.0
+    R_minimum_time: float = 1.0
+    dt_max: float = 1.0
+    dt_min: float = 1.0e-3
+    penalty_initial_minimum_time_inequality: float = 1.0
+    penalty_initial_minimum_time_equality: float = 1.0
+    penalty_scaling_minimum_time_inequality: float = 1.0
+    penalty_scaling_minimum_time_equality: float = 1.0
+    projected_newton: bool = False
+    projected_newton_tolerance: float = 1.0e-3
+
+    def copy(self):
+        return _copy.deepcopy(self)
+
+
+def to_tog_options(opts) -> abi.tog_options:
+    """Flatten reference option structs into the C ABI's POD ``tog_options``."""
+    o = abi.default_options()
+    if isinstance(opts, ALTROSolverOptions):
+        opts = opts.opts_al
+    if isinstance(opts, AugmentedLagrangianSolverOptions):
+        al, il = opts, opts.opts_uncon
+    else:
+        al, il = AugmentedLagrangianSolverOptions(), opts
+    o.cost_tolerance = il.cost_tolerance
+    o.gradient_norm_tolerance = il.gradient_norm_tolerance
+    o.iterations = int(il.iterations)
+    o.dJ_counter_limit = int(il.dJ_counter_limit)
+    o.square_root = int(bool(il.square_root))
+    if il.bp_reg_type not in ("control", "state"):
+        raise ValueError("bp_reg_type must be :control or :state")
+    o.bp_reg_type = 0 if il.bp_reg_type == "control" else 1
+    if il.gradient_type not in ("todorov", "feedforward"):
+        raise NotImplementedError("gradient_type :ℓ2/:ℓinf are not built")
+    o.gradient_type = 0 if il.gradient_type == "todorov" else 1
+    o.iterations_linesearch = int(il.iterations_linesearch)
+    o.line_search_lower_bound = il.line_search_lower_bound
+    o.line_search_upper_bound = il.line_search_upper_bound
+    o.bp_reg_increase_factor = il.bp_reg_increase_factor
+    o.bp_reg_max = il.bp_reg_max
+    o.bp_reg_min = il.bp_reg_min
+    o.bp_reg_fp = il.bp_reg_fp
+    o.max_cost_value = il.max_cost_value
+    o.max_state_value = il.max_state_value
+    o.max_control_value = il.max_control_value
+    o.al_cost_tolerance = al.cost_tolerance
+    o.al_cost_tolerance_intermediate = al.cost_tolerance_intermediate
+    o.al_gradient_norm_tolerance = al.gradient_norm_tolerance
+    o.al_gradient_norm_tolerance_intermediate = al.gradient_norm_tolerance_intermediate
+    o.constraint_tolerance = al.constraint_tolerance
+    o.dual_min = al.dual_min
+    o.dual_max = al.dual_max
+    o.penalty_max = al.penalty_max
+    o.penalty_initial = al.penalty_initial
+    o.penalty_scaling = al.penalty_scaling
+    o.al_iterations = int(al.iterations)
+    o.kickout_max_penalty = int(bool(al.kickout_max_penalty))
+    return o
+
+
+def solver_name(opts) -> str:
+    """src/solvers.jl:35-41."""
+    if isinstance(opts, iLQRSolverOptions):
+        return "iLQR"
+    if isinstance(opts, ALTROSolverOptions):
+        return "ALTRO"
+    if isinstance(opts, AugmentedLagrangianSolverOptions):
+        return "AL-" + solver_name(opts.opts_uncon)
+    return solver_name(opts.opts)
+
+
+# ----------------------------------------------------------------------------- solvers
+
+class AbstractSolver:
+    """``AbstractSolver{T}`` (src/solvers.jl:7). Holds ``opts``, ``stats`` and the device handle."""
+
+    mode = abi.MODE_ILQR
+
+    def __init__(self, prob, opts, device: int = 0, stream=None):
+        self.opts = opts
+        self.stats: dict = {}
+        self.handle = BatchHandle(prob, to_tog_options(opts), device=device, stream=stream)
+        self.n, self.m, self.N = prob.model.n, prob.model.m, prob.N
+
+    def size(self):
+        return self.n, self.m, self.N
+
+    def reset_b(self):
+        self.stats = {}
+
+    # ---- device views (copies to host), reference field names
+    @property
+    def K(self):
+        return self.handle.get(abi.FIELD_K)
+
+    @property
+    def d(self):
+        return self.handle.get(abi.FIELD_D)
+
+    @property
+    def Xbar(self):
+        return self.handle.get(abi.FIELD_XBAR)
+
+    @property
+    def Ubar(self):
+        return self.handle.get(abi.FIELD_UBAR)
+
+    @property
+    def rho(self):
+        return self.handle.get(abi.FIELD_RHO)
+
+
+class iLQRSolver(AbstractSolver):
+    """``iLQRSolver`` (ilqr_solver.jl:93-144)."""
+
+    mode = abi.MODE_ILQR
+
+
+class AugmentedLagrangianSolver(AbstractSolver):
+    """``AugmentedLagrangianSolver`` (augmented_lagrangian_solver.jl:101-140)."""
+
+    mode = abi.MODE_AL
+
+    @property
+    def lam(self):
+        return self.handle.get(abi.FIELD_LAMBDA)
+
+    @property
+    def mu(self):
+        return self.handle.get(abi.FIELD_MU)
+
+    @property
+    def C(self):
+        return self.handle.get(abi.FIELD_C)
+
+
+class ALTROSolver(AugmentedLagrangianSolver):
+    """``ALTROSolver`` (altro_solver.jl:70-94): AL phase only (projected_newton=false)."""
+
+
+def AbstractSolverFor(prob, opts, **kw):
+    """``AbstractSolver(prob, opts)`` dispatch on the options type (src/solvers.jl:60-62)."""
+    if isinstance(opts, iLQRSolverOptions):
+        return iLQRSolver(prob, opts, **kw)
+    if isinstance(opts, ALTROSolverOptions):
+        _altro_check(prob, opts)
+        return ALTROSolver(prob, opts, **kw)
+    if isinstance(opts, AugmentedLagrangianSolverOptions):
+        return AugmentedLagrangianSolver(prob, opts, **kw)
+    raise ValueError("Can't create an Abstract Solver without knowing the type of the Solver Options")
+
+
+def _altro_check(prob, opts):
+    if opts.projected_newton:
+        raise NotImplementedError("ALTRO projected-Newton phase is SURVEY.md §8(f) 'next' (not built)")
+    if np.isfinite(prob._X).all():
+        raise NotImplementedError("infeasible-start ALTRO (X0 given) is SURVEY.md §8(f) 'next' (not built)")
+
+
+def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int = 0):
+    """``solve!(prob, opts)`` / ``solve!(prob, solver)`` (src/solvers.jl:91-94). Mutates
+    ``prob.X``/``prob.U`` in place and returns the solver."""
+    if isinstance(solver_or_opts, AbstractSolver):
+        solver = solver_or_opts
+        solver.handle.upload_state(prob)
+    else:
+        opts = solver_or_opts
+        if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
+            # solve!(prob, ::AugmentedLagrangianSolverOptions) on an unconstrained problem
+            # falls back to the unconstrained solver (augmented_lagrangian_methods.jl:33-36)
+            opts = opts.opts_uncon
+        solver = AbstractSolverFor(prob, opts, device=device)
+    mode = solver.mode
+    h = solver.handle
+    h.solve(mode, max_steps=max_steps if max_steps is not None else _default_max_steps(solver))
+    h.download_state(prob)
+    solver.stats = h.stats_dict()
+    flags = solver.stats["flags"]
+    if np.any(flags & abi.TRAJ_COST_INCREASED):
+        raise RuntimeError("Error: Cost increased during Forward Pass")
+    return solver
+
+
+def _default_max_steps(solver):
+    o = to_tog_options(solver.opts)
+    if solver.mode == abi.MODE_AL:
+        return int(o.iterations) * int(o.al_iterations) + 1
+    return int(o.iterations) + 1
+
+
+def solve(prob, solver_or_opts, **kw):
+    """``solve(prob, opts)`` (src/solvers.jl:104-123): returns ``(prob_copy, solver)``."""
+    p0 = prob.copy()
+    s = solve_b(p0, solver_or_opts, **kw)
+    return p0, s
