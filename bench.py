@@ -1,0 +1,192 @@
+"""bench.py — batched iLQR iterations/sec on MI355X (BASELINE.json metric).
+
+One step = one batched AL-iLQR ``step!`` (jacobians -> cost expansion + square-root backward pass
+-> forward-pass line search -> bookkeeping / AL dual+penalty update) for every active trajectory of
+the per-GPU batch. Workload: BASELINE.json configs[2] (quadrotor n=13 m=4 N=101, AL-iLQR with
+u in [0,15] + goal, sqrt backward pass), 8192 trajectories per GPU, synthetic random starts
+(SURVEY.md §8(d)); inputs resident in HBM before timing. ``value`` = Σ trajectory-iterations
+completed on all GPUs / max-over-ranks wall time.
+
+Multi-GPU: one process per GPU (torch.distributed.run); trajectories are independent so each rank
+solves its own shard (weak scaling). The only collective is one RCCL all-reduce per step of the
+batch statistics [n_active, Σ cost, max c_max].
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import __graft_entry__  # noqa: E402
+
+METRIC = "iLQR iterations/sec (batched trajectories), quadrotor n=13 m=4 N=101"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def kernel_bytes(n, m, N, p_stage, p_term, trials):
+    """Algorithmic HBM bytes per trajectory-step for each kernel (SURVEY.md §8(d) staged design;
+    DESIGN.md §4 lists the terms)."""
+    K = N - 1
+    jac = 8 * K * ((n + m) + n * (n + m))                       # read x,u ; write [A|B]
+    bwd = 8 * (K * (n * (n + m) + (n + m) + m * (n + 1))        # read [A|B], x,u ; write K,d
+               + n + 2 * (K * p_stage + p_term))                # x_N ; read λ, μ
+    fwd = 8 * (trials * K * (2 * (n + m) + m * (n + 1))         # per trial: read x,u,K,d ; write x̄,ū
+               + 2 * K * (n + m)                                # accept: copy X̄,Ū -> X,U
+               + trials * 3 * (K * p_stage + p_term))           # λ, μ read, C written per trial
+    return {"jacobian": jac, "backward": bwd, "forward": fwd}
+
+
+def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
+    """The C oracle ("port" of the reference algorithm) on the host cores: full AL-iLQR solves of
+    config-3 trajectories, OpenMP over trajectories. Bounded sample (~`seconds` of work)."""
+    threads = threads or min(16, len(os.sched_getaffinity(0)))
+    B = 2 * threads
+    prob, opts = pkg.Problems.config_quadrotor(B=B, offset=100000)
+    t = time.perf_counter()
+    steps = orc.solve_batch(prob, opts, nthreads=threads)
+    dt = time.perf_counter() - t
+    if dt < seconds:  # scale the sample up to ~`seconds`
+        B2 = int(min(4096, B * max(1.0, (seconds - dt) / max(dt, 1e-3))))
+        B2 = max(threads, B2 - B2 % threads)
+        prob, opts = pkg.Problems.config_quadrotor(B=B2, offset=200000)
+        t = time.perf_counter()
+        steps2 = orc.solve_batch(prob, opts, nthreads=threads)
+        dt2 = time.perf_counter() - t
+        steps, dt, B = steps + steps2, dt + dt2, B + B2
+    return {"value": steps / dt, "unit": "iLQR iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{B} config-3 trajectories solved to AL convergence ({steps} iLQR steps, "
+                      f"{dt:.1f} s) by oracle/tog_oracle.c, OpenMP over trajectories"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8192, help="trajectories per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    pkg = __graft_entry__.load_package()
+    abi = pkg.abi
+    B = args.batch
+    prob, opts = pkg.Problems.config_quadrotor(B=B, offset=rank * B)
+    stream = None
+    if dist is not None:
+        import torch
+
+        stream = torch.cuda.current_stream().cuda_stream  # libtog and RCCL share one stream
+    solver = pkg.AbstractSolverFor(prob, opts, device=local_rank, stream=stream)
+    h = solver.handle
+    n, m, N = prob.model.n, prob.model.m, prob.N
+
+    stats_t = gathered = None
+    if dist is not None:
+        stats_t = torch.zeros(3, dtype=torch.float64, device=f"cuda:{local_rank}")
+        gathered = torch.zeros(3 * world, dtype=torch.float64, device=f"cuda:{local_rank}")
+
+    def allreduce_stats():
+        # batch statistics [n_active, Σ cost, max c_max] of every shard: written on-device by
+        # k_batch_stats and exchanged with ONE RCCL collective, stream-ordered (no host sync)
+        if dist is None:
+            return
+        abi.check(h.lib, h.lib.tog_batch_stats_device(h.h, ctypes.c_void_p(stats_t.data_ptr())))
+        dist.all_gather_into_tensor(gathered, stats_t)
+
+    h.solve_init(abi.MODE_AL)
+    h.solve_step(args.warmup)
+    h.synchronize()
+    steps0 = h.total_steps()
+    if dist is not None:
+        dist.barrier()
+    h.synchronize()
+    h.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        h.solve_step(1)
+        allreduce_stats()
+    h.synchronize()
+    if dist is not None:
+        import torch
+
+        torch.cuda.synchronize()
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    ms, launches = h.profile_read()
+    h.profile(False)
+    steps_done = h.total_steps() - steps0
+    St = h.get(abi.FIELD_STATS)
+    trials = float(np.mean(St[:, abi.STAT_LS_TRIALS][St[:, abi.STAT_LS_TRIALS] > 0])) if np.any(
+        St[:, abi.STAT_LS_TRIALS] > 0) else 1.0
+
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([float(steps_done), elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tot = t.clone()
+        dist.all_reduce(tot[0:1])
+        mx = t.clone()
+        dist.all_reduce(mx[1:2], op=dist.ReduceOp.MAX)
+        steps_all, elapsed = float(tot[0].item()), float(mx[1].item())
+    else:
+        steps_all = float(steps_done)
+
+    value = steps_all / elapsed
+    # roofline for the dominant kernel (largest total device time over the timed region)
+    kb = kernel_bytes(n, m, N, 8, 13, trials)
+    names = ["jacobian", "backward", "forward"]
+    dom = int(np.argmax(ms))
+    avg_ms = ms[dom] / max(1, launches[dom])
+    # algorithmic bytes per launch = per-trajectory bytes x trajectories processed per launch
+    per_launch_traj = steps_done / max(1, launches[dom])
+    alg_bytes = kb[names[dom]] * per_launch_traj
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": names[dom],
+                "kernel_ms": {nm_: round(float(ms[i] / max(1, launches[i])), 4) for i, nm_ in enumerate(names)}}
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            orc = __graft_entry__.load_oracle()
+            cpu = cpu_baseline(pkg, orc, seconds=args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "iLQR iterations/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded random starts: x0[1:3]+N(0,1), U0 = hover + 0.1 N(0,1))",
+            "config": {"workload": "quadrotor point-to-point, AL-iLQR, u in [0,15] + goal, sqrt backward pass "
+                                   "(BASELINE.json configs[2])", "n": n, "m": m, "N": N,
+                       "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"batch-shard x{world}",
+                       "mean_line_search_trials": round(trials, 3)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -279,6 +279,18 @@ int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps);
 /* per-trajectory tog_traj_flag bits; flags_out: (B) int32 */
 int32_t tog_status(tog_handle* h, int32_t* flags_out);
 
+/* per-kernel timing with HIP events recorded on the handle's stream around every launch issued by
+   tog_solve_step (used by bench.py for the live roofline). */
+enum tog_kernel_id {
+  TOG_KERNEL_JACOBIAN = 0,
+  TOG_KERNEL_BACKWARD = 1,
+  TOG_KERNEL_FORWARD = 2,
+  TOG_NKERNELS = 3
+};
+int32_t tog_profile(tog_handle* h, int32_t enable);
+/* blocking: total milliseconds and launch counts per tog_kernel_id since tog_profile(h, 1) */
+int32_t tog_profile_read(tog_handle* h, double* total_ms, int64_t* launches);
+
 /* human readable message for the last error on this thread */
 const char* tog_last_error(void);
 

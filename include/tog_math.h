@@ -1,0 +1,80 @@
+/*
+ * tog_math.h — deterministic transcendental primitives shared by host and device code.
+ *
+ * The hot path's arithmetic contract: every kernel and the CPU oracle evaluate the
+ * same IEEE-754 fp64 operation sequence — no compiler contraction (-ffp-contract=off), explicit
+ * fma() exactly where both sides write it, correctly rounded division and sqrt — so GPU results are
+ * bit-identical to the CPU restatement. libm's sin/cos (glibc) and the GPU's OCML sin/cos may differ
+ * in the last ulp, so the models that need them (cartpole, car, pendulum) use this one
+ * implementation on both sides: fdlibm's __kernel_sin/__kernel_cos polynomials on [-pi/4, pi/4]
+ * after a two-constant Cody-Waite reduction by pi/2 (accurate to ~1 ulp for |x| < 2^19).
+ */
+#ifndef TOG_MATH_H
+#define TOG_MATH_H
+
+#include <math.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define TOG_HD __host__ __device__ inline
+#else
+#define TOG_HD static inline
+#endif
+
+TOG_HD double tog__ksin(double x) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double z = x * x;
+  const double v = z * x;
+  const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  return x + v * (S1 + z * r);
+}
+
+TOG_HD double tog__kcos(double x) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double z = x * x;
+  const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + z * r);
+}
+
+/* reduce x to r in [-pi/4, pi/4], returns the quadrant */
+TOG_HD int tog__rem_pio2(double x, double* r) {
+  const double invpio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00;  /* first 33 bits of pi/2 */
+  const double pio2_1t = 6.07710050650619224932e-11; /* pi/2 - pio2_1 */
+  const double fn = rint(x * invpio2);
+  *r = (x - fn * pio2_1) - fn * pio2_1t;
+  return (int)((long long)fn & 3);
+}
+
+TOG_HD double tog_sin(double x) {
+  if (!isfinite(x)) return x - x; /* NaN */
+  if (fabs(x) < 7.85398163397448278999e-01) return tog__ksin(x);
+  double r;
+  const int q = tog__rem_pio2(x, &r);
+  switch (q) {
+    case 0: return tog__ksin(r);
+    case 1: return tog__kcos(r);
+    case 2: return -tog__ksin(r);
+    default: return -tog__kcos(r);
+  }
+}
+
+TOG_HD double tog_cos(double x) {
+  if (!isfinite(x)) return x - x;
+  if (fabs(x) < 7.85398163397448278999e-01) return tog__kcos(x);
+  double r;
+  const int q = tog__rem_pio2(x, &r);
+  switch (q) {
+    case 0: return tog__kcos(r);
+    case 1: return -tog__ksin(r);
+    case 2: return -tog__kcos(r);
+    default: return tog__ksin(r);
+  }
+}
+
+#endif /* TOG_MATH_H */

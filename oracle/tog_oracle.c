@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include "../include/tog.h"
+#include "../include/tog_math.h"
 
 #define DMAX 24 /* max partials: n+m+1 */
 #define OC_EXPORT __attribute__((visibility("default")))
@@ -70,7 +71,7 @@ static inline dual dneg(dual a) {
 static inline dual dmul(dual a, dual b) {
   dual r;
   r.v = a.v * b.v;
-  for (int i = 0; i < g_nd; i++) r.p[i] = b.v * a.p[i] + a.v * b.p[i];
+  for (int i = 0; i < g_nd; i++) r.p[i] = fma(b.v, a.p[i], a.v * b.p[i]);
   return r;
 }
 static inline dual dscale(dual a, double s) { /* Real * Dual */
@@ -90,7 +91,7 @@ static inline dual ddiv(dual a, dual b) {
   dual r;
   double iy = 1.0 / b.v, c2 = -(a.v / (b.v * b.v));
   r.v = a.v / b.v;
-  for (int i = 0; i < g_nd; i++) r.p[i] = a.p[i] * iy + b.p[i] * c2;
+  for (int i = 0; i < g_nd; i++) r.p[i] = fma(a.p[i], iy, b.p[i] * c2);
   return r;
 }
 static inline dual dinv(dual a) { /* inv(x): 1/v, -p/v^2 */
@@ -102,15 +103,15 @@ static inline dual dinv(dual a) { /* inv(x): 1/v, -p/v^2 */
 }
 static inline dual dsin(dual a) {
   dual r;
-  r.v = sin(a.v);
-  double c = cos(a.v);
+  r.v = tog_sin(a.v);
+  double c = tog_cos(a.v);
   for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
   return r;
 }
 static inline dual dcos(dual a) {
   dual r;
-  r.v = cos(a.v);
-  double c = -sin(a.v);
+  r.v = tog_cos(a.v);
+  double c = -tog_sin(a.v);
   for (int i = 0; i < g_nd; i++) r.p[i] = c * a.p[i];
   return r;
 }
@@ -380,7 +381,7 @@ static void matTmul(double* C, const double* A, int k, int r, const double* B, i
   for (int j = 0; j < c; j++)
     for (int i = 0; i < r; i++) {
       double s = 0.0;
-      for (int l = 0; l < k; l++) s += A[IDX(l, i, k)] * B[IDX(l, j, k)];
+      for (int l = 0; l < k; l++) s = fma(A[IDX(l, i, k)], B[IDX(l, j, k)], s);
       C[IDX(i, j, r)] = s;
     }
 }
@@ -389,7 +390,7 @@ static void matmul(double* C, const double* A, int r, int k, const double* B, in
   for (int j = 0; j < c; j++)
     for (int i = 0; i < r; i++) {
       double s = 0.0;
-      for (int l = 0; l < k; l++) s += A[IDX(i, l, r)] * B[IDX(l, j, k)];
+      for (int l = 0; l < k; l++) s = fma(A[IDX(i, l, r)], B[IDX(l, j, k)], s);
       C[IDX(i, j, r)] = s;
     }
 }
@@ -409,24 +410,11 @@ static void qr_R(double* R, double* P, int rows, int cols) {
   int kmax = rows < cols ? rows : cols;
   for (int j = 0; j < kmax; j++) {
     double alpha = P[IDX(j, j, rows)];
-    double xnorm = 0.0;
-    {
-      /* dnrm2 with scaling */
-      double scale = 0.0, ssq = 1.0;
-      for (int i = j + 1; i < rows; i++) {
-        double a = P[IDX(i, j, rows)];
-        if (a != 0.0) {
-          double absxi = fabs(a);
-          if (scale < absxi) {
-            ssq = 1.0 + ssq * (scale / absxi) * (scale / absxi);
-            scale = absxi;
-          } else {
-            ssq += (absxi / scale) * (absxi / scale);
-          }
-        }
-      }
-      xnorm = scale * sqrt(ssq);
-    }
+    /* ‖P[j+1:rows, j]‖ as a plain fma sum of squares (LAPACK's dnrm2 rescales to avoid overflow;
+       identical up to rounding for these magnitudes; DESIGN.md §3 arithmetic contract) */
+    double ss = 0.0;
+    for (int i = j + 1; i < rows; i++) ss = fma(P[IDX(i, j, rows)], P[IDX(i, j, rows)], ss);
+    double xnorm = sqrt(ss);
     if (xnorm == 0.0) continue; /* tau = 0, H = I */
     double beta = -copysign(lapy2(alpha, xnorm), alpha);
     double tau = (beta - alpha) / beta;
@@ -436,10 +424,10 @@ static void qr_R(double* R, double* P, int rows, int cols) {
     /* apply H = I - tau v v' to P[j:rows, j+1:cols], v = [1; P[j+1:rows, j]] */
     for (int c = j + 1; c < cols; c++) {
       double w = P[IDX(j, c, rows)];
-      for (int i = j + 1; i < rows; i++) w += P[IDX(i, j, rows)] * P[IDX(i, c, rows)];
+      for (int i = j + 1; i < rows; i++) w = fma(P[IDX(i, j, rows)], P[IDX(i, c, rows)], w);
       w *= tau;
       P[IDX(j, c, rows)] -= w;
-      for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] -= P[IDX(i, j, rows)] * w;
+      for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] = fma(-P[IDX(i, j, rows)], w, P[IDX(i, c, rows)]);
     }
   }
   for (int j = 0; j < cols; j++)
@@ -502,7 +490,7 @@ static void solve_upper(const double* A, int n, double* B, int nrhs) {
     for (int j = n - 1; j >= 0; j--) {
       double xj = B[IDX(j, c, n)] / A[IDX(j, j, n)];
       B[IDX(j, c, n)] = xj;
-      for (int i = j - 1; i >= 0; i--) B[IDX(i, c, n)] -= A[IDX(i, j, n)] * xj;
+      for (int i = j - 1; i >= 0; i--) B[IDX(i, c, n)] = fma(-A[IDX(i, j, n)], xj, B[IDX(i, c, n)]);
     }
 }
 static void solve_lower(const double* A, int n, double* B, int nrhs) {
@@ -510,7 +498,7 @@ static void solve_lower(const double* A, int n, double* B, int nrhs) {
     for (int j = 0; j < n; j++) {
       double xj = B[IDX(j, c, n)] / A[IDX(j, j, n)];
       B[IDX(j, c, n)] = xj;
-      for (int i = j + 1; i < n; i++) B[IDX(i, c, n)] -= A[IDX(i, j, n)] * xj;
+      for (int i = j + 1; i < n; i++) B[IDX(i, c, n)] = fma(-A[IDX(i, j, n)], xj, B[IDX(i, c, n)]);
     }
 }
 static void lu_solve(const double* Ain, int n, double* B, int nrhs) {
@@ -546,7 +534,7 @@ static void lu_solve(const double* Ain, int n, double* B, int nrhs) {
       for (int i = k + 1; i < n; i++) A[IDX(i, k, n)] *= r;
     }
     for (int j = k + 1; j < n; j++)
-      for (int i = k + 1; i < n; i++) A[IDX(i, j, n)] -= A[IDX(i, k, n)] * A[IDX(k, j, n)];
+      for (int i = k + 1; i < n; i++) A[IDX(i, j, n)] = fma(-A[IDX(i, k, n)], A[IDX(k, j, n)], A[IDX(i, j, n)]);
   }
   for (int c = 0; c < nrhs; c++) {
     double* b = B + (size_t)c * n;
@@ -557,10 +545,10 @@ static void lu_solve(const double* Ain, int n, double* B, int nrhs) {
         b[piv[k]] = t;
       }
     for (int j = 0; j < n; j++)
-      for (int i = j + 1; i < n; i++) b[i] -= A[IDX(i, j, n)] * b[j];
+      for (int i = j + 1; i < n; i++) b[i] = fma(-A[IDX(i, j, n)], b[j], b[i]);
     for (int j = n - 1; j >= 0; j--) {
       b[j] /= A[IDX(j, j, n)];
-      for (int i = 0; i < j; i++) b[i] -= A[IDX(i, j, n)] * b[j];
+      for (int i = 0; i < j; i++) b[i] = fma(-A[IDX(i, j, n)], b[j], b[i]);
     }
   }
   free(A);
@@ -970,20 +958,20 @@ static double stage_cost(const oc_solver* s, const double* x, const double* u, d
   double xQx = 0, uRu = 0, qx = 0, ru = 0, uHx = 0;
   for (int j = 0; j < n; j++) {
     double t = 0;
-    for (int i = 0; i < n; i++) t += (0.5 * x[i]) * s->Q[IDX(i, j, n)];
-    xQx += t * x[j];
+    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], s->Q[IDX(i, j, n)], t);
+    xQx = fma(t, x[j], xQx);
   }
   for (int j = 0; j < m; j++) {
     double t = 0;
-    for (int i = 0; i < m; i++) t += (0.5 * u[i]) * s->R[IDX(i, j, m)];
-    uRu += t * u[j];
+    for (int i = 0; i < m; i++) t = fma(0.5 * u[i], s->R[IDX(i, j, m)], t);
+    uRu = fma(t, u[j], uRu);
   }
-  for (int i = 0; i < n; i++) qx += s->q[i] * x[i];
-  for (int i = 0; i < m; i++) ru += s->r[i] * u[i];
+  for (int i = 0; i < n; i++) qx = fma(s->q[i], x[i], qx);
+  for (int i = 0; i < m; i++) ru = fma(s->r[i], u[i], ru);
   for (int j = 0; j < n; j++) {
     double t = 0;
-    for (int i = 0; i < m; i++) t += u[i] * s->H[IDX(i, j, m)];
-    uHx += t * x[j];
+    for (int i = 0; i < m; i++) t = fma(u[i], s->H[IDX(i, j, m)], t);
+    uHx = fma(t, x[j], uHx);
   }
   return ((((xQx + uRu) + qx) + ru) + s->c + uHx) * dt;
 }
@@ -992,10 +980,10 @@ static double terminal_cost(const oc_solver* s, const double* x) {
   double xQx = 0, qx = 0;
   for (int j = 0; j < n; j++) {
     double t = 0;
-    for (int i = 0; i < n; i++) t += (0.5 * x[i]) * s->Qf[IDX(i, j, n)];
-    xQx += t * x[j];
+    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], s->Qf[IDX(i, j, n)], t);
+    xQx = fma(t, x[j], xQx);
   }
-  for (int i = 0; i < n; i++) qx += s->qf[i] * x[i];
+  for (int i = 0; i < n; i++) qx = fma(s->qf[i], x[i], qx);
   return (xQx + qx) + s->cf;
 }
 
@@ -1036,12 +1024,12 @@ static double al_cost(oc_solver* s, const double* X, const double* U) {
     double lc = 0.0, cIc = 0.0;
     for (int i = 0; i < s->p[k]; i++) {
       size_t j = (size_t)k * P + i;
-      lc += s->lam[j] * s->C[j];
+      lc = fma(s->lam[j], s->C[j], lc);
     }
     for (int i = 0; i < s->p[k]; i++) {
       size_t j = (size_t)k * P + i;
       double w = s->active[j] ? s->mu[j] : 0.0;
-      cIc += (s->C[j] * w) * s->C[j];
+      cIc = fma(s->C[j] * w, s->C[j], cIc);
     }
     Jc += lc + 0.5 * cIc;
   }
@@ -1085,7 +1073,7 @@ OC_EXPORT int oc_rollout(oc_solver* s, double alpha) {
     /* Ū = U + K*δx + alpha*d */
     for (int i = 0; i < m; i++) {
       double t = 0.0;
-      for (int j = 0; j < n; j++) t += Kk[IDX(i, j, m)] * dx[j];
+      for (int j = 0; j < n; j++) t = fma(Kk[IDX(i, j, m)], dx[j], t);
       ub[i] = (s->U[(size_t)(k - 1) * m + i] + t) + alpha * dk[i];
     }
     oc_discrete_f(s->model, s->integ, s->Xb + (size_t)k * n, xb, ub, s->dt);
@@ -1129,14 +1117,14 @@ static void expansion_stage(oc_solver* s, int k) {
   /* Q.x .= cost.Q*x + cost.q + cost.H'*u ; Q.u .= cost.R*u + cost.r + cost.H*x ; then Q*dt */
   for (int i = 0; i < n; i++) {
     double a = 0, b = 0;
-    for (int j = 0; j < n; j++) a += s->Q[IDX(i, j, n)] * x[j];
-    for (int j = 0; j < m; j++) b += s->H[IDX(j, i, m)] * u[j];
+    for (int j = 0; j < n; j++) a = fma(s->Q[IDX(i, j, n)], x[j], a);
+    for (int j = 0; j < m; j++) b = fma(s->H[IDX(j, i, m)], u[j], b);
     Qx[i] = ((a + s->q[i]) + b) * dt;
   }
   for (int i = 0; i < m; i++) {
     double a = 0, b = 0;
-    for (int j = 0; j < m; j++) a += s->R[IDX(i, j, m)] * u[j];
-    for (int j = 0; j < n; j++) b += s->H[IDX(i, j, m)] * x[j];
+    for (int j = 0; j < m; j++) a = fma(s->R[IDX(i, j, m)], u[j], a);
+    for (int j = 0; j < n; j++) b = fma(s->H[IDX(i, j, m)], x[j], b);
     Qu[i] = ((a + s->r[i]) + b) * dt;
   }
   for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = s->Q[i] * dt;
@@ -1149,7 +1137,7 @@ static void expansion_terminal(oc_solver* s) {
   for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = s->Qf[i];
   for (int i = 0; i < n; i++) {
     double a = 0;
-    for (int j = 0; j < n; j++) a += s->Qf[IDX(i, j, n)] * x[j];
+    for (int j = 0; j < n; j++) a = fma(s->Qf[IDX(i, j, n)], x[j], a);
     s->Qx[(size_t)k * n + i] = a + s->qf[i];
   }
 }
@@ -1200,7 +1188,7 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
       for (int j = 0; j < n; j++)
         for (int i = 0; i < n; i++) {
           double t = 0;
-          for (int r = 0; r < p; r++) t += (cx[r + p * i] * w[r]) * cx[r + p * j];
+          for (int r = 0; r < p; r++) t = fma(cx[r + p * i] * w[r], cx[r + p * j], t);
           Qxx[IDX(i, j, n)] += t;
         }
       if (!term) {
@@ -1209,13 +1197,13 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
         for (int j = 0; j < m; j++)
           for (int i = 0; i < m; i++) {
             double t = 0;
-            for (int r = 0; r < p; r++) t += (cu[r + p * i] * w[r]) * cu[r + p * j];
+            for (int r = 0; r < p; r++) t = fma(cu[r + p * i] * w[r], cu[r + p * j], t);
             Quu[IDX(i, j, m)] += t;
           }
         for (int j = 0; j < n; j++)
           for (int i = 0; i < m; i++) {
             double t = 0;
-            for (int r = 0; r < p; r++) t += (cu[r + p * i] * w[r]) * cx[r + p * j];
+            for (int r = 0; r < p; r++) t = fma(cu[r + p * i] * w[r], cx[r + p * j], t);
             Qux[IDX(i, j, m)] += t;
           }
       }
@@ -1237,14 +1225,14 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
     /* Q.x .+= cx'g ; Q.u .+= cu'g */
     for (int i = 0; i < n; i++) {
       double t = 0;
-      for (int r = 0; r < p; r++) t += cx[r + p * i] * g[r];
+      for (int r = 0; r < p; r++) t = fma(cx[r + p * i], g[r], t);
       Qx[i] += t;
     }
     if (!term) {
       double* Qu = s->Qu + (size_t)k * m;
       for (int i = 0; i < m; i++) {
         double t = 0;
-        for (int r = 0; r < p; r++) t += cu[r + p * i] * g[r];
+        for (int r = 0; r < p; r++) t = fma(cu[r + p * i], g[r], t);
         Qu[i] += t;
       }
     }
@@ -1365,11 +1353,11 @@ static void backward_std(oc_solver* s) {
     /* ΔV[1] += d'*Q.u ; ΔV[2] += 0.5*d'*Q.uu*d */
     {
       double a = 0.0, b = 0.0;
-      for (int i = 0; i < m; i++) a += dk[i] * Qu[i];
+      for (int i = 0; i < m; i++) a = fma(dk[i], Qu[i], a);
       for (int j = 0; j < m; j++) {
         double t = 0.0;
-        for (int i = 0; i < m; i++) t += (0.5 * dk[i]) * Quu[IDX(i, j, m)];
-        b += t * dk[j];
+        for (int i = 0; i < m; i++) t = fma(0.5 * dk[i], Quu[IDX(i, j, m)], t);
+        b = fma(t, dk[j], b);
       }
       s->dV[0] += a;
       s->dV[1] += b;
@@ -1456,7 +1444,7 @@ static void backward_sqrt(oc_solver* s) {
       for (int j = 0; j < m; j++) /* K'*Quu' : n x m, (K'Quu')[i,j] = Σ_l K[l,i] Quu[j,l] */
         for (int i = 0; i < n; i++) {
           double acc = 0;
-          for (int l = 0; l < m; l++) acc += Kk[IDX(l, i, m)] * Quu[IDX(j, l, m)];
+          for (int l = 0; l < m; l++) acc = fma(Kk[IDX(l, i, m)], Quu[IDX(j, l, m)], acc);
           KtUt[IDX(i, j, n)] = acc;
         }
       matmul(Ud, Quu, m, m, dk, 1);
@@ -1493,9 +1481,9 @@ static void backward_sqrt(oc_solver* s) {
     /* ΔV */
     {
       double a = 0.0, Ud[8], b = 0.0;
-      for (int i = 0; i < m; i++) a += dk[i] * Qu[i];
+      for (int i = 0; i < m; i++) a = fma(dk[i], Qu[i], a);
       matmul(Ud, Quu, m, m, dk, 1);
-      for (int i = 0; i < m; i++) b += Ud[i] * Ud[i];
+      for (int i = 0; i < m; i++) b = fma(Ud[i], Ud[i], b);
       s->dV[0] += a;
       s->dV[1] += 0.5 * b;
     }
@@ -1570,7 +1558,7 @@ static double calc_gradient(oc_solver* s) {
     double g = 0.0;
     for (int k = 0; k < N - 1; k++) {
       double t = 0;
-      for (int i = 0; i < m; i++) t += s->d[(size_t)k * m + i] * s->d[(size_t)k * m + i];
+      for (int i = 0; i < m; i++) t = fma(s->d[(size_t)k * m + i], s->d[(size_t)k * m + i], t);
       t = sqrt(t);
       if (t > g) g = t;
     }

@@ -215,12 +215,15 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_total_steps.argtypes = [vp, C.POINTER(C.c_int64)]
     lib.tog_solve.argtypes = [vp, C.c_int32, C.c_int32]
     lib.tog_status.argtypes = [vp, _ip]
+    lib.tog_profile.argtypes = [vp, C.c_int32]
+    lib.tog_profile_read.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     lib.tog_last_error.restype = C.c_char_p
     for name in ("tog_create", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
-                 "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status"):
+                 "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
+                 "tog_profile_read"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -234,8 +237,11 @@ EXPORTED_SYMBOLS = (
     "tog_synchronize", "tog_set_state", "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims",
     "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
-    "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_last_error",
+    "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
+    "tog_last_error",
 )
+KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
+NKERNELS = 3
 
 
 def check(lib, rc):

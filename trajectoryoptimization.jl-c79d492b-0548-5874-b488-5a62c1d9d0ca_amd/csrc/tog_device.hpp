@@ -1,0 +1,555 @@
+// tog_device.hpp — device-side data model and numerics shared by every HIP kernel.
+//
+// Reference: TrajectoryOptimization.jl (file:line citations are relative to /root/reference).
+// Everything here is fp64. Models are written once, templated on the scalar type, so the same
+// code evaluates the primal discrete dynamics (rollouts) and the ForwardDiff-equivalent dual
+// number Jacobians (src/model.jl:491-522).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/tog.h"
+#include "../../include/tog_math.h"
+
+namespace tog {
+
+constexpr int NMAX = 16;  // max states (Kuka n=14 is "next")
+constexpr int MMAX = 8;   // max controls
+
+// ---------------------------------------------------------------------------------------------
+// Constraint rows. A ConstraintSet (src/constraint_sets.jl) is flattened on the host into rows in
+// the order of the reference's constraint vector C[k] (labels in insertion order; BoundConstraint
+// parts [x_max; u_max; x_min; u_min] with infinite bounds trimmed, src/constraints.jl:155-188).
+enum RowType : int {
+  ROW_XMAX = 0,  // c = x[i] - a            (inequality)
+  ROW_UMAX = 1,  // c = u[i] - a
+  ROW_XMIN = 2,  // c = a - x[i]
+  ROW_UMIN = 3,  // c = a - u[i]
+  ROW_GOAL = 4,  // c = x[i] - a            (equality, goal_constraint src/constraints.jl:299-304)
+  ROW_CIRCLE = 5,  // c = -((x1-a)^2 + (x2-b)^2 - r^2)            src/utils.jl:140-144
+  ROW_SPHERE = 6   // c = -((x1-a)^2 + (x2-b)^2 + (x3-c)^2 - r^2)  src/utils.jl:150-156
+};
+
+struct ConRow {
+  int type;
+  int idx;
+  double a, b, c, r;
+};
+
+// Problem description resident in device memory (read through uniform scalar loads).
+struct DevProblem {
+  int n, m, N, pmax;
+  int model, integ, nrows, pad0;
+  long long B;
+  double dt;
+  double Q[NMAX * NMAX], R[MMAX * MMAX], H[MMAX * NMAX], q[NMAX], r[MMAX], c;
+  double Qf[NMAX * NMAX], qf[NMAX], cf;
+  // upper Cholesky factors for the square-root expansion (src/objective.jl:70-94):
+  // cholesky(Q*dt).U, cholesky(R*dt).U, cholesky(Qf).U — identical at every knot, factored once.
+  double cQ[NMAX * NMAX], cR[MMAX * MMAX], cQf[NMAX * NMAX];
+  int sqrt_ok;  // 0 if one of the Hessians is not PD (reference: error(...))
+  int pad1;
+  const int* knot_off;  // [N] first row of knot k
+  const int* knot_cnt;  // [N] rows at knot k (p_k)
+  const ConRow* rows;
+  tog_options o;
+};
+
+// Per-trajectory solver state (the scalar fields of iLQRSolver/AugmentedLagrangianSolver and
+// their stats dicts, ilqr_solver.jl:93-154, augmented_lagrangian_solver.jl:101-140).
+struct TrajState {
+  double rho, drho;          // ρ, dρ
+  double J;                  // J_prev of the inner loop (cost of the current X, U)
+  double dJ, grad, alpha, z, expected;
+  double dV0, dV1;           // ΔV of the last backward pass
+  double c_max, mu_max;
+  double cost_tol, grad_tol; // current inner tolerances (set_tolerances!, :39-50)
+  int iters, zero_cnt, al_iter, total_steps, ls_trials, bp_restarts, flags, active;
+};
+
+struct DevBuffers {
+  double* x0;   // (n, B)
+  double* X;    // (n, N, B)
+  double* U;    // (m, N-1, B)
+  double* Xb;   // X̄
+  double* Ub;   // Ū
+  double* AB;   // (n, n+m, N-1, B)  [A | B] per knot, column-major
+  double* K;    // (m, n, N-1, B)
+  double* d;    // (m, N-1, B)
+  double* lam;  // (pmax, N, B)
+  double* mu;   // (pmax, N, B)
+  double* C;    // (pmax, N, B)
+  double* Sdbg; // (n, n, N, B) or null
+  double* sdbg; // (n, N, B) or null
+  double* Qscr; // (nq, N, B) accumulated Q blocks for the restart replay path
+  TrajState* st;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Scalar helpers (double and Dual share names)
+__host__ __device__ __forceinline__ double sin_(double x) { return tog_sin(x); }
+__host__ __device__ __forceinline__ double cos_(double x) { return tog_cos(x); }
+__host__ __device__ __forceinline__ double sqrt_(double x) { return sqrt(x); }
+__host__ __device__ __forceinline__ double inv_(double x) { return 1.0 / x; }
+__host__ __device__ __forceinline__ double val_(double x) { return x; }
+__host__ __device__ __forceinline__ double cst_(double x, double) { return x; }
+
+// ForwardDiff.Dual with W partials (Manifest.toml:164-168, ForwardDiff v0.10.3 dual.jl):
+//   x*y -> (xv*yv, yv*x.p + xv*y.p);  x/y -> (xv/yv, x.p*inv(yv) + y.p*(-(xv/(yv*yv))))
+template <int W>
+struct Dual {
+  double v;
+  double g[W];
+};
+
+template <int W>
+__host__ __device__ __forceinline__ double val_(const Dual<W>& a) { return a.v; }
+
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> dconst(double v) {
+  Dual<W> r;
+  r.v = v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = 0.0;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> cst_(double x, const Dual<W>&) { return dconst<W>(x); }
+
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator+(const Dual<W>& a, const Dual<W>& b) {
+  Dual<W> r;
+  r.v = a.v + b.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = a.g[i] + b.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator-(const Dual<W>& a, const Dual<W>& b) {
+  Dual<W> r;
+  r.v = a.v - b.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = a.g[i] - b.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator-(const Dual<W>& a) {
+  Dual<W> r;
+  r.v = -a.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = -a.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator*(const Dual<W>& a, const Dual<W>& b) {
+  Dual<W> r;
+  r.v = a.v * b.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = fma(b.v, a.g[i], a.v * b.g[i]);
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator*(double s, const Dual<W>& a) {
+  Dual<W> r;
+  r.v = s * a.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = s * a.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator*(const Dual<W>& a, double s) {
+  Dual<W> r;
+  r.v = a.v * s;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = a.g[i] * s;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator/(const Dual<W>& a, double s) {
+  Dual<W> r;
+  r.v = a.v / s;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = a.g[i] / s;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator+(const Dual<W>& a, double s) {
+  Dual<W> r = a;
+  r.v = a.v + s;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator+(double s, const Dual<W>& a) {
+  Dual<W> r = a;
+  r.v = s + a.v;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator-(const Dual<W>& a, double s) {
+  Dual<W> r = a;
+  r.v = a.v - s;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator/(const Dual<W>& a, const Dual<W>& b) {
+  Dual<W> r;
+  const double iy = 1.0 / b.v, c2 = -(a.v / (b.v * b.v));
+  r.v = a.v / b.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = fma(a.g[i], iy, b.g[i] * c2);
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> inv_(const Dual<W>& a) {
+  Dual<W> r;
+  r.v = 1.0 / a.v;
+  const double c = -(1.0 / (a.v * a.v));
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = c * a.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> sin_(const Dual<W>& a) {
+  Dual<W> r;
+  r.v = tog_sin(a.v);
+  const double c = tog_cos(a.v);
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = c * a.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> cos_(const Dual<W>& a) {
+  Dual<W> r;
+  r.v = tog_cos(a.v);
+  const double c = -tog_sin(a.v);
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = c * a.g[i];
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> sqrt_(const Dual<W>& a) {
+  Dual<W> r;
+  r.v = sqrt(a.v);
+  const double c = 1.0 / (2.0 * r.v);
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = c * a.g[i];
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Continuous dynamics  ẋ = f(x, u)  
+
+struct DoubleIntegrator {  // dynamics/double_integrator.jl:1-4
+  static constexpr int n = 2, m = 1, id = TOG_MODEL_DOUBLE_INTEGRATOR;
+  template <class T>
+  __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    xd[0] = x[1];
+    xd[1] = u[0];
+  }
+};
+
+struct Pendulum {  // dynamics/pendulum.jl:3-12
+  static constexpr int n = 2, m = 1, id = TOG_MODEL_PENDULUM;
+  template <class T>
+  __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    const double mm = 1.0, b = 0.1, lc = 0.5, I = 0.25, g = 9.81;
+    xd[0] = x[1];
+    xd[1] = ((u[0] - (mm * g * lc) * sin_(x[0])) - b * x[1]) / I;
+  }
+};
+
+struct Car {  // dynamics/car.jl:3-8
+  static constexpr int n = 3, m = 2, id = TOG_MODEL_CAR;
+  template <class T>
+  __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    xd[0] = u[0] * cos_(x[2]);
+    xd[1] = u[0] * sin_(x[2]);
+    xd[2] = u[1];
+  }
+};
+
+struct Cartpole {  // dynamics/cartpole.jl:9-36 ; qdd = -H \ (C*qd + G - B*u), generic 2x2 LU
+  static constexpr int n = 4, m = 1, id = TOG_MODEL_CARTPOLE;
+  template <class T>
+  __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    const double mc = 1.0, mp = 0.2, l = 0.5, g = 9.81;
+    T s, c;
+    if (isfinite(val_(x[1]))) {
+      s = sin_(x[1]);
+      c = cos_(x[1]);
+    } else {  // cartpole.jl:18-24
+      s = cst_(INFINITY, x[1]);
+      c = cst_(INFINITY, x[1]);
+    }
+    T a11 = cst_(mc + mp, x[0]);
+    T a12 = (mp * l) * c;
+    T a21 = a12;
+    T a22 = cst_(mp * (l * l), x[0]);
+    const T zero = cst_(0.0, x[0]);
+    T C12 = ((-mp) * x[3]) * l * s;
+    T b1 = ((zero * x[2] + C12 * x[3]) + zero) - u[0];
+    T b2 = ((zero * x[2] + zero * x[3]) + (mp * g * l) * s) - 0.0 * u[0];
+    if (fabs(val_(a21)) > fabs(val_(a11))) {  // partial pivoting
+      T t = a11; a11 = a21; a21 = t;
+      t = a12; a12 = a22; a22 = t;
+      t = b1; b1 = b2; b2 = t;
+    }
+    T l21 = a21 * inv_(a11);
+    T u22 = a22 - l21 * a12;
+    T y2 = b2 - l21 * b1;
+    T q2 = y2 / u22;
+    T q1 = (b1 - a12 * q2) / a11;
+    xd[0] = x[2];
+    xd[1] = x[3];
+    xd[2] = -q1;
+    xd[3] = -q2;
+  }
+};
+
+// Hamilton product a⊗b as dynamics/quaternions.jl:23-27 computes it (q2 = a, q1 = b).
+template <class T>
+__device__ __forceinline__ void qmul(T* r, const T* a, const T* b) {
+  const T& s1 = b[0];
+  const T& s2 = a[0];
+  const T dot = (b[1] * a[1] + b[2] * a[2]) + b[3] * a[3];
+  r[0] = s1 * s2 - dot;
+  const T cx = a[2] * b[3] - a[3] * b[2];
+  const T cy = a[3] * b[1] - a[1] * b[3];
+  const T cz = a[1] * b[2] - a[2] * b[1];
+  r[1] = (s1 * a[1] + s2 * b[1]) + cx;
+  r[2] = (s1 * a[2] + s2 * b[2]) + cy;
+  r[3] = (s1 * a[3] + s2 * b[3]) + cz;
+}
+
+struct Quadrotor {  // dynamics/quadrotor.jl:10-71, params :1-7
+  static constexpr int n = 13, m = 4, id = TOG_MODEL_QUADROTOR;
+  template <class T>
+  __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    const double mass = 0.5, L = 0.175, kf = 1.0, km = 0.0245;
+    const double J0 = 0.0023, J1 = 0.0023, J2 = 0.004;
+    const double Ji0 = 1.0 / 0.0023, Ji1 = 1.0 / 0.0023, Ji2 = 1.0 / 0.004;
+    // q = normalize(x[4:7]) = inv(norm(q))*q
+    const T nrm2 = ((x[3] * x[3] + x[4] * x[4]) + x[5] * x[5]) + x[6] * x[6];
+    const T inrm = inv_(sqrt_(nrm2));
+    T q[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) q[i] = inrm * x[3 + i];
+    const T F1 = kf * u[0], F2 = kf * u[1], F3 = kf * u[2], F4 = kf * u[3];
+    const T Fz = ((F1 + F2) + F3) + F4;
+    const T M1 = km * u[0], M2 = km * u[1], M3 = km * u[2], M4 = km * u[3];
+    const T tau0 = L * (F2 - F4);
+    const T tau1 = L * (F3 - F1);
+    const T tau2 = ((M1 - M2) + M3) - M4;
+    xd[0] = x[7];
+    xd[1] = x[8];
+    xd[2] = x[9];
+    // ẋ[4:7] = 0.5*q*Quaternion(0, ω)
+    {
+      T hq[4], w4[4], r[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) hq[i] = 0.5 * q[i];
+      w4[0] = cst_(0.0, x[0]);
+      w4[1] = x[10];
+      w4[2] = x[11];
+      w4[3] = x[12];
+      qmul(r, hq, w4);
+#pragma unroll
+      for (int i = 0; i < 4; i++) xd[3 + i] = r[i];
+    }
+    // ẋ[8:10] = g + (1/m)*vec(q*Quaternion(0,F)*inv(q))
+    {
+      T F4q[4], t1[4], qi[4], t2[4];
+      F4q[0] = cst_(0.0, x[0]);
+      F4q[1] = F4q[0];
+      F4q[2] = F4q[0];
+      F4q[3] = Fz;
+      qmul(t1, q, F4q);
+      qi[0] = q[0];
+      qi[1] = -q[1];
+      qi[2] = -q[2];
+      qi[3] = -q[3];
+      qmul(t2, t1, qi);
+      const double im = 1.0 / mass;
+      xd[7] = 0.0 + im * t2[1];
+      xd[8] = 0.0 + im * t2[2];
+      xd[9] = -9.81 + im * t2[3];
+    }
+    // ẋ[11:13] = Jinv*(τ - ω × (Jω))
+    {
+      const T Jw0 = J0 * x[10], Jw1 = J1 * x[11], Jw2 = J2 * x[12];
+      const T c0 = x[11] * Jw2 - x[12] * Jw1;
+      const T c1 = x[12] * Jw0 - x[10] * Jw2;
+      const T c2 = x[10] * Jw1 - x[11] * Jw0;
+      xd[10] = Ji0 * (tau0 - c0);
+      xd[11] = Ji1 * (tau1 - c1);
+      xd[12] = Ji2 * (tau2 - c2);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Explicit Runge-Kutta discretisation with runtime dt (src/integration.jl:115-158). Running-sum
+// form keeps the reference's left-to-right association: RK4 ((k1 + 2k2) + 2k3) + k4,
+// RK3 (k1 + 4k2) + k3, with RK3's third stage at (x - k1) + 2k2.
+template <class M, int INTEG, class T>
+__device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, double dt) {
+  constexpr int n = M::n;
+  T k[n], s[n], t[n];
+  M::f(k, x, u);
+#pragma unroll
+  for (int i = 0; i < n; i++) k[i] = k[i] * dt;
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    s[i] = k[i];
+    t[i] = x[i] + k[i] / 2.0;
+  }
+  M::f(k, t, u);
+#pragma unroll
+  for (int i = 0; i < n; i++) k[i] = k[i] * dt;
+  if constexpr (INTEG == TOG_RK4) {
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      s[i] = s[i] + 2.0 * k[i];
+      t[i] = x[i] + k[i] / 2.0;
+    }
+    M::f(k, t, u);
+#pragma unroll
+    for (int i = 0; i < n; i++) k[i] = k[i] * dt;
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      s[i] = s[i] + 2.0 * k[i];
+      t[i] = x[i] + k[i];
+    }
+    M::f(k, t, u);
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      k[i] = k[i] * dt;
+      s[i] = s[i] + k[i];
+      xn[i] = x[i] + s[i] / 6.0;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      t[i] = (x[i] - s[i]) + 2.0 * k[i];  // s == k1 here
+      s[i] = s[i] + 4.0 * k[i];
+    }
+    M::f(k, t, u);
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      k[i] = k[i] * dt;
+      s[i] = s[i] + k[i];
+      xn[i] = x[i] + s[i] / 6.0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Costs (src/cost.jl:171-181), same association as the oracle. The outer loops are kept rolled:
+// fully unrolled, the compiler hoists all of Q into registers across the knot loop and spills.
+template <int n, int m>
+__device__ __forceinline__ double stage_cost(const DevProblem* P, const double* x, const double* u) {
+  double xQx = 0.0, uRu = 0.0, qx = 0.0, ru = 0.0, uHx = 0.0;
+#pragma unroll 1
+  for (int j = 0; j < n; j++) {
+    double t = 0.0;
+    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Q[i + n * j], t);
+    xQx = fma(t, x[j], xQx);
+  }
+#pragma unroll 1
+  for (int j = 0; j < m; j++) {
+    double t = 0.0;
+    for (int i = 0; i < m; i++) t = fma(0.5 * u[i], P->R[i + m * j], t);
+    uRu = fma(t, u[j], uRu);
+  }
+#pragma unroll 1
+  for (int i = 0; i < n; i++) qx = fma(P->q[i], x[i], qx);
+#pragma unroll 1
+  for (int i = 0; i < m; i++) ru = fma(P->r[i], u[i], ru);
+#pragma unroll 1
+  for (int j = 0; j < n; j++) {
+    double t = 0.0;
+    for (int i = 0; i < m; i++) t = fma(u[i], P->H[i + m * j], t);
+    uHx = fma(t, x[j], uHx);
+  }
+  return ((((xQx + uRu) + qx) + ru) + P->c + uHx) * P->dt;
+}
+
+template <int n>
+__device__ __forceinline__ double terminal_cost(const DevProblem* P, const double* x) {
+  double xQx = 0.0, qx = 0.0;
+#pragma unroll 1
+  for (int j = 0; j < n; j++) {
+    double t = 0.0;
+    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Qf[i + n * j], t);
+    xQx = fma(t, x[j], xQx);
+  }
+#pragma unroll 1
+  for (int i = 0; i < n; i++) qx = fma(P->qf[i], x[i], qx);
+  return (xQx + qx) + P->cf;
+}
+
+// constraint row value (u == nullptr at the terminal knot: only x rows exist there)
+__device__ __forceinline__ double row_value(const ConRow& r, const double* x, const double* u) {
+  switch (r.type) {
+    case ROW_XMAX: return x[r.idx] - r.a;
+    case ROW_UMAX: return u[r.idx] - r.a;
+    case ROW_XMIN: return r.a - x[r.idx];
+    case ROW_UMIN: return r.a - u[r.idx];
+    case ROW_GOAL: return x[r.idx] - r.a;
+    case ROW_CIRCLE: {
+      const double dx = x[0] - r.a, dy = x[1] - r.b;
+      return -((dx * dx + dy * dy) - r.r * r.r);
+    }
+    default: {
+      const double dx = x[0] - r.a, dy = x[1] - r.b, dz = x[2] - r.c;
+      return -(((dx * dx + dy * dy) + dz * dz) - r.r * r.r);
+    }
+  }
+}
+__device__ __forceinline__ bool row_inequality(const ConRow& r) { return r.type != ROW_GOAL; }
+
+// d c / d [x; u] of a row: writes up to 3 (index, value) pairs, index in [0, n+m)
+__device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n, int* idx, double* v) {
+  switch (r.type) {
+    case ROW_XMAX: idx[0] = r.idx; v[0] = 1.0; return 1;
+    case ROW_UMAX: idx[0] = n + r.idx; v[0] = 1.0; return 1;
+    case ROW_XMIN: idx[0] = r.idx; v[0] = -1.0; return 1;
+    case ROW_UMIN: idx[0] = n + r.idx; v[0] = -1.0; return 1;
+    case ROW_GOAL: idx[0] = r.idx; v[0] = 1.0; return 1;
+    case ROW_CIRCLE:
+      idx[0] = 0; v[0] = -(2.0 * (x[0] - r.a));
+      idx[1] = 1; v[1] = -(2.0 * (x[1] - r.b));
+      return 2;
+    default:
+      idx[0] = 0; v[0] = -(2.0 * (x[0] - r.a));
+      idx[1] = 1; v[1] = -(2.0 * (x[1] - r.b));
+      idx[2] = 2; v[2] = -(2.0 * (x[2] - r.c));
+      return 3;
+  }
+}
+
+// regularization_update! (ilqr_methods.jl:164-176)
+__device__ __forceinline__ void reg_increase(const DevProblem* P, TrajState& s) {
+  const double f = P->o.bp_reg_increase_factor;
+  s.drho = fmax(s.drho * f, f);
+  s.rho = fmax(s.rho * s.drho, P->o.bp_reg_min);
+  if (s.rho > P->o.bp_reg_max) s.flags |= TOG_TRAJ_MAX_REG;
+}
+__device__ __forceinline__ void reg_decrease(const DevProblem* P, TrajState& s) {
+  const double f = P->o.bp_reg_increase_factor;
+  s.drho = fmin(s.drho / f, 1.0 / f);
+  const double rd = s.rho * s.drho;
+  s.rho = rd * (double)(rd > P->o.bp_reg_min);
+}
+
+__device__ __forceinline__ double lapy2(double x, double y) {  // LAPACK dlapy2
+  const double xa = fabs(x), ya = fabs(y);
+  const double w = fmax(xa, ya), z = fmin(xa, ya);
+  if (z == 0.0) return w;
+  const double t = z / w;
+  return w * sqrt(1.0 + t * t);
+}
+
+}  // namespace tog

@@ -1,0 +1,1360 @@
+// tog_kernels.hpp — HIP kernels of the batched iLQR / AL-iLQR hot path (gfx950, wave64, fp64).
+//
+// Kernel map (SURVEY.md §2 "kernel set the build must create"):
+//   k_init          solve!/reset! + initial rollout + initial (AL) cost      ilqr_methods.jl:3-20, augmented_lagrangian_methods.jl:2-16
+//   k_rollout_open  rollout!(prob)                                           src/rollout.jl:25-38
+//   k_jacobian      jacobian!(prob, solver): ForwardDiff duals through RK3/4 src/model.jl:301-306, 491-522
+//   k_backward      cost_expansion! + backwardpass! (std / sqrt)             ilqr_methods.jl:55-62, backward_pass.jl:1-192
+//   k_forward       forwardpass! line search + solve! bookkeeping + AL dual/penalty update
+//                                                                           forward_pass.jl:5-85, ilqr_methods.jl:21-45,
+//                                                                           augmented_lagrangian_methods.jl:53-126
+//   k_cost / k_rollout / k_update_constraints   step-level entry points
+//   k_batch_stats   batch reduction (n_active, ΣJ, max c_max) for stopping / the RCCL all-reduce
+//
+// Mapping: the Riccati recursion is strictly serial in the knot index, so parallelism comes from
+// the batch. k_backward runs one 64-lane wavefront per trajectory with the whole per-knot working
+// set (S, [A|B], Q blocks, QR workspaces) in LDS; k_jacobian runs one thread per
+// (trajectory, knot, partial-chunk); rollouts run one thread per trajectory.
+#pragma once
+
+#include "tog_device.hpp"
+
+namespace tog {
+
+constexpr int PCAP = 32;  // max constraint rows per knot handled by the LDS layout
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroups: s_barrier is ~free
+
+template <class M>
+__host__ __device__ constexpr int nq_of() {
+  return M::n + M::m + M::n * M::n + M::m * M::m + M::m * M::n;
+}
+
+// =============================================================================================
+// Thread-level trajectory helpers
+// =============================================================================================
+
+// AL/objective cost of (Xs, Us) for trajectory b (objective.jl:40-48, augmented_lagrangian_methods.jl:298-313).
+// Writes the constraint values C when Cout != nullptr (A.10: cost() updates C as a side effect).
+template <class M>
+__device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, const double* Xs,
+                            const double* Us, bool al, double* Cout) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  double J = 0.0, Jc = 0.0;
+  for (int k = 0; k < N - 1; k++) J += stage_cost<n, m>(P, Xs + (size_t)k * n, Us + (size_t)k * m);
+  J += terminal_cost<n>(P, Xs + (size_t)(N - 1) * n);
+  if (!al) return J;
+  const double* lam = Bf.lam + (size_t)b * N * pmax;
+  const double* mu = Bf.mu + (size_t)b * N * pmax;
+  for (int k = 0; k < N; k++) {
+    const int cnt = P->knot_cnt[k];
+    if (cnt == 0) continue;
+    const ConRow* rows = P->rows + P->knot_off[k];
+    const double* x = Xs + (size_t)k * n;
+    const double* u = (k < N - 1) ? Us + (size_t)k * m : nullptr;
+    double lc = 0.0, cIc = 0.0;
+    for (int i = 0; i < cnt; i++) {
+      const double c = row_value(rows[i], x, u);
+      const double l = lam[(size_t)k * pmax + i];
+      const bool a = row_inequality(rows[i]) ? ((c >= 0.0) || (l > 0.0)) : true;
+      const double w = a ? mu[(size_t)k * pmax + i] : 0.0;
+      lc = fma(l, c, lc);
+      cIc = fma(c * w, c, cIc);
+      if (Cout) Cout[(size_t)k * pmax + i] = c;
+    }
+    Jc += lc + 0.5 * cIc;
+  }
+  return J + Jc;
+}
+
+// rollout!(prob, solver, α) (src/rollout.jl:2-23): writes X̄, Ū; false on divergence / NaN.
+template <class M, int INTEG>
+__device__ bool traj_rollout(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  const double* K = Bf.K + (size_t)b * (N - 1) * m * n;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  double* Xb = Bf.Xb + (size_t)b * N * n;
+  double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
+  double xb[n], dx[n], ub[m], xn[n];
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    xb[i] = Bf.x0[(size_t)b * n + i];
+    Xb[i] = xb[i];
+  }
+  const double smax = P->o.max_state_value, umax = P->o.max_control_value;
+  for (int k = 1; k < N; k++) {
+    const double* x = X + (size_t)(k - 1) * n;
+#pragma unroll
+    for (int i = 0; i < n; i++) dx[i] = xb[i] - x[i];
+    const double* Kk = K + (size_t)(k - 1) * m * n;
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      double t = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; j++) t = fma(Kk[i + m * j], dx[j], t);
+      ub[i] = (U[(size_t)(k - 1) * m + i] + t) + alpha * d[(size_t)(k - 1) * m + i];
+      Ub[(size_t)(k - 1) * m + i] = ub[i];
+    }
+    discrete_step<M, INTEG>(xn, xb, ub, P->dt);
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      xb[i] = xn[i];
+      Xb[(size_t)k * n + i] = xn[i];
+      ok = ok && (fabs(xn[i]) < smax);
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) ok = ok && (fabs(ub[i]) < umax);
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// open-loop rollout!(X, model, U, dt) (src/rollout.jl:33-38) into X, if any X is non-finite.
+template <class M, int INTEG>
+__device__ void traj_rollout_open(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  bool finite = true;
+  for (int i = 0; i < n * N; i++) finite = finite && isfinite(X[i]);
+  if (finite) return;
+  double x[n], xn[n], u[m];
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    x[i] = Bf.x0[(size_t)b * n + i];
+    X[i] = x[i];
+  }
+  for (int k = 0; k < N - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < m; i++) u[i] = U[(size_t)k * m + i];
+    discrete_step<M, INTEG>(xn, x, u, P->dt);
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      x[i] = xn[i];
+      X[(size_t)(k + 1) * n + i] = xn[i];
+    }
+  }
+}
+
+// gradient_todorov (ilqr_methods.jl:122-129, A.3) / gradient_feedforward (:135-137)
+template <class M>
+__device__ double traj_gradient(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b) {
+  constexpr int m = M::m;
+  const int N = P->N;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  if (P->o.gradient_type == 1) {
+    double g = 0.0;
+    for (int k = 0; k < N - 1; k++) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < m; i++) t = fma(d[k * m + i], d[k * m + i], t);
+      g = fmax(g, sqrt(t));
+    }
+    return g;
+  }
+  double sum = 0.0;
+  for (int k = 0; k < N - 1; k++) {
+    double mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      const double v = fabs(d[k * m + i]) / (fabs(U[k * m + i]) + 1.0);
+      if (v > mx || isnan(v)) mx = v;
+    }
+    sum += mx;
+  }
+  return sum / N;
+}
+
+// max_violation(solver) (augmented_lagrangian_methods.jl:171-184) from the stored C
+__device__ inline double traj_max_violation(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b) {
+  const int N = P->N, pmax = P->pmax;
+  const double* C = Bf.C + (size_t)b * N * pmax;
+  double c_max = 0.0;
+  for (int k = 0; k < N; k++) {
+    const int cnt = P->knot_cnt[k];
+    if (cnt == 0) continue;
+    const ConRow* rows = P->rows + P->knot_off[k];
+    double e = 0.0, im = -INFINITY;
+    int ni = 0;
+    for (int i = 0; i < cnt; i++) {
+      const double c = C[(size_t)k * pmax + i];
+      if (row_inequality(rows[i])) {
+        ni++;
+        im = fmax(im, c);
+      } else {
+        e = fmax(e, fabs(c));
+      }
+    }
+    c_max = fmax(e, c_max);
+    if (ni > 0) c_max = fmax(fmax(0.0, im), c_max);
+  }
+  return c_max;
+}
+
+__device__ inline void set_tolerances(const DevProblem* __restrict__ P, TrajState& s, int mode) {
+  // set_tolerances! (augmented_lagrangian_methods.jl:39-50)
+  if (mode == TOG_MODE_AL) {
+    const bool last = (s.al_iter == P->o.al_iterations);
+    s.cost_tol = last ? P->o.al_cost_tolerance : P->o.al_cost_tolerance_intermediate;
+    s.grad_tol = last ? P->o.al_gradient_norm_tolerance : P->o.al_gradient_norm_tolerance_intermediate;
+  } else {
+    s.cost_tol = P->o.cost_tolerance;
+    s.grad_tol = P->o.gradient_norm_tolerance;
+  }
+}
+
+// =============================================================================================
+// k_init: reset! + (AL) multiplier init + rollout!(prob) + initial record_iteration!
+// =============================================================================================
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_init(const DevProblem* __restrict__ P, DevBuffers Bf, int mode) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  TrajState s = {};
+  s.active = 1;
+  s.J = INFINITY;
+  traj_rollout_open<M, INTEG>(P, Bf, b);
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  double* C = Bf.C + (size_t)b * N * pmax;
+  if (mode == TOG_MODE_AL) {
+    for (int i = 0; i < N * pmax; i++) {
+      Bf.lam[(size_t)b * N * pmax + i] = 0.0;
+      Bf.mu[(size_t)b * N * pmax + i] = P->o.penalty_initial;
+    }
+    (void)traj_cost<M>(P, Bf, b, X, U, true, C);
+    s.c_max = traj_max_violation(P, Bf, b);
+    s.mu_max = P->o.penalty_initial;
+    s.al_iter = 1;
+  }
+  set_tolerances(P, s, mode);
+  s.J = traj_cost<M>(P, Bf, b, X, U, mode == TOG_MODE_AL, mode == TOG_MODE_AL ? C : nullptr);
+  s.iters = 1;  // record_iteration!(…, J_prev, Inf)
+  s.dJ = INFINITY;
+  s.zero_cnt = 0;
+  s.grad = INFINITY;
+  Bf.st[b] = s;
+}
+
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_rollout_open(const DevProblem* __restrict__ P, DevBuffers Bf) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  traj_rollout_open<M, INTEG>(P, Bf, b);
+}
+
+template <class M>
+__global__ void __launch_bounds__(64) k_cost(const DevProblem* __restrict__ P, DevBuffers Bf, int al, int use_bar,
+                                             double* Jout) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  const double* X = (use_bar ? Bf.Xb : Bf.X) + (size_t)b * N * n;
+  const double* U = (use_bar ? Bf.Ub : Bf.U) + (size_t)b * (N - 1) * m;
+  Jout[b] = traj_cost<M>(P, Bf, b, X, U, al != 0, al ? Bf.C + (size_t)b * N * P->pmax : nullptr);
+}
+
+template <class M>
+__global__ void __launch_bounds__(64) k_update_constraints(const DevProblem* __restrict__ P, DevBuffers Bf) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  for (int k = 0; k < N; k++) {
+    const int cnt = P->knot_cnt[k];
+    const ConRow* rows = P->rows + P->knot_off[k];
+    for (int i = 0; i < cnt; i++)
+      Bf.C[((size_t)b * N + k) * pmax + i] = row_value(rows[i], X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
+  }
+}
+
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_rollout(const DevProblem* __restrict__ P, DevBuffers Bf, double alpha,
+                                                int* ok) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  ok[b] = traj_rollout<M, INTEG>(P, Bf, b, alpha) ? 1 : 0;
+}
+
+// =============================================================================================
+// k_jacobian: ∇F[k] = ∂f_d/∂[x;u] by forward-mode duals, one thread per (traj, knot, chunk)
+// src/model.jl:491-512 (ForwardDiff.jacobian! of fd_aug!); the dt column is never consumed by
+// iLQR (backward_pass.jl:30,110) and is not materialised.
+// =============================================================================================
+template <class M, int INTEG, int W>
+__global__ void __launch_bounds__(256) k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
+  constexpr int n = M::n, m = M::m, L = n + m, NCH = (L + W - 1) / W;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int N = P->N;
+  const int c = (int)(t % NCH);
+  const long long bk = t / NCH;
+  const int k = (int)(bk % (N - 1));
+  const long long b = bk / (N - 1);
+  if (!Bf.st[b].active) return;
+  const double* x = Bf.X + ((size_t)b * N + k) * n;
+  const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
+  Dual<W> xd[n], ud[m], xn[n];
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    xd[i].v = x[i];
+#pragma unroll
+    for (int w = 0; w < W; w++) xd[i].g[w] = (i == c * W + w) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < m; i++) {
+    ud[i].v = u[i];
+#pragma unroll
+    for (int w = 0; w < W; w++) ud[i].g[w] = (n + i == c * W + w) ? 1.0 : 0.0;
+  }
+  discrete_step<M, INTEG>(xn, xd, ud, P->dt);
+  double* out = Bf.AB + ((size_t)b * (N - 1) + k) * n * L;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int col = c * W + w;
+    if (col < L) {
+#pragma unroll
+      for (int i = 0; i < n; i++) out[i + n * col] = xn[i].g[w];
+    }
+  }
+}
+
+// =============================================================================================
+// Wave-level small dense linear algebra on LDS (column-major). All 64 lanes cooperate; sizes are
+// compile-time so every loop unrolls. Callers synchronise (wsync) between dependent steps.
+// =============================================================================================
+
+// C (R x Cc) [+]= op(A) * op(B);  op(A) is R x Kd, op(B) is Kd x Cc
+template <int R, int Kd, int Cc, bool TA, bool TB, bool ACC>
+__device__ __forceinline__ void wmm(double* C, const double* A, int lda, const double* B, int ldb) {
+  for (int e = threadIdx.x; e < R * Cc; e += WAVE) {
+    const int i = e % R, j = e / R;
+    double s = 0.0;
+#pragma unroll
+    for (int l = 0; l < Kd; l++) {
+      const double a = TA ? A[l + lda * i] : A[i + lda * l];
+      const double bb = TB ? B[j + ldb * l] : B[l + ldb * j];
+      s = fma(a, bb, s);
+    }
+    C[i + R * j] = ACC ? C[i + R * j] + s : s;
+  }
+}
+
+// Householder QR of the rows x cols matrix A (ld = rows) in place; R ends up in the upper
+// triangle of the top cols rows (LAPACK dgeqr2/dlarfg; Julia qr(P).R, backward_pass.jl:172-183).
+// wv: LDS scratch >= cols. All lanes participate.
+template <int COLS>
+__device__ void wqr(double* A, int rows, double* wv) {
+  const int lane = threadIdx.x;
+  const int kmax = rows < COLS ? rows : COLS;
+  for (int j = 0; j < kmax; j++) {
+    double ss = 0.0;
+    for (int i = j + 1; i < rows; i++) {
+      const double a = A[i + rows * j];
+      ss = fma(a, a, ss);
+    }
+    const double xnorm = sqrt(ss);
+    if (xnorm == 0.0) continue;  // tau = 0, H = I (uniform branch: every lane computed ss)
+    const double alpha = A[j + rows * j];
+    const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+    const double tau = (beta - alpha) / beta;
+    const double sc = 1.0 / (alpha - beta);
+    wsync();
+    for (int i = j + 1 + lane; i < rows; i += WAVE) A[i + rows * j] *= sc;
+    wsync();
+    if (lane > j && lane < COLS) {
+      const int c = lane;
+      double w = A[j + rows * c];
+      for (int i = j + 1; i < rows; i++) w = fma(A[i + rows * j], A[i + rows * c], w);
+      w *= tau;
+      A[j + rows * c] -= w;
+      wv[c] = w;
+    }
+    wsync();
+    const int nc = COLS - j - 1, nr = rows - j - 1;
+    for (int e = lane; e < nc * nr; e += WAVE) {
+      const int i = j + 1 + e % nr, c = j + 1 + e / nr;
+      A[i + rows * c] = fma(-A[i + rows * j], wv[c], A[i + rows * c]);
+    }
+    if (lane == 0) A[j + rows * j] = beta;
+    wsync();
+  }
+}
+
+// =============================================================================================
+// k_backward: cost expansion + Riccati backward pass, one wave per trajectory
+// =============================================================================================
+template <class M, bool SQRT>
+struct BwdLds {
+  static constexpr int n = M::n, m = M::m, L = n + m;
+  static constexpr int WR = n + (n > PCAP ? n : PCAP);  // QR workspace rows
+  double S[n * n];
+  double s[n];
+  double AB[n * L];
+  double Qxx[n * n];
+  double Quu[m * m];
+  double Qux[m * n];
+  double Qx[n];
+  double Qu[m];
+  double T1[n * L];
+  double Kt[m * n];
+  double dd[m];
+  double F[m * m];     // LU / Cholesky factor of Quu_reg, or its R factor (sqrt)
+  double KtQ[n * m];
+  double tmp1[n * m];
+  double tmp2[m * m];
+  double Wq[WR * n];   // QR workspace
+  double xk[n];
+  double uk[m];
+  double cval[PCAP], wv[PCAP], wsv[PCAP], gv[PCAP];
+  double cx[PCAP * n];
+  double cu[PCAP * m];
+  double red[WAVE];
+  int piv[m];
+  int flag;
+  int pad;
+};
+
+// stage / terminal expansion into the Q blocks (cost.jl:183-198, objective.jl:51-94, AL terms
+// augmented_lagrangian_methods.jl:186-276). u == nullptr marks the terminal knot.
+template <class M, bool SQRT, bool AL>
+__device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, int k,
+                           BwdLds<M, SQRT>& sh) {
+  constexpr int n = M::n, m = M::m;
+  const int lane = threadIdx.x;
+  const int N = P->N;
+  const bool term = (k == N - 1);
+  const double dt = P->dt;
+  if (!term) {
+    if (lane < n) {
+      const int i = lane;
+      double a = 0.0, bb = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], sh.xk[j], a);
+#pragma unroll
+      for (int j = 0; j < m; j++) bb = fma(P->H[j + m * i], sh.uk[j], bb);
+      sh.Qx[i] = ((a + P->q[i]) + bb) * dt;
+    } else if (lane < n + m) {
+      const int i = lane - n;
+      double a = 0.0, bb = 0.0;
+#pragma unroll
+      for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], sh.uk[j], a);
+#pragma unroll
+      for (int j = 0; j < n; j++) bb = fma(P->H[i + m * j], sh.xk[j], bb);
+      sh.Qu[i] = ((a + P->r[i]) + bb) * dt;
+    }
+    for (int e = lane; e < n * n; e += WAVE) sh.Qxx[e] = SQRT ? P->cQ[e] : P->Q[e] * dt;
+    for (int e = lane; e < m * m; e += WAVE) sh.Quu[e] = SQRT ? P->cR[e] : P->R[e] * dt;
+    for (int e = lane; e < m * n; e += WAVE) sh.Qux[e] = P->H[e] * dt;
+  } else {
+    for (int e = lane; e < n * n; e += WAVE) sh.Qxx[e] = SQRT ? P->cQf[e] : P->Qf[e];
+    if (lane < n) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; j++) a = fma(P->Qf[lane + n * j], sh.xk[j], a);
+      sh.Qx[lane] = a + P->qf[lane];
+    }
+  }
+  if (!AL) return;
+  const int p = P->knot_cnt[k];
+  if (p == 0) return;
+  const ConRow* rows = P->rows + P->knot_off[k];
+  const int pmax = P->pmax;
+  const double* lam = Bf.lam + ((size_t)b * N + k) * pmax;
+  const double* mu = Bf.mu + ((size_t)b * N + k) * pmax;
+  for (int e = lane; e < p * n; e += WAVE) sh.cx[e] = 0.0;
+  for (int e = lane; e < p * m; e += WAVE) sh.cu[e] = 0.0;
+  wsync();
+  if (lane < p) {
+    const int r = lane;
+    const double c = row_value(rows[r], sh.xk, term ? nullptr : sh.uk);
+    const double l = lam[r];
+    const bool a = row_inequality(rows[r]) ? ((c >= 0.0) || (l > 0.0)) : true;
+    const double w = a ? mu[r] : 0.0;
+    sh.cval[r] = c;
+    sh.wv[r] = w;
+    sh.wsv[r] = a ? sqrt(mu[r]) : 0.0;
+    sh.gv[r] = w * c + l;
+    int idx[3];
+    double v[3];
+    const int nz = row_grad(rows[r], sh.xk, n, idx, v);
+    for (int z = 0; z < nz; z++) {
+      if (idx[z] < n)
+        sh.cx[r + p * idx[z]] = v[z];
+      else
+        sh.cu[r + p * (idx[z] - n)] = v[z];
+    }
+  }
+  wsync();
+  if (!SQRT) {
+    // Q.xx .+= cx'Iμ*cx ; Q.uu .+= cu'Iμ*cu ; Q.ux .+= cu'Iμ*cx
+    for (int e = lane; e < n * n; e += WAVE) {
+      const int i = e % n, j = e / n;
+      double t = 0.0;
+      for (int r = 0; r < p; r++) t = fma(sh.cx[r + p * i] * sh.wv[r], sh.cx[r + p * j], t);
+      sh.Qxx[e] += t;
+    }
+    if (!term) {
+      for (int e = lane; e < m * m; e += WAVE) {
+        const int i = e % m, j = e / m;
+        double t = 0.0;
+        for (int r = 0; r < p; r++) t = fma(sh.cu[r + p * i] * sh.wv[r], sh.cu[r + p * j], t);
+        sh.Quu[e] += t;
+      }
+      for (int e = lane; e < m * n; e += WAVE) {
+        const int i = e % m, j = e / m;
+        double t = 0.0;
+        for (int r = 0; r < p; r++) t = fma(sh.cu[r + p * i] * sh.wv[r], sh.cx[r + p * j], t);
+        sh.Qux[e] += t;
+      }
+    }
+  } else {
+    // chol_plus!(Q.xx, Iμ_sqrt*cx) ; chol_plus!(Q.uu, Iμ_sqrt*cu)   (no ux term, A.5)
+    const int rows_x = n + p;
+    for (int e = lane; e < rows_x * n; e += WAVE) {
+      const int i = e % rows_x, j = e / rows_x;
+      sh.Wq[e] = (i < n) ? sh.Qxx[i + n * j] : sh.wsv[i - n] * sh.cx[(i - n) + p * j];
+    }
+    wsync();
+    wqr<n>(sh.Wq, rows_x, sh.red);
+    for (int e = lane; e < n * n; e += WAVE) {
+      const int i = e % n, j = e / n;
+      sh.Qxx[e] = (i <= j) ? sh.Wq[i + rows_x * j] : 0.0;
+    }
+    wsync();
+    if (!term) {
+      const int rows_u = m + p;
+      for (int e = lane; e < rows_u * m; e += WAVE) {
+        const int i = e % rows_u, j = e / rows_u;
+        sh.Wq[e] = (i < m) ? sh.Quu[i + m * j] : sh.wsv[i - m] * sh.cu[(i - m) + p * j];
+      }
+      wsync();
+      wqr<m>(sh.Wq, rows_u, sh.red);
+      for (int e = lane; e < m * m; e += WAVE) {
+        const int i = e % m, j = e / m;
+        sh.Quu[e] = (i <= j) ? sh.Wq[i + rows_u * j] : 0.0;
+      }
+    }
+  }
+  // Q.x .+= cx'g ; Q.u .+= cu'g
+  if (lane < n) {
+    double t = 0.0;
+    for (int r = 0; r < p; r++) t = fma(sh.cx[r + p * lane], sh.gv[r], t);
+    sh.Qx[lane] += t;
+  } else if (!term && lane < n + m) {
+    const int i = lane - n;
+    double t = 0.0;
+    for (int r = 0; r < p; r++) t = fma(sh.cu[r + p * i], sh.gv[r], t);
+    sh.Qu[i] += t;
+  }
+}
+
+template <class M, bool SQRT>
+__device__ __forceinline__ void bwd_store_q(double* q, BwdLds<M, SQRT>& sh) {
+  constexpr int n = M::n, m = M::m;
+  for (int e = threadIdx.x; e < nq_of<M>(); e += WAVE) {
+    double v;
+    if (e < n) v = sh.Qx[e];
+    else if (e < n + m) v = sh.Qu[e - n];
+    else if (e < n + m + n * n) v = sh.Qxx[e - n - m];
+    else if (e < n + m + n * n + m * m) v = sh.Quu[e - n - m - n * n];
+    else v = sh.Qux[e - n - m - n * n - m * m];
+    q[e] = v;
+  }
+}
+template <class M, bool SQRT>
+__device__ __forceinline__ void bwd_load_q(const double* q, BwdLds<M, SQRT>& sh) {
+  constexpr int n = M::n, m = M::m;
+  for (int e = threadIdx.x; e < nq_of<M>(); e += WAVE) {
+    const double v = q[e];
+    if (e < n) sh.Qx[e] = v;
+    else if (e < n + m) sh.Qu[e - n] = v;
+    else if (e < n + m + n * n) sh.Qxx[e - n - m] = v;
+    else if (e < n + m + n * n + m * m) sh.Quu[e - n - m - n * n] = v;
+    else sh.Qux[e - n - m - n * n - m * m] = v;
+  }
+}
+
+// LU with partial pivoting of the m x m matrix F in place (dgetrf; Julia `\`), lane 0 only.
+template <int m>
+__device__ __forceinline__ void lu_factor(double* F, int* piv) {
+  for (int k = 0; k < m; k++) {
+    int p = k;
+    double amax = fabs(F[k + m * k]);
+    for (int i = k + 1; i < m; i++)
+      if (fabs(F[i + m * k]) > amax) {
+        amax = fabs(F[i + m * k]);
+        p = i;
+      }
+    piv[k] = p;
+    if (p != k)
+      for (int j = 0; j < m; j++) {
+        const double t = F[k + m * j];
+        F[k + m * j] = F[p + m * j];
+        F[p + m * j] = t;
+      }
+    const double akk = F[k + m * k];
+    if (akk != 0.0) {
+      const double r = 1.0 / akk;
+      for (int i = k + 1; i < m; i++) F[i + m * k] *= r;
+    }
+    for (int j = k + 1; j < m; j++)
+      for (int i = k + 1; i < m; i++) F[i + m * j] = fma(-F[i + m * k], F[k + m * j], F[i + m * j]);
+  }
+}
+template <int m>
+__device__ __forceinline__ void lu_solve_col(const double* F, const int* piv, double* bcol) {
+  for (int k = 0; k < m; k++)
+    if (piv[k] != k) {
+      const double t = bcol[k];
+      bcol[k] = bcol[piv[k]];
+      bcol[piv[k]] = t;
+    }
+  for (int j = 0; j < m; j++)
+    for (int i = j + 1; i < m; i++) bcol[i] = fma(-F[i + m * j], bcol[j], bcol[i]);
+  for (int j = m - 1; j >= 0; j--) {
+    bcol[j] /= F[j + m * j];
+    for (int i = 0; i < j; i++) bcol[i] = fma(-F[i + m * j], bcol[j], bcol[i]);
+  }
+}
+
+// 2-norm condition number test cond(R) > 1e8 for an upper-triangular m x m R (backward_pass.jl:129).
+// Exact decision via Frobenius bounds cond_2 <= ‖R‖_F‖R⁻¹‖_F <= m·cond_2; a one-sided Jacobi SVD
+// settles the (rare) ambiguous band. Lane 0 only.
+template <int m>
+__device__ bool cond_exceeds(const double* Rm, double thresh) {
+  double Ri[m * m];
+  for (int i = 0; i < m * m; i++) Ri[i] = 0.0;
+  for (int c = 0; c < m; c++) {
+    Ri[c + m * c] = 1.0;
+    for (int j = m - 1; j >= 0; j--) {
+      const double xj = Ri[j + m * c] / Rm[j + m * j];
+      Ri[j + m * c] = xj;
+      for (int i = j - 1; i >= 0; i--) Ri[i + m * c] -= Rm[i + m * j] * xj;
+    }
+  }
+  double nr = 0.0, ni = 0.0;
+  for (int i = 0; i < m * m; i++) {
+    nr += Rm[i] * Rm[i];
+    ni += Ri[i] * Ri[i];
+  }
+  const double cF = sqrt(nr) * sqrt(ni);
+  if (cF <= thresh) return false;
+  if (cF / m > thresh) return true;
+  // ambiguous: one-sided Jacobi singular values
+  double A[m * m];
+  for (int i = 0; i < m * m; i++) A[i] = Rm[i];
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double off = 0.0;
+    for (int p = 0; p < m - 1; p++)
+      for (int q = p + 1; q < m; q++) {
+        double al = 0, be = 0, ga = 0;
+        for (int i = 0; i < m; i++) {
+          al += A[i + m * p] * A[i + m * p];
+          be += A[i + m * q] * A[i + m * q];
+          ga += A[i + m * p] * A[i + m * q];
+        }
+        if (ga == 0.0) continue;
+        const double c0 = fabs(ga) / sqrt(al * be);
+        off = fmax(off, c0);
+        if (c0 < 1e-15) continue;
+        const double zeta = (be - al) / (2.0 * ga);
+        const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+        for (int i = 0; i < m; i++) {
+          const double ap = A[i + m * p], aq = A[i + m * q];
+          A[i + m * p] = cs * ap - sn * aq;
+          A[i + m * q] = sn * ap + cs * aq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  double smax = 0.0, smin = INFINITY;
+  for (int j = 0; j < m; j++) {
+    double s2 = 0.0;
+    for (int i = 0; i < m; i++) s2 += A[i + m * j] * A[i + m * j];
+    smax = fmax(smax, sqrt(s2));
+    smin = fmin(smin, sqrt(s2));
+  }
+  return (smax / smin) > thresh;
+}
+
+template <class M, int SQRTI, int ALI>
+__global__ void __launch_bounds__(64) k_backward(const DevProblem* __restrict__ P, DevBuffers Bf, int flags) {
+  constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
+  constexpr int n = M::n, m = M::m, L = n + m, NQ = nq_of<M>();
+  __shared__ BwdLds<M, SQRT> sh;
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P->N;
+  TrajState s = Bf.st[b];
+  if (!s.active) return;
+  const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
+  const double* Xg = Bf.X + (size_t)b * N * n;
+  const double* Ug = Bf.U + (size_t)b * (N - 1) * m;
+  double* Kg = Bf.K + (size_t)b * (N - 1) * m * n;
+  double* dg = Bf.d + (size_t)b * (N - 1) * m;
+  const double* ABg = Bf.AB + (size_t)b * (N - 1) * n * L;
+  double* Qs = Bf.Qscr + (size_t)b * N * NQ;
+  const double rho0 = s.rho, drho0 = s.drho;
+  bool faithful = false;  // replay mode that reproduces the A.1 re-accumulation exactly
+  int kmin = N - 1;       // lowest knot whose accumulated Q is stored in Qscr
+  int restarts = 0;
+  double dV0 = 0.0, dV1 = 0.0;
+  const bool state_reg = (P->o.bp_reg_type == 1);
+
+attempt:
+  dV0 = 0.0;
+  dV1 = 0.0;
+  // terminal cost-to-go: S[N] = Q[N] (backward_pass.jl:20-21 / :100-101)
+  if (lane < n) sh.xk[lane] = Xg[(size_t)(N - 1) * n + lane];
+  wsync();
+  bwd_expand<M, SQRT, AL>(P, Bf, b, N - 1, sh);
+  wsync();
+  for (int e = lane; e < n * n; e += WAVE) sh.S[e] = sh.Qxx[e];
+  if (lane < n) sh.s[lane] = sh.Qx[lane];
+  wsync();
+  if (store_S) {
+    for (int e = lane; e < n * n; e += WAVE) Bf.Sdbg[((size_t)b * N + (N - 1)) * n * n + e] = sh.S[e];
+    if (lane < n) Bf.sdbg[((size_t)b * N + (N - 1)) * n + lane] = sh.s[lane];
+  }
+
+  for (int k = N - 2; k >= 0; k--) {
+    // ---- load ∇F[k] = [A|B] and (x_k, u_k)
+    const double* abk = ABg + (size_t)k * n * L;
+    for (int e = lane; e < n * L; e += WAVE) sh.AB[e] = abk[e];
+    if (lane < n) sh.xk[lane] = Xg[(size_t)k * n + lane];
+    else if (lane < n + m) sh.uk[lane - n] = Ug[(size_t)k * m + lane - n];
+    wsync();
+    if (faithful && k >= kmin) {
+      bwd_load_q<M, SQRT>(Qs + (size_t)k * NQ, sh);
+    } else {
+      bwd_expand<M, SQRT, AL>(P, Bf, b, k, sh);
+    }
+    wsync();
+    const double* A = sh.AB;
+    const double* Bm = sh.AB + n * n;
+    // ---- Q.x += A's ; Q.u += B's
+    if (lane < n) {
+      double t = 0.0;
+#pragma unroll
+      for (int l = 0; l < n; l++) t = fma(A[l + n * lane], sh.s[l], t);
+      sh.Qx[lane] += t;
+    } else if (lane < n + m) {
+      const int i = lane - n;
+      double t = 0.0;
+#pragma unroll
+      for (int l = 0; l < n; l++) t = fma(Bm[l + n * i], sh.s[l], t);
+      sh.Qu[i] += t;
+    }
+    if (!SQRT) {
+      // T1 = [A B]' S (L x n), then Qxx += (A'S)A ; Quu += (B'S)B ; Qux += (B'S)A  (A.16 association,
+      // backward_pass.jl:32-36)
+      wmm<L, n, n, true, false, false>(sh.T1, sh.AB, n, sh.S, n);
+      wsync();
+      wmm<n, n, n, false, false, true>(sh.Qxx, sh.T1, L, A, n);
+      wmm<m, n, m, false, false, true>(sh.Quu, sh.T1 + n, L, Bm, n);
+      wmm<m, n, n, false, false, true>(sh.Qux, sh.T1 + n, L, A, n);
+      wsync();
+    } else {
+      // tmp_x = S*A, tmp_u = S*B ; Q.xx ← qr([Q.xx; tmp_x]).R ; Q.uu ← qr([Q.uu; tmp_u]).R ;
+      // Q.ux += tmp_u'tmp_x   (backward_pass.jl:112-118)
+      wmm<n, n, L, false, false, false>(sh.T1, sh.S, n, sh.AB, n);
+      wsync();
+      wmm<m, n, n, true, false, true>(sh.Qux, sh.T1 + n * n, n, sh.T1, n);
+      {
+        constexpr int rows = 2 * n;
+        for (int e = lane; e < rows * n; e += WAVE) {
+          const int i = e % rows, j = e / rows;
+          sh.Wq[e] = (i < n) ? sh.Qxx[i + n * j] : sh.T1[(i - n) + n * j];
+        }
+        wsync();
+        wqr<n>(sh.Wq, rows, sh.red);
+        for (int e = lane; e < n * n; e += WAVE) {
+          const int i = e % n, j = e / n;
+          sh.Qxx[e] = (i <= j) ? sh.Wq[i + rows * j] : 0.0;
+        }
+        wsync();
+      }
+      {
+        constexpr int rows = m + n;
+        for (int e = lane; e < rows * m; e += WAVE) {
+          const int i = e % rows, j = e / rows;
+          sh.Wq[e] = (i < m) ? sh.Quu[i + m * j] : sh.T1[(i - m) + n * (n + j)];
+        }
+        wsync();
+        wqr<m>(sh.Wq, rows, sh.red);
+        for (int e = lane; e < m * m; e += WAVE) {
+          const int i = e % m, j = e / m;
+          sh.Quu[e] = (i <= j) ? sh.Wq[i + rows * j] : 0.0;
+        }
+        wsync();
+      }
+    }
+    if (faithful) {
+      bwd_store_q<M, SQRT>(Qs + (size_t)k * NQ, sh);
+      kmin = k < kmin ? k : kmin;
+    }
+    // ---- regularisation (backward_pass.jl:38-48 / :120-126) and the restart test
+    if (!SQRT) {
+      if (lane == 0) {
+        double G[m * m];
+        for (int e = 0; e < m * m; e++) G[e] = sh.Quu[e];
+        if (!state_reg) {
+          for (int i = 0; i < m; i++) G[i + m * i] += s.rho;
+        } else {
+          for (int j = 0; j < m; j++)
+            for (int i = 0; i < m; i++) {
+              double t = 0.0;
+              for (int l = 0; l < n; l++) t = fma(Bm[l + n * i], Bm[l + n * j], t);
+              G[i + m * j] += s.rho * t;
+            }
+        }
+        // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle
+        double U[m * m];
+        bool pd = true;
+        for (int j = 0; j < m && pd; j++) {
+          double d0 = G[j + m * j];
+          for (int l = 0; l < j; l++) d0 -= U[l + m * j] * U[l + m * j];
+          if (!(d0 > 0.0)) {
+            pd = false;
+            break;
+          }
+          const double ujj = sqrt(d0);
+          U[j + m * j] = ujj;
+          for (int c = j + 1; c < m; c++) {
+            double t = G[j + m * c];
+            for (int l = 0; l < j; l++) t -= U[l + m * j] * U[l + m * c];
+            U[j + m * c] = t / ujj;
+          }
+        }
+        sh.flag = pd ? 1 : 0;
+        if (pd) {
+          lu_factor<m>(G, sh.piv);
+          for (int e = 0; e < m * m; e++) sh.F[e] = G[e];
+        }
+      }
+    } else {
+      if (lane == 0) {
+        // Quu_reg = qr([Q.uu; sqrt(ρ)*I]).R  (:control)  or  qr([Q.uu; sqrt(ρ)*B]).R  (:state)
+        const int rows = state_reg ? m + n : 2 * m;
+        double Wl[(m + n) * m];
+        for (int j = 0; j < m; j++)
+          for (int i = 0; i < rows; i++) {
+            double v;
+            if (i < m) v = sh.Quu[i + m * j];
+            else if (state_reg) v = sqrt(s.rho) * Bm[(i - m) + n * j];
+            else v = (i - m == j) ? sqrt(s.rho) : 0.0;
+            Wl[i + rows * j] = v;
+          }
+        for (int j = 0; j < m; j++) {  // serial Householder (m x m, tiny)
+          double ss = 0.0;
+          for (int i = j + 1; i < rows; i++) ss = fma(Wl[i + rows * j], Wl[i + rows * j], ss);
+          const double xnorm = sqrt(ss);
+          if (xnorm == 0.0) continue;
+          const double alpha = Wl[j + rows * j];
+          const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+          const double tau = (beta - alpha) / beta;
+          const double sc = 1.0 / (alpha - beta);
+          for (int i = j + 1; i < rows; i++) Wl[i + rows * j] *= sc;
+          Wl[j + rows * j] = beta;
+          for (int c = j + 1; c < m; c++) {
+            double w = Wl[j + rows * c];
+            for (int i = j + 1; i < rows; i++) w = fma(Wl[i + rows * j], Wl[i + rows * c], w);
+            w *= tau;
+            Wl[j + rows * c] -= w;
+            for (int i = j + 1; i < rows; i++) Wl[i + rows * c] = fma(-Wl[i + rows * j], w, Wl[i + rows * c]);
+          }
+        }
+        for (int j = 0; j < m; j++)
+          for (int i = 0; i < m; i++) sh.F[i + m * j] = (i <= j) ? Wl[i + rows * j] : 0.0;
+        sh.flag = cond_exceeds<m>(sh.F, 1e8) ? 0 : 1;
+      }
+    }
+    wsync();
+    if (!sh.flag) {
+      // non-PD / ill-conditioned: increase ρ and restart at N-1 (A.1: Q is NOT re-expanded)
+      if (!faithful) {
+        // first restart: replay this call from its start in faithful mode so that the
+        // re-accumulated Q blocks are exactly the reference's (deterministic replay)
+        faithful = true;
+        s.rho = rho0;
+        s.drho = drho0;
+        restarts = 0;
+        kmin = N - 1;
+        wsync();
+        goto attempt;
+      }
+      reg_increase(P, s);
+      restarts++;
+      if (restarts > 1000) {
+        s.flags |= TOG_TRAJ_MAX_REG;
+        break;
+      }
+      wsync();
+      goto attempt;
+    }
+    // ---- gains: K = -(Quu_reg \ Qux_reg), d = -(Quu_reg \ Q.u)
+    if (lane <= n) {
+      double col[m];
+      if (lane < n) {
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          double v = sh.Qux[i + m * lane];
+          if (state_reg) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < n; l++) t = fma(Bm[l + n * i], A[l + n * lane], t);
+            v += s.rho * t;
+          }
+          col[i] = v;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < m; i++) col[i] = sh.Qu[i];
+      }
+      if (!SQRT) {
+        lu_solve_col<m>(sh.F, sh.piv, col);
+      } else {
+        // Quu_reg' \ col (forward substitution), then Quu_reg \ (back substitution)
+        for (int j = 0; j < m; j++) {
+          const double xj = col[j] / sh.F[j + m * j];
+          col[j] = xj;
+          for (int i = j + 1; i < m; i++) col[i] = fma(-sh.F[j + m * i], xj, col[i]);
+        }
+        for (int j = m - 1; j >= 0; j--) {
+          const double xj = col[j] / sh.F[j + m * j];
+          col[j] = xj;
+          for (int i = j - 1; i >= 0; i--) col[i] = fma(-sh.F[i + m * j], xj, col[i]);
+        }
+      }
+      if (lane < n) {
+#pragma unroll
+        for (int i = 0; i < m; i++) sh.Kt[i + m * lane] = -1.0 * col[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < m; i++) sh.dd[i] = -1.0 * col[i];
+      }
+    }
+    wsync();
+    // ---- write K[k], d[k]
+    for (int e = lane; e < m * n; e += WAVE) Kg[(size_t)k * m * n + e] = sh.Kt[e];
+    if (lane < m) dg[(size_t)k * m + lane] = sh.dd[lane];
+    if (!SQRT) {
+      // KtQ = K' * Q.uu (n x m)
+      wmm<n, m, m, true, false, false>(sh.KtQ, sh.Kt, m, sh.Quu, m);
+      wsync();
+      // S[k].x = Q.x + (K'Q.uu) d + K' Q.u + Q.ux' d
+      if (lane < n) {
+        double a = 0.0, bb = 0.0, c = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          a = fma(sh.KtQ[lane + n * l], sh.dd[l], a);
+          bb = fma(sh.Kt[l + m * lane], sh.Qu[l], bb);
+          c = fma(sh.Qux[l + m * lane], sh.dd[l], c);
+        }
+        sh.s[lane] = ((sh.Qx[lane] + a) + bb) + c;
+      }
+      // S[k].xx = Q.xx + (K'Q.uu)K + K'Q.ux + Q.ux'K, symmetrised (into T1 then S)
+      for (int e = lane; e < n * n; e += WAVE) {
+        const int i = e % n, j = e / n;
+        double a = 0.0, bb = 0.0, c = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          a = fma(sh.KtQ[i + n * l], sh.Kt[l + m * j], a);
+          bb = fma(sh.Kt[l + m * i], sh.Qux[l + m * j], bb);
+          c = fma(sh.Qux[l + m * i], sh.Kt[l + m * j], c);
+        }
+        sh.T1[e] = ((sh.Qxx[e] + a) + bb) + c;
+      }
+      wsync();
+      for (int e = lane; e < n * n; e += WAVE) {
+        const int i = e % n, j = e / n;
+        sh.S[e] = 0.5 * (sh.T1[i + n * j] + sh.T1[j + n * i]);
+      }
+      if (lane == 0) {
+        double a = 0.0, bb = 0.0;
+        for (int i = 0; i < m; i++) a = fma(sh.dd[i], sh.Qu[i], a);
+        for (int j = 0; j < m; j++) {
+          double t = 0.0;
+          for (int i = 0; i < m; i++) t = fma(0.5 * sh.dd[i], sh.Quu[i + m * j], t);
+          bb = fma(t, sh.dd[j], bb);
+        }
+        dV0 += a;
+        dV1 += bb;
+      }
+      wsync();
+    } else {
+      // Ud = Q.uu d (m) and KtQ = K'Q.uu' (n x m)
+      if (lane < m) {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) t = fma(sh.Quu[lane + m * l], sh.dd[l], t);
+        sh.red[lane] = t;
+      }
+      for (int e = lane; e < n * m; e += WAVE) {
+        const int i = e % n, j = e / n;
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) t = fma(sh.Kt[l + m * i], sh.Quu[j + m * l], t);
+        sh.KtQ[e] = t;
+      }
+      // tmp1 = (Q.xx') \ Q.ux'   (n x m; forward substitution with the lower-triangular Q.xx')
+      if (lane < m) {
+        const int c = lane;
+        double col[n];
+#pragma unroll
+        for (int i = 0; i < n; i++) col[i] = sh.Qux[c + m * i];
+        for (int j = 0; j < n; j++) {
+          const double xj = col[j] / sh.Qxx[j + n * j];
+          col[j] = xj;
+          for (int i = j + 1; i < n; i++) col[i] = fma(-sh.Qxx[j + n * i], xj, col[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < n; i++) sh.tmp1[i + n * c] = col[i];
+      }
+      wsync();
+      // S[k].x = Q.x + (K'Q.uu')(Q.uu d) + K'Q.u + Q.ux'd
+      if (lane < n) {
+        double a = 0.0, bb = 0.0, c = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          a = fma(sh.KtQ[lane + n * l], sh.red[l], a);
+          bb = fma(sh.Kt[l + m * lane], sh.Qu[l], bb);
+          c = fma(sh.Qux[l + m * lane], sh.dd[l], c);
+        }
+        sh.s[lane] = ((sh.Qx[lane] + a) + bb) + c;
+      }
+      // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! with each row of tmp1 (backward_pass.jl:186-192)
+      if (lane == 0) {
+        double U[m * m], v[m];
+        for (int e = 0; e < m * m; e++) U[e] = sh.Quu[e];
+        bool okd = true;
+        for (int r = 0; r < n && okd; r++) {
+          for (int j = 0; j < m; j++) v[j] = sh.tmp1[r + n * j];
+          for (int i = 0; i < m; i++) {
+            const double Aii = U[i + m * i];
+            const double sn = v[i] / Aii;
+            const double s2 = sn * sn;
+            if (s2 > 1.0) {
+              okd = false;
+              break;
+            }
+            const double c = sqrt(1.0 - s2);
+            U[i + m * i] = c * Aii;
+            for (int j = i + 1; j < m; j++) {
+              const double tmp = (U[i + m * j] - sn * v[j]) / c;
+              v[j] = c * v[j] - sn * tmp;
+              U[i + m * j] = tmp;
+            }
+          }
+        }
+        if (!okd) {
+          s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
+          for (int e = 0; e < m * m; e++) U[e] = sh.Quu[e];
+        }
+        for (int e = 0; e < m * m; e++) sh.tmp2[e] = U[e];
+        // ΔV
+        double a = 0.0, bb = 0.0;
+        for (int i = 0; i < m; i++) a = fma(sh.dd[i], sh.Qu[i], a);
+        for (int i = 0; i < m; i++) bb = fma(sh.red[i], sh.red[i], bb);
+        dV0 += a;
+        dV1 += 0.5 * bb;
+        sh.flag = okd ? 1 : 0;
+      }
+      wsync();
+      if (!sh.flag) s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
+      // S[k].xx = qr([Q.xx + tmp1*K; tmp2*K]).R
+      {
+        constexpr int rows = n + m;
+        for (int e = lane; e < rows * n; e += WAVE) {
+          const int i = e % rows, j = e / rows;
+          double v = 0.0;
+          if (i < n) {
+#pragma unroll
+            for (int l = 0; l < m; l++) v = fma(sh.tmp1[i + n * l], sh.Kt[l + m * j], v);
+            v = sh.Qxx[i + n * j] + v;
+          } else {
+            const int ii = i - n;
+#pragma unroll
+            for (int l = 0; l < m; l++) v = fma(sh.tmp2[ii + m * l], sh.Kt[l + m * j], v);
+          }
+          sh.Wq[e] = v;
+        }
+        wsync();
+        wqr<n>(sh.Wq, rows, sh.red);
+        for (int e = lane; e < n * n; e += WAVE) {
+          const int i = e % n, j = e / n;
+          sh.S[e] = (i <= j) ? sh.Wq[i + rows * j] : 0.0;
+        }
+        wsync();
+      }
+    }
+    if (store_S) {
+      for (int e = lane; e < n * n; e += WAVE) Bf.Sdbg[((size_t)b * N + k) * n * n + e] = sh.S[e];
+      if (lane < n) Bf.sdbg[((size_t)b * N + k) * n + lane] = sh.s[lane];
+    }
+  }
+  reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
+  if (lane == 0) {
+    s.dV0 = dV0;
+    s.dV1 = dV1;
+    s.bp_restarts = restarts + (faithful ? 1 : 0);
+    Bf.st[b] = s;
+  }
+}
+
+// =============================================================================================
+// k_forward: forwardpass! + solve! bookkeeping + AL outer update; one thread per trajectory
+// =============================================================================================
+template <class M, int INTEG>
+__device__ double forward_line_search(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b,
+                                      TrajState& s, double J_prev, bool al) {
+  const tog_options& o = P->o;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  double* C = al ? Bf.C + (size_t)b * N * P->pmax : nullptr;
+  double J = INFINITY, alpha = 1.0, z = -1.0, expected = 0.0;
+  int iter = 0, trials = 0;
+  while ((z <= o.line_search_lower_bound || z > o.line_search_upper_bound) && J >= J_prev) {
+    if (iter > o.iterations_linesearch) {
+      double* Xb = Bf.Xb + (size_t)b * N * n;
+      double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
+      const double* X = Bf.X + (size_t)b * N * n;
+      const double* U = Bf.U + (size_t)b * (N - 1) * m;
+      for (int i = 0; i < N * n; i++) Xb[i] = X[i];
+      for (int i = 0; i < (N - 1) * m; i++) Ub[i] = U[i];
+      J = traj_cost<M>(P, Bf, b, Xb, Ub, al, C);
+      z = 0.0;
+      alpha = 0.0;
+      expected = 0.0;
+      reg_increase(P, s);
+      s.rho += o.bp_reg_fp;
+      break;
+    }
+    const bool ok = traj_rollout<M, INTEG>(P, Bf, b, alpha);
+    trials++;
+    if (!ok) {
+      iter++;
+      alpha /= 2.0;
+      continue;
+    }
+    J = traj_cost<M>(P, Bf, b, Bf.Xb + (size_t)b * N * n, Bf.Ub + (size_t)b * (N - 1) * m, al, C);
+    expected = -alpha * (s.dV0 + alpha * s.dV1);
+    z = (expected > 0.0) ? (J_prev - J) / expected : -1.0;
+    iter++;
+    alpha /= 2.0;
+  }
+  s.alpha = 2.0 * alpha;
+  s.z = z;
+  s.expected = expected;
+  s.ls_trials = trials;
+  if (J > J_prev) s.flags |= TOG_TRAJ_COST_INCREASED;
+  return J;
+}
+
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_forward(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+                                                int bookkeeping, const double* Jprev_in, double* Jout) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  TrajState s = Bf.st[b];
+  if (!s.active) return;
+  const bool al = (mode == TOG_MODE_AL);
+  const double J_prev = bookkeeping ? s.J : Jprev_in[b];
+  const double J = forward_line_search<M, INTEG>(P, Bf, b, s, J_prev, al);
+  if (Jout) Jout[b] = J;
+  if (!bookkeeping) {
+    Bf.st[b] = s;
+    return;
+  }
+  const tog_options& o = P->o;
+  s.total_steps++;
+  bool inner_done = false;
+  if (s.flags & TOG_TRAJ_COST_INCREASED) {  // reference: error(...) terminates the solve
+    s.active = 0;
+    Bf.st[b] = s;
+    return;
+  }
+  if (J > o.max_cost_value) {  // ilqr_methods.jl:25-28 (@warn, return without copying X̄)
+    s.flags |= TOG_TRAJ_COST_BLOWUP;
+    inner_done = true;
+  } else {
+    double* X = Bf.X + (size_t)b * N * n;
+    double* U = Bf.U + (size_t)b * (N - 1) * m;
+    const double* Xb = Bf.Xb + (size_t)b * N * n;
+    const double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
+    for (int i = 0; i < N * n; i++) X[i] = Xb[i];
+    for (int i = 0; i < (N - 1) * m; i++) U[i] = Ub[i];
+    s.dJ = fabs(J - s.J);
+    s.J = J;
+    s.iters++;
+    s.grad = traj_gradient<M>(P, Bf, b);
+    s.zero_cnt = (s.dJ == 0.0) ? s.zero_cnt + 1 : 0;
+    // evaluate_convergence (ilqr_methods.jl:139-162)
+    if ((0.0 < s.dJ && s.dJ < s.cost_tol) || s.grad < s.grad_tol || s.iters >= o.iterations ||
+        s.zero_cnt > o.dJ_counter_limit) {
+      inner_done = true;
+      if (s.iters >= o.iterations) s.flags |= TOG_TRAJ_MAX_ITERS;
+    }
+  }
+  if (inner_done) {
+    if (!al) {
+      s.flags |= TOG_TRAJ_CONVERGED;
+      s.active = 0;
+    } else {
+      // AL step! tail (augmented_lagrangian_methods.jl:53-67): J = cost(prob), dual_update!,
+      // penalty_update!, record_iteration!, evaluate_convergence
+      const double* X = Bf.X + (size_t)b * N * n;
+      const double* U = Bf.U + (size_t)b * (N - 1) * m;
+      double* C = Bf.C + (size_t)b * N * pmax;
+      double* lam = Bf.lam + (size_t)b * N * pmax;
+      double* mu = Bf.mu + (size_t)b * N * pmax;
+      (void)traj_cost<M>(P, Bf, b, X, U, true, C);
+      double mumax = 0.0;
+      for (int k = 0; k < N; k++) {
+        const int cnt = P->knot_cnt[k];
+        const ConRow* rows = P->rows + P->knot_off[k];
+        for (int i = 0; i < cnt; i++) {
+          const size_t q = (size_t)k * pmax + i;
+          double l = lam[q] + mu[q] * C[q];
+          l = fmax(o.dual_min, fmin(o.dual_max, l));
+          if (row_inequality(rows[i])) l = fmax(0.0, l);
+          lam[q] = l;
+          mu[q] = fmax(0.0, fmin(o.penalty_max, o.penalty_scaling * mu[q]));
+          mumax = fmax(mumax, mu[q]);
+        }
+      }
+      s.mu_max = mumax;
+      s.c_max = traj_max_violation(P, Bf, b);
+      bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (s.c_max < o.constraint_tolerance);
+      if (conv) {
+        s.flags |= TOG_TRAJ_AL_CONVERGED;
+        s.active = 0;
+      } else if (s.al_iter >= o.al_iterations) {
+        s.flags |= TOG_TRAJ_AL_MAX_ITERS;
+        s.active = 0;
+      } else {
+        // next outer iteration: reset!(solver_uncon), set_tolerances!, solve! init (rollout no-op)
+        s.al_iter++;
+        set_tolerances(P, s, mode);
+        s.rho = 0.0;
+        s.drho = 0.0;
+        s.J = traj_cost<M>(P, Bf, b, X, U, true, C);
+        s.iters = 1;
+        s.dJ = INFINITY;
+        s.zero_cnt = 0;
+      }
+    }
+  }
+  Bf.st[b] = s;
+}
+
+// =============================================================================================
+// Per-model launch table
+// =============================================================================================
+struct ModelOps {
+  int n, m;
+  void (*init)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, hipStream_t);
+  void (*rollout_open)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
+  void (*jacobian)(const DevProblem*, const DevBuffers&, long long B, int N, int integ, hipStream_t);
+  void (*backward)(const DevProblem*, const DevBuffers&, long long B, int sqrt, int al, int flags, hipStream_t);
+  void (*forward)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, int bookkeeping,
+                  const double* Jprev, double* Jout, hipStream_t);
+  void (*cost)(const DevProblem*, const DevBuffers&, long long B, int al, int use_bar, double* J, hipStream_t);
+  void (*rollout)(const DevProblem*, const DevBuffers&, long long B, int integ, double alpha, int* ok, hipStream_t);
+  void (*update_constraints)(const DevProblem*, const DevBuffers&, long long B, hipStream_t);
+  int bwd_lds_bytes;
+};
+
+template <class M>
+struct ModelLaunch {
+  // dual partials per thread: all of them for small models, chunks of 4 otherwise (512-register
+  // budget with no scratch for the quadrotor RK4 step)
+  static constexpr int JW = (M::n + M::m) <= 6 ? (M::n + M::m) : 4;
+  static unsigned grid(long long total, int blk) { return (unsigned)((total + blk - 1) / blk); }
+  static void init(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, hipStream_t st) {
+    if (integ == TOG_RK4)
+      hipLaunchKernelGGL((k_init<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
+    else
+      hipLaunchKernelGGL((k_init<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
+  }
+  static void rollout_open(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, hipStream_t st) {
+    if (integ == TOG_RK4)
+      hipLaunchKernelGGL((k_rollout_open<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+    else
+      hipLaunchKernelGGL((k_rollout_open<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+  }
+  static void jacobian(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int integ, hipStream_t st) {
+    constexpr int NCH = (M::n + M::m + JW - 1) / JW;
+    const long long total = B * (long long)(N - 1) * NCH;
+    if (integ == TOG_RK4)
+      hipLaunchKernelGGL((k_jacobian<M, TOG_RK4, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+    else
+      hipLaunchKernelGGL((k_jacobian<M, TOG_RK3, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+  }
+  static void backward(const DevProblem* P, const DevBuffers& Bf, long long B, int sq, int al, int flags,
+                       hipStream_t st) {
+    const dim3 g((unsigned)B), blk(64);
+    if (sq) {
+      if (al) hipLaunchKernelGGL((k_backward<M, 1, 1>), g, blk, 0, st, P, Bf, flags);
+      else hipLaunchKernelGGL((k_backward<M, 1, 0>), g, blk, 0, st, P, Bf, flags);
+    } else {
+      if (al) hipLaunchKernelGGL((k_backward<M, 0, 1>), g, blk, 0, st, P, Bf, flags);
+      else hipLaunchKernelGGL((k_backward<M, 0, 0>), g, blk, 0, st, P, Bf, flags);
+    }
+  }
+  static void forward(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, int bk,
+                      const double* Jp, double* Jo, hipStream_t st) {
+    if (integ == TOG_RK4)
+      hipLaunchKernelGGL((k_forward<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+    else
+      hipLaunchKernelGGL((k_forward<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+  }
+  static void cost(const DevProblem* P, const DevBuffers& Bf, long long B, int al, int bar, double* J,
+                   hipStream_t st) {
+    hipLaunchKernelGGL((k_cost<M>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, al, bar, J);
+  }
+  static void rollout(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, double alpha, int* ok,
+                      hipStream_t st) {
+    if (integ == TOG_RK4)
+      hipLaunchKernelGGL((k_rollout<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
+    else
+      hipLaunchKernelGGL((k_rollout<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
+  }
+  static void update_constraints(const DevProblem* P, const DevBuffers& Bf, long long B, hipStream_t st) {
+    hipLaunchKernelGGL((k_update_constraints<M>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+  }
+  static ModelOps ops() {
+    ModelOps o;
+    o.n = M::n;
+    o.m = M::m;
+    o.init = init;
+    o.rollout_open = rollout_open;
+    o.jacobian = jacobian;
+    o.backward = backward;
+    o.forward = forward;
+    o.cost = cost;
+    o.rollout = rollout;
+    o.update_constraints = update_constraints;
+    o.bwd_lds_bytes = (int)sizeof(BwdLds<M, true>);
+    return o;
+  }
+};
+
+}  // namespace tog

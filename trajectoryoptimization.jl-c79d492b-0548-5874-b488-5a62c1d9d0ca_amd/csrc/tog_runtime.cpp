@@ -1,0 +1,770 @@
+// tog_runtime.cpp — C ABI (include/tog.h) over the HIP kernels. Host code only: device buffers,
+// problem marshalling (tog_problem_desc -> DevProblem + constraint rows), launch sequencing.
+//
+// Ownership: the handle owns every device buffer; callers own host arrays. One host thread per
+// handle; handles are independent (one per GPU for multi-GPU runs).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "tog_kernels.hpp"
+
+using namespace tog;
+
+namespace tog {
+const ModelOps* ops_double_integrator();
+const ModelOps* ops_cartpole();
+const ModelOps* ops_quadrotor();
+const ModelOps* ops_car();
+const ModelOps* ops_pendulum();
+}  // namespace tog
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHECK(expr)                                                                   \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(TOG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct tog_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int model = 0, integ = 0, n = 0, m = 0, N = 0, pmax = 0, nrows = 0, nq = 0;
+  long long B = 0;
+  int mode = TOG_MODE_ILQR;
+  tog_options opts;
+  DevProblem hostP;
+  DevProblem* dP = nullptr;
+  int* d_knot_off = nullptr;
+  int* d_knot_cnt = nullptr;
+  ConRow* d_rows = nullptr;
+  DevBuffers buf = {};
+  const ModelOps* ops = nullptr;
+  double* d_scratch = nullptr;  // B doubles (J_prev / J_out staging)
+  double* d_scratch2 = nullptr; // B doubles
+  int* d_iscratch = nullptr;    // B ints
+  double* d_stats = nullptr;    // 3 doubles
+  std::vector<void*> allocs;
+  // live per-kernel timing (tog_profile)
+  bool profiling = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<int> ev_kind;  // kernel id per recorded (start, end) pair
+  size_t ev_used = 0;
+};
+
+static hipEvent_t next_event(tog_handle* h) {
+  if (h->ev_used == h->ev_pool.size()) {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    h->ev_pool.push_back(e);
+  }
+  return h->ev_pool[h->ev_used++];
+}
+
+// launch `fn` bracketed by timing events when profiling is on
+template <class F>
+static void timed(tog_handle* h, int kind, F&& fn) {
+  if (!h->profiling) {
+    fn();
+    return;
+  }
+  hipEvent_t a = next_event(h), b = next_event(h);
+  (void)hipEventRecord(a, h->stream);
+  fn();
+  (void)hipEventRecord(b, h->stream);
+  h->ev_kind.push_back(kind);
+}
+
+static const ModelOps* ops_for(int model) {
+  switch (model) {
+    case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_double_integrator();
+    case TOG_MODEL_CARTPOLE: return ops_cartpole();
+    case TOG_MODEL_QUADROTOR: return ops_quadrotor();
+    case TOG_MODEL_CAR: return ops_car();
+    case TOG_MODEL_PENDULUM: return ops_pendulum();
+  }
+  return nullptr;
+}
+
+// upper Cholesky (dpotrf 'U') of a symmetric matrix; returns false if not PD
+static bool host_chol_upper(const double* A, int n, double* U) {
+  for (int i = 0; i < n * n; i++) U[i] = 0.0;
+  for (int j = 0; j < n; j++) {
+    double s = A[j + n * j];
+    for (int k = 0; k < j; k++) s -= U[k + n * j] * U[k + n * j];
+    if (!(s > 0.0)) return false;
+    const double ujj = sqrt(s);
+    U[j + n * j] = ujj;
+    for (int c = j + 1; c < n; c++) {
+      double t = A[j + n * c];
+      for (int k = 0; k < j; k++) t -= U[k + n * j] * U[k + n * c];
+      U[j + n * c] = t / ujj;
+    }
+  }
+  return true;
+}
+
+// Flatten the ordered constraint sets into per-knot rows (src/constraint_sets.jl:64-131).
+static int build_rows(const tog_problem_desc* d, std::vector<ConRow>& rows, std::vector<int>& off,
+                      std::vector<int>& cnt) {
+  const int n = d->n, m = d->m, N = d->N;
+  off.assign(N, 0);
+  cnt.assign(N, 0);
+  for (int k = 0; k < N; k++) {
+    off[k] = (int)rows.size();
+    const int si = d->knot_set ? d->knot_set[k] : -1;
+    if (si < 0) continue;
+    if (si >= d->n_sets) return fail(TOG_ERR_ARG, "knot_set index out of range");
+    const bool term = (k == N - 1);
+    const tog_constraint_set& set = d->sets[si];
+    for (int c = 0; c < set.n_con; c++) {
+      const tog_constraint& con = set.con[c];
+      const double* D = con.data;
+      switch (con.type) {
+        case TOG_CON_BOUND: {
+          // data = [x_max(n), x_min(n), u_max(m), u_min(m)]; order [x_max; u_max; x_min; u_min]
+          for (int i = 0; i < n; i++)
+            if (isfinite(D[i])) rows.push_back({ROW_XMAX, i, D[i], 0, 0, 0});
+          if (!term)
+            for (int i = 0; i < m; i++)
+              if (isfinite(D[2 * n + i])) rows.push_back({ROW_UMAX, i, D[2 * n + i], 0, 0, 0});
+          for (int i = 0; i < n; i++)
+            if (isfinite(D[n + i])) rows.push_back({ROW_XMIN, i, D[n + i], 0, 0, 0});
+          if (!term)
+            for (int i = 0; i < m; i++)
+              if (isfinite(D[2 * n + m + i])) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
+          break;
+        }
+        case TOG_CON_GOAL:
+          if (term)
+            for (int i = 0; i < n; i++) rows.push_back({ROW_GOAL, i, D[i], 0, 0, 0});
+          break;
+        case TOG_CON_CIRCLES:
+          if (!term)
+            for (int o = 0; o < con.count; o++)
+              rows.push_back({ROW_CIRCLE, 0, D[3 * o], D[3 * o + 1], 0.0, D[3 * o + 2]});
+          break;
+        case TOG_CON_SPHERES:
+          if (!term)
+            for (int o = 0; o < con.count; o++)
+              rows.push_back({ROW_SPHERE, 0, D[4 * o], D[4 * o + 1], D[4 * o + 2], D[4 * o + 3]});
+          break;
+        default:
+          return fail(TOG_ERR_ARG, "unknown constraint type");
+      }
+    }
+    cnt[k] = (int)rows.size() - off[k];
+    if (cnt[k] > PCAP) return fail(TOG_ERR_UNSUPPORTED, "more than PCAP constraint rows at one knot");
+  }
+  return TOG_OK;
+}
+
+template <class T>
+static int dalloc(tog_handle* h, T** p, size_t count) {
+  void* v = nullptr;
+  HIPCHECK(hipMalloc(&v, count * sizeof(T) > 0 ? count * sizeof(T) : 16));
+  h->allocs.push_back(v);
+  *p = (T*)v;
+  return TOG_OK;
+}
+
+// =============================================================================================
+// k_batch_stats: [n_active, Σ J, max c_max] (input to the cross-GPU RCCL all-reduce)
+// =============================================================================================
+static __global__ void __launch_bounds__(1024) k_batch_stats(const TrajState* __restrict__ st, long long B, double* out) {
+  __shared__ double sa[1024], sj[1024], sc[1024];
+  const int t = threadIdx.x;
+  double a = 0.0, j = 0.0, c = 0.0;
+  for (long long b = t; b < B; b += blockDim.x) {
+    a += st[b].active ? 1.0 : 0.0;
+    j += st[b].J;
+    c = fmax(c, st[b].c_max);
+  }
+  sa[t] = a;
+  sj[t] = j;
+  sc[t] = c;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (t < w) {
+      sa[t] += sa[t + w];
+      sj[t] += sj[t + w];
+      sc[t] = fmax(sc[t], sc[t + w]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out[0] = sa[0];
+    out[1] = sj[0];
+    out[2] = sc[0];
+  }
+}
+
+
+__global__ void k_fill(double* p, size_t count, double v) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) p[i] = v;
+}
+
+static void fill(tog_handle* h, double* p, size_t count, double v) {
+  if (!count) return;
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, h->stream, p, count, v);
+}
+
+__global__ void k_reset_state(TrajState* st, long long B, double mu0) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  TrajState s = {};
+  s.active = 1;
+  (void)mu0;
+  st[b] = s;
+}
+
+extern "C" {
+
+int32_t tog_version(void) { return TOG_ABI_VERSION; }
+
+int32_t tog_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+void tog_default_options(tog_options* o) {
+  memset(o, 0, sizeof(*o));
+  o->cost_tolerance = 1e-4;
+  o->gradient_norm_tolerance = 1e-5;
+  o->iterations = 300;
+  o->dJ_counter_limit = 10;
+  o->square_root = 0;
+  o->bp_reg_type = 0;
+  o->gradient_type = 0;
+  o->iterations_linesearch = 20;
+  o->line_search_lower_bound = 1e-8;
+  o->line_search_upper_bound = 10.0;
+  o->bp_reg_increase_factor = 1.6;
+  o->bp_reg_max = 1e8;
+  o->bp_reg_min = 1e-8;
+  o->bp_reg_fp = 10.0;
+  o->max_cost_value = 1e8;
+  o->max_state_value = 1e8;
+  o->max_control_value = 1e8;
+  o->al_cost_tolerance = 1e-4;
+  o->al_cost_tolerance_intermediate = 1e-3;
+  o->al_gradient_norm_tolerance = 1e-5;
+  o->al_gradient_norm_tolerance_intermediate = 1e-5;
+  o->constraint_tolerance = 1e-3;
+  o->dual_min = -1e8;
+  o->dual_max = 1e8;
+  o->penalty_max = 1e8;
+  o->penalty_initial = 1.0;
+  o->penalty_scaling = 10.0;
+  o->al_iterations = 30;
+  o->kickout_max_penalty = 0;
+}
+
+const char* tog_last_error(void) { return g_err.c_str(); }
+
+int32_t tog_destroy(tog_handle* h) {
+  if (!h) return TOG_OK;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) (void)hipFree(p);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+  delete h;
+  return TOG_OK;
+}
+
+int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t device, tog_handle** out) {
+  if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
+  *out = nullptr;
+  const ModelOps* ops = ops_for(d->model);
+  if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
+  if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
+  if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
+  if (d->batch < 1) return fail(TOG_ERR_ARG, "batch must be >= 1");
+  if (!(d->dt > 0)) return fail(TOG_ERR_ARG, "dt must be strictly positive");  // src/problem.jl:66-68
+  if (d->integrator != TOG_RK3 && d->integrator != TOG_RK4) return fail(TOG_ERR_UNSUPPORTED, "integrator");
+  int ndev = tog_device_count();
+  if (device < 0 || device >= ndev) return fail(TOG_ERR_DEVICE, "no such HIP device");
+  tog_handle* h = new tog_handle();
+  h->device = device;
+  HIPCHECK(hipSetDevice(device));
+  HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  h->own_stream = true;
+  h->model = d->model;
+  h->integ = d->integrator;
+  h->n = d->n;
+  h->m = d->m;
+  h->N = d->N;
+  h->B = d->batch;
+  h->opts = *opts;
+  h->ops = ops;
+  const int n = h->n, m = h->m, N = h->N;
+  h->nq = n + m + n * n + m * m + m * n;
+
+  std::vector<ConRow> rows;
+  std::vector<int> off, cnt;
+  int rc = build_rows(d, rows, off, cnt);
+  if (rc) {
+    tog_destroy(h);
+    return rc;
+  }
+  h->nrows = (int)rows.size();
+  h->pmax = 0;
+  for (int k = 0; k < N; k++) h->pmax = cnt[k] > h->pmax ? cnt[k] : h->pmax;
+
+  DevProblem& P = h->hostP;
+  memset(&P, 0, sizeof(P));
+  P.n = n;
+  P.m = m;
+  P.N = N;
+  P.pmax = h->pmax;
+  P.model = d->model;
+  P.integ = d->integrator;
+  P.nrows = h->nrows;
+  P.B = h->B;
+  P.dt = d->dt;
+  memcpy(P.Q, d->Q, sizeof(double) * n * n);
+  memcpy(P.R, d->R, sizeof(double) * m * m);
+  memcpy(P.H, d->H, sizeof(double) * m * n);
+  memcpy(P.q, d->q, sizeof(double) * n);
+  memcpy(P.r, d->r, sizeof(double) * m);
+  P.c = d->c;
+  memcpy(P.Qf, d->Qf, sizeof(double) * n * n);
+  memcpy(P.qf, d->qf, sizeof(double) * n);
+  P.cf = d->cf;
+  {
+    double Qdt[NMAX * NMAX], Rdt[MMAX * MMAX];
+    for (int i = 0; i < n * n; i++) Qdt[i] = P.Q[i] * P.dt;
+    for (int i = 0; i < m * m; i++) Rdt[i] = P.R[i] * P.dt;
+    bool ok = host_chol_upper(Qdt, n, P.cQ) && host_chol_upper(Rdt, m, P.cR) && host_chol_upper(P.Qf, n, P.cQf);
+    P.sqrt_ok = ok ? 1 : 0;
+    if (opts->square_root && !ok) {
+      tog_destroy(h);
+      return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
+    }
+  }
+  P.o = *opts;
+  const size_t B = (size_t)h->B, P1 = (size_t)(h->pmax > 0 ? h->pmax : 1);
+  if ((rc = dalloc(h, &h->d_knot_off, N)) || (rc = dalloc(h, &h->d_knot_cnt, N)) ||
+      (rc = dalloc(h, &h->d_rows, rows.size() + 1)) || (rc = dalloc(h, &h->dP, 1))) {
+    tog_destroy(h);
+    return rc;
+  }
+  HIPCHECK(hipMemcpy(h->d_knot_off, off.data(), sizeof(int) * N, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(h->d_knot_cnt, cnt.data(), sizeof(int) * N, hipMemcpyHostToDevice));
+  if (!rows.empty()) HIPCHECK(hipMemcpy(h->d_rows, rows.data(), sizeof(ConRow) * rows.size(), hipMemcpyHostToDevice));
+  P.knot_off = h->d_knot_off;
+  P.knot_cnt = h->d_knot_cnt;
+  P.rows = h->d_rows;
+  HIPCHECK(hipMemcpy(h->dP, &P, sizeof(P), hipMemcpyHostToDevice));
+
+  DevBuffers& b = h->buf;
+  if ((rc = dalloc(h, &b.x0, B * n)) || (rc = dalloc(h, &b.X, B * N * n)) || (rc = dalloc(h, &b.U, B * (N - 1) * m)) ||
+      (rc = dalloc(h, &b.Xb, B * N * n)) || (rc = dalloc(h, &b.Ub, B * (N - 1) * m)) ||
+      (rc = dalloc(h, &b.AB, B * (N - 1) * n * (n + m))) || (rc = dalloc(h, &b.K, B * (N - 1) * m * n)) ||
+      (rc = dalloc(h, &b.d, B * (N - 1) * m)) || (rc = dalloc(h, &b.lam, B * N * P1)) ||
+      (rc = dalloc(h, &b.mu, B * N * P1)) || (rc = dalloc(h, &b.C, B * N * P1)) ||
+      (rc = dalloc(h, &b.Qscr, B * N * h->nq)) || (rc = dalloc(h, &b.st, B)) ||
+      (rc = dalloc(h, &h->d_scratch, B)) || (rc = dalloc(h, &h->d_scratch2, B)) ||
+      (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4))) {
+    tog_destroy(h);
+    return rc;
+  }
+  b.Sdbg = nullptr;
+  b.sdbg = nullptr;
+  // reference constructor state: X = NaN, U = 0, K = d = 0, λ = 0, μ = μ_init (=1),
+  // ρ = dρ = 0 (ilqr_solver.jl:118-144, augmented_lagrangian_solver.jl:143-169)
+  fill(h, b.x0, B * n, 0.0);
+  fill(h, b.X, B * N * n, NAN);
+  fill(h, b.U, B * (N - 1) * m, 0.0);
+  fill(h, b.Xb, B * N * n, 0.0);
+  fill(h, b.Ub, B * (N - 1) * m, 0.0);
+  fill(h, b.AB, B * (N - 1) * n * (n + m), 0.0);
+  fill(h, b.K, B * (N - 1) * m * n, 0.0);
+  fill(h, b.d, B * (N - 1) * m, 0.0);
+  fill(h, b.lam, B * N * P1, 0.0);
+  fill(h, b.mu, B * N * P1, 1.0);
+  fill(h, b.C, B * N * P1, 0.0);
+  hipLaunchKernelGGL(k_reset_state, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, h->stream, b.st, (long long)B, 1.0);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  *out = h;
+  return TOG_OK;
+}
+
+int32_t tog_set_stream(tog_handle* h, void* s) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  if (h->own_stream) HIPCHECK(hipStreamDestroy(h->stream));
+  if (s) {
+    h->stream = (hipStream_t)s;
+    h->own_stream = false;
+  } else {
+    HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->own_stream = true;
+  }
+  return TOG_OK;
+}
+
+int32_t tog_synchronize(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+int32_t tog_dims(tog_handle* h, int64_t* o) {
+  if (!h || !o) return fail(TOG_ERR_ARG, "null argument");
+  o[0] = h->n;
+  o[1] = h->m;
+  o[2] = h->N;
+  o[3] = h->B;
+  o[4] = h->pmax;
+  o[5] = h->mode;
+  return TOG_OK;
+}
+
+static size_t field_count(tog_handle* h, int field, double** dptr) {
+  const size_t B = h->B, n = h->n, m = h->m, N = h->N, P1 = h->pmax > 0 ? h->pmax : 1;
+  DevBuffers& b = h->buf;
+  switch (field) {
+    case TOG_FIELD_X: *dptr = b.X; return B * N * n;
+    case TOG_FIELD_U: *dptr = b.U; return B * (N - 1) * m;
+    case TOG_FIELD_XBAR: *dptr = b.Xb; return B * N * n;
+    case TOG_FIELD_UBAR: *dptr = b.Ub; return B * (N - 1) * m;
+    case TOG_FIELD_K: *dptr = b.K; return B * (N - 1) * m * n;
+    case TOG_FIELD_D: *dptr = b.d; return B * (N - 1) * m;
+    case TOG_FIELD_LAMBDA: *dptr = b.lam; return B * N * P1;
+    case TOG_FIELD_MU: *dptr = b.mu; return B * N * P1;
+    case TOG_FIELD_C: *dptr = b.C; return B * N * P1;
+    case TOG_FIELD_X0: *dptr = b.x0; return B * n;
+    case TOG_FIELD_S: *dptr = b.Sdbg; return B * N * n * n;
+    case TOG_FIELD_SX: *dptr = b.sdbg; return B * N * n;
+  }
+  *dptr = nullptr;
+  return 0;
+}
+
+int32_t tog_get_device_ptr(tog_handle* h, int32_t field, void** dptr) {
+  if (!h || !dptr) return fail(TOG_ERR_ARG, "null argument");
+  double* p = nullptr;
+  field_count(h, field, &p);
+  if (field == TOG_FIELD_STATS) {
+    *dptr = h->buf.st;
+    return TOG_OK;
+  }
+  if (!p) return fail(TOG_ERR_ARG, "field has no device buffer");
+  *dptr = p;
+  return TOG_OK;
+}
+
+static int get_states(tog_handle* h, std::vector<TrajState>& st) {
+  st.resize(h->B);
+  HIPCHECK(hipMemcpyAsync(st.data(), h->buf.st, sizeof(TrajState) * h->B, hipMemcpyDeviceToHost, h->stream));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+static int put_states(tog_handle* h, const std::vector<TrajState>& st) {
+  HIPCHECK(hipMemcpyAsync(h->buf.st, st.data(), sizeof(TrajState) * h->B, hipMemcpyHostToDevice, h->stream));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+int32_t tog_get(tog_handle* h, int32_t field, double* out) {
+  if (!h || !out) return fail(TOG_ERR_ARG, "null argument");
+  HIPCHECK(hipSetDevice(h->device));
+  const size_t n = h->n, m = h->m, N = h->N, B = h->B;
+  DevBuffers& b = h->buf;
+  if (field == TOG_FIELD_A || field == TOG_FIELD_B) {
+    // strided extraction of ∇F[k].xx / .xu from the [A|B] blocks
+    const size_t L = n + m, cols = (field == TOG_FIELD_A) ? n : m, c0 = (field == TOG_FIELD_A) ? 0 : n;
+    HIPCHECK(hipMemcpy2DAsync(out, sizeof(double) * n * cols, b.AB + c0 * n, sizeof(double) * n * L,
+                              sizeof(double) * n * cols, B * (N - 1), hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    return TOG_OK;
+  }
+  if (field == TOG_FIELD_STATS || field == TOG_FIELD_DV || field == TOG_FIELD_RHO) {
+    std::vector<TrajState> st;
+    int rc = get_states(h, st);
+    if (rc) return rc;
+    for (size_t i = 0; i < B; i++) {
+      const TrajState& s = st[i];
+      if (field == TOG_FIELD_DV) {
+        out[2 * i] = s.dV0;
+        out[2 * i + 1] = s.dV1;
+      } else if (field == TOG_FIELD_RHO) {
+        out[2 * i] = s.rho;
+        out[2 * i + 1] = s.drho;
+      } else {
+        double* o = out + i * TOG_NSTATS;
+        for (int j = 0; j < TOG_NSTATS; j++) o[j] = 0.0;
+        o[TOG_STAT_J] = s.J;
+        o[TOG_STAT_DJ] = s.dJ;
+        o[TOG_STAT_GRADIENT] = s.grad;
+        o[TOG_STAT_ITERATIONS] = s.iters;
+        o[TOG_STAT_ZERO_COUNT] = s.zero_cnt;
+        o[TOG_STAT_ALPHA] = s.alpha;
+        o[TOG_STAT_Z] = s.z;
+        o[TOG_STAT_C_MAX] = s.c_max;
+        o[TOG_STAT_AL_ITER] = s.al_iter;
+        o[TOG_STAT_TOTAL_STEPS] = s.total_steps;
+        o[TOG_STAT_LS_TRIALS] = s.ls_trials;
+        o[TOG_STAT_BP_RESTARTS] = s.bp_restarts;
+        o[TOG_STAT_FLAGS] = s.flags | (s.active ? TOG_TRAJ_ACTIVE : 0);
+        o[TOG_STAT_PENALTY_MAX] = s.mu_max;
+      }
+    }
+    return TOG_OK;
+  }
+  double* p = nullptr;
+  size_t count = field_count(h, field, &p);
+  if (!p) return fail(TOG_ERR_ARG, "field not available (S/SX need a backward pass with TOG_BP_STORE_S)");
+  HIPCHECK(hipMemcpyAsync(out, p, sizeof(double) * count, hipMemcpyDeviceToHost, h->stream));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+int32_t tog_set(tog_handle* h, int32_t field, const double* in) {
+  if (!h || !in) return fail(TOG_ERR_ARG, "null argument");
+  HIPCHECK(hipSetDevice(h->device));
+  if (field == TOG_FIELD_DV || field == TOG_FIELD_RHO) {
+    std::vector<TrajState> st;
+    int rc = get_states(h, st);
+    if (rc) return rc;
+    for (size_t i = 0; i < (size_t)h->B; i++) {
+      if (field == TOG_FIELD_DV) {
+        st[i].dV0 = in[2 * i];
+        st[i].dV1 = in[2 * i + 1];
+      } else {
+        st[i].rho = in[2 * i];
+        st[i].drho = in[2 * i + 1];
+      }
+    }
+    return put_states(h, st);
+  }
+  if (field == TOG_FIELD_A || field == TOG_FIELD_B || field == TOG_FIELD_STATS)
+    return fail(TOG_ERR_ARG, "field is read-only");
+  double* p = nullptr;
+  size_t count = field_count(h, field, &p);
+  if (!p) return fail(TOG_ERR_ARG, "field not settable");
+  HIPCHECK(hipMemcpyAsync(p, in, sizeof(double) * count, hipMemcpyHostToDevice, h->stream));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+int32_t tog_set_state(tog_handle* h, const double* x0, const double* U, const double* X) {
+  if (!h || !x0 || !U) return fail(TOG_ERR_ARG, "null argument");
+  HIPCHECK(hipSetDevice(h->device));
+  const size_t n = h->n, m = h->m, N = h->N, B = h->B;
+  HIPCHECK(hipMemcpyAsync(h->buf.x0, x0, sizeof(double) * B * n, hipMemcpyHostToDevice, h->stream));
+  HIPCHECK(hipMemcpyAsync(h->buf.U, U, sizeof(double) * B * (N - 1) * m, hipMemcpyHostToDevice, h->stream));
+  if (X)
+    HIPCHECK(hipMemcpyAsync(h->buf.X, X, sizeof(double) * B * N * n, hipMemcpyHostToDevice, h->stream));
+  else
+    fill(h, h->buf.X, B * N * n, NAN);
+  hipLaunchKernelGGL(k_reset_state, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, h->stream, h->buf.st, (long long)B,
+                     1.0);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+// ------------------------------------------------------------------------------ step level
+int32_t tog_rollout_open_loop(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  h->ops->rollout_open(h->dP, h->buf, h->B, h->integ, h->stream);
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_jacobians(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream);
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_update_constraints(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  h->ops->update_constraints(h->dP, h->buf, h->B, h->stream);
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_cost(tog_handle* h, int32_t al, double* J_out) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  h->ops->cost(h->dP, h->buf, h->B, al, 0, h->d_scratch, h->stream);
+  HIPCHECK(hipGetLastError());
+  if (J_out) {
+    HIPCHECK(hipMemcpyAsync(J_out, h->d_scratch, sizeof(double) * h->B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+  }
+  return TOG_OK;
+}
+
+int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, double* dV_out) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  if (sq && !h->hostP.sqrt_ok) return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass");
+  if ((flags & TOG_BP_STORE_S) && !h->buf.Sdbg) {
+    int rc;
+    const size_t B = h->B, n = h->n, N = h->N;
+    if ((rc = dalloc(h, &h->buf.Sdbg, B * N * n * n)) || (rc = dalloc(h, &h->buf.sdbg, B * N * n))) return rc;
+  }
+  h->ops->backward(h->dP, h->buf, h->B, sq, al, flags, h->stream);
+  HIPCHECK(hipGetLastError());
+  if (dV_out) return tog_get(h, TOG_FIELD_DV, dV_out);
+  return TOG_OK;
+}
+
+int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double* J_out) {
+  if (!h || !J_prev) return fail(TOG_ERR_ARG, "null argument");
+  HIPCHECK(hipSetDevice(h->device));
+  HIPCHECK(hipMemcpyAsync(h->d_scratch, J_prev, sizeof(double) * h->B, hipMemcpyHostToDevice, h->stream));
+  h->ops->forward(h->dP, h->buf, h->B, h->integ, al ? TOG_MODE_AL : TOG_MODE_ILQR, 0, h->d_scratch, h->d_scratch2,
+                  h->stream);
+  HIPCHECK(hipGetLastError());
+  if (J_out) {
+    HIPCHECK(hipMemcpyAsync(J_out, h->d_scratch2, sizeof(double) * h->B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+  }
+  return TOG_OK;
+}
+
+int32_t tog_rollout(tog_handle* h, double alpha, int32_t* ok_out) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  h->ops->rollout(h->dP, h->buf, h->B, h->integ, alpha, h->d_iscratch, h->stream);
+  HIPCHECK(hipGetLastError());
+  if (ok_out) {
+    HIPCHECK(hipMemcpyAsync(ok_out, h->d_iscratch, sizeof(int) * h->B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+  }
+  return TOG_OK;
+}
+
+// ------------------------------------------------------------------------------ solve level
+int32_t tog_solve_init(tog_handle* h, int32_t mode) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (mode != TOG_MODE_ILQR && mode != TOG_MODE_AL) return fail(TOG_ERR_ARG, "mode");
+  HIPCHECK(hipSetDevice(h->device));
+  h->mode = mode;
+  h->ops->init(h->dP, h->buf, h->B, h->integ, mode, h->stream);
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  const int al = (h->mode == TOG_MODE_AL);
+  for (int i = 0; i < nsteps; i++) {
+    timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
+    timed(h, TOG_KERNEL_BACKWARD,
+          [&] { h->ops->backward(h->dP, h->buf, h->B, h->opts.square_root, al, 0, h->stream); });
+    timed(h, TOG_KERNEL_FORWARD,
+          [&] { h->ops->forward(h->dP, h->buf, h->B, h->integ, h->mode, 1, nullptr, nullptr, h->stream); });
+  }
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_batch_stats_device(tog_handle* h, void* dptr3) {
+  if (!h || !dptr3) return fail(TOG_ERR_ARG, "null argument");
+  HIPCHECK(hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_batch_stats, dim3(1), dim3(1024), 0, h->stream, h->buf.st, (long long)h->B, (double*)dptr3);
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_batch_stats(tog_handle* h, double* out3) {
+  if (!h || !out3) return fail(TOG_ERR_ARG, "null argument");
+  int rc = tog_batch_stats_device(h, h->d_stats);
+  if (rc) return rc;
+  HIPCHECK(hipMemcpyAsync(out3, h->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, h->stream));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+int32_t tog_total_steps(tog_handle* h, int64_t* out) {
+  if (!h || !out) return fail(TOG_ERR_ARG, "null argument");
+  std::vector<TrajState> st;
+  int rc = get_states(h, st);
+  if (rc) return rc;
+  int64_t t = 0;
+  for (const auto& s : st) t += s.total_steps;
+  *out = t;
+  return TOG_OK;
+}
+
+int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps) {
+  int rc = tog_solve_init(h, mode);
+  if (rc) return rc;
+  const int chunk = 4;
+  double stats[3];
+  for (int done = 0; done < max_steps; done += chunk) {
+    rc = tog_solve_step(h, chunk < max_steps - done ? chunk : max_steps - done);
+    if (rc) return rc;
+    rc = tog_batch_stats(h, stats);
+    if (rc) return rc;
+    if (stats[0] == 0.0) break;
+  }
+  return TOG_OK;
+}
+
+int32_t tog_profile(tog_handle* h, int32_t enable) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  HIPCHECK(hipSetDevice(h->device));
+  if (enable) {
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    h->ev_used = 0;
+    h->ev_kind.clear();
+  }
+  h->profiling = enable != 0;
+  return TOG_OK;
+}
+
+int32_t tog_profile_read(tog_handle* h, double* total_ms, int64_t* launches) {
+  if (!h || !total_ms || !launches) return fail(TOG_ERR_ARG, "null argument");
+  HIPCHECK(hipSetDevice(h->device));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  for (int i = 0; i < TOG_NKERNELS; i++) {
+    total_ms[i] = 0.0;
+    launches[i] = 0;
+  }
+  for (size_t p = 0; p < h->ev_kind.size(); p++) {
+    float ms = 0.f;
+    HIPCHECK(hipEventElapsedTime(&ms, h->ev_pool[2 * p], h->ev_pool[2 * p + 1]));
+    total_ms[h->ev_kind[p]] += ms;
+    launches[h->ev_kind[p]] += 1;
+  }
+  return TOG_OK;
+}
+
+int32_t tog_status(tog_handle* h, int32_t* flags_out) {
+  if (!h || !flags_out) return fail(TOG_ERR_ARG, "null argument");
+  std::vector<TrajState> st;
+  int rc = get_states(h, st);
+  if (rc) return rc;
+  for (size_t i = 0; i < st.size(); i++) flags_out[i] = st[i].flags | (st[i].active ? TOG_TRAJ_ACTIVE : 0);
+  return TOG_OK;
+}
+
+}  // extern "C"

@@ -136,6 +136,15 @@ class BatchHandle:
         abi.check(self.lib, self.lib.tog_total_steps(self.h, C.byref(v)))
         return int(v.value)
 
+    def profile(self, enable: bool):
+        abi.check(self.lib, self.lib.tog_profile(self.h, int(bool(enable))))
+
+    def profile_read(self):
+        ms = np.zeros(abi.NKERNELS)
+        cnt = (C.c_int64 * abi.NKERNELS)()
+        abi.check(self.lib, self.lib.tog_profile_read(self.h, abi.as_dp(ms), cnt))
+        return ms, np.array(list(cnt), dtype=np.int64)
+
     def synchronize(self):
         abi.check(self.lib, self.lib.tog_synchronize(self.h))
 
