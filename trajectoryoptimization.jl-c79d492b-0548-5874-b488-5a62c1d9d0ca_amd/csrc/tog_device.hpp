@@ -50,6 +50,9 @@ struct DevProblem {
   // cholesky(Q*dt).U, cholesky(R*dt).U, cholesky(Qf).U — identical at every knot, factored once.
   double cQ[NMAX * NMAX], cR[MMAX * MMAX], cQf[NMAX * NMAX];
   int sqrt_ok;  // 0 if one of the Hessians is not PD (reference: error(...))
+  // structure flags: Q, R, Qf diagonal and H == 0. The dense fma loops then only ever add exact
+  // zeros off the diagonal, so the diagonal fast paths are bit-identical to them.
+  int diag_cost;
   int pad1;
   const int* knot_off;  // [N] first row of knot k
   const int* knot_cnt;  // [N] rows at knot k (p_k)
@@ -69,6 +72,12 @@ struct TrajState {
   int iters, zero_cnt, al_iter, total_steps, ls_trials, bp_restarts, flags, active;
 };
 
+// the regularisation scalars the backward pass mutates (kept in registers)
+struct RegState {
+  double rho, drho;
+  int flags;
+};
+
 struct DevBuffers {
   double* x0;   // (n, B)
   double* X;    // (n, N, B)
@@ -84,6 +93,9 @@ struct DevBuffers {
   double* Sdbg; // (n, n, N, B) or null
   double* sdbg; // (n, N, B) or null
   double* Qscr; // (nq, N, B) accumulated Q blocks for the restart replay path
+  double* lsJ;  // (NC, B) speculative line-search trial costs
+  int* lsok;    // (NC, B) speculative line-search trial rollout status
+  int nc;       // candidates evaluated per trajectory per launch (<= 64)
   TrajState* st;
 };
 
@@ -451,41 +463,53 @@ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, dou
 template <int n, int m>
 __device__ __forceinline__ double stage_cost(const DevProblem* P, const double* x, const double* u) {
   double xQx = 0.0, uRu = 0.0, qx = 0.0, ru = 0.0, uHx = 0.0;
+  if (P->diag_cost) {
+#pragma unroll
+    for (int j = 0; j < n; j++) xQx = fma((0.5 * x[j]) * P->Q[j + n * j], x[j], xQx);
+#pragma unroll
+    for (int j = 0; j < m; j++) uRu = fma((0.5 * u[j]) * P->R[j + m * j], u[j], uRu);
+  } else {
 #pragma unroll 1
-  for (int j = 0; j < n; j++) {
-    double t = 0.0;
-    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Q[i + n * j], t);
-    xQx = fma(t, x[j], xQx);
+    for (int j = 0; j < n; j++) {
+      double t = 0.0;
+      for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Q[i + n * j], t);
+      xQx = fma(t, x[j], xQx);
+    }
+#pragma unroll 1
+    for (int j = 0; j < m; j++) {
+      double t = 0.0;
+      for (int i = 0; i < m; i++) t = fma(0.5 * u[i], P->R[i + m * j], t);
+      uRu = fma(t, u[j], uRu);
+    }
+#pragma unroll 1
+    for (int j = 0; j < n; j++) {
+      double t = 0.0;
+      for (int i = 0; i < m; i++) t = fma(u[i], P->H[i + m * j], t);
+      uHx = fma(t, x[j], uHx);
+    }
   }
-#pragma unroll 1
-  for (int j = 0; j < m; j++) {
-    double t = 0.0;
-    for (int i = 0; i < m; i++) t = fma(0.5 * u[i], P->R[i + m * j], t);
-    uRu = fma(t, u[j], uRu);
-  }
-#pragma unroll 1
+#pragma unroll
   for (int i = 0; i < n; i++) qx = fma(P->q[i], x[i], qx);
-#pragma unroll 1
+#pragma unroll
   for (int i = 0; i < m; i++) ru = fma(P->r[i], u[i], ru);
-#pragma unroll 1
-  for (int j = 0; j < n; j++) {
-    double t = 0.0;
-    for (int i = 0; i < m; i++) t = fma(u[i], P->H[i + m * j], t);
-    uHx = fma(t, x[j], uHx);
-  }
   return ((((xQx + uRu) + qx) + ru) + P->c + uHx) * P->dt;
 }
 
 template <int n>
 __device__ __forceinline__ double terminal_cost(const DevProblem* P, const double* x) {
   double xQx = 0.0, qx = 0.0;
+  if (P->diag_cost) {
+#pragma unroll
+    for (int j = 0; j < n; j++) xQx = fma((0.5 * x[j]) * P->Qf[j + n * j], x[j], xQx);
+  } else {
 #pragma unroll 1
-  for (int j = 0; j < n; j++) {
-    double t = 0.0;
-    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Qf[i + n * j], t);
-    xQx = fma(t, x[j], xQx);
+    for (int j = 0; j < n; j++) {
+      double t = 0.0;
+      for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Qf[i + n * j], t);
+      xQx = fma(t, x[j], xQx);
+    }
   }
-#pragma unroll 1
+#pragma unroll
   for (int i = 0; i < n; i++) qx = fma(P->qf[i], x[i], qx);
   return (xQx + qx) + P->cf;
 }
@@ -531,13 +555,15 @@ __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n,
 }
 
 // regularization_update! (ilqr_methods.jl:164-176)
-__device__ __forceinline__ void reg_increase(const DevProblem* P, TrajState& s) {
+template <class St>
+__device__ __forceinline__ void reg_increase(const DevProblem* P, St& s) {
   const double f = P->o.bp_reg_increase_factor;
   s.drho = fmax(s.drho * f, f);
   s.rho = fmax(s.rho * s.drho, P->o.bp_reg_min);
   if (s.rho > P->o.bp_reg_max) s.flags |= TOG_TRAJ_MAX_REG;
 }
-__device__ __forceinline__ void reg_decrease(const DevProblem* P, TrajState& s) {
+template <class St>
+__device__ __forceinline__ void reg_decrease(const DevProblem* P, St& s) {
   const double f = P->o.bp_reg_increase_factor;
   s.drho = fmin(s.drho / f, 1.0 / f);
   const double rd = s.rho * s.drho;

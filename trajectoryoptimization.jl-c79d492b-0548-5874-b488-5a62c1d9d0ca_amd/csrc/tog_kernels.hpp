@@ -423,6 +423,13 @@ struct BwdLds {
   double cx[PCAP * n];
   double cu[PCAP * m];
   double red[WAVE];
+  // lane-0 serial scratch (kept in LDS: private arrays with runtime indexing spill to scratch memory)
+  double G[m * m];
+  double Uc[m * m];
+  double Wl[(m + n) * m];
+  double Ri[m * m];
+  double Aj[m * m];
+  double vv[m];
   int piv[m];
   int flag;
   int pad;
@@ -617,16 +624,26 @@ __device__ __forceinline__ void lu_factor(double* F, int* piv) {
 }
 template <int m>
 __device__ __forceinline__ void lu_solve_col(const double* F, const int* piv, double* bcol) {
-  for (int k = 0; k < m; k++)
-    if (piv[k] != k) {
-      const double t = bcol[k];
-      bcol[k] = bcol[piv[k]];
-      bcol[piv[k]] = t;
-    }
+  // (fully unrolled so that bcol lives in registers)
+#pragma unroll
+  for (int k = 0; k < m; k++) {
+    const int p = piv[k];
+#pragma unroll
+    for (int i = k + 1; i < m; i++)
+      if (i == p) {  // compile-time indices only: bcol stays in registers
+        const double t = bcol[k];
+        bcol[k] = bcol[i];
+        bcol[i] = t;
+      }
+  }
+#pragma unroll
   for (int j = 0; j < m; j++)
+#pragma unroll
     for (int i = j + 1; i < m; i++) bcol[i] = fma(-F[i + m * j], bcol[j], bcol[i]);
+#pragma unroll
   for (int j = m - 1; j >= 0; j--) {
     bcol[j] /= F[j + m * j];
+#pragma unroll
     for (int i = 0; i < j; i++) bcol[i] = fma(-F[i + m * j], bcol[j], bcol[i]);
   }
 }
@@ -635,8 +652,7 @@ __device__ __forceinline__ void lu_solve_col(const double* F, const int* piv, do
 // Exact decision via Frobenius bounds cond_2 <= ‖R‖_F‖R⁻¹‖_F <= m·cond_2; a one-sided Jacobi SVD
 // settles the (rare) ambiguous band. Lane 0 only.
 template <int m>
-__device__ bool cond_exceeds(const double* Rm, double thresh) {
-  double Ri[m * m];
+__device__ bool cond_exceeds(const double* Rm, double thresh, double* Ri, double* A) {
   for (int i = 0; i < m * m; i++) Ri[i] = 0.0;
   for (int c = 0; c < m; c++) {
     Ri[c + m * c] = 1.0;
@@ -655,7 +671,6 @@ __device__ bool cond_exceeds(const double* Rm, double thresh) {
   if (cF <= thresh) return false;
   if (cF / m > thresh) return true;
   // ambiguous: one-sided Jacobi singular values
-  double A[m * m];
   for (int i = 0; i < m * m; i++) A[i] = Rm[i];
   for (int sweep = 0; sweep < 60; sweep++) {
     double off = 0.0;
@@ -700,8 +715,11 @@ __global__ void __launch_bounds__(64) k_backward(const DevProblem* __restrict__ 
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
   const int N = P->N;
-  TrajState s = Bf.st[b];
-  if (!s.active) return;
+  if (!Bf.st[b].active) return;
+  RegState s;
+  s.rho = Bf.st[b].rho;
+  s.drho = Bf.st[b].drho;
+  s.flags = Bf.st[b].flags;
   const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
   const double* Xg = Bf.X + (size_t)b * N * n;
   const double* Ug = Bf.U + (size_t)b * (N - 1) * m;
@@ -811,7 +829,7 @@ attempt:
     // ---- regularisation (backward_pass.jl:38-48 / :120-126) and the restart test
     if (!SQRT) {
       if (lane == 0) {
-        double G[m * m];
+        double* G = sh.G;
         for (int e = 0; e < m * m; e++) G[e] = sh.Quu[e];
         if (!state_reg) {
           for (int i = 0; i < m; i++) G[i + m * i] += s.rho;
@@ -824,7 +842,7 @@ attempt:
             }
         }
         // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle
-        double U[m * m];
+        double* U = sh.Uc;
         bool pd = true;
         for (int j = 0; j < m && pd; j++) {
           double d0 = G[j + m * j];
@@ -851,7 +869,7 @@ attempt:
       if (lane == 0) {
         // Quu_reg = qr([Q.uu; sqrt(ρ)*I]).R  (:control)  or  qr([Q.uu; sqrt(ρ)*B]).R  (:state)
         const int rows = state_reg ? m + n : 2 * m;
-        double Wl[(m + n) * m];
+        double* Wl = sh.Wl;
         for (int j = 0; j < m; j++)
           for (int i = 0; i < rows; i++) {
             double v;
@@ -881,7 +899,7 @@ attempt:
         }
         for (int j = 0; j < m; j++)
           for (int i = 0; i < m; i++) sh.F[i + m * j] = (i <= j) ? Wl[i + rows * j] : 0.0;
-        sh.flag = cond_exceeds<m>(sh.F, 1e8) ? 0 : 1;
+        sh.flag = cond_exceeds<m>(sh.F, 1e8, sh.Ri, sh.Aj) ? 0 : 1;
       }
     }
     wsync();
@@ -930,14 +948,18 @@ attempt:
         lu_solve_col<m>(sh.F, sh.piv, col);
       } else {
         // Quu_reg' \ col (forward substitution), then Quu_reg \ (back substitution)
+#pragma unroll
         for (int j = 0; j < m; j++) {
           const double xj = col[j] / sh.F[j + m * j];
           col[j] = xj;
+#pragma unroll
           for (int i = j + 1; i < m; i++) col[i] = fma(-sh.F[j + m * i], xj, col[i]);
         }
+#pragma unroll
         for (int j = m - 1; j >= 0; j--) {
           const double xj = col[j] / sh.F[j + m * j];
           col[j] = xj;
+#pragma unroll
           for (int i = j - 1; i >= 0; i--) col[i] = fma(-sh.F[i + m * j], xj, col[i]);
         }
       }
@@ -1018,9 +1040,11 @@ attempt:
         double col[n];
 #pragma unroll
         for (int i = 0; i < n; i++) col[i] = sh.Qux[c + m * i];
+#pragma unroll
         for (int j = 0; j < n; j++) {
           const double xj = col[j] / sh.Qxx[j + n * j];
           col[j] = xj;
+#pragma unroll
           for (int i = j + 1; i < n; i++) col[i] = fma(-sh.Qxx[j + n * i], xj, col[i]);
         }
 #pragma unroll
@@ -1040,7 +1064,8 @@ attempt:
       }
       // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! with each row of tmp1 (backward_pass.jl:186-192)
       if (lane == 0) {
-        double U[m * m], v[m];
+        double* U = sh.Uc;
+        double* v = sh.vv;
         for (int e = 0; e < m * m; e++) U[e] = sh.Quu[e];
         bool okd = true;
         for (int r = 0; r < n && okd; r++) {
@@ -1110,101 +1135,171 @@ attempt:
   }
   reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
   if (lane == 0) {
-    s.dV0 = dV0;
-    s.dV1 = dV1;
-    s.bp_restarts = restarts + (faithful ? 1 : 0);
-    Bf.st[b] = s;
+    TrajState& g = Bf.st[b];
+    g.rho = s.rho;
+    g.drho = s.drho;
+    g.flags = s.flags;
+    g.dV0 = dV0;
+    g.dV1 = dV1;
+    g.bp_restarts = restarts + (faithful ? 1 : 0);
   }
 }
 
 // =============================================================================================
-// k_forward: forwardpass! + solve! bookkeeping + AL outer update; one thread per trajectory
+// k_forward: forwardpass! + solve! bookkeeping + AL outer update.
+//
+// The reference's backtracking line search (forward_pass.jl:19-65) tries α = 1, 1/2, 1/4, ... one
+// rollout at a time. Trial j always uses α = 2^-j, and whether it is accepted depends only on its own
+// rollout (ok_j, J_j) and on the trials before it. So a FTEAM-lane team per trajectory evaluates
+// FTEAM trials speculatively in one round (cost only, no writes), lane 0 replays the sequential
+// acceptance logic over (ok_j, J_j) in order -- bit-identical decisions -- and the accepted α is
+// replayed once more, writing the new trajectory in place. One round covers iterations_linesearch=20.
 // =============================================================================================
-template <class M, int INTEG>
-__device__ double forward_line_search(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b,
-                                      TrajState& s, double J_prev, bool al) {
-  const tog_options& o = P->o;
-  constexpr int n = M::n, m = M::m;
-  const int N = P->N;
-  double* C = al ? Bf.C + (size_t)b * N * P->pmax : nullptr;
-  double J = INFINITY, alpha = 1.0, z = -1.0, expected = 0.0;
-  int iter = 0, trials = 0;
-  while ((z <= o.line_search_lower_bound || z > o.line_search_upper_bound) && J >= J_prev) {
-    if (iter > o.iterations_linesearch) {
-      double* Xb = Bf.Xb + (size_t)b * N * n;
-      double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
-      const double* X = Bf.X + (size_t)b * N * n;
-      const double* U = Bf.U + (size_t)b * (N - 1) * m;
-      for (int i = 0; i < N * n; i++) Xb[i] = X[i];
-      for (int i = 0; i < (N - 1) * m; i++) Ub[i] = U[i];
-      J = traj_cost<M>(P, Bf, b, Xb, Ub, al, C);
-      z = 0.0;
-      alpha = 0.0;
-      expected = 0.0;
-      reg_increase(P, s);
-      s.rho += o.bp_reg_fp;
-      break;
-    }
-    const bool ok = traj_rollout<M, INTEG>(P, Bf, b, alpha);
-    trials++;
-    if (!ok) {
-      iter++;
-      alpha /= 2.0;
-      continue;
-    }
-    J = traj_cost<M>(P, Bf, b, Bf.Xb + (size_t)b * N * n, Bf.Ub + (size_t)b * (N - 1) * m, al, C);
-    expected = -alpha * (s.dV0 + alpha * s.dV1);
-    z = (expected > 0.0) ? (J_prev - J) / expected : -1.0;
-    iter++;
-    alpha /= 2.0;
-  }
-  s.alpha = 2.0 * alpha;
-  s.z = z;
-  s.expected = expected;
-  s.ls_trials = trials;
-  if (J > J_prev) s.flags |= TOG_TRAJ_COST_INCREASED;
-  return J;
+constexpr int FTEAM = 32;
+
+__device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS traffic within the wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <class M, int INTEG>
-__global__ void __launch_bounds__(64) k_forward(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
-                                                int bookkeeping, const double* Jprev_in, double* Jout) {
-  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= P->B) return;
+// One closed-loop rollout at α (src/rollout.jl:2-23) fused with the cost of the rolled-out
+// trajectory (objective.jl:40-48 / AL cost augmented_lagrangian_methods.jl:298-313), summed in the
+// oracle's order. WMODE 0: cost only. WMODE 1: also write X̄, Ū. WMODE 2: write the new trajectory in
+// place into X, U (the accepted step; old X[k] is read before it is overwritten) and return the
+// todorov gradient of the new U (ilqr_methods.jl:122-129).
+template <class M, int INTEG, int WMODE>
+__device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha,
+                             bool al, double& Jout, double* grad_out) {
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
-  TrajState s = Bf.st[b];
-  if (!s.active) return;
-  const bool al = (mode == TOG_MODE_AL);
-  const double J_prev = bookkeeping ? s.J : Jprev_in[b];
-  const double J = forward_line_search<M, INTEG>(P, Bf, b, s, J_prev, al);
-  if (Jout) Jout[b] = J;
-  if (!bookkeeping) {
-    Bf.st[b] = s;
-    return;
+  double* X = Bf.X + (size_t)b * N * n;
+  double* U = Bf.U + (size_t)b * (N - 1) * m;
+  const double* K = Bf.K + (size_t)b * (N - 1) * m * n;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  double* Xb = Bf.Xb + (size_t)b * N * n;
+  double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
+  const double* lam = Bf.lam + (size_t)b * N * pmax;
+  const double* mu = Bf.mu + (size_t)b * N * pmax;
+  const double smax = P->o.max_state_value, umax = P->o.max_control_value;
+  double xb[n], xold[n], ub[m], xn[n];
+  double J = 0.0, Jc = 0.0, gsum = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    xb[i] = Bf.x0[(size_t)b * n + i];
+    xold[i] = X[i];
+    if (WMODE == 1) Xb[i] = xb[i];
+    if (WMODE == 2) X[i] = xb[i];
   }
+  for (int k = 1; k < N; k++) {
+    const double* Kk = K + (size_t)(k - 1) * m * n;
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      double t = 0.0;
+#pragma unroll
+      for (int j = 0; j < n; j++) t = fma(Kk[i + m * j], xb[j] - xold[j], t);
+      ub[i] = (U[(size_t)(k - 1) * m + i] + t) + alpha * d[(size_t)(k - 1) * m + i];
+    }
+    if (WMODE == 1) {
+#pragma unroll
+      for (int i = 0; i < m; i++) Ub[(size_t)(k - 1) * m + i] = ub[i];
+    }
+    if (WMODE == 2) {
+      double mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        U[(size_t)(k - 1) * m + i] = ub[i];
+        const double v = fabs(d[(size_t)(k - 1) * m + i]) / (fabs(ub[i]) + 1.0);
+        if (v > mx || isnan(v)) mx = v;
+      }
+      gsum += mx;
+    }
+    // stage cost and AL terms of knot k-1 (x̄_{k-1}, ū_{k-1})
+    J += stage_cost<n, m>(P, xb, ub);
+    if (al) {
+      const int cnt = P->knot_cnt[k - 1];
+      if (cnt) {
+        const ConRow* rows = P->rows + P->knot_off[k - 1];
+        double lc = 0.0, cIc = 0.0;
+        for (int i = 0; i < cnt; i++) {
+          const double c = row_value(rows[i], xb, ub);
+          const double l = lam[(size_t)(k - 1) * pmax + i];
+          const bool a = row_inequality(rows[i]) ? ((c >= 0.0) || (l > 0.0)) : true;
+          const double w = a ? mu[(size_t)(k - 1) * pmax + i] : 0.0;
+          lc = fma(l, c, lc);
+          cIc = fma(c * w, c, cIc);
+        }
+        Jc += lc + 0.5 * cIc;
+      }
+    }
+    discrete_step<M, INTEG>(xn, xb, ub, P->dt);
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      xb[i] = xn[i];
+      ok = ok && (fabs(xn[i]) < smax);
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) ok = ok && (fabs(ub[i]) < umax);
+    if (WMODE == 2) {
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        xold[i] = X[(size_t)k * n + i];
+        X[(size_t)k * n + i] = xn[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < n; i++) xold[i] = X[(size_t)k * n + i];
+      if (WMODE == 1) {
+#pragma unroll
+        for (int i = 0; i < n; i++) Xb[(size_t)k * n + i] = xn[i];
+      }
+    }
+    if (!ok) return false;
+  }
+  J += terminal_cost<n>(P, xb);
+  if (al) {
+    const int cnt = P->knot_cnt[N - 1];
+    if (cnt) {
+      const ConRow* rows = P->rows + P->knot_off[N - 1];
+      double lc = 0.0, cIc = 0.0;
+      for (int i = 0; i < cnt; i++) {
+        const double c = row_value(rows[i], xb, nullptr);
+        const double l = lam[(size_t)(N - 1) * pmax + i];
+        const bool a = row_inequality(rows[i]) ? ((c >= 0.0) || (l > 0.0)) : true;
+        const double w = a ? mu[(size_t)(N - 1) * pmax + i] : 0.0;
+        lc = fma(l, c, lc);
+        cIc = fma(c * w, c, cIc);
+      }
+      Jc += lc + 0.5 * cIc;
+    }
+    J = J + Jc;
+  }
+  Jout = J;
+  if (grad_out) *grad_out = gsum / N;
+  return true;
+}
+
+// solve! bookkeeping after an accepted forward pass (ilqr_methods.jl:21-42) and the AL outer update
+// when the inner solve finished (augmented_lagrangian_methods.jl:53-126). One lane per trajectory.
+template <class M>
+__device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, TrajState& s,
+                                 double J, bool copied, double grad, int mode) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
   const tog_options& o = P->o;
+  const bool al = (mode == TOG_MODE_AL);
   s.total_steps++;
   bool inner_done = false;
-  if (s.flags & TOG_TRAJ_COST_INCREASED) {  // reference: error(...) terminates the solve
-    s.active = 0;
-    Bf.st[b] = s;
-    return;
-  }
   if (J > o.max_cost_value) {  // ilqr_methods.jl:25-28 (@warn, return without copying X̄)
     s.flags |= TOG_TRAJ_COST_BLOWUP;
     inner_done = true;
   } else {
-    double* X = Bf.X + (size_t)b * N * n;
-    double* U = Bf.U + (size_t)b * (N - 1) * m;
-    const double* Xb = Bf.Xb + (size_t)b * N * n;
-    const double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
-    for (int i = 0; i < N * n; i++) X[i] = Xb[i];
-    for (int i = 0; i < (N - 1) * m; i++) U[i] = Ub[i];
+    (void)copied;
     s.dJ = fabs(J - s.J);
     s.J = J;
     s.iters++;
-    s.grad = traj_gradient<M>(P, Bf, b);
+    s.grad = grad;
     s.zero_cnt = (s.dJ == 0.0) ? s.zero_cnt + 1 : 0;
     // evaluate_convergence (ilqr_methods.jl:139-162)
     if ((0.0 < s.dJ && s.dJ < s.cost_tol) || s.grad < s.grad_tol || s.iters >= o.iterations ||
@@ -1213,53 +1308,150 @@ __global__ void __launch_bounds__(64) k_forward(const DevProblem* __restrict__ P
       if (s.iters >= o.iterations) s.flags |= TOG_TRAJ_MAX_ITERS;
     }
   }
-  if (inner_done) {
-    if (!al) {
-      s.flags |= TOG_TRAJ_CONVERGED;
-      s.active = 0;
+  if (!inner_done) return;
+  if (!al) {
+    s.flags |= TOG_TRAJ_CONVERGED;
+    s.active = 0;
+    return;
+  }
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  double* C = Bf.C + (size_t)b * N * pmax;
+  double* lam = Bf.lam + (size_t)b * N * pmax;
+  double* mu = Bf.mu + (size_t)b * N * pmax;
+  (void)traj_cost<M>(P, Bf, b, X, U, true, C);  // J = cost(prob): updates C
+  double mumax = 0.0;
+  for (int k = 0; k < N; k++) {
+    const int cnt = P->knot_cnt[k];
+    const ConRow* rows = P->rows + P->knot_off[k];
+    for (int i = 0; i < cnt; i++) {
+      const size_t q = (size_t)k * pmax + i;
+      double l = lam[q] + mu[q] * C[q];  // dual_update! (:107-118)
+      l = fmax(o.dual_min, fmin(o.dual_max, l));
+      if (row_inequality(rows[i])) l = fmax(0.0, l);
+      lam[q] = l;
+      mu[q] = fmax(0.0, fmin(o.penalty_max, o.penalty_scaling * mu[q]));  // penalty_update! (:121-126)
+      mumax = fmax(mumax, mu[q]);
+    }
+  }
+  s.mu_max = mumax;
+  s.c_max = traj_max_violation(P, Bf, b);
+  const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (s.c_max < o.constraint_tolerance);
+  if (conv) {
+    s.flags |= TOG_TRAJ_AL_CONVERGED;
+    s.active = 0;
+  } else if (s.al_iter >= o.al_iterations) {
+    s.flags |= TOG_TRAJ_AL_MAX_ITERS;
+    s.active = 0;
+  } else {
+    // next outer iteration: reset!(solver_uncon), set_tolerances!, solve! init (rollout is a no-op)
+    s.al_iter++;
+    set_tolerances(P, s, mode);
+    s.rho = 0.0;
+    s.drho = 0.0;
+    s.J = traj_cost<M>(P, Bf, b, X, U, true, C);
+    s.iters = 1;
+    s.dJ = INFINITY;
+    s.zero_cnt = 0;
+  }
+}
+
+// speculative trials: one lane per (trajectory, trial j), α_j = 2^-j, cost only
+template <class M, int INTEG>
+__global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int NC = Bf.nc;
+  if (t >= P->B * NC) return;
+  const long long b = t / NC;
+  const int j = (int)(t % NC);
+  if (!Bf.st[b].active) return;
+  double Jj = INFINITY;
+  const bool ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr);
+  Bf.lsJ[t] = Jj;
+  Bf.lsok[t] = ok ? 1 : 0;
+}
+
+// decision (sequential acceptance logic replayed over the speculative trials, forward_pass.jl:19-65),
+// commit (in-place replay of the accepted α, or the max-iterations fallback) and bookkeeping.
+// One thread per trajectory.
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+                                                  int bookkeeping, const double* Jprev_in, double* Jout) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  if (!Bf.st[b].active) return;
+  constexpr int n = M::n, m = M::m;
+  const tog_options& o = P->o;
+  const bool al = (mode == TOG_MODE_AL);
+  const int N = P->N, NC = Bf.nc;
+  TrajState s = Bf.st[b];
+  const double J_prev = bookkeeping ? s.J : Jprev_in[b];
+  double J = INFINITY, z = -1.0, expected = 0.0, alpha_last = 0.0;
+  int trials = 0, state = 0;
+  for (int jj = 0;; jj++) {
+    if (!((z <= o.line_search_lower_bound || z > o.line_search_upper_bound) && J >= J_prev)) {
+      state = 1;
+      break;
+    }
+    if (jj > o.iterations_linesearch) {
+      state = 2;
+      break;
+    }
+    trials++;
+    const double aj = ldexp(1.0, -jj);
+    bool ok;
+    double Jj;
+    if (jj < NC) {
+      ok = Bf.lsok[b * NC + jj] != 0;
+      Jj = Bf.lsJ[b * NC + jj];
+    } else {  // beyond the speculative window (iterations_linesearch >= 64): evaluate in place
+      ok = rollout_cost<M, INTEG, 0>(P, Bf, b, aj, al, Jj, nullptr);
+    }
+    if (!ok) continue;
+    J = Jj;
+    expected = -aj * (s.dV0 + aj * s.dV1);
+    z = (expected > 0.0) ? (J_prev - J) / expected : -1.0;
+    alpha_last = aj;
+  }
+  double grad = 0.0;
+  bool copied = false;
+  if (state == 2) {
+    // max line-search iterations: X̄ = X, J = cost(X̄), ρ↑ and ρ += bp_reg_fp (forward_pass.jl:22-37)
+    const double* X = Bf.X + (size_t)b * N * n;
+    const double* U = Bf.U + (size_t)b * (N - 1) * m;
+    if (!bookkeeping) {
+      double* Xb = Bf.Xb + (size_t)b * N * n;
+      double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
+      for (int i = 0; i < N * n; i++) Xb[i] = X[i];
+      for (int i = 0; i < (N - 1) * m; i++) Ub[i] = U[i];
+    }
+    J = traj_cost<M>(P, Bf, b, X, U, al, al ? Bf.C + (size_t)b * N * P->pmax : nullptr);
+    z = 0.0;
+    expected = 0.0;
+    alpha_last = 0.0;
+    reg_increase(P, s);
+    s.rho += o.bp_reg_fp;
+    grad = traj_gradient<M>(P, Bf, b);
+    copied = true;
+  } else if (!bookkeeping) {
+    double Jw;
+    rollout_cost<M, INTEG, 1>(P, Bf, b, alpha_last, al, Jw, nullptr);  // writes X̄, Ū
+  } else if (!(J > o.max_cost_value)) {
+    double Jw;
+    rollout_cost<M, INTEG, 2>(P, Bf, b, alpha_last, al, Jw, &grad);  // X, U <- X̄, Ū in place
+    copied = true;
+  }
+  s.alpha = alpha_last;
+  s.z = z;
+  s.expected = expected;
+  s.ls_trials = trials;
+  if (J > J_prev) s.flags |= TOG_TRAJ_COST_INCREASED;
+  if (Jout) Jout[b] = J;
+  if (bookkeeping) {
+    if (s.flags & TOG_TRAJ_COST_INCREASED) {
+      s.active = 0;  // reference: error("Cost increased during Forward Pass")
     } else {
-      // AL step! tail (augmented_lagrangian_methods.jl:53-67): J = cost(prob), dual_update!,
-      // penalty_update!, record_iteration!, evaluate_convergence
-      const double* X = Bf.X + (size_t)b * N * n;
-      const double* U = Bf.U + (size_t)b * (N - 1) * m;
-      double* C = Bf.C + (size_t)b * N * pmax;
-      double* lam = Bf.lam + (size_t)b * N * pmax;
-      double* mu = Bf.mu + (size_t)b * N * pmax;
-      (void)traj_cost<M>(P, Bf, b, X, U, true, C);
-      double mumax = 0.0;
-      for (int k = 0; k < N; k++) {
-        const int cnt = P->knot_cnt[k];
-        const ConRow* rows = P->rows + P->knot_off[k];
-        for (int i = 0; i < cnt; i++) {
-          const size_t q = (size_t)k * pmax + i;
-          double l = lam[q] + mu[q] * C[q];
-          l = fmax(o.dual_min, fmin(o.dual_max, l));
-          if (row_inequality(rows[i])) l = fmax(0.0, l);
-          lam[q] = l;
-          mu[q] = fmax(0.0, fmin(o.penalty_max, o.penalty_scaling * mu[q]));
-          mumax = fmax(mumax, mu[q]);
-        }
-      }
-      s.mu_max = mumax;
-      s.c_max = traj_max_violation(P, Bf, b);
-      bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (s.c_max < o.constraint_tolerance);
-      if (conv) {
-        s.flags |= TOG_TRAJ_AL_CONVERGED;
-        s.active = 0;
-      } else if (s.al_iter >= o.al_iterations) {
-        s.flags |= TOG_TRAJ_AL_MAX_ITERS;
-        s.active = 0;
-      } else {
-        // next outer iteration: reset!(solver_uncon), set_tolerances!, solve! init (rollout no-op)
-        s.al_iter++;
-        set_tolerances(P, s, mode);
-        s.rho = 0.0;
-        s.drho = 0.0;
-        s.J = traj_cost<M>(P, Bf, b, X, U, true, C);
-        s.iters = 1;
-        s.dJ = INFINITY;
-        s.zero_cnt = 0;
-      }
+      step_bookkeeping<M>(P, Bf, b, s, J, copied, grad, mode);
     }
   }
   Bf.st[b] = s;
@@ -1321,10 +1513,14 @@ struct ModelLaunch {
   }
   static void forward(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, int bk,
                       const double* Jp, double* Jo, hipStream_t st) {
-    if (integ == TOG_RK4)
-      hipLaunchKernelGGL((k_forward<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
-    else
-      hipLaunchKernelGGL((k_forward<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+    const unsigned gs = grid(B * (long long)Bf.nc, 256);  // one lane per (trajectory, trial)
+    if (integ == TOG_RK4) {
+      hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), 0, st, P, Bf, mode);
+      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+    } else {
+      hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), 0, st, P, Bf, mode);
+      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+    }
   }
   static void cost(const DevProblem* P, const DevBuffers& Bf, long long B, int al, int bar, double* J,
                    hipStream_t st) {

@@ -350,6 +350,16 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
     for (int i = 0; i < m * m; i++) Rdt[i] = P.R[i] * P.dt;
     bool ok = host_chol_upper(Qdt, n, P.cQ) && host_chol_upper(Rdt, m, P.cR) && host_chol_upper(P.Qf, n, P.cQf);
     P.sqrt_ok = ok ? 1 : 0;
+    bool diag = true;
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < n; i++)
+        if (i != j && (P.Q[i + n * j] != 0.0 || P.Qf[i + n * j] != 0.0)) diag = false;
+    for (int j = 0; j < m; j++)
+      for (int i = 0; i < m; i++)
+        if (i != j && P.R[i + m * j] != 0.0) diag = false;
+    for (int i = 0; i < m * n; i++)
+      if (P.H[i] != 0.0) diag = false;
+    P.diag_cost = diag ? 1 : 0;
     if (opts->square_root && !ok) {
       tog_destroy(h);
       return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
@@ -378,12 +388,15 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
       (rc = dalloc(h, &b.mu, B * N * P1)) || (rc = dalloc(h, &b.C, B * N * P1)) ||
       (rc = dalloc(h, &b.Qscr, B * N * h->nq)) || (rc = dalloc(h, &b.st, B)) ||
       (rc = dalloc(h, &h->d_scratch, B)) || (rc = dalloc(h, &h->d_scratch2, B)) ||
-      (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4))) {
+      (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4)) ||
+      (rc = dalloc(h, &b.lsJ, B * 64)) || (rc = dalloc(h, &b.lsok, B * 64))) {
     tog_destroy(h);
     return rc;
   }
   b.Sdbg = nullptr;
   b.sdbg = nullptr;
+  b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
+  if (b.nc < 1) b.nc = 1;
   // reference constructor state: X = NaN, U = 0, K = d = 0, λ = 0, μ = μ_init (=1),
   // ρ = dρ = 0 (ilqr_solver.jl:118-144, augmented_lagrangian_solver.jl:143-169)
   fill(h, b.x0, B * n, 0.0);
