@@ -1,0 +1,1130 @@
+// tog_bwd_team.hpp — cost expansion + Riccati backward pass (std and square-root), column-per-lane.
+//
+// Reference: src/solvers/ilqr/backward_pass.jl:9-192 (+ cost expansion, ilqr_methods.jl:55-62,
+// objective.jl:51-94, augmented_lagrangian_methods.jl:186-276).
+//
+// Mapping (MI355X, wave64): a TEAM of 16 lanes owns one trajectory, 4 trajectories per wave (8-lane
+// teams, 8 per wave, for n <= 7). Lane c holds column c of every n x n / m x n block (S, A, Q.xx,
+// Q.ux, K, ...) in registers and lane n holds the feed-forward column d. A product that needs another
+// lane's column reads it from the team's LDS "bus" (column stores, broadcast reads — conflict-free),
+// so every flop runs on registers. Householder QR is column-distributed: lane j forms reflector j and
+// publishes it on the bus, lanes c > j apply it to their own column.
+//
+// Arithmetic contract: every output element is produced by one lane with the same
+// fma sequence, in the same order, as oracle/tog_oracle.c (and the LDS kernel k_backward), so
+// results are bit-identical. Terms that are exact zeros by structure (S below its diagonal, sparse
+// constraint Jacobians) are skipped: fma(0, y, t) == t.
+#pragma once
+// (included by tog_kernels.hpp after the LDS kernels; relies on their helpers)
+
+namespace tog {
+
+// Scheduling fence: keeps the compiler from hoisting a whole phase's bus reads (hundreds of LDS
+// loads) ahead of their FMAs, which would need ~2x the registers of the logical working set.
+#define TEAM_FENCE() asm volatile("" ::: "memory")
+
+constexpr int PX = 20;  // rows with a state gradient per knot kept in registers (sqrt AL expansion)
+
+template <class M>
+struct TeamCfg {
+  static constexpr int n = M::n, m = M::m, L = n + m;
+  static constexpr int TEAM = (n + 1 <= 8) ? 8 : 16;
+  static constexpr int TPW = WAVE / TEAM;
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int PU = 2 * m;  // rows with a control gradient per knot (bound constraints)
+  // largest bus message: [A B] or W (n*L), S-update operands (3nm), tmp1 + s (32 + nm + n),
+  // S / T (n*n + n), Quu (+B for :state), QR reflector (rows + 1)
+  static constexpr int BUS =
+      cmax(cmax(n * L, 3 * n * m), cmax(cmax(32 + n * m + n, n * n + n), cmax(m * m + n * m, n + PX + 2)));
+  static constexpr int R2 = cmax(L * n, n * n + n);  // second region: W / S columns / T
+  static constexpr int BUSP = cmax(BUS, n * L + R2) + 2;  // per-team stride (+2: no bank aliasing between teams)
+  static constexpr int RQ = cmax(2 * n, n + PX);  // register column of the Q.xx QR workspaces
+};
+
+struct RowInfo {  // one constraint row of the current knot (AL terms)
+  double c, w, ws, g;
+  double v[3];
+  int idx[3];
+  int nnz;
+};
+
+template <class M>
+struct BwdTeamLds {
+  using C = TeamCfg<M>;
+  double bus[C::TPW][C::BUSP];
+  RowInfo rows[C::TPW][PCAP];
+  int xrows[C::TPW][PCAP];  // rows of this knot with a state gradient, in row order
+  int urows[C::TPW][PCAP];  // rows of this knot with a control gradient, in row order
+  int nx[C::TPW], nu[C::TPW];
+};
+
+// Host-side admissibility of the team kernel for a problem (otherwise the LDS kernel runs).
+inline bool team_rows_fit(const int* knot_off, const int* knot_cnt, const ConRow* rows, int N, int n, int m) {
+  if (n + 1 > 16 || m > n) return false;
+  for (int k = 0; k < N; k++) {
+    int nx = 0, nu = 0;
+    if (knot_cnt[k] > PCAP) return false;
+    for (int r = 0; r < knot_cnt[k]; r++) {
+      const int t = rows[knot_off[k] + r].type;
+      if (t == ROW_UMAX || t == ROW_UMIN) nu++;
+      else nx++;
+    }
+    if (nx > PX || nu > 2 * m) return false;
+  }
+  return true;
+}
+
+// lane-parallel constraint evaluation into the team's row table (constraint_sets.jl:106-131,
+// active_set augmented_lagrangian_methods.jl:190-195). x, u point at global memory (rows index them
+// with runtime indices, which must not address register arrays); u == nullptr at the terminal knot.
+template <class M>
+__device__ __forceinline__ void team_rows(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, int k,
+                                          const double* x, const double* u, RowInfo* rows, int* xr, int* ur, int* nx,
+                                          int* nu, int tl, int TEAM) {
+  constexpr int n = M::n;
+  const int N = P->N, pmax = P->pmax;
+  const int p = P->knot_cnt[k];
+  const ConRow* cr = P->rows + P->knot_off[k];
+  const double* lam = Bf.lam + ((size_t)b * N + k) * pmax;
+  const double* mu = Bf.mu + ((size_t)b * N + k) * pmax;
+  for (int r = tl; r < p; r += TEAM) {
+    RowInfo ri;
+    const double c = row_value(cr[r], x, u);
+    const double l = lam[r];
+    const bool a = row_inequality(cr[r]) ? ((c >= 0.0) || (l > 0.0)) : true;
+    ri.c = c;
+    ri.w = a ? mu[r] : 0.0;
+    ri.ws = a ? sqrt(mu[r]) : 0.0;
+    ri.g = ri.w * c + l;
+    ri.nnz = row_grad(cr[r], x, n, ri.idx, ri.v);
+    rows[r] = ri;
+  }
+  if (tl == 0) {
+    int cx = 0, cu = 0;
+    for (int r = 0; r < p; r++) {
+      const int t = cr[r].type;
+      if (t == ROW_UMAX || t == ROW_UMIN) ur[cu++] = r;
+      else xr[cx++] = r;
+    }
+    *nx = cx;
+    *nu = cu;
+  }
+}
+
+// entry of a row's gradient at [x;u] index `col` (0 if structurally zero)
+__device__ __forceinline__ double row_at(const RowInfo& r, int col) {
+  double v = 0.0;
+  for (int z = 0; z < r.nnz; z++)
+    if (r.idx[z] == col) v = r.v[z];
+  return v;
+}
+
+// Column-distributed Householder QR (LAPACK dgeqr2/dlarfg as in Julia qr(P).R, and wqr): `a` is this
+// lane's column (ROWS entries, the first `rows` in use — the rest are zero and inert) of a matrix
+// whose columns live in lanes 0..COLS-1 of the team.
+template <int ROWS, int COLS>
+__device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus) {
+#pragma unroll
+  for (int j = 0; j < COLS; j++) {
+    if (j < rows) {
+      if (tl == j) {
+        double ss = 0.0;
+#pragma unroll
+        for (int i = j + 1; i < ROWS; i++)
+          if (i < rows) ss = fma(a[i], a[i], ss);
+        const double xnorm = sqrt(ss);
+        double tau = 0.0;
+        if (xnorm != 0.0) {
+          const double alpha = a[j];
+          const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+          tau = (beta - alpha) / beta;
+          const double sc = 1.0 / (alpha - beta);
+#pragma unroll
+          for (int i = j + 1; i < ROWS; i++)
+            if (i < rows) {
+              a[i] *= sc;
+              bus[i] = a[i];
+            }
+          a[j] = beta;
+        }
+        bus[0] = tau;
+      }
+      team_sync();
+      const double tau = bus[0];
+      if (tau != 0.0 && tl > j && tl < COLS) {
+        double w = a[j];
+#pragma unroll
+        for (int i = j + 1; i < ROWS; i++)
+          if (i < rows) w = fma(bus[i], a[i], w);
+        w *= tau;
+        a[j] -= w;
+#pragma unroll
+        for (int i = j + 1; i < ROWS; i++)
+          if (i < rows) a[i] = fma(-bus[i], w, a[i]);
+      }
+      team_sync();
+    }
+  }
+}
+
+// cond(R) > thresh for an upper-triangular m x m R in registers (same decision procedure and
+// arithmetic as cond_exceeds; backward_pass.jl:129)
+template <int m>
+__device__ __forceinline__ bool cond_exceeds_reg(const double (&R)[m][m], double thresh) {
+  double Ri[m][m];
+#pragma unroll
+  for (int c = 0; c < m; c++) {
+#pragma unroll
+    for (int i = 0; i < m; i++) Ri[i][c] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = m - 1; j >= 0; j--) {
+      const double xj = Ri[j][c] / R[j][j];
+      Ri[j][c] = xj;
+#pragma unroll
+      for (int i = j - 1; i >= 0; i--) Ri[i][c] -= R[i][j] * xj;
+    }
+  }
+  double nr = 0.0, ni = 0.0;
+#pragma unroll
+  for (int j = 0; j < m; j++)
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      nr += R[i][j] * R[i][j];
+      ni += Ri[i][j] * Ri[i][j];
+    }
+  const double cF = sqrt(nr) * sqrt(ni);
+  if (cF <= thresh) return false;
+  if (cF / m > thresh) return true;
+  double A[m][m];  // ambiguous band: one-sided Jacobi singular values
+#pragma unroll
+  for (int j = 0; j < m; j++)
+#pragma unroll
+    for (int i = 0; i < m; i++) A[i][j] = R[i][j];
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double off = 0.0;
+#pragma unroll
+    for (int p = 0; p < m - 1; p++)
+#pragma unroll
+      for (int q = p + 1; q < m; q++) {
+        double al = 0, be = 0, ga = 0;
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          al += A[i][p] * A[i][p];
+          be += A[i][q] * A[i][q];
+          ga += A[i][p] * A[i][q];
+        }
+        if (ga == 0.0) continue;
+        const double c0 = fabs(ga) / sqrt(al * be);
+        off = fmax(off, c0);
+        if (c0 < 1e-15) continue;
+        const double zeta = (be - al) / (2.0 * ga);
+        const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          const double ap = A[i][p], aq = A[i][q];
+          A[i][p] = cs * ap - sn * aq;
+          A[i][q] = sn * ap + cs * aq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  double smax = 0.0, smin = INFINITY;
+#pragma unroll
+  for (int j = 0; j < m; j++) {
+    double s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < m; i++) s2 += A[i][j] * A[i][j];
+    smax = fmax(smax, sqrt(s2));
+    smin = fmin(smin, sqrt(s2));
+  }
+  return (smax / smin) > thresh;
+}
+
+#ifndef TOG_BWD_WAVES
+#define TOG_BWD_WAVES 2
+#endif
+template <class M, int SQRTI, int ALI>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD_WAVES))) k_bwd_team(const DevProblem* P, DevBuffers Bf, int flags) {
+  // (P is deliberately not __restrict__: that would let LICM hoist ~100 loop-invariant problem
+  // constants out of the knot loop and keep them in registers for the whole kernel)
+  using Cfg = TeamCfg<M>;
+  constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
+  constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, RQ = Cfg::RQ, PU = Cfg::PU, NQ = nq_of<M>();
+  static_assert(m <= n && n + 1 <= TEAM, "team layout");
+  __shared__ BwdTeamLds<M> sh;
+  const int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
+  const long long b = (long long)blockIdx.x * Cfg::TPW + team;
+  const int N = P->N;
+  const bool live = (b < P->B) && Bf.st[b].active;
+  double* bus = sh.bus[team];
+  const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
+  const bool state_reg = (P->o.bp_reg_type == 1);
+  const double dt = P->dt;
+  const long long bb = live ? b : 0;  // safe base for idle teams (they never store)
+  const double* Xg = Bf.X + (size_t)bb * N * n;
+  const double* Ug = Bf.U + (size_t)bb * (N - 1) * m;
+  const double* ABg = Bf.AB + (size_t)bb * (N - 1) * n * L;
+  double* Kg = Bf.K + (size_t)bb * (N - 1) * m * n;
+  double* dg = Bf.d + (size_t)bb * (N - 1) * m;
+  double* Qs = Bf.Qscr + (size_t)bb * N * NQ;
+  const bool colx = tl < n;  // this lane owns a state column
+  const bool colu = tl < m;  // this lane owns a control column
+  const int c = colx ? tl : 0;
+  const int cu = colu ? tl : 0;
+  RegState s;
+  s.rho = live ? Bf.st[b].rho : 0.0;
+  s.drho = live ? Bf.st[b].drho : 0.0;
+  s.flags = live ? Bf.st[b].flags : 0;
+  const double rho0 = s.rho, drho0 = s.drho;
+  bool faithful = false;  // replay mode reproducing the A.1 re-accumulation exactly
+  int kmin = N - 1, restarts = 0;
+  double dV0 = 0.0, dV1 = 0.0;
+  double Sc[n], sv[n];  // column c of S (std: symmetric; sqrt: upper factor) ; s (replicated)
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    Sc[i] = 0.0;
+    sv[i] = 0.0;
+  }
+  double sown = 0.0;  // s[c]
+  int k = N - 1;      // N-1: (re)start from the terminal expansion
+  bool done = !live;
+
+  while (!done) {
+    const bool term = (k == N - 1);
+    const double* xg = Xg + (size_t)k * n;
+    const double* ug = term ? nullptr : Ug + (size_t)k * m;
+    // ---------------------------------------------------------------- expansion (or Q replay)
+    double Qxc[n], Quuc[m], Quxc[m], Qu[m], Qxs;
+    const bool replay = faithful && !term && k >= kmin;
+    if (replay) {
+      const double* q = Qs + (size_t)k * NQ;
+      Qxs = q[c];
+#pragma unroll
+      for (int i = 0; i < m; i++) Qu[i] = q[n + i];
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] = q[n + m + i + n * c];
+#pragma unroll
+      for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
+#pragma unroll
+      for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
+    } else {
+      const double xc = xg[c];
+      if (!term) {
+        double a = 0.0, bq = 0.0;
+        if (P->diag_cost) {
+          a = fma(P->Q[c + n * c], xc, 0.0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < n; j++) a = fma(P->Q[c + n * j], xg[j], a);
+#pragma unroll
+          for (int j = 0; j < m; j++) bq = fma(P->H[j + m * c], ug[j], bq);
+        }
+        Qxs = ((a + P->q[c]) + bq) * dt;
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          double a2 = 0.0, b2 = 0.0;
+          if (P->diag_cost) {
+            a2 = fma(P->R[i + m * i], ug[i], 0.0);
+          } else {
+#pragma unroll
+            for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
+#pragma unroll
+            for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
+          }
+          Qu[i] = ((a2 + P->r[i]) + b2) * dt;
+        }
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
+#pragma unroll
+        for (int i = 0; i < m; i++) Quuc[i] = SQRT ? P->cR[i + m * cu] : P->R[i + m * cu] * dt;
+#pragma unroll
+        for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;
+      } else {
+        double a = 0.0;
+        if (P->diag_cost) {
+          a = fma(P->Qf[c + n * c], xc, 0.0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < n; j++) a = fma(P->Qf[c + n * j], xg[j], a);
+        }
+        Qxs = a + P->qf[c];
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQf[i + n * c] : P->Qf[i + n * c];
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          Qu[i] = 0.0;
+          Quuc[i] = 0.0;
+          Quxc[i] = 0.0;
+        }
+      }
+      if (AL && P->knot_cnt[k] > 0) {
+        RowInfo* rows = sh.rows[team];
+        team_rows<M>(P, Bf, b, k, xg, ug, rows, sh.xrows[team], sh.urows[team], &sh.nx[team], &sh.nu[team], tl,
+                     TEAM);
+        team_sync();
+        const int p = P->knot_cnt[k];
+        const int nx = sh.nx[team], nu = sh.nu[team];
+        const int* xr = sh.xrows[team];
+        const int* ur = sh.urows[team];
+        if (!SQRT) {
+          // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order)
+          double tX[n], tUx[m], tUu[m];
+#pragma unroll
+          for (int i = 0; i < n; i++) tX[i] = 0.0;
+#pragma unroll
+          for (int i = 0; i < m; i++) {
+            tUx[i] = 0.0;
+            tUu[i] = 0.0;
+          }
+          for (int r = 0; r < p; r++) {
+            const RowInfo& ri = rows[r];
+            const double vxc = colx ? row_at(ri, c) : 0.0;
+            const double vuc = (colu && !term) ? row_at(ri, n + cu) : 0.0;
+            if (vxc == 0.0 && vuc == 0.0) continue;
+            for (int z = 0; z < ri.nnz; z++) {
+              const int id = ri.idx[z];
+              const double vw = ri.v[z] * ri.w;
+#pragma unroll
+              for (int i = 0; i < n; i++)
+                if (id == i && vxc != 0.0) tX[i] = fma(vw, vxc, tX[i]);
+#pragma unroll
+              for (int i = 0; i < m; i++)
+                if (id == n + i) {
+                  if (vxc != 0.0) tUx[i] = fma(vw, vxc, tUx[i]);
+                  if (vuc != 0.0) tUu[i] = fma(vw, vuc, tUu[i]);
+                }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < n; i++) Qxc[i] += tX[i];
+          if (!term) {
+#pragma unroll
+            for (int i = 0; i < m; i++) {
+              Quuc[i] += tUu[i];
+              Quxc[i] += tUx[i];
+            }
+          }
+        } else {
+          // chol_plus!(Q.xx, Iμ_sqrt cx): QR of [Q.xx; ws.*cx]; rows without a state gradient are
+          // zero rows of the stacked matrix and do not change R
+          if (nx > 0) {
+            double a[RQ];
+#pragma unroll
+            for (int i = 0; i < RQ; i++) {
+              if (i < n) {
+                a[i] = Qxc[i];
+              } else if (i - n < nx) {
+                const RowInfo& ri = rows[xr[i - n]];
+                a[i] = ri.ws * row_at(ri, c);
+              } else {
+                a[i] = 0.0;
+              }
+            }
+            team_qr<RQ, n>(a, n + nx, tl, bus);
+#pragma unroll
+            for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
+          }
+          // chol_plus!(Q.uu, Iμ_sqrt cu)
+          if (!term && nu > 0) {
+            double a[m + PU];
+#pragma unroll
+            for (int i = 0; i < m + PU; i++) {
+              if (i < m) {
+                a[i] = Quuc[i];
+              } else if (i - m < nu) {
+                const RowInfo& ri = rows[ur[i - m]];
+                a[i] = ri.ws * row_at(ri, n + cu);
+              } else {
+                a[i] = 0.0;
+              }
+            }
+            team_qr<m + PU, m>(a, m + nu, tl, bus);
+#pragma unroll
+            for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+          }
+        }
+        // Q.x .+= cx'g ; Q.u .+= cu'g
+        {
+          double tx = 0.0;
+          for (int z = 0; z < nx; z++) {
+            const RowInfo& ri = rows[xr[z]];
+            const double v = colx ? row_at(ri, c) : 0.0;
+            if (v != 0.0) tx = fma(v, ri.g, tx);
+          }
+          Qxs += tx;
+          if (!term) {
+            double tu[m];
+#pragma unroll
+            for (int i = 0; i < m; i++) tu[i] = 0.0;
+            for (int z = 0; z < nu; z++) {
+              const RowInfo& ri = rows[ur[z]];
+              const int id = ri.idx[0];
+#pragma unroll
+              for (int i = 0; i < m; i++)
+                if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < m; i++) Qu[i] += tu[i];
+          }
+        }
+        team_sync();
+      }
+    }
+    if (term) {
+      // S[N] = Q[N] (backward_pass.jl:20-21 / :100-101)
+#pragma unroll
+      for (int i = 0; i < n; i++) Sc[i] = Qxc[i];
+      sown = Qxs;
+      if (colx) bus[tl] = Qxs;
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < n; i++) sv[i] = bus[i];
+      team_sync();
+      if (store_S && colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = Sc[i];
+        Bf.sdbg[((size_t)b * N + k) * n + tl] = sown;
+      }
+      dV0 = 0.0;
+      dV1 = 0.0;
+      k = N - 2;
+      continue;
+    }
+    // ---------------------------------------------------------------- ∇F[k] = [A|B] columns
+    double Ac[n], Bc[n];
+    {
+      const double* abk = ABg + (size_t)k * n * L;
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        Ac[i] = abk[i + n * c];
+        Bc[i] = abk[i + n * (n + cu)];
+      }
+    }
+    // ---------------------------------------------------------------- Q.x += A's ; Q.u += B's
+    {
+      double t = 0.0;
+#pragma unroll
+      for (int l = 0; l < n; l++) t = fma(Ac[l], sv[l], t);
+      Qxs += t;
+      double tu = 0.0;
+#pragma unroll
+      for (int l = 0; l < n; l++) tu = fma(Bc[l], sv[l], tu);
+      if (colu) bus[tl] = tu;
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < m; i++) Qu[i] += bus[i];
+      team_sync();
+    }
+    // [A B] columns on the bus (first region)
+    double* bus2 = bus + n * L;
+    if (colx) {
+#pragma unroll
+      for (int i = 0; i < n; i++) bus[i + n * tl] = Ac[i];
+    }
+    if (colu) {
+#pragma unroll
+      for (int i = 0; i < n; i++) bus[i + n * (n + tl)] = Bc[i];
+    }
+    if (!SQRT) {
+      // T1 = [A B]' S (L x n), then Q.xx += (A'S)A ; Q.uu += (B'S)B ; Q.ux += (B'S)A (backward_pass.jl:32-36)
+      team_sync();
+      // W = [A B]' S, column c per lane, written straight to the second bus region
+      if (colx) {
+#pragma unroll 1
+        for (int i = 0; i < L; i++) {
+          double t = 0.0;
+#pragma unroll
+          for (int l = 0; l < n; l++) t = fma(bus[l + n * i], Sc[l], t);
+          bus2[i + L * tl] = t;
+        }
+      }
+      team_sync();
+      // reductions over l kept rolled (register accumulators, l ascending as in the oracle)
+      double tq[n], tuu[m], tux[m];
+#pragma unroll
+      for (int i = 0; i < n; i++) tq[i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        tuu[i] = 0.0;
+        tux[i] = 0.0;
+      }
+#pragma unroll 1
+      for (int l = 0; l < n; l++) {
+        const double al = bus[l + n * c];
+        const double bl = bus[l + n * (n + cu)];
+#pragma unroll
+        for (int i = 0; i < n; i++) tq[i] = fma(bus2[i + L * l], al, tq[i]);
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          const double w = bus2[n + i + L * l];
+          tuu[i] = fma(w, bl, tuu[i]);
+          tux[i] = fma(w, al, tux[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] += tq[i];
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        Quuc[i] += tuu[i];
+        Quxc[i] += tux[i];
+      }
+      team_sync();
+    } else {
+      // tmp_x = S A, tmp_u = S B ; Q.ux += tmp_u' tmp_x ; Q.xx <- qr([Q.xx; tmp_x]).R ;
+      // Q.uu <- qr([Q.uu; tmp_u]).R   (backward_pass.jl:112-118). Dense products, l ascending.
+      if (colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) bus2[i + n * tl] = Sc[i];
+      }
+      team_sync();
+      double TX[n], TU[n];
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        TX[i] = 0.0;
+        TU[i] = 0.0;
+      }
+#pragma unroll 1
+      for (int l = 0; l < n; l++) {
+        const double al = bus[l + n * c];
+        const double bl = bus[l + n * (n + cu)];
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          const double sil = bus2[i + n * l];
+          TX[i] = fma(sil, al, TX[i]);
+          TU[i] = fma(sil, bl, TU[i]);
+        }
+      }
+      team_sync();
+      // tmp_u columns (lanes < m) and this lane's tmp_x column on the bus
+      if (colu) {
+#pragma unroll
+        for (int i = 0; i < n; i++) bus[i + n * tl] = TU[i];
+      }
+      if (colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) bus2[i + n * tl] = TX[i];
+      }
+      team_sync();
+      {
+        double t[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) t[i] = 0.0;
+#pragma unroll 1
+        for (int l = 0; l < n; l++) {
+          const double tx = bus2[l + n * c];
+#pragma unroll
+          for (int i = 0; i < m; i++) t[i] = fma(bus[l + n * i], tx, t[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) Quxc[i] += t[i];
+      }
+      team_sync();
+      {
+        double a[2 * n];
+#pragma unroll
+        for (int i = 0; i < 2 * n; i++) a[i] = (i < n) ? Qxc[i] : TX[i - n];
+        team_qr<2 * n, n>(a, 2 * n, tl, bus);
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
+      }
+      {
+        double a[m + n];
+#pragma unroll
+        for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : TU[i - m];
+        team_qr<m + n, m>(a, m + n, tl, bus);
+#pragma unroll
+        for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+      }
+    }
+    if (faithful) {
+      double* q = Qs + (size_t)k * NQ;
+      if (colx) {
+        q[tl] = Qxs;
+#pragma unroll
+        for (int i = 0; i < n; i++) q[n + m + i + n * tl] = Qxc[i];
+#pragma unroll
+        for (int i = 0; i < m; i++) q[n + m + n * n + m * m + i + m * tl] = Quxc[i];
+      }
+      if (colu) {
+#pragma unroll
+        for (int i = 0; i < m; i++) q[n + m + n * n + i + m * tl] = Quuc[i];
+      }
+      if (tl == 0) {
+#pragma unroll
+        for (int i = 0; i < m; i++) q[n + i] = Qu[i];
+      }
+      kmin = k < kmin ? k : kmin;
+    }
+    // ---------------------------------------------------------------- regularise, test, gains
+    // (backward_pass.jl:38-48 / :120-126). Every lane needs the full Q.uu: all-gather its columns.
+    if (colu) {
+#pragma unroll
+      for (int i = 0; i < m; i++) bus[i + m * tl] = Quuc[i];
+      if (state_reg) {  // (:state regularisation only; reloaded to keep [A|B] out of registers)
+        const double* bk = ABg + (size_t)k * n * L + n * (n + tl);
+#pragma unroll
+        for (int i = 0; i < n; i++) bus[m * m + i + n * tl] = bk[i];
+      }
+    }
+    team_sync();
+    double Quu[m][m];
+#pragma unroll
+    for (int j = 0; j < m; j++)
+#pragma unroll
+      for (int i = 0; i < m; i++) Quu[i][j] = bus[i + m * j];
+    // right-hand side of this lane: Qux_reg column (state reg adds ρ B'A), or Q.u for lane n
+    double col[m];
+    if (colx) {
+#pragma unroll
+      for (int i = 0; i < m; i++) col[i] = Quxc[i];
+      if (state_reg) {
+        const double* ak = ABg + (size_t)k * n * L + n * c;
+        double t[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) t[i] = 0.0;
+#pragma unroll 1
+        for (int l = 0; l < n; l++) {
+          const double a = ak[l];
+#pragma unroll
+          for (int i = 0; i < m; i++) t[i] = fma(bus[m * m + l + n * i], a, t[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) col[i] += s.rho * t[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < m; i++) col[i] = Qu[i];
+    }
+    double F[m][m];
+    bool ok = true;
+    int piv[m];
+    if (!SQRT) {
+#pragma unroll
+      for (int j = 0; j < m; j++)
+#pragma unroll
+        for (int i = 0; i < m; i++) F[i][j] = Quu[i][j];
+      if (!state_reg) {
+#pragma unroll
+        for (int i = 0; i < m; i++) F[i][i] += s.rho;
+      } else {
+        double t[m][m];
+#pragma unroll
+        for (int j = 0; j < m; j++)
+#pragma unroll
+          for (int i = 0; i < m; i++) t[i][j] = 0.0;
+#pragma unroll 1
+        for (int l = 0; l < n; l++) {
+          double bl[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) bl[i] = bus[m * m + l + n * i];
+#pragma unroll
+          for (int j = 0; j < m; j++)
+#pragma unroll
+            for (int i = 0; i < m; i++) t[i][j] = fma(bl[i], bl[j], t[i][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < m; j++)
+#pragma unroll
+          for (int i = 0; i < m; i++) F[i][j] += s.rho * t[i][j];
+      }
+      team_sync();
+      // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle
+      {
+        double U[m][m];
+#pragma unroll
+        for (int j = 0; j < m; j++) {
+          double d0 = F[j][j];
+#pragma unroll
+          for (int l = 0; l < j; l++) d0 -= U[l][j] * U[l][j];
+          if (!(d0 > 0.0)) ok = false;
+          const double ujj = sqrt(d0);
+          U[j][j] = ujj;
+#pragma unroll
+          for (int cc = j + 1; cc < m; cc++) {
+            double t = F[j][cc];
+#pragma unroll
+            for (int l = 0; l < j; l++) t -= U[l][j] * U[l][cc];
+            U[j][cc] = t / ujj;
+          }
+        }
+      }
+      // LU with partial pivoting (dgetrf; Julia `\`)
+#pragma unroll
+      for (int kk = 0; kk < m; kk++) {
+        int p = kk;
+        double amax = fabs(F[kk][kk]);
+#pragma unroll
+        for (int i = kk + 1; i < m; i++)
+          if (fabs(F[i][kk]) > amax) {
+            amax = fabs(F[i][kk]);
+            p = i;
+          }
+        piv[kk] = p;
+#pragma unroll
+        for (int i = kk + 1; i < m; i++)
+          if (i == p) {
+#pragma unroll
+            for (int j = 0; j < m; j++) {
+              const double t = F[kk][j];
+              F[kk][j] = F[i][j];
+              F[i][j] = t;
+            }
+          }
+        const double akk = F[kk][kk];
+        if (akk != 0.0) {
+          const double r = 1.0 / akk;
+#pragma unroll
+          for (int i = kk + 1; i < m; i++) F[i][kk] *= r;
+        }
+#pragma unroll
+        for (int j = kk + 1; j < m; j++)
+#pragma unroll
+          for (int i = kk + 1; i < m; i++) F[i][j] = fma(-F[i][kk], F[kk][j], F[i][j]);
+      }
+    } else {
+      team_sync();
+      // Quu_reg = qr([Q.uu; sqrt(ρ) I]).R (:control) or qr([Q.uu; sqrt(ρ) B]).R (:state),
+      // column-distributed over lanes < m, then all-gathered
+      {
+        const double sr = sqrt(s.rho);
+        double a[m + n];
+#pragma unroll
+        for (int i = 0; i < m + n; i++) {
+          double v = 0.0;
+          if (i < m) v = Quuc[i];
+          else if (state_reg) v = sr * ABg[(size_t)k * n * L + n * (n + cu) + (i - m)];
+          else if (i - m == tl) v = sr;
+          a[i] = v;
+        }
+        team_qr<m + n, m>(a, state_reg ? m + n : 2 * m, tl, bus);
+        if (colu) {
+#pragma unroll
+          for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
+        }
+      }
+      team_sync();
+#pragma unroll
+      for (int j = 0; j < m; j++)
+#pragma unroll
+        for (int i = 0; i < m; i++) F[i][j] = bus[i + m * j];
+      team_sync();
+      ok = !cond_exceeds_reg<m>(F, 1e8);
+    }
+    if (!ok) {
+      // non-PD / cond > 1e8: increase ρ and restart at N-1; Q blocks are NOT re-expanded (A.1)
+      if (!faithful) {
+        faithful = true;  // replay this call from its start in faithful mode
+        s.rho = rho0;
+        s.drho = drho0;
+        restarts = 0;
+        kmin = N - 1;
+      } else {
+        reg_increase(P, s);
+        restarts++;
+        if (restarts > 1000) {
+          s.flags |= TOG_TRAJ_MAX_REG;
+          done = true;
+        }
+      }
+      k = N - 1;
+      continue;
+    }
+    if (!SQRT) {
+      // K = -(Quu_reg \ Qux_reg), d = -(Quu_reg \ Q.u)
+#pragma unroll
+      for (int kk = 0; kk < m; kk++) {
+#pragma unroll
+        for (int i = kk + 1; i < m; i++)
+          if (i == piv[kk]) {
+            const double t = col[kk];
+            col[kk] = col[i];
+            col[i] = t;
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < m; j++)
+#pragma unroll
+        for (int i = j + 1; i < m; i++) col[i] = fma(-F[i][j], col[j], col[i]);
+#pragma unroll
+      for (int j = m - 1; j >= 0; j--) {
+        col[j] /= F[j][j];
+#pragma unroll
+        for (int i = 0; i < j; i++) col[i] = fma(-F[i][j], col[j], col[i]);
+      }
+    } else {
+      // K = -Quu_reg \ (Quu_reg' \ Qux_reg)
+#pragma unroll
+      for (int j = 0; j < m; j++) {
+        const double xj = col[j] / F[j][j];
+        col[j] = xj;
+#pragma unroll
+        for (int i = j + 1; i < m; i++) col[i] = fma(-F[j][i], xj, col[i]);
+      }
+#pragma unroll
+      for (int j = m - 1; j >= 0; j--) {
+        const double xj = col[j] / F[j][j];
+        col[j] = xj;
+#pragma unroll
+        for (int i = j - 1; i >= 0; i--) col[i] = fma(-F[i][j], xj, col[i]);
+      }
+    }
+    double Kc[m];
+#pragma unroll
+    for (int i = 0; i < m; i++) Kc[i] = -1.0 * col[i];
+    if (tl == n) {
+#pragma unroll
+      for (int i = 0; i < m; i++) bus[i] = Kc[i];
+    }
+    team_sync();
+    double d[m];
+#pragma unroll
+    for (int i = 0; i < m; i++) d[i] = bus[i];
+    team_sync();
+    if (colx) {
+#pragma unroll
+      for (int i = 0; i < m; i++) Kg[(size_t)k * m * n + i + m * tl] = Kc[i];
+    }
+    if (tl == n) {
+#pragma unroll
+      for (int i = 0; i < m; i++) dg[(size_t)k * m + i] = Kc[i];
+    }
+    if (!SQRT) {
+      double KtQ[m];  // row c of K' Q.uu
+#pragma unroll
+      for (int j = 0; j < m; j++) {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) t = fma(Kc[l], Quu[l][j], t);
+        KtQ[j] = t;
+      }
+      // s[c] = Q.x[c] + (K'Q.uu)[c,:] d + K[:,c]'Q.u + Q.ux[:,c]'d
+      {
+        double a = 0.0, b2 = 0.0, c2 = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          a = fma(KtQ[l], d[l], a);
+          b2 = fma(Kc[l], Qu[l], b2);
+          c2 = fma(Quxc[l], d[l], c2);
+        }
+        sown = ((Qxs + a) + b2) + c2;
+      }
+      // T[i][c] = Q.xx[i][c] + (K'Q.uu)[i,:]K[:,c] + K[:,i]'Q.ux[:,c] + Q.ux[:,i]'K[:,c]
+      if (colx) {
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          bus[l + m * tl] = KtQ[l];
+          bus[n * m + l + m * tl] = Kc[l];
+          bus[2 * n * m + l + m * tl] = Quxc[l];
+        }
+      }
+      team_sync();
+      double T[n];
+      {
+        double ta[n], tb[n], tc[n];
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          ta[i] = 0.0;
+          tb[i] = 0.0;
+          tc[i] = 0.0;
+        }
+#pragma unroll 1
+        for (int l = 0; l < m; l++) {
+          const double kl = bus[n * m + l + m * c];       // K[l][c]
+          const double ql = bus[2 * n * m + l + m * c];   // Q.ux[l][c]
+#pragma unroll
+          for (int i = 0; i < n; i++) {
+            ta[i] = fma(bus[l + m * i], kl, ta[i]);
+            tb[i] = fma(bus[n * m + l + m * i], ql, tb[i]);
+            tc[i] = fma(bus[2 * n * m + l + m * i], kl, tc[i]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < n; i++) T[i] = ((Qxc[i] + ta[i]) + tb[i]) + tc[i];
+      }
+      team_sync();
+      // S = 0.5 (T + T'); all-gather s
+      if (colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) bus[i + n * tl] = T[i];
+        bus[n * n + tl] = sown;
+      }
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        Sc[i] = 0.5 * (T[i] + bus[c + n * i]);
+        sv[i] = bus[n * n + i];
+      }
+      team_sync();
+      {
+        double a = 0.0, b2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < m; i++) a = fma(d[i], Qu[i], a);
+#pragma unroll
+        for (int j = 0; j < m; j++) {
+          double t = 0.0;
+#pragma unroll
+          for (int i = 0; i < m; i++) t = fma(0.5 * d[i], Quu[i][j], t);
+          b2 = fma(t, d[j], b2);
+        }
+        dV0 += a;
+        dV1 += b2;
+      }
+    } else {
+      double Ud[m], KtU[m];  // Q.uu d ; row c of K' Q.uu'
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) t = fma(Quu[i][l], d[l], t);
+        Ud[i] = t;
+      }
+#pragma unroll
+      for (int j = 0; j < m; j++) {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) t = fma(Kc[l], Quu[j][l], t);
+        KtU[j] = t;
+      }
+      {
+        double a = 0.0, b2 = 0.0, c2 = 0.0;
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          a = fma(KtU[l], Ud[l], a);
+          b2 = fma(Kc[l], Qu[l], b2);
+          c2 = fma(Quxc[l], d[l], c2);
+        }
+        sown = ((Qxs + a) + b2) + c2;
+      }
+      // tmp1 = (Q.xx') \ Q.ux' by distributed forward substitution: lane i owns row i of tmp1
+      double t1[m];
+#pragma unroll
+      for (int i = 0; i < m; i++) t1[i] = Quxc[i];
+#pragma unroll
+      for (int j = 0; j < n; j++) {
+        if (tl == j) {
+#pragma unroll
+          for (int i = 0; i < m; i++) {
+            t1[i] = t1[i] / Qxc[j];
+            bus[i] = t1[i];
+          }
+        }
+        team_sync();
+        if (tl > j && colx) {
+#pragma unroll
+          for (int i = 0; i < m; i++) t1[i] = fma(-Qxc[j], bus[i], t1[i]);
+        }
+        team_sync();
+      }
+      // all-gather tmp1 (row-major at bus[TB + r*m + j]) and s
+      constexpr int TB = 32;
+      if (colx) {
+#pragma unroll
+        for (int i = 0; i < m; i++) bus[TB + tl * m + i] = t1[i];
+        bus[TB + n * m + tl] = sown;
+      }
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < n; i++) sv[i] = bus[TB + n * m + i];
+      // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! by each row of tmp1 (backward_pass.jl:186-192)
+      double U2[m][m];
+#pragma unroll
+      for (int j = 0; j < m; j++)
+#pragma unroll
+        for (int i = 0; i < m; i++) U2[i][j] = Quu[i][j];
+      bool okd = true;
+#pragma unroll 1
+      for (int r = 0; r < n; r++) {
+        double v[m];
+#pragma unroll
+        for (int j = 0; j < m; j++) v[j] = bus[TB + r * m + j];
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          if (okd) {
+            const double Aii = U2[i][i];
+            const double sn = v[i] / Aii;
+            const double s2 = sn * sn;
+            if (s2 > 1.0) {
+              okd = false;
+            } else {
+              const double cs = sqrt(1.0 - s2);
+              U2[i][i] = cs * Aii;
+#pragma unroll
+              for (int j = i + 1; j < m; j++) {
+                const double tmp = (U2[i][j] - sn * v[j]) / cs;
+                v[j] = cs * v[j] - sn * tmp;
+                U2[i][j] = tmp;
+              }
+            }
+          }
+        }
+        if (!okd) break;
+      }
+      if (!okd) {
+        s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
+#pragma unroll
+        for (int j = 0; j < m; j++)
+#pragma unroll
+          for (int i = 0; i < m; i++) U2[i][j] = Quu[i][j];
+      }
+      // S[k] = qr([Q.xx + tmp1 K; tmp2 K]).R
+      {
+        constexpr int RS = n + m;
+        double a[RS];
+        {
+          double v[n];
+#pragma unroll
+          for (int i = 0; i < n; i++) v[i] = 0.0;
+#pragma unroll
+          for (int l = 0; l < m; l++) {
+#pragma unroll
+            for (int i = 0; i < n; i++) v[i] = fma(bus[TB + i * m + l], Kc[l], v[i]);
+            TEAM_FENCE();
+          }
+#pragma unroll
+          for (int i = 0; i < n; i++) a[i] = Qxc[i] + v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          double v = 0.0;
+#pragma unroll
+          for (int l = 0; l < m; l++) v = fma(U2[i][l], Kc[l], v);
+          a[n + i] = v;
+        }
+        team_sync();
+        team_qr<RS, n>(a, RS, tl, bus);
+#pragma unroll
+        for (int i = 0; i < n; i++) Sc[i] = (i <= tl) ? a[i] : 0.0;
+      }
+      {
+        double a = 0.0, b2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < m; i++) a = fma(d[i], Qu[i], a);
+#pragma unroll
+        for (int i = 0; i < m; i++) b2 = fma(Ud[i], Ud[i], b2);
+        dV0 += a;
+        dV1 += 0.5 * b2;
+      }
+    }
+    if (store_S && colx) {
+#pragma unroll
+      for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = Sc[i];
+      Bf.sdbg[((size_t)b * N + k) * n + tl] = sown;
+    }
+    if (k == 0) done = true;
+    else k--;
+  }
+  if (!live) return;
+  reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
+  if (tl == 0) {
+    TrajState& g = Bf.st[b];
+    g.rho = s.rho;
+    g.drho = s.drho;
+    g.flags = s.flags;
+    g.dV0 = dV0;
+    g.dV1 = dV1;
+    g.bp_restarts = restarts + (faithful ? 1 : 0);
+  }
+}
+
+}  // namespace tog

@@ -1460,12 +1460,17 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
 // =============================================================================================
 // Per-model launch table
 // =============================================================================================
+}  // namespace tog
+#include "tog_bwd_team.hpp"
+namespace tog {
+
 struct ModelOps {
   int n, m;
   void (*init)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, hipStream_t);
   void (*rollout_open)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*jacobian)(const DevProblem*, const DevBuffers&, long long B, int N, int integ, hipStream_t);
-  void (*backward)(const DevProblem*, const DevBuffers&, long long B, int sqrt, int al, int flags, hipStream_t);
+  void (*backward)(const DevProblem*, const DevBuffers&, long long B, int sqrt, int al, int flags, int team,
+                   hipStream_t);
   void (*forward)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, int bookkeeping,
                   const double* Jprev, double* Jout, hipStream_t);
   void (*cost)(const DevProblem*, const DevBuffers&, long long B, int al, int use_bar, double* J, hipStream_t);
@@ -1500,8 +1505,20 @@ struct ModelLaunch {
     else
       hipLaunchKernelGGL((k_jacobian<M, TOG_RK3, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
   }
-  static void backward(const DevProblem* P, const DevBuffers& Bf, long long B, int sq, int al, int flags,
+  static void backward(const DevProblem* P, const DevBuffers& Bf, long long B, int sq, int al, int flags, int team,
                        hipStream_t st) {
+    if (team) {  // column-per-lane teams, TPW trajectories per wave (tog_bwd_team.hpp)
+      constexpr int TPW = TeamCfg<M>::TPW;
+      const dim3 g((unsigned)((B + TPW - 1) / TPW)), blk(64);
+      if (sq) {
+        if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1>), g, blk, 0, st, P, Bf, flags);
+        else hipLaunchKernelGGL((k_bwd_team<M, 1, 0>), g, blk, 0, st, P, Bf, flags);
+      } else {
+        if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1>), g, blk, 0, st, P, Bf, flags);
+        else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, 0, st, P, Bf, flags);
+      }
+      return;
+    }
     const dim3 g((unsigned)B), blk(64);
     if (sq) {
       if (al) hipLaunchKernelGGL((k_backward<M, 1, 1>), g, blk, 0, st, P, Bf, flags);

@@ -50,6 +50,7 @@ struct tog_handle {
   ConRow* d_rows = nullptr;
   DevBuffers buf = {};
   const ModelOps* ops = nullptr;
+  int bwd_team = 0;  // backward pass on column-per-lane teams (else one wave per trajectory, LDS)
   double* d_scratch = nullptr;  // B doubles (J_prev / J_out staging)
   double* d_scratch2 = nullptr; // B doubles
   int* d_iscratch = nullptr;    // B ints
@@ -375,6 +376,12 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   HIPCHECK(hipMemcpy(h->d_knot_off, off.data(), sizeof(int) * N, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(h->d_knot_cnt, cnt.data(), sizeof(int) * N, hipMemcpyHostToDevice));
   if (!rows.empty()) HIPCHECK(hipMemcpy(h->d_rows, rows.data(), sizeof(ConRow) * rows.size(), hipMemcpyHostToDevice));
+  {
+    // TOG_BWD=lds forces the one-wave-per-trajectory LDS backward kernel (A/B checks)
+    const char* ev = getenv("TOG_BWD");
+    const bool force_lds = ev && strcmp(ev, "lds") == 0;
+    h->bwd_team = (!force_lds && team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m)) ? 1 : 0;
+  }
   P.knot_off = h->d_knot_off;
   P.knot_cnt = h->d_knot_cnt;
   P.rows = h->d_rows;
@@ -641,7 +648,7 @@ int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, 
     const size_t B = h->B, n = h->n, N = h->N;
     if ((rc = dalloc(h, &h->buf.Sdbg, B * N * n * n)) || (rc = dalloc(h, &h->buf.sdbg, B * N * n))) return rc;
   }
-  h->ops->backward(h->dP, h->buf, h->B, sq, al, flags, h->stream);
+  h->ops->backward(h->dP, h->buf, h->B, sq, al, flags, h->bwd_team, h->stream);
   HIPCHECK(hipGetLastError());
   if (dV_out) return tog_get(h, TOG_FIELD_DV, dV_out);
   return TOG_OK;
@@ -691,7 +698,7 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   for (int i = 0; i < nsteps; i++) {
     timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
     timed(h, TOG_KERNEL_BACKWARD,
-          [&] { h->ops->backward(h->dP, h->buf, h->B, h->opts.square_root, al, 0, h->stream); });
+          [&] { h->ops->backward(h->dP, h->buf, h->B, h->opts.square_root, al, 0, h->bwd_team, h->stream); });
     timed(h, TOG_KERNEL_FORWARD,
           [&] { h->ops->forward(h->dP, h->buf, h->B, h->integ, h->mode, 1, nullptr, nullptr, h->stream); });
   }
