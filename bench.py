@@ -90,7 +90,8 @@ def main():
     pkg = __graft_entry__.load_package()
     abi = pkg.abi
     B = args.batch
-    prob, opts = pkg.Problems.config_quadrotor(B=B, offset=rank * B)
+    offset, count = pkg.distributed.shard(B * world, rank, world)  # weak scaling: B trajectories per GPU
+    prob, opts = pkg.Problems.config_quadrotor(B=count, offset=offset)
     stream = None
     if dist is not None:
         import torch
@@ -111,7 +112,7 @@ def main():
         if dist is None:
             return
         abi.check(h.lib, h.lib.tog_batch_stats_device(h.h, ctypes.c_void_p(stats_t.data_ptr())))
-        dist.all_gather_into_tensor(gathered, stats_t)
+        pkg.distributed.reduce_stats(stats_t, gathered, dist)
 
     h.solve_init(abi.MODE_AL)
     h.solve_step(args.warmup)
@@ -141,18 +142,10 @@ def main():
         St[:, abi.STAT_LS_TRIALS] > 0) else 1.0
 
     if dist is not None:
-        import torch
-
-        t = torch.tensor([float(steps_done), elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        tot = t.clone()
-        dist.all_reduce(tot[0:1])
-        mx = t.clone()
-        dist.all_reduce(mx[1:2], op=dist.ReduceOp.MAX)
-        steps_all, elapsed = float(tot[0].item()), float(mx[1].item())
+        value, steps_all, elapsed = pkg.distributed.job_rate(steps_done, elapsed, dist, device=f"cuda:{local_rank}")
     else:
         steps_all = float(steps_done)
-
-    value = steps_all / elapsed
+        value = steps_all / elapsed
     # roofline for the dominant kernel (largest total device time over the timed region)
     kb = kernel_bytes(n, m, N, 8, 13, trials)
     names = ["jacobian", "backward", "forward"]

@@ -7,7 +7,8 @@
  * bit-identical to the CPU restatement. libm's sin/cos (glibc) and the GPU's OCML sin/cos may differ
  * in the last ulp, so the models that need them (cartpole, car, pendulum) use this one
  * implementation on both sides: fdlibm's __kernel_sin/__kernel_cos polynomials on [-pi/4, pi/4]
- * after a two-constant Cody-Waite reduction by pi/2 (accurate to ~1 ulp for |x| < 2^19).
+ * after a two-constant Cody-Waite reduction by pi/2: within 2 ulp of libm for |x| < 2^19, except
+ * right next to the zeros (x ~ k*pi) where the absolute error stays below 2^-80.
  */
 #ifndef TOG_MATH_H
 #define TOG_MATH_H

@@ -597,6 +597,9 @@ static double cond2(const double* Ain, int n) {
 }
 
 OC_EXPORT double oc_cond2(const double* A, int n) { return cond2(A, n); }
+/* the deterministic sin/cos shared with the GPU (include/tog_math.h), for tests */
+OC_EXPORT double oc_sin(double x) { return tog_sin(x); }
+OC_EXPORT double oc_cos(double x) { return tog_cos(x); }
 OC_EXPORT void oc_qr_R(double* R, double* P, int rows, int cols) { qr_R(R, P, rows, cols); }
 
 /* chol_minus(A, B) (backward_pass.jl:186-192): Cholesky(copy(A), :U, 0) then

@@ -20,6 +20,7 @@ from .solvers import (AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolve
                       to_tog_options)
 from .steps import backwardpass_b, cost, cost_expansion_b, forwardpass_b, jacobian_b, rollout_b
 from . import problems as Problems
+from . import distributed
 
 __all__ = [
     "abi", "BoundConstraint", "CircleConstraints", "Constraints", "ConstraintSet", "Dynamics", "GoalConstraint",

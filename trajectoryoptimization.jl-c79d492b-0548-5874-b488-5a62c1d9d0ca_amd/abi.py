@@ -21,6 +21,9 @@ TOG_ABI_VERSION = 1
 # models (include/tog.h tog_model_id)
 MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM = range(5)
 MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1)}
+# status codes (include/tog.h tog_status_code)
+OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
+
 RK3, RK4 = 0, 1
 CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES = range(4)
 MODE_ILQR, MODE_AL = 0, 1

@@ -157,6 +157,39 @@ def car_sqrt_bp(constrained=False):
     return Problem(model_d, obj, np.ones((N - 1, m)), constraints=cons, x0=x0, N=N, dt=dt)
 
 
+def pendulum(integration="rk3", U0=None):
+    """problems/pendulum.jl:1-35: rk3, N=31, dt=0.15, Q=R=Qf=1e-3 I, xf=[π,0], |u|<=3 at
+    k<N, goal at N, U=ones."""
+    model_d = rk4(Dynamics.pendulum) if integration == "rk4" else rk3(Dynamics.pendulum)
+    n, m = 2, 1
+    Q, R = 1e-3 * np.eye(n), 1e-3 * np.eye(m)
+    x0, xf = np.zeros(n), np.array([math.pi, 0.0])
+    N, dt = 31, 0.15
+    if U0 is None:
+        U0 = np.ones((N - 1, m))
+    cons = Constraints(N)
+    bnd = BoundConstraint(n, m, u_min=-3.0, u_max=3.0)
+    for k in range(N - 1):
+        cons[k] += bnd
+    cons[N - 1] += goal_constraint(xf)
+    obj = LQRObjective(Q, R, Q, xf, N)
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+
+
+def car_parallel_park(U0=None):
+    """test/car_tests.jl:4-32: car, rk3, N=101, dt=0.1, Q=R=1e-2 I, Qf=1000 I, x0=0, xf=[0,1,0],
+    U=ones, unconstrained (iLQR with cost_tolerance=1e-5)."""
+    model_d = rk3(Dynamics.car)
+    n, m = 3, 2
+    Q, R, Qf = 1e-2 * np.eye(n), 1e-2 * np.eye(m), 1000.0 * np.eye(n)
+    x0, xf = np.zeros(n), np.array([0.0, 1.0, 0.0])
+    N, dt = 101, 0.1
+    if U0 is None:
+        U0 = np.ones((N - 1, m))
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    return Problem(model_d, obj, U0, x0=x0, xf=xf, N=N, dt=dt)
+
+
 # ---------------------------------------------------------------------------- BASELINE configs
 
 def _per_traj_rng(seed0, B, fn):
