@@ -44,6 +44,22 @@ def kernel_bytes(n, m, N, p_stage, p_term, trials):
     return {"jacobian": jac, "backward": bwd, "forward": fwd}
 
 
+def measured_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_traffic.json,
+    written by tools/rocpd_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
+    this same bench command, FETCH_SIZE x2 per the gfx950 correction). None if absent."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)["per_launch"].get(kernel)
+    if not t:
+        return None, None
+    return round(t["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
     """The C oracle ("port" of the reference algorithm) on the host cores: full AL-iLQR solves of
     config-3 trajectories, OpenMP over trajectories. Bounded sample (~`seconds` of work)."""
@@ -155,8 +171,10 @@ def main():
     per_launch_traj = steps_done / max(1, launches[dom])
     alg_bytes = kb[names[dom]] * per_launch_traj
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    traffic, tsrc = measured_traffic(names[dom])
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": names[dom],
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
+                "algorithmic_bytes_per_launch": round(alg_bytes), "kernel": names[dom],
                 "kernel_ms": {nm_: round(float(ms[i] / max(1, launches[i])), 4) for i, nm_ in enumerate(names)}}
 
     if rank == 0:
