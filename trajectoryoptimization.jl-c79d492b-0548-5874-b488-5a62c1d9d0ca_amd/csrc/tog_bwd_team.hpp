@@ -37,30 +37,40 @@ struct TeamCfg {
   static constexpr int BUS =
       cmax(cmax(n * L, 3 * n * m), cmax(cmax(32 + n * m + n, n * n + n), cmax(m * m + n * m, n + PX + 2)));
   static constexpr int R2 = cmax(L * n, n * n + n);  // second region: W / S columns / T
-  static constexpr int BUSP = cmax(BUS, n * L + R2) + 2;  // per-team stride (+2: no bank aliasing between teams)
+  static constexpr int BUSP = cmax(BUS, n * L + R2);   // static part of the per-team stride (doubles)
   static constexpr int RQ = cmax(2 * n, n + PX);  // register column of the Q.xx QR workspaces
 };
 
-struct RowInfo {  // one constraint row of the current knot (AL terms)
-  double c, w, ws, g;
+struct RowInfo {  // one constraint row of the current knot (AL terms), 64 B
+  double w, ws, g;
   double v[3];
   int idx[3];
   int nnz;
 };
 
+// Dynamic LDS layout of k_bwd_team (sizes from the host, bwd_team_layout):
+//   per team (stride doubles): [region 1: n*L][region 2: max(R2, rows area)]
+//     rows area (inside region 2, used only during the expansion): RowInfo[pmax], int xr[pmax],
+//     int ur[pmax], x[n], u[m]
+//   per block: ConRow cache[nrows] (deduplicated row table), int knot_off[N], int knot_cnt[N]
 template <class M>
-struct BwdTeamLds {
+__host__ __device__ inline int bwd_team_stride(int pmax) {
   using C = TeamCfg<M>;
-  double bus[C::TPW][C::BUSP];
-  RowInfo rows[C::TPW][PCAP];
-  int xrows[C::TPW][PCAP];  // rows of this knot with a state gradient, in row order
-  int urows[C::TPW][PCAP];  // rows of this knot with a control gradient, in row order
-  int nx[C::TPW], nu[C::TPW];
-};
+  const int rows_area = M::n * C::L + pmax * 8 + pmax + M::n + M::m;  // doubles (2 int lists = pmax doubles)
+  int s = C::BUSP > rows_area ? C::BUSP : rows_area;
+  s += (34 - s % 32) % 32;  // s = 2 mod 32: the TPW teams' broadcast reads land on distinct banks
+  return s;
+}
+inline size_t bwd_team_shmem(int stride, int tpw, int nrows, int N) {
+  return sizeof(double) * (size_t)stride * tpw + sizeof(ConRow) * (size_t)nrows + sizeof(int) * 2 * (size_t)N;
+}
 
 // Host-side admissibility of the team kernel for a problem (otherwise the LDS kernel runs).
-inline bool team_rows_fit(const int* knot_off, const int* knot_cnt, const ConRow* rows, int N, int n, int m) {
-  if (n + 1 > 16 || m > n) return false;
+constexpr int TEAM_MAX_ROWS = 128;   // deduplicated row table cached in LDS
+constexpr int TEAM_MAX_KNOTS = 1024;
+inline bool team_rows_fit(const int* knot_off, const int* knot_cnt, const ConRow* rows, int N, int n, int m,
+                          int nrows) {
+  if (n + 1 > 16 || m > n || nrows > TEAM_MAX_ROWS || N > TEAM_MAX_KNOTS) return false;
   for (int k = 0; k < N; k++) {
     int nx = 0, nu = 0;
     if (knot_cnt[k] > PCAP) return false;
@@ -75,40 +85,44 @@ inline bool team_rows_fit(const int* knot_off, const int* knot_cnt, const ConRow
 }
 
 // lane-parallel constraint evaluation into the team's row table (constraint_sets.jl:106-131,
-// active_set augmented_lagrangian_methods.jl:190-195). x, u point at global memory (rows index them
-// with runtime indices, which must not address register arrays); u == nullptr at the terminal knot.
+// active_set augmented_lagrangian_methods.jl:190-195). cr: this knot's rows in the LDS row cache;
+// x, u: the knot's state/control staged in LDS (u == nullptr at the terminal knot). The ordered
+// lists of rows with a state / control gradient are built with ballots (team-uniform control flow).
 template <class M>
-__device__ __forceinline__ void team_rows(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, int k,
-                                          const double* x, const double* u, RowInfo* rows, int* xr, int* ur, int* nx,
-                                          int* nu, int tl, int TEAM) {
+__device__ __forceinline__ void team_rows(const DevBuffers& Bf, long long b, int k, int N, int pmax, int p,
+                                          const ConRow* cr, const double* x, const double* u, RowInfo* rows,
+                                          int* xr, int* ur, int& nx, int& nu, int team, int tl, int TEAM) {
   constexpr int n = M::n;
-  const int N = P->N, pmax = P->pmax;
-  const int p = P->knot_cnt[k];
-  const ConRow* cr = P->rows + P->knot_off[k];
   const double* lam = Bf.lam + ((size_t)b * N + k) * pmax;
   const double* mu = Bf.mu + ((size_t)b * N + k) * pmax;
-  for (int r = tl; r < p; r += TEAM) {
-    RowInfo ri;
-    const double c = row_value(cr[r], x, u);
-    const double l = lam[r];
-    const bool a = row_inequality(cr[r]) ? ((c >= 0.0) || (l > 0.0)) : true;
-    ri.c = c;
-    ri.w = a ? mu[r] : 0.0;
-    ri.ws = a ? sqrt(mu[r]) : 0.0;
-    ri.g = ri.w * c + l;
-    ri.nnz = row_grad(cr[r], x, n, ri.idx, ri.v);
-    rows[r] = ri;
-  }
-  if (tl == 0) {
-    int cx = 0, cu = 0;
-    for (int r = 0; r < p; r++) {
-      const int t = cr[r].type;
-      if (t == ROW_UMAX || t == ROW_UMIN) ur[cu++] = r;
-      else xr[cx++] = r;
+  const unsigned long long tmask = (TEAM >= 64 ? ~0ull : ((1ull << TEAM) - 1ull)) << (team * TEAM);
+  const unsigned long long below = tmask & ((1ull << threadIdx.x) - 1ull);
+  int cx = 0, cu = 0;
+  for (int base = 0; base < p; base += TEAM) {
+    const int r = base + tl;
+    bool isx = false, isu = false;
+    if (r < p) {
+      const ConRow row = cr[r];
+      const double c = row_value(row, x, u);
+      const double l = lam[r];
+      const bool a = row_inequality(row) ? ((c >= 0.0) || (l > 0.0)) : true;
+      RowInfo ri;
+      ri.w = a ? mu[r] : 0.0;
+      ri.ws = a ? sqrt(mu[r]) : 0.0;
+      ri.g = ri.w * c + l;
+      ri.nnz = row_grad(row, x, n, ri.idx, ri.v);
+      rows[r] = ri;
+      isu = (row.type == ROW_UMAX || row.type == ROW_UMIN);
+      isx = !isu;
     }
-    *nx = cx;
-    *nu = cu;
+    const unsigned long long bx = __ballot(isx) & tmask, bu = __ballot(isu) & tmask;
+    if (isx) xr[cx + __popcll(bx & below)] = r;
+    if (isu) ur[cu + __popcll(bu & below)] = r;
+    cx += __popcll(bx);
+    cu += __popcll(bu);
   }
+  nx = cx;
+  nu = cu;
 }
 
 // entry of a row's gradient at [x;u] index `col` (0 if structurally zero)
@@ -252,12 +266,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
   constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, RQ = Cfg::RQ, PU = Cfg::PU, NQ = nq_of<M>();
   static_assert(m <= n && n + 1 <= TEAM, "team layout");
-  __shared__ BwdTeamLds<M> sh;
+  extern __shared__ double team_lds[];
   const int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
   const long long b = (long long)blockIdx.x * Cfg::TPW + team;
-  const int N = P->N;
+  const int N = P->N, pmax = P->pmax;
+  const int stride = Bf.bwd_stride;
+  double* bus = team_lds + (size_t)team * stride;
+  // block-wide caches: deduplicated constraint rows and the per-knot tables (read every knot)
+  ConRow* row_cache = reinterpret_cast<ConRow*>(team_lds + (size_t)Cfg::TPW * stride);
+  int* koff = reinterpret_cast<int*>(row_cache + P->nrows);
+  int* kcnt = koff + N;
+  if (AL) {
+    const int nr = P->nrows;
+    const double* src = reinterpret_cast<const double*>(P->rows);
+    double* dst = reinterpret_cast<double*>(row_cache);
+    for (int e = threadIdx.x; e < nr * (int)(sizeof(ConRow) / 8); e += 64) dst[e] = src[e];
+    for (int e = threadIdx.x; e < N; e += 64) {
+      koff[e] = P->knot_off[e];
+      kcnt[e] = P->knot_cnt[e];
+    }
+    __syncthreads();
+  }
   const bool live = (b < P->B) && Bf.st[b].active;
-  double* bus = sh.bus[team];
   const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
   const bool state_reg = (P->o.bp_reg_type == 1);
   const double dt = P->dt;
@@ -358,15 +388,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           Quxc[i] = 0.0;
         }
       }
-      if (AL && P->knot_cnt[k] > 0) {
-        RowInfo* rows = sh.rows[team];
-        team_rows<M>(P, Bf, b, k, xg, ug, rows, sh.xrows[team], sh.urows[team], &sh.nx[team], &sh.nu[team], tl,
-                     TEAM);
+      if (AL && kcnt[k] > 0) {
+        const int p = kcnt[k];
+        // rows area inside the second bus region (free during the expansion)
+        RowInfo* rows = reinterpret_cast<RowInfo*>(bus + n * L);
+        int* xr = reinterpret_cast<int*>(rows + pmax);
+        int* ur = xr + pmax;
+        double* xs = bus + n * L + pmax * 8 + pmax;
+        double* us = xs + n;
+        if (colx) xs[tl] = xc;
+        if (!term && colu) us[tl] = ug[tl];
         team_sync();
-        const int p = P->knot_cnt[k];
-        const int nx = sh.nx[team], nu = sh.nu[team];
-        const int* xr = sh.xrows[team];
-        const int* ur = sh.urows[team];
+        int nx, nu;
+        team_rows<M>(Bf, b, k, N, pmax, p, row_cache + koff[k], xs, term ? nullptr : us, rows, xr, ur, nx, nu, team,
+                     tl, TEAM);
+        team_sync();
         if (!SQRT) {
           // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order)
           double tX[n], tUx[m], tUu[m];
@@ -1026,46 +1062,75 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       team_sync();
 #pragma unroll
       for (int i = 0; i < n; i++) sv[i] = bus[TB + n * m + i];
-      // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! by each row of tmp1 (backward_pass.jl:186-192)
+      // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! by each row of tmp1 (backward_pass.jl:186-192).
+      // Systolic schedule: lane i owns row i of the factor; the downdate of (row r, column i) needs
+      // only (r, i-1) and (r-1, i), so step t runs (r = t - i, i) on every lane i < m: n+m-1 steps
+      // instead of n*m, each (r, i) with exactly the oracle's operations. x travels lane to lane
+      // through a double-buffered bus slot.
       double U2[m][m];
+      {
+        double urow[m], v[m];
 #pragma unroll
-      for (int j = 0; j < m; j++)
+        for (int jj = 0; jj < m; jj++) {
+          double q = 0.0;
 #pragma unroll
-        for (int i = 0; i < m; i++) U2[i][j] = Quu[i][j];
-      bool okd = true;
+          for (int ii = 0; ii < m; ii++)
+            if (ii == tl) q = Quu[ii][jj];
+          urow[jj] = q;
+          v[jj] = 0.0;
+        }
+        double* msg = bus2;  // [2][m][m]
+        bool okd = true;
 #pragma unroll 1
-      for (int r = 0; r < n; r++) {
-        double v[m];
+        for (int t = 0; t < n + m - 1; t++) {
+          const int r = t - tl;
+          if (colu && r >= 0 && r < n) {
+            if (tl == 0) {
 #pragma unroll
-        for (int j = 0; j < m; j++) v[j] = bus[TB + r * m + j];
-#pragma unroll
-        for (int i = 0; i < m; i++) {
-          if (okd) {
-            const double Aii = U2[i][i];
-            const double sn = v[i] / Aii;
-            const double s2 = sn * sn;
-            if (s2 > 1.0) {
-              okd = false;
+              for (int jj = 0; jj < m; jj++) v[jj] = bus[TB + r * m + jj];
             } else {
-              const double cs = sqrt(1.0 - s2);
-              U2[i][i] = cs * Aii;
+              const double* in = msg + ((t - 1) & 1) * m * m + (tl - 1) * m;
 #pragma unroll
-              for (int j = i + 1; j < m; j++) {
-                const double tmp = (U2[i][j] - sn * v[j]) / cs;
-                v[j] = cs * v[j] - sn * tmp;
-                U2[i][j] = tmp;
+              for (int jj = 0; jj < m; jj++) v[jj] = in[jj];
+            }
+            double Aii = urow[0], vi = v[0];
+#pragma unroll
+            for (int ii = 1; ii < m; ii++)
+              if (ii == tl) {
+                Aii = urow[ii];
+                vi = v[ii];
+              }
+            const double sn = vi / Aii;
+            const double s2 = sn * sn;
+            if (s2 > 1.0) okd = false;
+            const double cs = sqrt(1.0 - s2);
+#pragma unroll
+            for (int jj = 0; jj < m; jj++) {
+              if (jj == tl) urow[jj] = cs * Aii;
+              if (jj > tl) {
+                const double tmp = (urow[jj] - sn * v[jj]) / cs;
+                v[jj] = cs * v[jj] - sn * tmp;
+                urow[jj] = tmp;
               }
             }
+            double* out = msg + (t & 1) * m * m + tl * m;
+#pragma unroll
+            for (int jj = 0; jj < m; jj++) out[jj] = v[jj];
           }
+          team_sync();
         }
-        if (!okd) break;
-      }
-      if (!okd) {
-        s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
+        const unsigned long long tmask = (TEAM >= 64 ? ~0ull : ((1ull << TEAM) - 1ull)) << (team * TEAM);
+        const bool fail = (__ballot(!okd) & tmask) != 0ull;
+        if (colu) {
 #pragma unroll
-        for (int j = 0; j < m; j++)
+          for (int jj = 0; jj < m; jj++) bus2[2 * m * m + tl * m + jj] = (jj >= tl) ? urow[jj] : 0.0;
+        }
+        team_sync();
 #pragma unroll
-          for (int i = 0; i < m; i++) U2[i][j] = Quu[i][j];
+        for (int jj = 0; jj < m; jj++)
+#pragma unroll
+          for (int ii = 0; ii < m; ii++) U2[ii][jj] = fail ? Quu[ii][jj] : bus2[2 * m * m + ii * m + jj];
+        if (fail) s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
       }
       // S[k] = qr([Q.xx + tmp1 K; tmp2 K]).R
       {

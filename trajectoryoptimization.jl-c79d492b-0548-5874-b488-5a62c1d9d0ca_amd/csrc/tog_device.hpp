@@ -96,6 +96,9 @@ struct DevBuffers {
   double* lsJ;  // (NC, B) speculative line-search trial costs
   int* lsok;    // (NC, B) speculative line-search trial rollout status
   int nc;       // candidates evaluated per trajectory per launch (<= 64)
+  int bwd_stride;  // k_bwd_team: per-team LDS stride (doubles)
+  int bwd_shmem;   // k_bwd_team: dynamic LDS bytes per block
+  int pad_;
   TrajState* st;
 };
 

@@ -1477,6 +1477,8 @@ struct ModelOps {
   void (*rollout)(const DevProblem*, const DevBuffers&, long long B, int integ, double alpha, int* ok, hipStream_t);
   void (*update_constraints)(const DevProblem*, const DevBuffers&, long long B, hipStream_t);
   int bwd_lds_bytes;
+  int team_tpw;                    // trajectories per wave of k_bwd_team
+  int (*team_stride)(int pmax);    // per-team LDS stride of k_bwd_team (doubles)
 };
 
 template <class M>
@@ -1510,12 +1512,13 @@ struct ModelLaunch {
     if (team) {  // column-per-lane teams, TPW trajectories per wave (tog_bwd_team.hpp)
       constexpr int TPW = TeamCfg<M>::TPW;
       const dim3 g((unsigned)((B + TPW - 1) / TPW)), blk(64);
+      const unsigned sm = (unsigned)Bf.bwd_shmem;
       if (sq) {
-        if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1>), g, blk, 0, st, P, Bf, flags);
-        else hipLaunchKernelGGL((k_bwd_team<M, 1, 0>), g, blk, 0, st, P, Bf, flags);
+        if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1>), g, blk, sm, st, P, Bf, flags);
+        else hipLaunchKernelGGL((k_bwd_team<M, 1, 0>), g, blk, sm, st, P, Bf, flags);
       } else {
-        if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1>), g, blk, 0, st, P, Bf, flags);
-        else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, 0, st, P, Bf, flags);
+        if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1>), g, blk, sm, st, P, Bf, flags);
+        else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, sm, st, P, Bf, flags);
       }
       return;
     }
@@ -1566,6 +1569,8 @@ struct ModelLaunch {
     o.rollout = rollout;
     o.update_constraints = update_constraints;
     o.bwd_lds_bytes = (int)sizeof(BwdLds<M, true>);
+    o.team_tpw = TeamCfg<M>::TPW;
+    o.team_stride = bwd_team_stride<M>;
     return o;
   }
 };

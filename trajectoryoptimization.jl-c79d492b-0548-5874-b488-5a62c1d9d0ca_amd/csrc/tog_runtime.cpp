@@ -166,6 +166,16 @@ static int build_rows(const tog_problem_desc* d, std::vector<ConRow>& rows, std:
     }
     cnt[k] = (int)rows.size() - off[k];
     if (cnt[k] > PCAP) return fail(TOG_ERR_UNSUPPORTED, "more than PCAP constraint rows at one knot");
+    // knots with the same rows share one copy (stage knots of one ConstraintSet): the table stays
+    // small enough for the backward kernel to cache it in LDS
+    for (int j = 0; j < k; j++) {
+      if (cnt[j] != cnt[k] || cnt[k] == 0) continue;
+      if (memcmp(&rows[off[j]], &rows[off[k]], sizeof(ConRow) * cnt[k]) == 0) {
+        rows.resize(off[k]);
+        off[k] = off[j];
+        break;
+      }
+    }
   }
   return TOG_OK;
 }
@@ -380,7 +390,11 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
     // TOG_BWD=lds forces the one-wave-per-trajectory LDS backward kernel (A/B checks)
     const char* ev = getenv("TOG_BWD");
     const bool force_lds = ev && strcmp(ev, "lds") == 0;
-    h->bwd_team = (!force_lds && team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m)) ? 1 : 0;
+    h->bwd_team = (!force_lds && team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
+                      ? 1 : 0;
+    h->buf.bwd_stride = ops->team_stride(h->pmax);
+    h->buf.bwd_shmem = (int)bwd_team_shmem(h->buf.bwd_stride, ops->team_tpw, (int)rows.size(), N);
+    if (h->buf.bwd_shmem > 64 * 1024) h->bwd_team = 0;
   }
   P.knot_off = h->d_knot_off;
   P.knot_cnt = h->d_knot_cnt;
