@@ -187,6 +187,8 @@ def load_library(path: os.PathLike | None = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
+    if path is None and os.environ.get("TOG_LIBRARY"):  # A/B builds (e.g. tools/ab_build.sh)
+        path = os.environ["TOG_LIBRARY"]
     p = pathlib.Path(path) if path else LIB_PATH
     if not p.exists():
         raise RuntimeError(f"libtog.so not found at {p}: run __graft_entry__.build() (hipcc, gfx950)")

@@ -15,6 +15,7 @@
 // results are bit-identical. Terms that are exact zeros by structure (S below its diagonal, sparse
 // constraint Jacobians) are skipped: fma(0, y, t) == t.
 #pragma once
+#include <type_traits>
 // (included by tog_kernels.hpp after the LDS kernels; relies on their helpers)
 
 namespace tog {
@@ -53,11 +54,18 @@ struct RowInfo {  // one constraint row of the current knot (AL terms), 64 B
 //     rows area (inside region 2, used only during the expansion): RowInfo[pmax], int xr[pmax],
 //     int ur[pmax], x[n], u[m]
 //   per block: ConRow cache[nrows] (deduplicated row table), int knot_off[N], int knot_cnt[N]
+// S-region (persistent across knots, before region 1): std stores S column-major and s
+// (n*n + n); sqrt stores the upper factor packed by columns (column c at c(c+1)/2) and s.
 template <class M>
-__host__ __device__ inline int bwd_team_stride(int pmax) {
+__host__ __device__ constexpr int sreg_size(bool sqrt) {  // S, s, then the knot's Q.uu (m*m)
+  return (sqrt ? M::n * (M::n + 1) / 2 + M::n : M::n * M::n + M::n) + M::m * M::m;
+}
+template <class M>
+__host__ __device__ inline int bwd_team_stride(int pmax, int sqrt) {
   using C = TeamCfg<M>;
   const int rows_area = M::n * C::L + pmax * 8 + pmax + M::n + M::m;  // doubles (2 int lists = pmax doubles)
   int s = C::BUSP > rows_area ? C::BUSP : rows_area;
+  s += sreg_size<M>(sqrt != 0);
   s += (34 - s % 32) % 32;  // s = 2 mod 32: the TPW teams' broadcast reads land on distinct banks
   return s;
 }
@@ -181,78 +189,79 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
   }
 }
 
-// cond(R) > thresh for an upper-triangular m x m R in registers (same decision procedure and
-// arithmetic as cond_exceeds; backward_pass.jl:129)
+// cond(R) > thresh for an upper-triangular m x m R held by every lane of the team (same decision
+// procedure and arithmetic as cond_exceeds; backward_pass.jl:129). R^-1 is formed one column at a
+// time (few live registers); the Jacobi SVD of the rare ambiguous band runs on lane 0 of the team
+// in LDS scratch `w` (m*m + 1 doubles) and its verdict is broadcast.
 template <int m>
-__device__ __forceinline__ bool cond_exceeds_reg(const double (&R)[m][m], double thresh) {
-  double Ri[m][m];
-#pragma unroll
-  for (int c = 0; c < m; c++) {
-#pragma unroll
-    for (int i = 0; i < m; i++) Ri[i][c] = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-    for (int j = m - 1; j >= 0; j--) {
-      const double xj = Ri[j][c] / R[j][j];
-      Ri[j][c] = xj;
-#pragma unroll
-      for (int i = j - 1; i >= 0; i--) Ri[i][c] -= R[i][j] * xj;
-    }
-  }
+__device__ __forceinline__ bool cond_exceeds_team(const double (&R)[m][m], double thresh, double* w, int tl) {
   double nr = 0.0, ni = 0.0;
 #pragma unroll
-  for (int j = 0; j < m; j++)
+  for (int c = 0; c < m; c++) {
+    double ric[m];
+#pragma unroll
+    for (int i = 0; i < m; i++) ric[i] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = m - 1; j >= 0; j--) {
+      const double xj = ric[j] / R[j][j];
+      ric[j] = xj;
+#pragma unroll
+      for (int i = j - 1; i >= 0; i--) ric[i] -= R[i][j] * xj;
+    }
 #pragma unroll
     for (int i = 0; i < m; i++) {
-      nr += R[i][j] * R[i][j];
-      ni += Ri[i][j] * Ri[i][j];
+      nr += R[i][c] * R[i][c];
+      ni += ric[i] * ric[i];
     }
+  }
   const double cF = sqrt(nr) * sqrt(ni);
   if (cF <= thresh) return false;
   if (cF / m > thresh) return true;
-  double A[m][m];  // ambiguous band: one-sided Jacobi singular values
+  // ambiguous band (team-uniform): one-sided Jacobi singular values on lane 0
+  if (tl == 0) {
+    double* A = w;
 #pragma unroll
-  for (int j = 0; j < m; j++)
+    for (int j = 0; j < m; j++)
 #pragma unroll
-    for (int i = 0; i < m; i++) A[i][j] = R[i][j];
-  for (int sweep = 0; sweep < 60; sweep++) {
-    double off = 0.0;
-#pragma unroll
-    for (int p = 0; p < m - 1; p++)
-#pragma unroll
-      for (int q = p + 1; q < m; q++) {
-        double al = 0, be = 0, ga = 0;
-#pragma unroll
-        for (int i = 0; i < m; i++) {
-          al += A[i][p] * A[i][p];
-          be += A[i][q] * A[i][q];
-          ga += A[i][p] * A[i][q];
+      for (int i = 0; i < m; i++) A[i + m * j] = R[i][j];
+    for (int sweep = 0; sweep < 60; sweep++) {
+      double off = 0.0;
+      for (int p = 0; p < m - 1; p++)
+        for (int q = p + 1; q < m; q++) {
+          double al = 0, be = 0, ga = 0;
+          for (int i = 0; i < m; i++) {
+            al += A[i + m * p] * A[i + m * p];
+            be += A[i + m * q] * A[i + m * q];
+            ga += A[i + m * p] * A[i + m * q];
+          }
+          if (ga == 0.0) continue;
+          const double c0 = fabs(ga) / sqrt(al * be);
+          off = fmax(off, c0);
+          if (c0 < 1e-15) continue;
+          const double zeta = (be - al) / (2.0 * ga);
+          const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+          const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+          for (int i = 0; i < m; i++) {
+            const double ap = A[i + m * p], aq = A[i + m * q];
+            A[i + m * p] = cs * ap - sn * aq;
+            A[i + m * q] = sn * ap + cs * aq;
+          }
         }
-        if (ga == 0.0) continue;
-        const double c0 = fabs(ga) / sqrt(al * be);
-        off = fmax(off, c0);
-        if (c0 < 1e-15) continue;
-        const double zeta = (be - al) / (2.0 * ga);
-        const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
-#pragma unroll
-        for (int i = 0; i < m; i++) {
-          const double ap = A[i][p], aq = A[i][q];
-          A[i][p] = cs * ap - sn * aq;
-          A[i][q] = sn * ap + cs * aq;
-        }
-      }
-    if (off < 1e-15) break;
+      if (off < 1e-15) break;
+    }
+    double smax = 0.0, smin = INFINITY;
+    for (int j = 0; j < m; j++) {
+      double s2 = 0.0;
+      for (int i = 0; i < m; i++) s2 += A[i + m * j] * A[i + m * j];
+      smax = fmax(smax, sqrt(s2));
+      smin = fmin(smin, sqrt(s2));
+    }
+    w[m * m] = ((smax / smin) > thresh) ? 1.0 : 0.0;
   }
-  double smax = 0.0, smin = INFINITY;
-#pragma unroll
-  for (int j = 0; j < m; j++) {
-    double s2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < m; i++) s2 += A[i][j] * A[i][j];
-    smax = fmax(smax, sqrt(s2));
-    smin = fmin(smin, sqrt(s2));
-  }
-  return (smax / smin) > thresh;
+  team_sync();
+  const bool r = w[m * m] != 0.0;
+  team_sync();
+  return r;
 }
 
 #ifndef TOG_BWD_WAVES
@@ -271,7 +280,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   const long long b = (long long)blockIdx.x * Cfg::TPW + team;
   const int N = P->N, pmax = P->pmax;
   const int stride = Bf.bwd_stride;
-  double* bus = team_lds + (size_t)team * stride;
+  constexpr int SREG = sreg_size<M>(SQRT);
+  constexpr int SOFF = SQRT ? n * (n + 1) / 2 : n * n;  // offset of s in the S-region
+  double* Sreg = team_lds + (size_t)team * stride;      // S (persistent between knots)
+  double* QU = Sreg + SOFF + n;                          // Q.uu of the current knot (column-major)
+  double* bus = Sreg + SREG;                             // region 1 | region 2
   // block-wide caches: deduplicated constraint rows and the per-knot tables (read every knot)
   ConRow* row_cache = reinterpret_cast<ConRow*>(team_lds + (size_t)Cfg::TPW * stride);
   int* koff = reinterpret_cast<int*>(row_cache + P->nrows);
@@ -310,223 +323,233 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   bool faithful = false;  // replay mode reproducing the A.1 re-accumulation exactly
   int kmin = N - 1, restarts = 0;
   double dV0 = 0.0, dV1 = 0.0;
-  double Sc[n], sv[n];  // column c of S (std: symmetric; sqrt: upper factor) ; s (replicated)
-#pragma unroll
-  for (int i = 0; i < n; i++) {
-    Sc[i] = 0.0;
-    sv[i] = 0.0;
-  }
-  double sown = 0.0;  // s[c]
-  int k = N - 1;      // N-1: (re)start from the terminal expansion
+  double sown = 0.0;  // s[c] of the knot being produced
   bool done = !live;
 
-  while (!done) {
-    const bool term = (k == N - 1);
+  // cost expansion of knot k (terminal when TERM) into this lane's Q blocks; the AL terms use the
+  // team's row table (objective.jl:51-94, augmented_lagrangian_methods.jl:186-276)
+  auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
+                    double(&Quxc)[m]) {
+    constexpr bool term = decltype(term_c)::value;
     const double* xg = Xg + (size_t)k * n;
     const double* ug = term ? nullptr : Ug + (size_t)k * m;
-    // ---------------------------------------------------------------- expansion (or Q replay)
-    double Qxc[n], Quuc[m], Quxc[m], Qu[m], Qxs;
-    const bool replay = faithful && !term && k >= kmin;
-    if (replay) {
-      const double* q = Qs + (size_t)k * NQ;
-      Qxs = q[c];
-#pragma unroll
-      for (int i = 0; i < m; i++) Qu[i] = q[n + i];
-#pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = q[n + m + i + n * c];
-#pragma unroll
-      for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
-#pragma unroll
-      for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
-    } else {
-      const double xc = xg[c];
-      if (!term) {
-        double a = 0.0, bq = 0.0;
-        if (P->diag_cost) {
-          a = fma(P->Q[c + n * c], xc, 0.0);
-        } else {
-#pragma unroll
-          for (int j = 0; j < n; j++) a = fma(P->Q[c + n * j], xg[j], a);
-#pragma unroll
-          for (int j = 0; j < m; j++) bq = fma(P->H[j + m * c], ug[j], bq);
-        }
-        Qxs = ((a + P->q[c]) + bq) * dt;
-#pragma unroll
-        for (int i = 0; i < m; i++) {
-          double a2 = 0.0, b2 = 0.0;
-          if (P->diag_cost) {
-            a2 = fma(P->R[i + m * i], ug[i], 0.0);
-          } else {
-#pragma unroll
-            for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
-#pragma unroll
-            for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
-          }
-          Qu[i] = ((a2 + P->r[i]) + b2) * dt;
-        }
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
-#pragma unroll
-        for (int i = 0; i < m; i++) Quuc[i] = SQRT ? P->cR[i + m * cu] : P->R[i + m * cu] * dt;
-#pragma unroll
-        for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;
+    const double xc = xg[c];
+    if (!term) {
+      double a = 0.0, bq = 0.0;
+      if (P->diag_cost) {
+        a = fma(P->Q[c + n * c], xc, 0.0);
       } else {
-        double a = 0.0;
-        if (P->diag_cost) {
-          a = fma(P->Qf[c + n * c], xc, 0.0);
-        } else {
 #pragma unroll
-          for (int j = 0; j < n; j++) a = fma(P->Qf[c + n * j], xg[j], a);
-        }
-        Qxs = a + P->qf[c];
+        for (int j = 0; j < n; j++) a = fma(P->Q[c + n * j], xg[j], a);
 #pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQf[i + n * c] : P->Qf[i + n * c];
-#pragma unroll
-        for (int i = 0; i < m; i++) {
-          Qu[i] = 0.0;
-          Quuc[i] = 0.0;
-          Quxc[i] = 0.0;
-        }
+        for (int j = 0; j < m; j++) bq = fma(P->H[j + m * c], ug[j], bq);
       }
-      if (AL && kcnt[k] > 0) {
-        const int p = kcnt[k];
-        // rows area inside the second bus region (free during the expansion)
-        RowInfo* rows = reinterpret_cast<RowInfo*>(bus + n * L);
-        int* xr = reinterpret_cast<int*>(rows + pmax);
-        int* ur = xr + pmax;
-        double* xs = bus + n * L + pmax * 8 + pmax;
-        double* us = xs + n;
-        if (colx) xs[tl] = xc;
-        if (!term && colu) us[tl] = ug[tl];
-        team_sync();
-        int nx, nu;
-        team_rows<M>(Bf, b, k, N, pmax, p, row_cache + koff[k], xs, term ? nullptr : us, rows, xr, ur, nx, nu, team,
-                     tl, TEAM);
-        team_sync();
-        if (!SQRT) {
-          // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order)
-          double tX[n], tUx[m], tUu[m];
+      Qxs = ((a + P->q[c]) + bq) * dt;
 #pragma unroll
-          for (int i = 0; i < n; i++) tX[i] = 0.0;
-#pragma unroll
-          for (int i = 0; i < m; i++) {
-            tUx[i] = 0.0;
-            tUu[i] = 0.0;
-          }
-          for (int r = 0; r < p; r++) {
-            const RowInfo& ri = rows[r];
-            const double vxc = colx ? row_at(ri, c) : 0.0;
-            const double vuc = (colu && !term) ? row_at(ri, n + cu) : 0.0;
-            if (vxc == 0.0 && vuc == 0.0) continue;
-            for (int z = 0; z < ri.nnz; z++) {
-              const int id = ri.idx[z];
-              const double vw = ri.v[z] * ri.w;
-#pragma unroll
-              for (int i = 0; i < n; i++)
-                if (id == i && vxc != 0.0) tX[i] = fma(vw, vxc, tX[i]);
-#pragma unroll
-              for (int i = 0; i < m; i++)
-                if (id == n + i) {
-                  if (vxc != 0.0) tUx[i] = fma(vw, vxc, tUx[i]);
-                  if (vuc != 0.0) tUu[i] = fma(vw, vuc, tUu[i]);
-                }
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < n; i++) Qxc[i] += tX[i];
-          if (!term) {
-#pragma unroll
-            for (int i = 0; i < m; i++) {
-              Quuc[i] += tUu[i];
-              Quxc[i] += tUx[i];
-            }
-          }
+      for (int i = 0; i < m; i++) {
+        double a2 = 0.0, b2 = 0.0;
+        if (P->diag_cost) {
+          a2 = fma(P->R[i + m * i], ug[i], 0.0);
         } else {
-          // chol_plus!(Q.xx, Iμ_sqrt cx): QR of [Q.xx; ws.*cx]; rows without a state gradient are
-          // zero rows of the stacked matrix and do not change R
-          if (nx > 0) {
-            double a[RQ];
 #pragma unroll
-            for (int i = 0; i < RQ; i++) {
-              if (i < n) {
-                a[i] = Qxc[i];
-              } else if (i - n < nx) {
-                const RowInfo& ri = rows[xr[i - n]];
-                a[i] = ri.ws * row_at(ri, c);
-              } else {
-                a[i] = 0.0;
-              }
-            }
-            team_qr<RQ, n>(a, n + nx, tl, bus);
+          for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
 #pragma unroll
-            for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
-          }
-          // chol_plus!(Q.uu, Iμ_sqrt cu)
-          if (!term && nu > 0) {
-            double a[m + PU];
-#pragma unroll
-            for (int i = 0; i < m + PU; i++) {
-              if (i < m) {
-                a[i] = Quuc[i];
-              } else if (i - m < nu) {
-                const RowInfo& ri = rows[ur[i - m]];
-                a[i] = ri.ws * row_at(ri, n + cu);
-              } else {
-                a[i] = 0.0;
-              }
-            }
-            team_qr<m + PU, m>(a, m + nu, tl, bus);
-#pragma unroll
-            for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
-          }
+          for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
         }
-        // Q.x .+= cx'g ; Q.u .+= cu'g
-        {
-          double tx = 0.0;
-          for (int z = 0; z < nx; z++) {
-            const RowInfo& ri = rows[xr[z]];
-            const double v = colx ? row_at(ri, c) : 0.0;
-            if (v != 0.0) tx = fma(v, ri.g, tx);
-          }
-          Qxs += tx;
-          if (!term) {
-            double tu[m];
+        Qu[i] = ((a2 + P->r[i]) + b2) * dt;
+      }
 #pragma unroll
-            for (int i = 0; i < m; i++) tu[i] = 0.0;
-            for (int z = 0; z < nu; z++) {
-              const RowInfo& ri = rows[ur[z]];
-              const int id = ri.idx[0];
+      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
 #pragma unroll
-              for (int i = 0; i < m; i++)
-                if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
-            }
+      for (int i = 0; i < m; i++) Quuc[i] = SQRT ? P->cR[i + m * cu] : P->R[i + m * cu] * dt;
 #pragma unroll
-            for (int i = 0; i < m; i++) Qu[i] += tu[i];
-          }
-        }
-        team_sync();
+      for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;
+    } else {
+      double a = 0.0;
+      if (P->diag_cost) {
+        a = fma(P->Qf[c + n * c], xc, 0.0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < n; j++) a = fma(P->Qf[c + n * j], xg[j], a);
+      }
+      Qxs = a + P->qf[c];
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQf[i + n * c] : P->Qf[i + n * c];
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        Qu[i] = 0.0;
+        Quuc[i] = 0.0;
+        Quxc[i] = 0.0;
       }
     }
-    if (term) {
-      // S[N] = Q[N] (backward_pass.jl:20-21 / :100-101)
-#pragma unroll
-      for (int i = 0; i < n; i++) Sc[i] = Qxc[i];
-      sown = Qxs;
-      if (colx) bus[tl] = Qxs;
+    if (AL && kcnt[k] > 0) {
+      const int p = kcnt[k];
+      // rows area inside the second bus region (free during the expansion)
+      RowInfo* rows = reinterpret_cast<RowInfo*>(bus + n * L);
+      int* xr = reinterpret_cast<int*>(rows + pmax);
+      int* ur = xr + pmax;
+      double* xs = bus + n * L + pmax * 8 + pmax;
+      double* us = xs + n;
+      if (colx) xs[tl] = xc;
+      if (!term && colu) us[tl] = ug[tl];
       team_sync();
+      int nx, nu;
+      team_rows<M>(Bf, b, k, N, pmax, p, row_cache + koff[k], xs, term ? nullptr : us, rows, xr, ur, nx, nu, team,
+                   tl, TEAM);
+      team_sync();
+      if (!SQRT) {
+        // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order)
+        double tX[n], tUx[m], tUu[m];
 #pragma unroll
-      for (int i = 0; i < n; i++) sv[i] = bus[i];
+        for (int i = 0; i < n; i++) tX[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          tUx[i] = 0.0;
+          tUu[i] = 0.0;
+        }
+        for (int r = 0; r < p; r++) {
+          const RowInfo& ri = rows[r];
+          const double vxc = colx ? row_at(ri, c) : 0.0;
+          const double vuc = (colu && !term) ? row_at(ri, n + cu) : 0.0;
+          if (vxc == 0.0 && vuc == 0.0) continue;
+          for (int z = 0; z < ri.nnz; z++) {
+            const int id = ri.idx[z];
+            const double vw = ri.v[z] * ri.w;
+#pragma unroll
+            for (int i = 0; i < n; i++)
+              if (id == i && vxc != 0.0) tX[i] = fma(vw, vxc, tX[i]);
+#pragma unroll
+            for (int i = 0; i < m; i++)
+              if (id == n + i) {
+                if (vxc != 0.0) tUx[i] = fma(vw, vxc, tUx[i]);
+                if (vuc != 0.0) tUu[i] = fma(vw, vuc, tUu[i]);
+              }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] += tX[i];
+        if (!term) {
+#pragma unroll
+          for (int i = 0; i < m; i++) {
+            Quuc[i] += tUu[i];
+            Quxc[i] += tUx[i];
+          }
+        }
+      } else {
+        // chol_plus!(Q.xx, Iμ_sqrt cx): QR of [Q.xx; ws.*cx]; rows without a state gradient are
+        // zero rows of the stacked matrix and do not change R
+        if (nx > 0) {
+          double a[RQ];
+#pragma unroll
+          for (int i = 0; i < RQ; i++) {
+            if (i < n) {
+              a[i] = Qxc[i];
+            } else if (i - n < nx) {
+              const RowInfo& ri = rows[xr[i - n]];
+              a[i] = ri.ws * row_at(ri, c);
+            } else {
+              a[i] = 0.0;
+            }
+          }
+          team_qr<RQ, n>(a, n + nx, tl, bus);
+#pragma unroll
+          for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
+        }
+        // chol_plus!(Q.uu, Iμ_sqrt cu)
+        if (!term && nu > 0) {
+          double a[m + PU];
+#pragma unroll
+          for (int i = 0; i < m + PU; i++) {
+            if (i < m) {
+              a[i] = Quuc[i];
+            } else if (i - m < nu) {
+              const RowInfo& ri = rows[ur[i - m]];
+              a[i] = ri.ws * row_at(ri, n + cu);
+            } else {
+              a[i] = 0.0;
+            }
+          }
+          team_qr<m + PU, m>(a, m + nu, tl, bus);
+#pragma unroll
+          for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+        }
+      }
+      // Q.x .+= cx'g ; Q.u .+= cu'g
+      {
+        double tx = 0.0;
+        for (int z = 0; z < nx; z++) {
+          const RowInfo& ri = rows[xr[z]];
+          const double v = colx ? row_at(ri, c) : 0.0;
+          if (v != 0.0) tx = fma(v, ri.g, tx);
+        }
+        Qxs += tx;
+        if (!term) {
+          double tu[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) tu[i] = 0.0;
+          for (int z = 0; z < nu; z++) {
+            const RowInfo& ri = rows[ur[z]];
+            const int id = ri.idx[0];
+#pragma unroll
+            for (int i = 0; i < m; i++)
+              if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
+          }
+#pragma unroll
+          for (int i = 0; i < m; i++) Qu[i] += tu[i];
+        }
+      }
+      team_sync();
+    }
+  };
+
+  while (!done) {  // one attempt of the backward pass; a regularisation restart begins a new one
+    TEAM_FENCE();
+    {
+      double Qxc[n], Quuc[m], Quxc[m], Qu[m], Qxs;
+      expand(N - 1, std::integral_constant<bool, true>{}, Qxs, Qu, Qxc, Quuc, Quxc);
+      // S[N] = Q[N] (backward_pass.jl:20-21 / :100-101)
+      if (colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          if (SQRT) {
+            if (i <= tl) Sreg[tl * (tl + 1) / 2 + i] = Qxc[i];
+          } else {
+            Sreg[i + n * tl] = Qxc[i];
+          }
+        }
+        Sreg[SOFF + tl] = Qxs;
+      }
       team_sync();
       if (store_S && colx) {
 #pragma unroll
-        for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = Sc[i];
-        Bf.sdbg[((size_t)b * N + k) * n + tl] = sown;
+        for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + (N - 1)) * n * n + i + n * tl] = Qxc[i];
+        Bf.sdbg[((size_t)b * N + (N - 1)) * n + tl] = Qxs;
       }
-      dV0 = 0.0;
-      dV1 = 0.0;
-      k = N - 2;
-      continue;
+
     }
+    dV0 = 0.0;
+    dV1 = 0.0;
+    bool restart = false;
+    for (int k = N - 2; k >= 0; k--) {
+      // keep the per-lane problem constants (cQ/cR/H/Q columns) loaded per knot: hoisted out of
+      // the loop they would stay live across it and spill
+      TEAM_FENCE();
+      double Qxc[n], Quuc[m], Quxc[m], Qu[m], Qxs;
+      const bool replay = faithful && k >= kmin;
+      if (replay) {
+        const double* q = Qs + (size_t)k * NQ;
+        Qxs = q[c];
+  #pragma unroll
+        for (int i = 0; i < m; i++) Qu[i] = q[n + i];
+  #pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = q[n + m + i + n * c];
+  #pragma unroll
+        for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
+  #pragma unroll
+        for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
+      } else {
+        expand(k, std::integral_constant<bool, false>{}, Qxs, Qu, Qxc, Quuc, Quxc);
+      }
     // ---------------------------------------------------------------- ∇F[k] = [A|B] columns
     double Ac[n], Bc[n];
     {
@@ -541,11 +564,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     {
       double t = 0.0;
 #pragma unroll
-      for (int l = 0; l < n; l++) t = fma(Ac[l], sv[l], t);
+      for (int l = 0; l < n; l++) t = fma(Ac[l], Sreg[SOFF + l], t);
       Qxs += t;
       double tu = 0.0;
 #pragma unroll
-      for (int l = 0; l < n; l++) tu = fma(Bc[l], sv[l], tu);
+      for (int l = 0; l < n; l++) tu = fma(Bc[l], Sreg[SOFF + l], tu);
       if (colu) bus[tl] = tu;
       team_sync();
 #pragma unroll
@@ -567,6 +590,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       team_sync();
       // W = [A B]' S, column c per lane, written straight to the second bus region
       if (colx) {
+        double Sc[n];
+#pragma unroll
+        for (int l = 0; l < n; l++) Sc[l] = Sreg[l + n * c];
 #pragma unroll 1
         for (int i = 0; i < L; i++) {
           double t = 0.0;
@@ -609,11 +635,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     } else {
       // tmp_x = S A, tmp_u = S B ; Q.ux += tmp_u' tmp_x ; Q.xx <- qr([Q.xx; tmp_x]).R ;
       // Q.uu <- qr([Q.uu; tmp_u]).R   (backward_pass.jl:112-118). Dense products, l ascending.
-      if (colx) {
-#pragma unroll
-        for (int i = 0; i < n; i++) bus2[i + n * tl] = Sc[i];
-      }
-      team_sync();
       double TX[n], TU[n];
 #pragma unroll
       for (int i = 0; i < n; i++) {
@@ -624,9 +645,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       for (int l = 0; l < n; l++) {
         const double al = bus[l + n * c];
         const double bl = bus[l + n * (n + cu)];
+        const double* Sl = Sreg + l * (l + 1) / 2;  // packed column l (rows 0..l)
 #pragma unroll
         for (int i = 0; i < n; i++) {
-          const double sil = bus2[i + n * l];
+          const double sil = (i <= l) ? Sl[i] : 0.0;  // dense product, explicit zeros as the oracle
           TX[i] = fma(sil, al, TX[i]);
           TU[i] = fma(sil, bl, TU[i]);
         }
@@ -657,20 +679,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       }
       team_sync();
       {
-        double a[2 * n];
-#pragma unroll
-        for (int i = 0; i < 2 * n; i++) a[i] = (i < n) ? Qxc[i] : TX[i - n];
-        team_qr<2 * n, n>(a, 2 * n, tl, bus);
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
-      }
-      {
         double a[m + n];
 #pragma unroll
         for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : TU[i - m];
         team_qr<m + n, m>(a, m + n, tl, bus);
 #pragma unroll
         for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+      }
+      {
+        double a[2 * n];
+#pragma unroll
+        for (int i = 0; i < 2 * n; i++) a[i] = (i < n) ? Qxc[i] : TX[i - n];
+        team_qr<2 * n, n>(a, 2 * n, tl, bus);
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
       }
     }
     if (faithful) {
@@ -696,7 +718,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     // (backward_pass.jl:38-48 / :120-126). Every lane needs the full Q.uu: all-gather its columns.
     if (colu) {
 #pragma unroll
-      for (int i = 0; i < m; i++) bus[i + m * tl] = Quuc[i];
+      for (int i = 0; i < m; i++) QU[i + m * tl] = Quuc[i];
       if (state_reg) {  // (:state regularisation only; reloaded to keep [A|B] out of registers)
         const double* bk = ABg + (size_t)k * n * L + n * (n + tl);
 #pragma unroll
@@ -704,11 +726,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       }
     }
     team_sync();
-    double Quu[m][m];
-#pragma unroll
-    for (int j = 0; j < m; j++)
-#pragma unroll
-      for (int i = 0; i < m; i++) Quu[i][j] = bus[i + m * j];
     // right-hand side of this lane: Qux_reg column (state reg adds ρ B'A), or Q.u for lane n
     double col[m];
     if (colx) {
@@ -739,7 +756,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
       for (int j = 0; j < m; j++)
 #pragma unroll
-        for (int i = 0; i < m; i++) F[i][j] = Quu[i][j];
+        for (int i = 0; i < m; i++) F[i][j] = QU[i + m * j];
       if (!state_reg) {
 #pragma unroll
         for (int i = 0; i < m; i++) F[i][i] += s.rho;
@@ -845,7 +862,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
         for (int i = 0; i < m; i++) F[i][j] = bus[i + m * j];
       team_sync();
-      ok = !cond_exceeds_reg<m>(F, 1e8);
+      ok = !cond_exceeds_team<m>(F, 1e8, bus2, tl);
     }
     if (!ok) {
       // non-PD / cond > 1e8: increase ρ and restart at N-1; Q blocks are NOT re-expanded (A.1)
@@ -863,8 +880,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           done = true;
         }
       }
-      k = N - 1;
-      continue;
+      restart = true;
+      break;
     }
     if (!SQRT) {
       // K = -(Quu_reg \ Qux_reg), d = -(Quu_reg \ Q.u)
@@ -931,7 +948,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       for (int j = 0; j < m; j++) {
         double t = 0.0;
 #pragma unroll
-        for (int l = 0; l < m; l++) t = fma(Kc[l], Quu[l][j], t);
+        for (int l = 0; l < m; l++) t = fma(Kc[l], QU[l + m * j], t);
         KtQ[j] = t;
       }
       // s[c] = Q.x[c] + (K'Q.uu)[c,:] d + K[:,c]'Q.u + Q.ux[:,c]'d
@@ -983,13 +1000,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       if (colx) {
 #pragma unroll
         for (int i = 0; i < n; i++) bus[i + n * tl] = T[i];
-        bus[n * n + tl] = sown;
       }
       team_sync();
+      if (colx) {
 #pragma unroll
-      for (int i = 0; i < n; i++) {
-        Sc[i] = 0.5 * (T[i] + bus[c + n * i]);
-        sv[i] = bus[n * n + i];
+        for (int i = 0; i < n; i++) Sreg[i + n * tl] = 0.5 * (T[i] + bus[c + n * i]);
+        Sreg[SOFF + tl] = sown;
       }
       team_sync();
       {
@@ -1000,7 +1016,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         for (int j = 0; j < m; j++) {
           double t = 0.0;
 #pragma unroll
-          for (int i = 0; i < m; i++) t = fma(0.5 * d[i], Quu[i][j], t);
+          for (int i = 0; i < m; i++) t = fma(0.5 * d[i], QU[i + m * j], t);
           b2 = fma(t, d[j], b2);
         }
         dV0 += a;
@@ -1012,14 +1028,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       for (int i = 0; i < m; i++) {
         double t = 0.0;
 #pragma unroll
-        for (int l = 0; l < m; l++) t = fma(Quu[i][l], d[l], t);
+        for (int l = 0; l < m; l++) t = fma(QU[i + m * l], d[l], t);
         Ud[i] = t;
       }
 #pragma unroll
       for (int j = 0; j < m; j++) {
         double t = 0.0;
 #pragma unroll
-        for (int l = 0; l < m; l++) t = fma(Kc[l], Quu[j][l], t);
+        for (int l = 0; l < m; l++) t = fma(Kc[l], QU[j + m * l], t);
         KtU[j] = t;
       }
       {
@@ -1057,26 +1073,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       if (colx) {
 #pragma unroll
         for (int i = 0; i < m; i++) bus[TB + tl * m + i] = t1[i];
-        bus[TB + n * m + tl] = sown;
       }
       team_sync();
-#pragma unroll
-      for (int i = 0; i < n; i++) sv[i] = bus[TB + n * m + i];
       // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! by each row of tmp1 (backward_pass.jl:186-192).
       // Systolic schedule: lane i owns row i of the factor; the downdate of (row r, column i) needs
       // only (r, i-1) and (r-1, i), so step t runs (r = t - i, i) on every lane i < m: n+m-1 steps
       // instead of n*m, each (r, i) with exactly the oracle's operations. x travels lane to lane
       // through a double-buffered bus slot.
-      double U2[m][m];
+      const double* U2p;  // tmp2 (column-major): the downdated factor, or Q.uu on failure
       {
         double urow[m], v[m];
 #pragma unroll
         for (int jj = 0; jj < m; jj++) {
-          double q = 0.0;
-#pragma unroll
-          for (int ii = 0; ii < m; ii++)
-            if (ii == tl) q = Quu[ii][jj];
-          urow[jj] = q;
+          urow[jj] = colu ? QU[cu + m * jj] : 0.0;
           v[jj] = 0.0;
         }
         double* msg = bus2;  // [2][m][m]
@@ -1123,13 +1132,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         const bool fail = (__ballot(!okd) & tmask) != 0ull;
         if (colu) {
 #pragma unroll
-          for (int jj = 0; jj < m; jj++) bus2[2 * m * m + tl * m + jj] = (jj >= tl) ? urow[jj] : 0.0;
+          for (int jj = 0; jj < m; jj++) bus2[2 * m * m + tl + m * jj] = (jj >= tl) ? urow[jj] : 0.0;
         }
         team_sync();
-#pragma unroll
-        for (int jj = 0; jj < m; jj++)
-#pragma unroll
-          for (int ii = 0; ii < m; ii++) U2[ii][jj] = fail ? Quu[ii][jj] : bus2[2 * m * m + ii * m + jj];
+        U2p = fail ? QU : bus2 + 2 * m * m;
         if (fail) s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
       }
       // S[k] = qr([Q.xx + tmp1 K; tmp2 K]).R
@@ -1153,13 +1159,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         for (int i = 0; i < m; i++) {
           double v = 0.0;
 #pragma unroll
-          for (int l = 0; l < m; l++) v = fma(U2[i][l], Kc[l], v);
+          for (int l = 0; l < m; l++) v = fma(U2p[i + m * l], Kc[l], v);
           a[n + i] = v;
         }
         team_sync();
         team_qr<RS, n>(a, RS, tl, bus);
+        if (colx) {
 #pragma unroll
-        for (int i = 0; i < n; i++) Sc[i] = (i <= tl) ? a[i] : 0.0;
+          for (int i = 0; i < n; i++)
+            if (i <= tl) Sreg[tl * (tl + 1) / 2 + i] = a[i];
+          Sreg[SOFF + tl] = sown;
+        }
+        team_sync();
       }
       {
         double a = 0.0, b2 = 0.0;
@@ -1173,11 +1184,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     }
     if (store_S && colx) {
 #pragma unroll
-      for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = Sc[i];
+      for (int i = 0; i < n; i++)
+        Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] =
+            SQRT ? ((i <= tl) ? Sreg[tl * (tl + 1) / 2 + i] : 0.0) : Sreg[i + n * tl];
       Bf.sdbg[((size_t)b * N + k) * n + tl] = sown;
     }
-    if (k == 0) done = true;
-    else k--;
+    }
+    if (!restart) done = true;
   }
   if (!live) return;
   reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)

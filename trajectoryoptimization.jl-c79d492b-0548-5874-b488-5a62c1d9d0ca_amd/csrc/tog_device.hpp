@@ -96,9 +96,10 @@ struct DevBuffers {
   double* lsJ;  // (NC, B) speculative line-search trial costs
   int* lsok;    // (NC, B) speculative line-search trial rollout status
   int nc;       // candidates evaluated per trajectory per launch (<= 64)
-  int bwd_stride;  // k_bwd_team: per-team LDS stride (doubles)
-  int bwd_shmem;   // k_bwd_team: dynamic LDS bytes per block
-  int pad_;
+  int bwd_stride;     // k_bwd_team: per-team LDS stride (doubles) of the launch
+  int bwd_shmem;      // k_bwd_team: dynamic LDS bytes per block of the launch
+  int bwd_stride2[2]; // [std, sqrt] strides
+  int bwd_shmem2[2];  // [std, sqrt] LDS bytes
   TrajState* st;
 };
 

@@ -1478,7 +1478,7 @@ struct ModelOps {
   void (*update_constraints)(const DevProblem*, const DevBuffers&, long long B, hipStream_t);
   int bwd_lds_bytes;
   int team_tpw;                    // trajectories per wave of k_bwd_team
-  int (*team_stride)(int pmax);    // per-team LDS stride of k_bwd_team (doubles)
+  int (*team_stride)(int pmax, int sqrt);  // per-team LDS stride of k_bwd_team (doubles)
 };
 
 template <class M>
@@ -1512,13 +1512,16 @@ struct ModelLaunch {
     if (team) {  // column-per-lane teams, TPW trajectories per wave (tog_bwd_team.hpp)
       constexpr int TPW = TeamCfg<M>::TPW;
       const dim3 g((unsigned)((B + TPW - 1) / TPW)), blk(64);
-      const unsigned sm = (unsigned)Bf.bwd_shmem;
+      DevBuffers Bl = Bf;  // layout of this variant (the S-region differs between std and sqrt)
+      Bl.bwd_stride = Bf.bwd_stride2[sq ? 1 : 0];
+      Bl.bwd_shmem = Bf.bwd_shmem2[sq ? 1 : 0];
+      const unsigned sm = (unsigned)Bl.bwd_shmem;
       if (sq) {
-        if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1>), g, blk, sm, st, P, Bf, flags);
-        else hipLaunchKernelGGL((k_bwd_team<M, 1, 0>), g, blk, sm, st, P, Bf, flags);
+        if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1>), g, blk, sm, st, P, Bl, flags);
+        else hipLaunchKernelGGL((k_bwd_team<M, 1, 0>), g, blk, sm, st, P, Bl, flags);
       } else {
-        if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1>), g, blk, sm, st, P, Bf, flags);
-        else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, sm, st, P, Bf, flags);
+        if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1>), g, blk, sm, st, P, Bl, flags);
+        else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, sm, st, P, Bl, flags);
       }
       return;
     }

@@ -392,9 +392,11 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
     const bool force_lds = ev && strcmp(ev, "lds") == 0;
     h->bwd_team = (!force_lds && team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
                       ? 1 : 0;
-    h->buf.bwd_stride = ops->team_stride(h->pmax);
-    h->buf.bwd_shmem = (int)bwd_team_shmem(h->buf.bwd_stride, ops->team_tpw, (int)rows.size(), N);
-    if (h->buf.bwd_shmem > 64 * 1024) h->bwd_team = 0;
+    for (int sq = 0; sq < 2; sq++) {
+      h->buf.bwd_stride2[sq] = ops->team_stride(h->pmax, sq);
+      h->buf.bwd_shmem2[sq] = (int)bwd_team_shmem(h->buf.bwd_stride2[sq], ops->team_tpw, (int)rows.size(), N);
+      if (h->buf.bwd_shmem2[sq] > 64 * 1024) h->bwd_team = 0;
+    }
   }
   P.knot_off = h->d_knot_off;
   P.knot_cnt = h->d_knot_cnt;
