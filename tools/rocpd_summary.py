@@ -82,3 +82,19 @@ if __name__ == "__main__":
     t = main(src)
     if len(sys.argv) > 2 and t:
         pathlib.Path(sys.argv[2]).write_text(json.dumps({"source": src, "per_launch": t}, indent=1) + "\n")
+
+
+def sq_summary(d):
+    """Per-kernel averages of every PMC counter in <d>/sq/*.db (SQ stall/issue analysis)."""
+    d = pathlib.Path(d)
+    c = sqlite3.connect(next((d / "sq").glob("*.db")))
+    rows = c.execute("select kernel_name, counter_name, avg(value), count(*) from counters_collection "
+                     "group by kernel_name, counter_name").fetchall()
+    by = {}
+    for k, ctr, v, n in rows:
+        by.setdefault(k, {})[ctr] = v
+    for k, ctrs in sorted(by.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+        wc = ctrs.get("SQ_WAVE_CYCLES", 0) or 1
+        parts = " ".join(f"{ctr}={v:.3g}" for ctr, v in sorted(ctrs.items()))
+        frac = {x: ctrs.get(x, 0) / wc for x in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
+        print(short(k), "\n   ", parts, "\n    fractions of wave-cycles:", {a: round(b, 3) for a, b in frac.items()})

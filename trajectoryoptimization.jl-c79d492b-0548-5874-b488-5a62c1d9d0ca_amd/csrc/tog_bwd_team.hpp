@@ -143,9 +143,12 @@ __device__ __forceinline__ double row_at(const RowInfo& r, int col) {
 
 // Column-distributed Householder QR (LAPACK dgeqr2/dlarfg as in Julia qr(P).R, and wqr): `a` is this
 // lane's column (ROWS entries, the first `rows` in use — the rest are zero and inert) of a matrix
-// whose columns live in lanes 0..COLS-1 of the team.
-template <int ROWS, int COLS>
+// whose columns live in lanes 0..COLS-1 of the team. When the first TOP rows form an upper-triangular
+// block (the Cholesky factor being updated), rows j+1..TOP-1 of column j are exact zeros throughout
+// the sweep (no reflector touches them), so they are skipped: their terms are fma(0, y, t) == t.
+template <int ROWS, int COLS, int TOP = 0>
 __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus) {
+#define TQ_LIVE(i, j) ((i) < rows && !((i) > (j) && (i) < TOP))
 #pragma unroll
   for (int j = 0; j < COLS; j++) {
     if (j < rows) {
@@ -153,7 +156,7 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
         double ss = 0.0;
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (i < rows) ss = fma(a[i], a[i], ss);
+          if (TQ_LIVE(i, j)) ss = fma(a[i], a[i], ss);
         const double xnorm = sqrt(ss);
         double tau = 0.0;
         if (xnorm != 0.0) {
@@ -163,7 +166,7 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
           const double sc = 1.0 / (alpha - beta);
 #pragma unroll
           for (int i = j + 1; i < ROWS; i++)
-            if (i < rows) {
+            if (TQ_LIVE(i, j)) {
               a[i] *= sc;
               bus[i] = a[i];
             }
@@ -177,16 +180,17 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
         double w = a[j];
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (i < rows) w = fma(bus[i], a[i], w);
+          if (TQ_LIVE(i, j)) w = fma(bus[i], a[i], w);
         w *= tau;
         a[j] -= w;
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (i < rows) a[i] = fma(-bus[i], w, a[i]);
+          if (TQ_LIVE(i, j)) a[i] = fma(-bus[i], w, a[i]);
       }
       team_sync();
     }
   }
+#undef TQ_LIVE
 }
 
 // cond(R) > thresh for an upper-triangular m x m R held by every lane of the team (same decision
@@ -451,7 +455,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = 0.0;
             }
           }
-          team_qr<RQ, n>(a, n + nx, tl, bus);
+          team_qr<RQ, n, n>(a, n + nx, tl, bus);
 #pragma unroll
           for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
         }
@@ -469,7 +473,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = 0.0;
             }
           }
-          team_qr<m + PU, m>(a, m + nu, tl, bus);
+          team_qr<m + PU, m, m>(a, m + nu, tl, bus);
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
         }
@@ -682,7 +686,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         double a[m + n];
 #pragma unroll
         for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : TU[i - m];
-        team_qr<m + n, m>(a, m + n, tl, bus);
+        team_qr<m + n, m, m>(a, m + n, tl, bus);
 #pragma unroll
         for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
       }
@@ -690,7 +694,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         double a[2 * n];
 #pragma unroll
         for (int i = 0; i < 2 * n; i++) a[i] = (i < n) ? Qxc[i] : TX[i - n];
-        team_qr<2 * n, n>(a, 2 * n, tl, bus);
+        team_qr<2 * n, n, n>(a, 2 * n, tl, bus);
 #pragma unroll
         for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
       }
@@ -850,7 +854,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           else if (i - m == tl) v = sr;
           a[i] = v;
         }
-        team_qr<m + n, m>(a, state_reg ? m + n : 2 * m, tl, bus);
+        team_qr<m + n, m, m>(a, state_reg ? m + n : 2 * m, tl, bus);
         if (colu) {
 #pragma unroll
           for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
