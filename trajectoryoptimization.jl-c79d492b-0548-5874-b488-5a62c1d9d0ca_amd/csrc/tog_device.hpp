@@ -100,6 +100,8 @@ struct DevBuffers {
   int bwd_shmem;      // k_bwd_team: dynamic LDS bytes per block of the launch
   int bwd_stride2[2]; // [std, sqrt] strides
   int bwd_shmem2[2];  // [std, sqrt] LDS bytes
+  int rows_shmem;     // LDS bytes of a block's copy of the row tables (rollout kernels)
+  int pad2_;
   TrajState* st;
 };
 

@@ -1168,9 +1168,35 @@ __device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS tra
 // oracle's order. WMODE 0: cost only. WMODE 1: also write X̄, Ū. WMODE 2: write the new trajectory in
 // place into X, U (the accepted step; old X[k] is read before it is overwritten) and return the
 // todorov gradient of the new U (ilqr_methods.jl:122-129).
+// Constraint-row tables for the rollouts: the global ones, or a block's LDS copy (block_row_tables).
+struct RowTables {
+  const ConRow* rows;
+  const int* koff;
+  const int* kcnt;
+};
+__device__ __forceinline__ RowTables global_row_tables(const DevProblem* P) {
+  return RowTables{P->rows, P->knot_off, P->knot_cnt};
+}
+// Cooperative copy of the deduplicated row table and per-knot tables into dynamic LDS (all threads
+// of the block must call it). Needs P->nrows * sizeof(ConRow) + 2 * N * sizeof(int) bytes at `lds`.
+__device__ __forceinline__ RowTables block_row_tables(const DevProblem* P, void* lds) {
+  ConRow* rc = reinterpret_cast<ConRow*>(lds);
+  int* ko = reinterpret_cast<int*>(rc + P->nrows);
+  int* kc = ko + P->N;
+  const double* src = reinterpret_cast<const double*>(P->rows);
+  double* dst = reinterpret_cast<double*>(rc);
+  for (int e = threadIdx.x; e < P->nrows * (int)(sizeof(ConRow) / 8); e += blockDim.x) dst[e] = src[e];
+  for (int e = threadIdx.x; e < P->N; e += blockDim.x) {
+    ko[e] = P->knot_off[e];
+    kc[e] = P->knot_cnt[e];
+  }
+  __syncthreads();
+  return RowTables{rc, ko, kc};
+}
+
 template <class M, int INTEG, int WMODE>
 __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha,
-                             bool al, double& Jout, double* grad_out) {
+                             bool al, double& Jout, double* grad_out, const RowTables& RT) {
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
   double* X = Bf.X + (size_t)b * N * n;
@@ -1217,9 +1243,9 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     // stage cost and AL terms of knot k-1 (x̄_{k-1}, ū_{k-1})
     J += stage_cost<n, m>(P, xb, ub);
     if (al) {
-      const int cnt = P->knot_cnt[k - 1];
+      const int cnt = RT.kcnt[k - 1];
       if (cnt) {
-        const ConRow* rows = P->rows + P->knot_off[k - 1];
+        const ConRow* rows = RT.rows + RT.koff[k - 1];
         double lc = 0.0, cIc = 0.0;
         for (int i = 0; i < cnt; i++) {
           const double c = row_value(rows[i], xb, ub);
@@ -1259,9 +1285,9 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
   }
   J += terminal_cost<n>(P, xb);
   if (al) {
-    const int cnt = P->knot_cnt[N - 1];
+    const int cnt = RT.kcnt[N - 1];
     if (cnt) {
-      const ConRow* rows = P->rows + P->knot_off[N - 1];
+      const ConRow* rows = RT.rows + RT.koff[N - 1];
       double lc = 0.0, cIc = 0.0;
       for (int i = 0; i < cnt; i++) {
         const double c = row_value(rows[i], xb, nullptr);
@@ -1359,6 +1385,9 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
 // speculative trials: one lane per (trajectory, trial j), α_j = 2^-j, cost only
 template <class M, int INTEG>
 __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode) {
+  extern __shared__ double spec_lds[];
+  const RowTables RT =
+      (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, spec_lds) : global_row_tables(P);
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int NC = Bf.nc;
   if (t >= P->B * NC) return;
@@ -1366,7 +1395,7 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
   const int j = (int)(t % NC);
   if (!Bf.st[b].active) return;
   double Jj = INFINITY;
-  const bool ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr);
+  const bool ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
   Bf.lsJ[t] = Jj;
   Bf.lsok[t] = ok ? 1 : 0;
 }
@@ -1377,6 +1406,9 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
 template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
                                                   int bookkeeping, const double* Jprev_in, double* Jout) {
+  extern __shared__ double commit_lds[];
+  const RowTables RT =
+      (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, commit_lds) : global_row_tables(P);
   const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= P->B) return;
   if (!Bf.st[b].active) return;
@@ -1405,7 +1437,7 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
       ok = Bf.lsok[b * NC + jj] != 0;
       Jj = Bf.lsJ[b * NC + jj];
     } else {  // beyond the speculative window (iterations_linesearch >= 64): evaluate in place
-      ok = rollout_cost<M, INTEG, 0>(P, Bf, b, aj, al, Jj, nullptr);
+      ok = rollout_cost<M, INTEG, 0>(P, Bf, b, aj, al, Jj, nullptr, RT);
     }
     if (!ok) continue;
     J = Jj;
@@ -1435,10 +1467,10 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
     copied = true;
   } else if (!bookkeeping) {
     double Jw;
-    rollout_cost<M, INTEG, 1>(P, Bf, b, alpha_last, al, Jw, nullptr);  // writes X̄, Ū
+    rollout_cost<M, INTEG, 1>(P, Bf, b, alpha_last, al, Jw, nullptr, RT);  // writes X̄, Ū
   } else if (!(J > o.max_cost_value)) {
     double Jw;
-    rollout_cost<M, INTEG, 2>(P, Bf, b, alpha_last, al, Jw, &grad);  // X, U <- X̄, Ū in place
+    rollout_cost<M, INTEG, 2>(P, Bf, b, alpha_last, al, Jw, &grad, RT);  // X, U <- X̄, Ū in place
     copied = true;
   }
   s.alpha = alpha_last;
@@ -1538,11 +1570,11 @@ struct ModelLaunch {
                       const double* Jp, double* Jo, hipStream_t st) {
     const unsigned gs = grid(B * (long long)Bf.nc, 256);  // one lane per (trajectory, trial)
     if (integ == TOG_RK4) {
-      hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), 0, st, P, Bf, mode);
-      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+      hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), Bf.rows_shmem, st, P, Bf, mode);
+      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), Bf.rows_shmem, st, P, Bf, mode, bk, Jp, Jo);
     } else {
-      hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), 0, st, P, Bf, mode);
-      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode, bk, Jp, Jo);
+      hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), Bf.rows_shmem, st, P, Bf, mode);
+      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), Bf.rows_shmem, st, P, Bf, mode, bk, Jp, Jo);
     }
   }
   static void cost(const DevProblem* P, const DevBuffers& Bf, long long B, int al, int bar, double* J,

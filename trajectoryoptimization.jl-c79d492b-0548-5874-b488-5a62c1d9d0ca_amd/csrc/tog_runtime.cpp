@@ -392,6 +392,8 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
     const bool force_lds = ev && strcmp(ev, "lds") == 0;
     h->bwd_team = (!force_lds && team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
                       ? 1 : 0;
+    h->buf.rows_shmem = (int)(sizeof(ConRow) * rows.size() + sizeof(int) * 2 * (size_t)N);
+    if (h->buf.rows_shmem > 32 * 1024) h->buf.rows_shmem = 0;  // rollouts then read the global tables
     for (int sq = 0; sq < 2; sq++) {
       h->buf.bwd_stride2[sq] = ops->team_stride(h->pmax, sq);
       h->buf.bwd_shmem2[sq] = (int)bwd_team_shmem(h->buf.bwd_stride2[sq], ops->team_tpw, (int)rows.size(), N);
