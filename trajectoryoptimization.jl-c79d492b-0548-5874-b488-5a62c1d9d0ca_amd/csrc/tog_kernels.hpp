@@ -35,6 +35,35 @@ __host__ __device__ constexpr int nq_of() {
 // Thread-level trajectory helpers
 // =============================================================================================
 
+// AL terms λ'c + ½ c'Iμ c of one knot (augmented_lagrangian_methods.jl:298-313), rows in order. The
+// multipliers are loaded four rows at a time so their global loads overlap instead of serialising
+// one round trip per row. Ck (constraint values out) may be null.
+__device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const double* lamk, const double* muk,
+                                              const double* x, const double* u, double& lc, double& cIc,
+                                              double* Ck) {
+  for (int base = 0; base < cnt; base += 4) {
+    double lv[4], mv[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      lv[q] = (base + q < cnt) ? lamk[base + q] : 0.0;
+      mv[q] = (base + q < cnt) ? muk[base + q] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (base + q < cnt) {
+        const ConRow& r = rows[base + q];
+        const double c = row_value(r, x, u);
+        const double l = lv[q];
+        const bool a = row_inequality(r) ? ((c >= 0.0) || (l > 0.0)) : true;
+        const double w = a ? mv[q] : 0.0;
+        lc = fma(l, c, lc);
+        cIc = fma(c * w, c, cIc);
+        if (Ck) Ck[base + q] = c;
+      }
+    }
+  }
+}
+
 // AL/objective cost of (Xs, Us) for trajectory b (objective.jl:40-48, augmented_lagrangian_methods.jl:298-313).
 // Writes the constraint values C when Cout != nullptr (A.10: cost() updates C as a side effect).
 template <class M>
@@ -55,15 +84,8 @@ __device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& 
     const double* x = Xs + (size_t)k * n;
     const double* u = (k < N - 1) ? Us + (size_t)k * m : nullptr;
     double lc = 0.0, cIc = 0.0;
-    for (int i = 0; i < cnt; i++) {
-      const double c = row_value(rows[i], x, u);
-      const double l = lam[(size_t)k * pmax + i];
-      const bool a = row_inequality(rows[i]) ? ((c >= 0.0) || (l > 0.0)) : true;
-      const double w = a ? mu[(size_t)k * pmax + i] : 0.0;
-      lc = fma(l, c, lc);
-      cIc = fma(c * w, c, cIc);
-      if (Cout) Cout[(size_t)k * pmax + i] = c;
-    }
+    al_knot_terms(rows, cnt, lam + (size_t)k * pmax, mu + (size_t)k * pmax, x, u, lc, cIc,
+                  Cout ? Cout + (size_t)k * pmax : nullptr);
     Jc += lc + 0.5 * cIc;
   }
   return J + Jc;
@@ -1247,14 +1269,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       if (cnt) {
         const ConRow* rows = RT.rows + RT.koff[k - 1];
         double lc = 0.0, cIc = 0.0;
-        for (int i = 0; i < cnt; i++) {
-          const double c = row_value(rows[i], xb, ub);
-          const double l = lam[(size_t)(k - 1) * pmax + i];
-          const bool a = row_inequality(rows[i]) ? ((c >= 0.0) || (l > 0.0)) : true;
-          const double w = a ? mu[(size_t)(k - 1) * pmax + i] : 0.0;
-          lc = fma(l, c, lc);
-          cIc = fma(c * w, c, cIc);
-        }
+        al_knot_terms(rows, cnt, lam + (size_t)(k - 1) * pmax, mu + (size_t)(k - 1) * pmax, xb, ub, lc, cIc, nullptr);
         Jc += lc + 0.5 * cIc;
       }
     }
@@ -1289,14 +1304,8 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     if (cnt) {
       const ConRow* rows = RT.rows + RT.koff[N - 1];
       double lc = 0.0, cIc = 0.0;
-      for (int i = 0; i < cnt; i++) {
-        const double c = row_value(rows[i], xb, nullptr);
-        const double l = lam[(size_t)(N - 1) * pmax + i];
-        const bool a = row_inequality(rows[i]) ? ((c >= 0.0) || (l > 0.0)) : true;
-        const double w = a ? mu[(size_t)(N - 1) * pmax + i] : 0.0;
-        lc = fma(l, c, lc);
-        cIc = fma(c * w, c, cIc);
-      }
+      al_knot_terms(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax, xb, nullptr, lc, cIc,
+                    nullptr);
       Jc += lc + 0.5 * cIc;
     }
     J = J + Jc;
