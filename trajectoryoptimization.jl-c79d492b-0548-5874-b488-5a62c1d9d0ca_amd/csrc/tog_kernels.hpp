@@ -1239,14 +1239,52 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     if (WMODE == 1) Xb[i] = xb[i];
     if (WMODE == 2) X[i] = xb[i];
   }
+  // Software pipeline: the inputs of the next knot (K, U, d, X and the first RB multipliers) are
+  // loaded while the current knot computes, so every knot does not wait for its own HBM round trip.
+  constexpr int RB = 8;
+  double Kp[m * n], up[m], dp[m], xp[n], lp[RB], mp[RB];
+  auto prefetch = [&](int k) {  // inputs of the update that produces knot k+1
+    const double* Kk = K + (size_t)k * m * n;
+#pragma unroll
+    for (int e = 0; e < m * n; e++) Kp[e] = Kk[e];
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      up[i] = U[(size_t)k * m + i];
+      dp[i] = d[(size_t)k * m + i];
+    }
+    if (al) {
+      const int cnt = RT.kcnt[k];
+#pragma unroll
+      for (int q = 0; q < RB; q++) {
+        lp[q] = (q < cnt) ? lam[(size_t)k * pmax + q] : 0.0;
+        mp[q] = (q < cnt) ? mu[(size_t)k * pmax + q] : 0.0;
+      }
+    }
+  };
+  prefetch(0);
   for (int k = 1; k < N; k++) {
-    const double* Kk = K + (size_t)(k - 1) * m * n;
+    double Kk[m * n], uk[m], dk[m], lk[RB], mk[RB];
+#pragma unroll
+    for (int e = 0; e < m * n; e++) Kk[e] = Kp[e];
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      uk[i] = up[i];
+      dk[i] = dp[i];
+    }
+#pragma unroll
+    for (int q = 0; q < RB; q++) {
+      lk[q] = lp[q];
+      mk[q] = mp[q];
+    }
+    if (k < N - 1) prefetch(k);
+#pragma unroll
+    for (int i = 0; i < n; i++) xp[i] = X[(size_t)k * n + i];  // x_k of the current iterate (next x_old)
 #pragma unroll
     for (int i = 0; i < m; i++) {
       double t = 0.0;
 #pragma unroll
       for (int j = 0; j < n; j++) t = fma(Kk[i + m * j], xb[j] - xold[j], t);
-      ub[i] = (U[(size_t)(k - 1) * m + i] + t) + alpha * d[(size_t)(k - 1) * m + i];
+      ub[i] = (uk[i] + t) + alpha * dk[i];
     }
     if (WMODE == 1) {
 #pragma unroll
@@ -1257,7 +1295,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
 #pragma unroll
       for (int i = 0; i < m; i++) {
         U[(size_t)(k - 1) * m + i] = ub[i];
-        const double v = fabs(d[(size_t)(k - 1) * m + i]) / (fabs(ub[i]) + 1.0);
+        const double v = fabs(dk[i]) / (fabs(ub[i]) + 1.0);
         if (v > mx || isnan(v)) mx = v;
       }
       gsum += mx;
@@ -1269,7 +1307,21 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       if (cnt) {
         const ConRow* rows = RT.rows + RT.koff[k - 1];
         double lc = 0.0, cIc = 0.0;
-        al_knot_terms(rows, cnt, lam + (size_t)(k - 1) * pmax, mu + (size_t)(k - 1) * pmax, xb, ub, lc, cIc, nullptr);
+#pragma unroll
+        for (int q = 0; q < RB; q++) {
+          if (q < cnt) {
+            const ConRow& r = rows[q];
+            const double c = row_value(r, xb, ub);
+            const double l = lk[q];
+            const bool a = row_inequality(r) ? ((c >= 0.0) || (l > 0.0)) : true;
+            const double w = a ? mk[q] : 0.0;
+            lc = fma(l, c, lc);
+            cIc = fma(c * w, c, cIc);
+          }
+        }
+        if (cnt > RB)
+          al_knot_terms(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB, mu + (size_t)(k - 1) * pmax + RB, xb,
+                        ub, lc, cIc, nullptr);
         Jc += lc + 0.5 * cIc;
       }
     }
@@ -1282,19 +1334,15 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
 #pragma unroll
     for (int i = 0; i < m; i++) ok = ok && (fabs(ub[i]) < umax);
+#pragma unroll
+    for (int i = 0; i < n; i++) xold[i] = xp[i];
     if (WMODE == 2) {
 #pragma unroll
-      for (int i = 0; i < n; i++) {
-        xold[i] = X[(size_t)k * n + i];
-        X[(size_t)k * n + i] = xn[i];
-      }
-    } else {
+      for (int i = 0; i < n; i++) X[(size_t)k * n + i] = xn[i];
+    }
+    if (WMODE == 1) {
 #pragma unroll
-      for (int i = 0; i < n; i++) xold[i] = X[(size_t)k * n + i];
-      if (WMODE == 1) {
-#pragma unroll
-        for (int i = 0; i < n; i++) Xb[(size_t)k * n + i] = xn[i];
-      }
+      for (int i = 0; i < n; i++) Xb[(size_t)k * n + i] = xn[i];
     }
     if (!ok) return false;
   }
