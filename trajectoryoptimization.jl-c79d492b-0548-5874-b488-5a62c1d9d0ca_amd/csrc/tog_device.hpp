@@ -540,6 +540,16 @@ __device__ __forceinline__ double row_value(const ConRow& r, const double* x, co
 }
 __device__ __forceinline__ bool row_inequality(const ConRow& r) { return r.type != ROW_GOAL; }
 
+// The same row seen by every lane of a wave (lanes iterate knots and rows in lockstep over the
+// shared row table): make its type and index wave-uniform so that the switch is a scalar branch
+// and x[idx] an indexed register move, not a per-lane chain of compares and selects.
+__device__ __forceinline__ ConRow uniform_row(const ConRow& r) {
+  ConRow u = r;
+  u.type = __builtin_amdgcn_readfirstlane(r.type);
+  u.idx = __builtin_amdgcn_readfirstlane(r.idx);
+  return u;
+}
+
 // d c / d [x; u] of a row: writes up to 3 (index, value) pairs, index in [0, n+m)
 __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n, int* idx, double* v) {
   switch (r.type) {

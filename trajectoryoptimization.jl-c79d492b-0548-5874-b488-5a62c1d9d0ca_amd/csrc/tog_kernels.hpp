@@ -51,7 +51,7 @@ __device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       if (base + q < cnt) {
-        const ConRow& r = rows[base + q];
+        const ConRow r = uniform_row(rows[base + q]);
         const double c = row_value(r, x, u);
         const double l = lv[q];
         const bool a = row_inequality(r) ? ((c >= 0.0) || (l > 0.0)) : true;
@@ -299,7 +299,8 @@ __global__ void __launch_bounds__(64) k_update_constraints(const DevProblem* __r
     const int cnt = P->knot_cnt[k];
     const ConRow* rows = P->rows + P->knot_off[k];
     for (int i = 0; i < cnt; i++)
-      Bf.C[((size_t)b * N + k) * pmax + i] = row_value(rows[i], X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
+      Bf.C[((size_t)b * N + k) * pmax + i] =
+          row_value(uniform_row(rows[i]), X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
   }
 }
 
@@ -1310,7 +1311,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
 #pragma unroll
         for (int q = 0; q < RB; q++) {
           if (q < cnt) {
-            const ConRow& r = rows[q];
+            const ConRow r = uniform_row(rows[q]);
             const double c = row_value(r, xb, ub);
             const double l = lk[q];
             const bool a = row_inequality(r) ? ((c >= 0.0) || (l > 0.0)) : true;
