@@ -24,6 +24,15 @@ namespace tog {
 // loads) ahead of their FMAs, which would need ~2x the registers of the logical working set.
 #define TEAM_FENCE() asm volatile("" ::: "memory")
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 constexpr int PX = 20;  // rows with a state gradient per knot kept in registers (sqrt AL expansion)
 
 template <class M>
@@ -141,14 +150,69 @@ __device__ __forceinline__ double row_at(const RowInfo& r, int col) {
   return v;
 }
 
+// Broadcast lane L's value to the 16 lanes of its DPP row (= its team when TEAM == 16): a register
+// move (v_mov_b32_dpp row_newbcast:L), no LDS round trip. All lanes of the team must be active.
+template <int L>
+__device__ __forceinline__ double row_bcast(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(x & 0xffffffffll), 0x150 + L, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), 0x150 + L, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // Column-distributed Householder QR (LAPACK dgeqr2/dlarfg as in Julia qr(P).R, and wqr): `a` is this
 // lane's column (ROWS entries, the first `rows` in use — the rest are zero and inert) of a matrix
 // whose columns live in lanes 0..COLS-1 of the team. When the first TOP rows form an upper-triangular
 // block (the Cholesky factor being updated), rows j+1..TOP-1 of column j are exact zeros throughout
 // the sweep (no reflector touches them), so they are skipped: their terms are fma(0, y, t) == t.
-template <int ROWS, int COLS, int TOP = 0>
+template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16>
 __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus) {
 #define TQ_LIVE(i, j) ((i) < rows && !((i) > (j) && (i) < TOP))
+  if constexpr (TEAMW == 16) {
+    // reflectors broadcast by DPP row_newbcast (the team is one DPP row)
+    static_for<0, COLS>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if (j < rows) {
+        double tau = 0.0;
+        if (tl == j) {
+          double ss = 0.0;
+#pragma unroll
+          for (int i = j + 1; i < ROWS; i++)
+            if (TQ_LIVE(i, j)) ss = fma(a[i], a[i], ss);
+          const double xnorm = sqrt(ss);
+          if (xnorm != 0.0) {
+            const double alpha = a[j];
+            const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+            tau = (beta - alpha) / beta;
+            const double sc = 1.0 / (alpha - beta);
+#pragma unroll
+            for (int i = j + 1; i < ROWS; i++)
+              if (TQ_LIVE(i, j)) a[i] *= sc;
+            a[j] = beta;
+          }
+        }
+        tau = row_bcast<j>(tau);
+        if (tau != 0.0) {
+          double v[ROWS];
+#pragma unroll
+          for (int i = j + 1; i < ROWS; i++)
+            if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
+          if (tl > j && tl < COLS) {
+            double w = a[j];
+#pragma unroll
+            for (int i = j + 1; i < ROWS; i++)
+              if (TQ_LIVE(i, j)) w = fma(v[i], a[i], w);
+            w *= tau;
+            a[j] -= w;
+#pragma unroll
+            for (int i = j + 1; i < ROWS; i++)
+              if (TQ_LIVE(i, j)) a[i] = fma(-v[i], w, a[i]);
+          }
+        }
+      }
+    });
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < COLS; j++) {
     if (j < rows) {
@@ -455,7 +519,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = 0.0;
             }
           }
-          team_qr<RQ, n, n>(a, n + nx, tl, bus);
+          team_qr<RQ, n, n, TEAM>(a, n + nx, tl, bus);
 #pragma unroll
           for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
         }
@@ -473,7 +537,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = 0.0;
             }
           }
-          team_qr<m + PU, m, m>(a, m + nu, tl, bus);
+          team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
         }
@@ -686,7 +750,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         double a[m + n];
 #pragma unroll
         for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : TU[i - m];
-        team_qr<m + n, m, m>(a, m + n, tl, bus);
+        team_qr<m + n, m, m, TEAM>(a, m + n, tl, bus);
 #pragma unroll
         for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
       }
@@ -694,7 +758,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         double a[2 * n];
 #pragma unroll
         for (int i = 0; i < 2 * n; i++) a[i] = (i < n) ? Qxc[i] : TX[i - n];
-        team_qr<2 * n, n, n>(a, 2 * n, tl, bus);
+        team_qr<2 * n, n, n, TEAM>(a, 2 * n, tl, bus);
 #pragma unroll
         for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
       }
@@ -854,7 +918,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           else if (i - m == tl) v = sr;
           a[i] = v;
         }
-        team_qr<m + n, m, m>(a, state_reg ? m + n : 2 * m, tl, bus);
+        team_qr<m + n, m, m, TEAM>(a, state_reg ? m + n : 2 * m, tl, bus);
         if (colu) {
 #pragma unroll
           for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
@@ -1056,21 +1120,38 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       double t1[m];
 #pragma unroll
       for (int i = 0; i < m; i++) t1[i] = Quxc[i];
+      if constexpr (TEAM == 16) {
+        static_for<0, n>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if (tl == j) {
 #pragma unroll
-      for (int j = 0; j < n; j++) {
-        if (tl == j) {
-#pragma unroll
-          for (int i = 0; i < m; i++) {
-            t1[i] = t1[i] / Qxc[j];
-            bus[i] = t1[i];
+            for (int i = 0; i < m; i++) t1[i] = t1[i] / Qxc[j];
           }
-        }
-        team_sync();
-        if (tl > j && colx) {
+          double xj[m];
 #pragma unroll
-          for (int i = 0; i < m; i++) t1[i] = fma(-Qxc[j], bus[i], t1[i]);
+          for (int i = 0; i < m; i++) xj[i] = row_bcast<j>(t1[i]);
+          if (tl > j && colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = fma(-Qxc[j], xj[i], t1[i]);
+          }
+        });
+      } else {
+#pragma unroll
+        for (int j = 0; j < n; j++) {
+          if (tl == j) {
+#pragma unroll
+            for (int i = 0; i < m; i++) {
+              t1[i] = t1[i] / Qxc[j];
+              bus[i] = t1[i];
+            }
+          }
+          team_sync();
+          if (tl > j && colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = fma(-Qxc[j], bus[i], t1[i]);
+          }
+          team_sync();
         }
-        team_sync();
       }
       // all-gather tmp1 (row-major at bus[TB + r*m + j]) and s
       constexpr int TB = 32;
@@ -1167,7 +1248,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           a[n + i] = v;
         }
         team_sync();
-        team_qr<RS, n>(a, RS, tl, bus);
+        team_qr<RS, n, 0, TEAM>(a, RS, tl, bus);
         if (colx) {
 #pragma unroll
           for (int i = 0; i < n; i++)
