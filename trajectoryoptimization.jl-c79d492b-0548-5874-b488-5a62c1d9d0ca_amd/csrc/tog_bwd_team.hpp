@@ -160,6 +160,14 @@ __device__ __forceinline__ double row_bcast(double v) {
   return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+// Lane i of each DPP row receives lane i-1's value (row_shr:1); lane 0 keeps `old`.
+__device__ __forceinline__ double row_shr1(double v, double old) {
+  const long long x = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(x & 0xffffffffll), 0x111, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(x >> 32), 0x111, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // Column-distributed Householder QR (LAPACK dgeqr2/dlarfg as in Julia qr(P).R, and wqr): `a` is this
 // lane's column (ROWS entries, the first `rows` in use — the rest are zero and inert) of a matrix
 // whose columns live in lanes 0..COLS-1 of the team. When the first TOP rows form an upper-triangular
@@ -637,11 +645,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       double tu = 0.0;
 #pragma unroll
       for (int l = 0; l < n; l++) tu = fma(Bc[l], Sreg[SOFF + l], tu);
-      if (colu) bus[tl] = tu;
-      team_sync();
+      if constexpr (TEAM == 16) {
+        static_for<0, m>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          Qu[i] += row_bcast<i>(tu);
+        });
+      } else {
+        if (colu) bus[tl] = tu;
+        team_sync();
 #pragma unroll
-      for (int i = 0; i < m; i++) Qu[i] += bus[i];
-      team_sync();
+        for (int i = 0; i < m; i++) Qu[i] += bus[i];
+        team_sync();
+      }
     }
     // [A B] columns on the bus (first region)
     double* bus2 = bus + n * L;
@@ -919,17 +934,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           a[i] = v;
         }
         team_qr<m + n, m, m, TEAM>(a, state_reg ? m + n : 2 * m, tl, bus);
-        if (colu) {
+        if constexpr (TEAM == 16) {
+          static_for<0, m>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
 #pragma unroll
-          for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
+            for (int i = 0; i < m; i++) F[i][j] = (i <= j) ? row_bcast<j>(a[i]) : 0.0;
+          });
+        } else {
+          if (colu) {
+#pragma unroll
+            for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
+          }
         }
       }
-      team_sync();
+      if constexpr (TEAM != 16) {
+        team_sync();
 #pragma unroll
-      for (int j = 0; j < m; j++)
+        for (int j = 0; j < m; j++)
 #pragma unroll
-        for (int i = 0; i < m; i++) F[i][j] = bus[i + m * j];
-      team_sync();
+          for (int i = 0; i < m; i++) F[i][j] = bus[i + m * j];
+        team_sync();
+      }
       ok = !cond_exceeds_team<m>(F, 1e8, bus2, tl);
     }
     if (!ok) {
@@ -993,15 +1018,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     double Kc[m];
 #pragma unroll
     for (int i = 0; i < m; i++) Kc[i] = -1.0 * col[i];
-    if (tl == n) {
-#pragma unroll
-      for (int i = 0; i < m; i++) bus[i] = Kc[i];
-    }
-    team_sync();
     double d[m];
+    if constexpr (TEAM == 16) {
 #pragma unroll
-    for (int i = 0; i < m; i++) d[i] = bus[i];
-    team_sync();
+      for (int i = 0; i < m; i++) d[i] = row_bcast<n>(Kc[i]);
+    } else {
+      if (tl == n) {
+#pragma unroll
+        for (int i = 0; i < m; i++) bus[i] = Kc[i];
+      }
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < m; i++) d[i] = bus[i];
+      team_sync();
+    }
     if (colx) {
 #pragma unroll
       for (int i = 0; i < m; i++) Kg[(size_t)k * m * n + i + m * tl] = Kc[i];
@@ -1173,15 +1203,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           urow[jj] = colu ? QU[cu + m * jj] : 0.0;
           v[jj] = 0.0;
         }
-        double* msg = bus2;  // [2][m][m]
+        double* msg = bus2;  // [2][m][m] (8-lane teams)
         bool okd = true;
 #pragma unroll 1
         for (int t = 0; t < n + m - 1; t++) {
           const int r = t - tl;
+          double vin[m];
+          if constexpr (TEAM == 16) {
+#pragma unroll
+            for (int jj = 0; jj < m; jj++) vin[jj] = row_shr1(v[jj], 0.0);  // lane i-1's x from step t-1
+          }
           if (colu && r >= 0 && r < n) {
             if (tl == 0) {
 #pragma unroll
               for (int jj = 0; jj < m; jj++) v[jj] = bus[TB + r * m + jj];
+            } else if constexpr (TEAM == 16) {
+#pragma unroll
+              for (int jj = 0; jj < m; jj++) v[jj] = vin[jj];
             } else {
               const double* in = msg + ((t - 1) & 1) * m * m + (tl - 1) * m;
 #pragma unroll
@@ -1207,11 +1245,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
                 urow[jj] = tmp;
               }
             }
-            double* out = msg + (t & 1) * m * m + tl * m;
+            if constexpr (TEAM != 16) {
+              double* out = msg + (t & 1) * m * m + tl * m;
 #pragma unroll
-            for (int jj = 0; jj < m; jj++) out[jj] = v[jj];
+              for (int jj = 0; jj < m; jj++) out[jj] = v[jj];
+            }
           }
-          team_sync();
+          if constexpr (TEAM != 16) team_sync();
         }
         const unsigned long long tmask = (TEAM >= 64 ? ~0ull : ((1ull << TEAM) - 1ull)) << (team * TEAM);
         const bool fail = (__ballot(!okd) & tmask) != 0ull;
