@@ -173,49 +173,50 @@ __device__ __forceinline__ double row_shr1(double v, double old) {
 // whose columns live in lanes 0..COLS-1 of the team. When the first TOP rows form an upper-triangular
 // block (the Cholesky factor being updated), rows j+1..TOP-1 of column j are exact zeros throughout
 // the sweep (no reflector touches them), so they are skipped: their terms are fma(0, y, t) == t.
-template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16>
+// FULL: rows == ROWS is known at compile time (no per-entry liveness selects).
+template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16, bool FULL = false>
 __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus) {
-#define TQ_LIVE(i, j) ((i) < rows && !((i) > (j) && (i) < TOP))
+#define TQ_LIVE(i, j) ((FULL || (i) < rows) && !((i) > (j) && (i) < TOP))
   if constexpr (TEAMW == 16) {
-    // reflectors broadcast by DPP row_newbcast (the team is one DPP row)
+    // Reflectors broadcast by DPP row_newbcast (the team is one DPP row). The lane-predicated parts
+    // are written branch-free: every lane runs the reflector arithmetic on its own column (SIMT
+    // issues it once either way) and lane j's results are selected once per step, and the update
+    // uses w = 0 on lanes <= j, which leaves their live entries unchanged (x - 0, fma(v, 0, x)) and
+    // only touches the dead reflector storage below their diagonals.
     static_for<0, COLS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       if (j < rows) {
-        double tau = 0.0;
-        if (tl == j) {
-          double ss = 0.0;
+        const bool me = (tl == j);
+        double ss = 0.0;
 #pragma unroll
-          for (int i = j + 1; i < ROWS; i++)
-            if (TQ_LIVE(i, j)) ss = fma(a[i], a[i], ss);
-          const double xnorm = sqrt(ss);
-          if (xnorm != 0.0) {
-            const double alpha = a[j];
-            const double beta = -copysign(lapy2(alpha, xnorm), alpha);
-            tau = (beta - alpha) / beta;
-            const double sc = 1.0 / (alpha - beta);
+        for (int i = j + 1; i < ROWS; i++)
+          if (TQ_LIVE(i, j)) ss = fma(a[i], a[i], ss);
+        const double xnorm = sqrt(ss);
+        const double alpha = a[j];
+        const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+        const bool refl = me && (xnorm != 0.0);
+        const double tau_l = refl ? (beta - alpha) / beta : 0.0;
+        const double sc = refl ? 1.0 / (alpha - beta) : 1.0;
 #pragma unroll
-            for (int i = j + 1; i < ROWS; i++)
-              if (TQ_LIVE(i, j)) a[i] *= sc;
-            a[j] = beta;
-          }
-        }
-        tau = row_bcast<j>(tau);
+        for (int i = j + 1; i < ROWS; i++)
+          if (TQ_LIVE(i, j)) a[i] *= sc;
+        if (refl) a[j] = beta;
+        const double tau = row_bcast<j>(tau_l);
         if (tau != 0.0) {
           double v[ROWS];
 #pragma unroll
           for (int i = j + 1; i < ROWS; i++)
             if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
-          if (tl > j && tl < COLS) {
-            double w = a[j];
+          double w = a[j];
 #pragma unroll
-            for (int i = j + 1; i < ROWS; i++)
-              if (TQ_LIVE(i, j)) w = fma(v[i], a[i], w);
-            w *= tau;
-            a[j] -= w;
+          for (int i = j + 1; i < ROWS; i++)
+            if (TQ_LIVE(i, j)) w = fma(v[i], a[i], w);
+          w *= tau;
+          if (!(tl > j && tl < COLS)) w = 0.0;
+          a[j] -= w;
 #pragma unroll
-            for (int i = j + 1; i < ROWS; i++)
-              if (TQ_LIVE(i, j)) a[i] = fma(-v[i], w, a[i]);
-          }
+          for (int i = j + 1; i < ROWS; i++)
+            if (TQ_LIVE(i, j)) a[i] = fma(-v[i], w, a[i]);
         }
       }
     });
@@ -545,7 +546,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = 0.0;
             }
           }
-          team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
+          if (nu == PU)  // every control bounded on both sides: the common case, no row selects
+            team_qr<m + PU, m, m, TEAM, true>(a, m + PU, tl, bus);
+          else
+            team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
         }
@@ -924,27 +928,37 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       // column-distributed over lanes < m, then all-gathered
       {
         const double sr = sqrt(s.rho);
-        double a[m + n];
+        // one instantiation per regularisation type (uniform branch), each with its exact row count
+        auto qr_reg = [&](auto& a) {
+          constexpr int RR = sizeof(a) / sizeof(a[0]);
 #pragma unroll
-        for (int i = 0; i < m + n; i++) {
-          double v = 0.0;
-          if (i < m) v = Quuc[i];
-          else if (state_reg) v = sr * ABg[(size_t)k * n * L + n * (n + cu) + (i - m)];
-          else if (i - m == tl) v = sr;
-          a[i] = v;
-        }
-        team_qr<m + n, m, m, TEAM>(a, state_reg ? m + n : 2 * m, tl, bus);
-        if constexpr (TEAM == 16) {
-          static_for<0, m>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-#pragma unroll
-            for (int i = 0; i < m; i++) F[i][j] = (i <= j) ? row_bcast<j>(a[i]) : 0.0;
-          });
-        } else {
-          if (colu) {
-#pragma unroll
-            for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
+          for (int i = 0; i < RR; i++) {
+            double v = 0.0;
+            if (i < m) v = Quuc[i];
+            else if (state_reg) v = sr * ABg[(size_t)k * n * L + n * (n + cu) + (i - m)];
+            else if (i - m == tl) v = sr;
+            a[i] = v;
           }
+          team_qr<RR, m, m, TEAM, true>(a, RR, tl, bus);
+          if constexpr (TEAM == 16) {
+            static_for<0, m>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+#pragma unroll
+              for (int i = 0; i < m; i++) F[i][j] = (i <= j) ? row_bcast<j>(a[i]) : 0.0;
+            });
+          } else {
+            if (colu) {
+#pragma unroll
+              for (int i = 0; i < m; i++) bus[i + m * tl] = (i <= tl) ? a[i] : 0.0;
+            }
+          }
+        };
+        if (state_reg) {
+          double a[m + n];
+          qr_reg(a);
+        } else {
+          double a[2 * m];
+          qr_reg(a);
         }
       }
       if constexpr (TEAM != 16) {

@@ -318,7 +318,11 @@ __global__ void __launch_bounds__(64) k_rollout(const DevProblem* __restrict__ P
 // iLQR (backward_pass.jl:30,110) and is not materialised.
 // =============================================================================================
 template <class M, int INTEG, int W>
-__global__ void __launch_bounds__(256) k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
+#ifndef TOG_JAC_WAVES
+#define TOG_JAC_WAVES 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TOG_JAC_WAVES)))
+k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   constexpr int n = M::n, m = M::m, L = n + m, NCH = (L + W - 1) / W;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
@@ -1597,7 +1601,10 @@ template <class M>
 struct ModelLaunch {
   // dual partials per thread: all of them for small models, chunks of 4 otherwise (512-register
   // budget with no scratch for the quadrotor RK4 step)
-  static constexpr int JW = (M::n + M::m) <= 6 ? (M::n + M::m) : 4;
+#ifndef TOG_JW
+#define TOG_JW 4
+#endif
+  static constexpr int JW = (M::n + M::m) <= 6 ? (M::n + M::m) : TOG_JW;
   static unsigned grid(long long total, int blk) { return (unsigned)((total + blk - 1) / blk); }
   static void init(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, hipStream_t st) {
     if (integ == TOG_RK4)
