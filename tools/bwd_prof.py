@@ -1,0 +1,35 @@
+"""Backward-kernel section breakdown (GPU box). Build the timed variant first:
+    tools/ab_build.sh prof -DTOG_BWD_PROF
+    TOG_LIBRARY=build_ab/prof/libtog.so python tools/bwd_prof.py [steps]
+Runs the bench workload (config 3) for a few AL-iLQR steps and prints each knot-loop section's share
+of the summed shader-clock cycles (tog_bwd_team.hpp BPROF markers)."""
+import ctypes
+import sys
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+import __graft_entry__  # noqa: E402
+
+NAMES = ["terminal knot", "expand: Q.u += cu'g", "S [A B], Q.ux", "QR Q.uu", "QR Q.xx",
+         "regularise + cond", "gains solve", "K/d store, s, tmp1", "chol_minus", "S-update operands",
+         "QR S-update", "epilogue", "expand: cost terms (x/u loads)", "expand: team_rows (lam/mu, eval)",
+         "expand: chol_plus operands", "expand: chol_plus QR", "expand: Q.x += cx'g", "[A B] loads",
+         "-", "-"]
+pkg = __graft_entry__.load_package()
+abi = pkg.abi
+lib = abi.load_library()
+read = lib.tog_bwd_prof_read
+read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+prob, opts = pkg.Problems.config_quadrotor(B=8192)
+s = pkg.AbstractSolverFor(prob, opts)
+s.handle.solve_init(abi.MODE_AL)
+s.handle.solve_step(1)
+s.handle.synchronize()
+buf = (ctypes.c_ulonglong * 20)()
+read(buf)
+s.handle.solve_step(steps)
+s.handle.synchronize()
+assert read(buf) == 20
+tot = sum(buf)
+for nm, v in zip(NAMES, buf):
+    print(f"{nm:40s} {100.0 * v / tot:6.2f}%  {v / 1e9:10.3f} Gcyc")

@@ -7,3 +7,13 @@ const ModelOps* ops_quadrotor() {
   return &o;
 }
 }  // namespace tog
+
+#ifdef TOG_BWD_PROF
+// read (and reset) the backward-kernel section timers of the quadrotor instantiations
+extern "C" int tog_bwd_prof_read(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tog::tog_bwd_prof), sizeof(unsigned long long) * tog::BPROF_N) != hipSuccess)
+    return -1;
+  unsigned long long z[tog::BPROF_N] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(tog::tog_bwd_prof), z, sizeof(z)) == hipSuccess ? tog::BPROF_N : -1;
+}
+#endif

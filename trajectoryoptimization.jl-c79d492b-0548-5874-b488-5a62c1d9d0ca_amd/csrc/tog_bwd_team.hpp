@@ -48,6 +48,9 @@ struct TeamCfg {
       cmax(cmax(n * L, 3 * n * m), cmax(cmax(32 + n * m + n, n * n + n), cmax(m * m + n * m, n + PX + 2)));
   static constexpr int R2 = cmax(L * n, n * n + n);  // second region: W / S columns / T
   static constexpr int BUSP = cmax(BUS, n * L + R2);   // static part of the per-team stride (doubles)
+  // sqrt: S [A B] goes to region 1 next to S B, so region 2 only holds the cond / chol_minus scratch
+  static constexpr int R2S = cmax(3 * m * m, m * m + 1);
+  static constexpr int BUSPS = cmax(BUS, n * L + R2S);
   static constexpr int RQ = cmax(2 * n, n + PX);  // register column of the Q.xx QR workspaces
 };
 
@@ -63,17 +66,19 @@ struct RowInfo {  // one constraint row of the current knot (AL terms), 64 B
 //     rows area (inside region 2, used only during the expansion): RowInfo[pmax], int xr[pmax],
 //     int ur[pmax], x[n], u[m]
 //   per block: ConRow cache[nrows] (deduplicated row table), int knot_off[N], int knot_cnt[N]
-// S-region (persistent across knots, before region 1): std stores S column-major and s
-// (n*n + n); sqrt stores the upper factor packed by columns (column c at c(c+1)/2) and s.
+// S-region (persistent across knots, before region 1): S column-major and s (n*n + n); sqrt
+// stores its upper factor dense, explicit zeros below the diagonal, so the rolled S [A B] product
+// reads the oracle's dense operand without per-entry selects.
 template <class M>
-__host__ __device__ constexpr int sreg_size(bool sqrt) {  // S, s, then the knot's Q.uu (m*m)
-  return (sqrt ? M::n * (M::n + 1) / 2 + M::n : M::n * M::n + M::n) + M::m * M::m;
+__host__ __device__ constexpr int sreg_size(bool) {  // S, s, then the knot's Q.uu (m*m)
+  return M::n * M::n + M::n + M::m * M::m;
 }
 template <class M>
 __host__ __device__ inline int bwd_team_stride(int pmax, int sqrt) {
   using C = TeamCfg<M>;
   const int rows_area = M::n * C::L + pmax * 8 + pmax + M::n + M::m;  // doubles (2 int lists = pmax doubles)
-  int s = C::BUSP > rows_area ? C::BUSP : rows_area;
+  const int busp = sqrt ? C::BUSPS : C::BUSP;
+  int s = busp > rows_area ? busp : rows_area;
   s += sreg_size<M>(sqrt != 0);
   s += (34 - s % 32) % 32;  // s = 2 mod 32: the TPW teams' broadcast reads land on distinct banks
   return s;
@@ -344,6 +349,28 @@ __device__ __forceinline__ bool cond_exceeds_team(const double (&R)[m][m], doubl
 #ifndef TOG_BWD_WAVES
 #define TOG_BWD_WAVES 2
 #endif
+// Section timers of the knot loop (build with -DTOG_BWD_PROF; read with tog_bwd_prof_read): shader
+// clock deltas (s_memtime) summed per wave into SGPR accumulators, flushed once per wave.
+#ifdef TOG_BWD_PROF
+constexpr int BPROF_N = 20;
+static __device__ unsigned long long tog_bwd_prof[BPROF_N];
+#define BPROF_DECL                         \
+  unsigned long long bp_acc[BPROF_N] = {}; \
+  unsigned long long bp_t = __builtin_amdgcn_s_memtime();
+#define BPROF(id)                                               \
+  {                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    bp_acc[id] += t_ - bp_t;                                    \
+    bp_t = t_;                                                  \
+  }
+#define BPROF_FLUSH    \
+  if (threadIdx.x == 0) \
+    for (int i_ = 0; i_ < BPROF_N; i_++) atomicAdd(&tog_bwd_prof[i_], bp_acc[i_]);
+#else
+#define BPROF_DECL
+#define BPROF(id) {}
+#define BPROF_FLUSH
+#endif
 template <class M, int SQRTI, int ALI>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD_WAVES))) k_bwd_team(const DevProblem* P, DevBuffers Bf, int flags) {
   // (P is deliberately not __restrict__: that would let LICM hoist ~100 loop-invariant problem
@@ -358,7 +385,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   const int N = P->N, pmax = P->pmax;
   const int stride = Bf.bwd_stride;
   constexpr int SREG = sreg_size<M>(SQRT);
-  constexpr int SOFF = SQRT ? n * (n + 1) / 2 : n * n;  // offset of s in the S-region
+  constexpr int SOFF = n * n;                            // offset of s in the S-region
   double* Sreg = team_lds + (size_t)team * stride;      // S (persistent between knots)
   double* QU = Sreg + SOFF + n;                          // Q.uu of the current knot (column-major)
   double* bus = Sreg + SREG;                             // region 1 | region 2
@@ -402,6 +429,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   double dV0 = 0.0, dV1 = 0.0;
   double sown = 0.0;  // s[c] of the knot being produced
   bool done = !live;
+  BPROF_DECL
 
   // cost expansion of knot k (terminal when TERM) into this lane's Q blocks; the AL terms use the
   // team's row table (objective.jl:51-94, augmented_lagrangian_methods.jl:186-276)
@@ -459,6 +487,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         Quxc[i] = 0.0;
       }
     }
+    if (!term) BPROF(12)  // expand: cost terms (x/u loads)
     if (AL && kcnt[k] > 0) {
       const int p = kcnt[k];
       // rows area inside the second bus region (free during the expansion)
@@ -474,6 +503,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       team_rows<M>(Bf, b, k, N, pmax, p, row_cache + koff[k], xs, term ? nullptr : us, rows, xr, ur, nx, nu, team,
                    tl, TEAM);
       team_sync();
+      if (!term) BPROF(13)  // expand: team_rows (lam/mu loads, row eval)
       if (!SQRT) {
         // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order)
         double tX[n], tUx[m], tUu[m];
@@ -546,12 +576,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = 0.0;
             }
           }
+          if (!term) BPROF(14)  // expand: chol_plus operand rows
           if (nu == PU)  // every control bounded on both sides: the common case, no row selects
             team_qr<m + PU, m, m, TEAM, true>(a, m + PU, tl, bus);
           else
             team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+          if (!term) BPROF(15)  // expand: chol_plus QR
         }
       }
       // Q.x .+= cx'g ; Q.u .+= cu'g
@@ -563,6 +595,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           if (v != 0.0) tx = fma(v, ri.g, tx);
         }
         Qxs += tx;
+        if (!term) BPROF(16)  // expand: Q.x += cx'g
         if (!term) {
           double tu[m];
 #pragma unroll
@@ -591,11 +624,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       if (colx) {
 #pragma unroll
         for (int i = 0; i < n; i++) {
-          if (SQRT) {
-            if (i <= tl) Sreg[tl * (tl + 1) / 2 + i] = Qxc[i];
-          } else {
-            Sreg[i + n * tl] = Qxc[i];
-          }
+          Sreg[i + n * tl] = (SQRT && i > tl) ? 0.0 : Qxc[i];
         }
         Sreg[SOFF + tl] = Qxs;
       }
@@ -610,6 +639,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     dV0 = 0.0;
     dV1 = 0.0;
     bool restart = false;
+    BPROF(0)  // terminal knot
     for (int k = N - 2; k >= 0; k--) {
       // keep the per-lane problem constants (cQ/cR/H/Q columns) loaded per knot: hoisted out of
       // the loop they would stay live across it and spill
@@ -630,6 +660,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       } else {
         expand(k, std::integral_constant<bool, false>{}, Qxs, Qu, Qxc, Quuc, Quxc);
       }
+    BPROF(1)  // cost expansion remainder (Q.u += cu'g)
     // ---------------------------------------------------------------- ∇F[k] = [A|B] columns
     double Ac[n], Bc[n];
     {
@@ -640,6 +671,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         Bc[i] = abk[i + n * (n + cu)];
       }
     }
+#ifdef TOG_BWD_PROF
+    { volatile double sink_ = Ac[n - 1] + Bc[n - 1]; (void)sink_; }
+#endif
+    BPROF(17)  // [A B] loads
     // ---------------------------------------------------------------- Q.x += A's ; Q.u += B's
     {
       double t = 0.0;
@@ -732,23 +767,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       for (int l = 0; l < n; l++) {
         const double al = bus[l + n * c];
         const double bl = bus[l + n * (n + cu)];
-        const double* Sl = Sreg + l * (l + 1) / 2;  // packed column l (rows 0..l)
+        const double* Sl = Sreg + n * l;  // column l, explicit zeros below the diagonal
 #pragma unroll
         for (int i = 0; i < n; i++) {
-          const double sil = (i <= l) ? Sl[i] : 0.0;  // dense product, explicit zeros as the oracle
-          TX[i] = fma(sil, al, TX[i]);
-          TU[i] = fma(sil, bl, TU[i]);
+          TX[i] = fma(Sl[i], al, TX[i]);
+          TU[i] = fma(Sl[i], bl, TU[i]);
         }
       }
       team_sync();
-      // tmp_u columns (lanes < m) and this lane's tmp_x column on the bus
+      // tmp_u columns (lanes < m) then the tmp_x columns, both in region 1 ([A B] is dead)
+      double* busx = bus + n * m;
       if (colu) {
 #pragma unroll
         for (int i = 0; i < n; i++) bus[i + n * tl] = TU[i];
       }
       if (colx) {
 #pragma unroll
-        for (int i = 0; i < n; i++) bus2[i + n * tl] = TX[i];
+        for (int i = 0; i < n; i++) busx[i + n * tl] = TX[i];
       }
       team_sync();
       {
@@ -757,7 +792,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         for (int i = 0; i < m; i++) t[i] = 0.0;
 #pragma unroll 1
         for (int l = 0; l < n; l++) {
-          const double tx = bus2[l + n * c];
+          const double tx = busx[l + n * c];
 #pragma unroll
           for (int i = 0; i < m; i++) t[i] = fma(bus[l + n * i], tx, t[i]);
         }
@@ -765,6 +800,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         for (int i = 0; i < m; i++) Quxc[i] += t[i];
       }
       team_sync();
+      BPROF(2)  // S [A B], Q.ux
       {
         double a[m + n];
 #pragma unroll
@@ -773,6 +809,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
         for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
       }
+      BPROF(3)  // QR Q.uu
       {
         double a[2 * n];
 #pragma unroll
@@ -781,6 +818,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
         for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
       }
+      BPROF(4)  // QR Q.xx
     }
     if (faithful) {
       double* q = Qs + (size_t)k * NQ;
@@ -971,6 +1009,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       }
       ok = !cond_exceeds_team<m>(F, 1e8, bus2, tl);
     }
+    BPROF(5)  // regularise + cond
     if (!ok) {
       // non-PD / cond > 1e8: increase ρ and restart at N-1; Q blocks are NOT re-expanded (A.1)
       if (!faithful) {
@@ -1029,6 +1068,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         for (int i = j - 1; i >= 0; i--) col[i] = fma(-F[i][j], xj, col[i]);
       }
     }
+    BPROF(6)  // gains solve
     double Kc[m];
 #pragma unroll
     for (int i = 0; i < m; i++) Kc[i] = -1.0 * col[i];
@@ -1197,6 +1237,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           team_sync();
         }
       }
+      BPROF(7)  // K/d store, s, tmp1
       // all-gather tmp1 (row-major at bus[TB + r*m + j]) and s
       constexpr int TB = 32;
       if (colx) {
@@ -1277,6 +1318,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         U2p = fail ? QU : bus2 + 2 * m * m;
         if (fail) s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
       }
+      BPROF(8)  // chol_minus
       // S[k] = qr([Q.xx + tmp1 K; tmp2 K]).R
       {
         constexpr int RS = n + m;
@@ -1302,11 +1344,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           a[n + i] = v;
         }
         team_sync();
+        BPROF(9)  // S-update operands
         team_qr<RS, n, 0, TEAM>(a, RS, tl, bus);
         if (colx) {
 #pragma unroll
-          for (int i = 0; i < n; i++)
-            if (i <= tl) Sreg[tl * (tl + 1) / 2 + i] = a[i];
+          for (int i = 0; i < n; i++) Sreg[i + n * tl] = (i <= tl) ? a[i] : 0.0;
           Sreg[SOFF + tl] = sown;
         }
         team_sync();
@@ -1321,16 +1363,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         dV1 += 0.5 * b2;
       }
     }
+    BPROF(10)  // QR S-update (+ std-path S update)
     if (store_S && colx) {
 #pragma unroll
       for (int i = 0; i < n; i++)
         Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] =
-            SQRT ? ((i <= tl) ? Sreg[tl * (tl + 1) / 2 + i] : 0.0) : Sreg[i + n * tl];
+            Sreg[i + n * tl];
       Bf.sdbg[((size_t)b * N + k) * n + tl] = sown;
     }
     }
     if (!restart) done = true;
   }
+  BPROF(11)
+  BPROF_FLUSH
   if (!live) return;
   reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
   if (tl == 0) {
