@@ -155,6 +155,15 @@ __device__ __forceinline__ double row_at(const RowInfo& r, int col) {
   return v;
 }
 
+// Opaque copy (empty asm): addresses derived from it are recomputed where they are used instead of
+// being hoisted out of the knot loop, kept live across it and spilled (a scratch reload waits on
+// vmcnt, which also drains every global load in flight).
+template <class T>
+__device__ __forceinline__ T opaque(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // Broadcast lane L's value to the 16 lanes of its DPP row (= its team when TEAM == 16): a register
 // move (v_mov_b32_dpp row_newbcast:L), no LDS round trip. All lanes of the team must be active.
 template <int L>
@@ -354,18 +363,21 @@ __device__ __forceinline__ bool cond_exceeds_team(const double (&R)[m][m], doubl
 #ifdef TOG_BWD_PROF
 constexpr int BPROF_N = 20;
 static __device__ unsigned long long tog_bwd_prof[BPROF_N];
-#define BPROF_DECL                         \
-  unsigned long long bp_acc[BPROF_N] = {}; \
+// per-block LDS accumulators (non-returning ds_add_u64: no wait), only the last stamp in SGPRs
+#define BPROF_DECL                                             \
+  __shared__ unsigned long long bp_lds[BPROF_N];               \
+  if (threadIdx.x < BPROF_N) bp_lds[threadIdx.x] = 0ull;       \
+  __syncthreads();                                             \
   unsigned long long bp_t = __builtin_amdgcn_s_memtime();
-#define BPROF(id)                                               \
-  {                                                             \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    bp_acc[id] += t_ - bp_t;                                    \
-    bp_t = t_;                                                  \
+#define BPROF(id)                                                        \
+  {                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+    if (threadIdx.x == 0) atomicAdd(&bp_lds[id], t_ - bp_t);             \
+    bp_t = t_;                                                           \
   }
-#define BPROF_FLUSH    \
-  if (threadIdx.x == 0) \
-    for (int i_ = 0; i_ < BPROF_N; i_++) atomicAdd(&tog_bwd_prof[i_], bp_acc[i_]);
+#define BPROF_FLUSH                                                      \
+  __syncthreads();                                                       \
+  if (threadIdx.x < BPROF_N) atomicAdd(&tog_bwd_prof[threadIdx.x], bp_lds[threadIdx.x]);
 #else
 #define BPROF_DECL
 #define BPROF(id) {}
@@ -409,12 +421,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   const bool state_reg = (P->o.bp_reg_type == 1);
   const double dt = P->dt;
   const long long bb = live ? b : 0;  // safe base for idle teams (they never store)
-  const double* Xg = Bf.X + (size_t)bb * N * n;
-  const double* Ug = Bf.U + (size_t)bb * (N - 1) * m;
-  const double* ABg = Bf.AB + (size_t)bb * (N - 1) * n * L;
-  double* Kg = Bf.K + (size_t)bb * (N - 1) * m * n;
-  double* dg = Bf.d + (size_t)bb * (N - 1) * m;
-  double* Qs = Bf.Qscr + (size_t)bb * N * NQ;
+  // per-trajectory bases, formed at each use from an opaque copy of bb (see opaque())
+#define Xg (Bf.X + (size_t)opaque(bb) * N * n)
+#define Ug (Bf.U + (size_t)opaque(bb) * (N - 1) * m)
+#define ABg (Bf.AB + (size_t)opaque(bb) * (N - 1) * n * L)
+#define Kg (Bf.K + (size_t)opaque(bb) * (N - 1) * m * n)
+#define dg (Bf.d + (size_t)opaque(bb) * (N - 1) * m)
+#define Qs (Bf.Qscr + (size_t)opaque(bb) * N * NQ)
   const bool colx = tl < n;  // this lane owns a state column
   const bool colu = tl < m;  // this lane owns a control column
   const int c = colx ? tl : 0;
@@ -433,11 +446,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 
   // cost expansion of knot k (terminal when TERM) into this lane's Q blocks; the AL terms use the
   // team's row table (objective.jl:51-94, augmented_lagrangian_methods.jl:186-276)
+  const int c_ = c, cu_ = cu;
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
                     double(&Quxc)[m]) {
     constexpr bool term = decltype(term_c)::value;
     const double* xg = Xg + (size_t)k * n;
     const double* ug = term ? nullptr : Ug + (size_t)k * m;
+    const int c = opaque(c_), cu = opaque(cu_);  // per-lane columns of the problem constants
     const double xc = xg[c];
     if (!term) {
       double a = 0.0, bq = 0.0;
@@ -1388,5 +1403,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     g.bp_restarts = restarts + (faithful ? 1 : 0);
   }
 }
+#undef Xg
+#undef Ug
+#undef ABg
+#undef Kg
+#undef dg
+#undef Qs
 
 }  // namespace tog
