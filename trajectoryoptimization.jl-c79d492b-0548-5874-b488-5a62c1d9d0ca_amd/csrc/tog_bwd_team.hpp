@@ -446,17 +446,34 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 
   // cost expansion of knot k (terminal when TERM) into this lane's Q blocks; the AL terms use the
   // team's row table (objective.jl:51-94, augmented_lagrangian_methods.jl:186-276)
-  const int c_ = c, cu_ = cu;
+  const int diag_mode = P->diag_cost;  // read once (P is not __restrict__)
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
                     double(&Quxc)[m]) {
     constexpr bool term = decltype(term_c)::value;
     const double* xg = Xg + (size_t)k * n;
     const double* ug = term ? nullptr : Ug + (size_t)k * m;
-    const int c = opaque(c_), cu = opaque(cu_);  // per-lane columns of the problem constants
+    const int tlk = opaque(tl);  // per-lane columns of the problem constants, formed per knot
+    const int c = tlk < n ? tlk : 0, cu = tlk < m ? tlk : 0;
     const double xc = xg[c];
-    if (!term) {
+    if (!term && diag_mode == 2) {
+      // diagonal cost with +0.0 off-diagonals (host-checked): the per-lane constants are one
+      // diagonal entry each, the rest literal zeros -- the same values the general path loads
+      const double Qcc = P->Q[c + n * c], qc = P->q[c];
+      const double qd = SQRT ? P->cQ[c + n * c] : Qcc * dt;
+      const double rd = SQRT ? P->cR[cu + m * cu] : P->R[cu + m * cu] * dt;
+      Qxs = ((fma(Qcc, xc, 0.0) + qc) + 0.0) * dt;
+#pragma unroll
+      for (int i = 0; i < m; i++) Qu[i] = ((fma(P->R[i + m * i], ug[i], 0.0) + P->r[i]) + 0.0) * dt;
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] = (i == c) ? qd : 0.0;
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        Quuc[i] = (i == cu) ? rd : 0.0;
+        Quxc[i] = 0.0;
+      }
+    } else if (!term) {
       double a = 0.0, bq = 0.0;
-      if (P->diag_cost) {
+      if (diag_mode) {
         a = fma(P->Q[c + n * c], xc, 0.0);
       } else {
 #pragma unroll
@@ -468,7 +485,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
       for (int i = 0; i < m; i++) {
         double a2 = 0.0, b2 = 0.0;
-        if (P->diag_cost) {
+        if (diag_mode) {
           a2 = fma(P->R[i + m * i], ug[i], 0.0);
         } else {
 #pragma unroll
@@ -486,7 +503,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;
     } else {
       double a = 0.0;
-      if (P->diag_cost) {
+      if (diag_mode) {
         a = fma(P->Qf[c + n * c], xc, 0.0);
       } else {
 #pragma unroll

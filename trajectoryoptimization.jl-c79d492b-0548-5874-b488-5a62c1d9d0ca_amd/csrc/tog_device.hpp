@@ -52,7 +52,7 @@ struct DevProblem {
   int sqrt_ok;  // 0 if one of the Hessians is not PD (reference: error(...))
   // structure flags: Q, R, Qf diagonal and H == 0. The dense fma loops then only ever add exact
   // zeros off the diagonal, so the diagonal fast paths are bit-identical to them.
-  int diag_cost;
+  int diag_cost;  // 0 dense; 1 diagonal Q/R/Qf, H = 0; 2 = 1 with +0.0 off-diagonals (literal zeros)
   int pad1;
   const int* knot_off;  // [N] first row of knot k
   const int* knot_cnt;  // [N] rows at knot k (p_k)

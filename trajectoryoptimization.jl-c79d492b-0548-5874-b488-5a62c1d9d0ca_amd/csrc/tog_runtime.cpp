@@ -3,6 +3,7 @@
 //
 // Ownership: the handle owns every device buffer; callers own host arrays. One host thread per
 // handle; handles are independent (one per GPU for multi-GPU runs).
+#include <cmath>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <string.h>
@@ -370,7 +371,20 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
         if (i != j && P.R[i + m * j] != 0.0) diag = false;
     for (int i = 0; i < m * n; i++)
       if (P.H[i] != 0.0) diag = false;
-    P.diag_cost = diag ? 1 : 0;
+    // 2: diagonal with every off-diagonal entry (and H, and the factors' off-diagonals) +0.0 and
+    // dt > 0, so the kernels may use literal zeros for them and stay bit-identical
+    bool pz = diag && P.dt > 0.0;
+    auto offdiag_pz = [&](const double* A, int k) {
+      for (int j = 0; j < k; j++)
+        for (int i = 0; i < k; i++)
+          if (i != j && (A[i + k * j] != 0.0 || std::signbit(A[i + k * j]))) return false;
+      return true;
+    };
+    if (pz) pz = offdiag_pz(P.Q, n) && offdiag_pz(P.Qf, n) && offdiag_pz(P.R, m);
+    if (pz && ok) pz = offdiag_pz(P.cQ, n) && offdiag_pz(P.cQf, n) && offdiag_pz(P.cR, m);
+    for (int i = 0; pz && i < m * n; i++)
+      if (std::signbit(P.H[i])) pz = false;
+    P.diag_cost = diag ? (pz ? 2 : 1) : 0;
     if (opts->square_root && !ok) {
       tog_destroy(h);
       return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
