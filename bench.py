@@ -28,6 +28,22 @@ sys.path.insert(0, ROOT)
 import __graft_entry__  # noqa: E402
 
 METRIC = "iLQR iterations/sec (batched trajectories), quadrotor n=13 m=4 N=101"
+# --workload: the headline line is config 3 (BASELINE.json metric); the other BASELINE configs can
+# be measured the same way (secondary lines, their own metric string).
+WORKLOADS = {
+    "quadrotor": ("config_quadrotor", 8192, True,
+                  "quadrotor point-to-point, AL-iLQR, u in [0,15] + goal, sqrt backward pass (BASELINE.json configs[2])",
+                  "synthetic (seeded random starts: x0[1:3]+N(0,1), U0 = hover + 0.1 N(0,1))"),
+    "cartpole": ("config_cartpole", 1024, False,
+                 "cartpole swing-up, unconstrained iLQR (BASELINE.json configs[1])",
+                 "synthetic (seeded U0 = 0.01 + 0.5 N(0,1), x0 = 0)"),
+    "quad_maze": ("config_quad_maze", 8192, True,
+                  "quad_obs maze N=201, AL-iLQR, bounds + 4 cylinders + 3 spheres (BASELINE.json configs[3], per-GPU shard)",
+                  "synthetic (seeded x0[1:3] ~ U([-5,5]x[-3,0]x[8,12]), U0 = hover + 0.1 N(0,1))"),
+    "kuka": ("config_kuka", 4096, True,
+             "Kuka iiwa 7-DoF (RBD), AL-iLQR, terminal goal, notebook options (BASELINE.json configs[4])",
+             "synthetic (seeded x0[1:7] ~ U(-0.2,0.2), U0 = hold torque at x0)"),
+}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
@@ -87,7 +103,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8192, help="trajectories per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU (default: the config's)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="quadrotor")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -105,9 +122,10 @@ def main():
 
     pkg = __graft_entry__.load_package()
     abi = pkg.abi
-    B = args.batch
+    cfg_fn, B_default, al_mode, wl_desc, wl_data = WORKLOADS[args.workload]
+    B = args.batch or B_default
     offset, count = pkg.distributed.shard(B * world, rank, world)  # weak scaling: B trajectories per GPU
-    prob, opts = pkg.Problems.config_quadrotor(B=count, offset=offset)
+    prob, opts = getattr(pkg.Problems, cfg_fn)(B=count, offset=offset)
     stream = None
     if dist is not None:
         import torch
@@ -130,7 +148,7 @@ def main():
         abi.check(h.lib, h.lib.tog_batch_stats_device(h.h, ctypes.c_void_p(stats_t.data_ptr())))
         pkg.distributed.reduce_stats(stats_t, gathered, dist)
 
-    h.solve_init(abi.MODE_AL)
+    h.solve_init(abi.MODE_AL if al_mode else abi.MODE_ILQR)
     h.solve_step(args.warmup)
     h.synchronize()
     steps0 = h.total_steps()
@@ -163,7 +181,10 @@ def main():
         steps_all = float(steps_done)
         value = steps_all / elapsed
     # roofline for the dominant kernel (largest total device time over the timed region)
-    kb = kernel_bytes(n, m, N, 8, 13, trials)
+    cons = prob.constraints
+    p_stage = cons[0].num_constraints("stage") if al_mode else 0
+    p_term = cons[N - 1].num_constraints("terminal") if al_mode else 0
+    kb = kernel_bytes(n, m, N, p_stage, p_term, trials)
     names = ["jacobian", "backward", "forward"]
     dom = int(np.argmax(ms))
     avg_ms = ms[dom] / max(1, launches[dom])
@@ -171,7 +192,7 @@ def main():
     per_launch_traj = steps_done / max(1, launches[dom])
     alg_bytes = kb[names[dom]] * per_launch_traj
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-    traffic, tsrc = measured_traffic(names[dom])
+    traffic, tsrc = measured_traffic(names[dom]) if args.workload == "quadrotor" else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": round(alg_bytes), "kernel": names[dom],
@@ -179,16 +200,16 @@ def main():
 
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.workload == "quadrotor":
             orc = __graft_entry__.load_oracle()
             cpu = cpu_baseline(pkg, orc, seconds=args.cpu_seconds)
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "iLQR iterations/s", "n_gpus": world,
+            "metric": METRIC if args.workload == "quadrotor" else
+            f"iLQR iterations/sec (batched trajectories), {args.workload} n={n} m={m} N={N}", "value": round(value, 2), "unit": "iLQR iterations/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (seeded random starts: x0[1:3]+N(0,1), U0 = hover + 0.1 N(0,1))",
-            "config": {"workload": "quadrotor point-to-point, AL-iLQR, u in [0,15] + goal, sqrt backward pass "
-                                   "(BASELINE.json configs[2])", "n": n, "m": m, "N": N,
+            "data": wl_data,
+            "config": {"workload": wl_desc, "n": n, "m": m, "N": N,
                        "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"batch-shard x{world}",
                        "mean_line_search_trials": round(trials, 3)},
             "roofline": roofline,

@@ -60,7 +60,8 @@ enum tog_model_id {
   TOG_MODEL_QUADROTOR = 2,         /* dynamics/quadrotor.jl:10-71         n=13 m=4 */
   TOG_MODEL_CAR = 3,               /* dynamics/car.jl:3-8                 n=3  m=2 */
   TOG_MODEL_PENDULUM = 4,          /* dynamics/pendulum.jl:3-12           n=2  m=1 */
-  TOG_MODEL_COUNT = 5
+  TOG_MODEL_KUKA = 5,              /* src/model.jl:394-431 RBD Model(urdf) n=14 m=7 (include/tog_kuka.h) */
+  TOG_MODEL_COUNT = 6
 };
 
 enum tog_integrator {
@@ -219,6 +220,10 @@ typedef struct tog_handle tog_handle;
 
 /* ---------------------------------------------------------------- API */
 int32_t tog_version(void);
+/* dynamics_bias(state) at x = [q; v] for RBD models (TOG_MODEL_KUKA): c(q, v) into tau[m].
+   Replaces RigidBodyDynamics.dynamics_bias as used by hold_trajectory (dynamics/kuka.jl:117-132).
+   Host evaluation; TOG_ERR_UNSUPPORTED for analytical models. */
+int tog_dynamics_bias(int32_t model, const double* x, double* tau);
 int32_t tog_device_count(void);
 void tog_default_options(tog_options* opts);
 

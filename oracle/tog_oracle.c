@@ -29,6 +29,7 @@
 
 #include "../include/tog.h"
 #include "../include/tog_math.h"
+#include "../include/tog_kuka.h"
 
 #define DMAX 24 /* max partials: n+m+1 */
 #define OC_EXPORT __attribute__((visibility("default")))
@@ -133,8 +134,8 @@ static inline dual dsq(dual a) { /* x^2 (literal_pow -> ^(Dual,2)): v^2, 2v*p */
 /* =====================================================================
  * Continuous dynamics f!(xdot, x, u) on duals
  * ===================================================================== */
-static const int model_n[TOG_MODEL_COUNT] = {2, 4, 13, 3, 2};
-static const int model_m[TOG_MODEL_COUNT] = {1, 1, 4, 2, 1};
+static const int model_n[TOG_MODEL_COUNT] = {2, 4, 13, 3, 2, 14};
+static const int model_m[TOG_MODEL_COUNT] = {1, 1, 4, 2, 1, 7};
 
 /* dynamics/double_integrator.jl:1-4 */
 static void f_double_integrator(dual* xd, const dual* x, const dual* u) {
@@ -276,6 +277,275 @@ static void f_quadrotor(dual* xd, const dual* x, const dual* u) {
   for (int i = 0; i < 3; i++) xd[10 + i] = dscale(dsub(tau[i], cr[i]), Jinv[i]);
 }
 
+/* =====================================================================
+ * Kuka iiwa 7-DoF (BASELINE config 5): Model(urdf) src/model.jl:394-431 -> RigidBodyDynamics
+ * v2.1.0 dynamics!(ẋ, result, state, x, τ = I₇·u): q̇ = v, v̇ = M(q)⁻¹(τ − c(q,v)).
+ * RBD itself (Manifest.toml:467-472) is absent here; this restates its published algorithms:
+ * c(q,v) by recursive Newton-Euler with v̇ = 0 and the base accelerating at −g (dynamics_bias!),
+ * M(q) by the composite-rigid-body algorithm (mass_matrix!), then a Cholesky solve (RBD's
+ * dynamics_solve! for BLAS floats). Spatial quantities are carried in body coordinates
+ * (Featherstone); RBD works in world coordinates, so values agree with RBD to rounding only:
+ * PARITY UNPINNED against RBD; pinned to physics by tests/test_kuka.py. The HIP
+ * model (csrc/tog_device.hpp Kuka) performs the identical operation sequence.
+ * Kinematic/inertial tables: include/tog_kuka.h (from dynamics/urdf/kuka_iiwa.urdf:76-290).
+ * ===================================================================== */
+static const double KK_R0[7][9] = TOG_KUKA_R0;
+static const double KK_P[7][3] = TOG_KUKA_P;
+static const double KK_MASS[7] = TOG_KUKA_MASS;
+static const double KK_COM[7][3] = TOG_KUKA_COM;
+static const double KK_IC[7][6] = TOG_KUKA_IC;
+
+/* dual + real constant: partials untouched (ForwardDiff +(::Dual, ::Real)) */
+static inline dual daddc(dual a, double s) {
+  a.v = a.v + s;
+  return a;
+}
+/* body first moment h = m·c and inertia about the body origin IO = Ic + m(|c|²1 − c cᵀ) */
+static void kk_body(int j, double* h, double IO[3][3]) {
+  const double m = KK_MASS[j];
+  const double* c = KK_COM[j];
+  const double* I = KK_IC[j];
+  const double cc = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+  const double Ic[3][3] = {{I[0], I[1], I[2]}, {I[1], I[3], I[4]}, {I[2], I[4], I[5]}};
+  for (int a = 0; a < 3; a++) {
+    h[a] = m * c[a];
+    for (int b = 0; b < 3; b++) IO[a][b] = Ic[a][b] + m * ((a == b ? cc : 0.0) - c[a] * c[b]);
+  }
+}
+/* y = R0ᵀ x (parent -> joint frame) and y = R0 x (joint -> parent) */
+static void kk_r0t(int j, dual* y, const dual* x) {
+  const double* R = KK_R0[j];
+  for (int a = 0; a < 3; a++) y[a] = dadd(dadd(dscale(x[0], R[a]), dscale(x[1], R[3 + a])), dscale(x[2], R[6 + a]));
+}
+static void kk_r0(int j, dual* y, const dual* x) {
+  const double* R = KK_R0[j];
+  for (int a = 0; a < 3; a++)
+    y[a] = dadd(dadd(dscale(x[0], R[3 * a]), dscale(x[1], R[3 * a + 1])), dscale(x[2], R[3 * a + 2]));
+}
+/* E x = Rz(q)ᵀ R0ᵀ x (parent -> child body) */
+static void kk_E(int j, dual c, dual s, dual* y, const dual* x) {
+  dual t[3];
+  kk_r0t(j, t, x);
+  y[0] = dadd(dmul(c, t[0]), dmul(s, t[1]));
+  y[1] = dsub(dmul(c, t[1]), dmul(s, t[0]));
+  y[2] = t[2];
+}
+/* Eᵀ x = R0 Rz(q) x (child body -> parent) */
+static void kk_Et(int j, dual c, dual s, dual* y, const dual* x) {
+  dual t[3];
+  t[0] = dsub(dmul(c, x[0]), dmul(s, x[1]));
+  t[1] = dadd(dmul(s, x[0]), dmul(c, x[1]));
+  t[2] = x[2];
+  kk_r0(j, y, t);
+}
+static void kk_cross(dual* y, const dual* a, const dual* b) {
+  y[0] = dsub(dmul(a[1], b[2]), dmul(a[2], b[1]));
+  y[1] = dsub(dmul(a[2], b[0]), dmul(a[0], b[2]));
+  y[2] = dsub(dmul(a[0], b[1]), dmul(a[1], b[0]));
+}
+static void kk_cross_dc(dual* y, const dual* a, const double* r) { /* a × r, r constant */
+  y[0] = dsub(dscale(a[1], r[2]), dscale(a[2], r[1]));
+  y[1] = dsub(dscale(a[2], r[0]), dscale(a[0], r[2]));
+  y[2] = dsub(dscale(a[0], r[1]), dscale(a[1], r[0]));
+}
+static void kk_cross_cd(dual* y, const double* r, const dual* b) { /* r × b, r constant */
+  y[0] = dsub(dscale(b[2], r[1]), dscale(b[1], r[2]));
+  y[1] = dsub(dscale(b[0], r[2]), dscale(b[2], r[0]));
+  y[2] = dsub(dscale(b[1], r[0]), dscale(b[0], r[1]));
+}
+static void kk_symv(dual* y, const double IO[3][3], const dual* x) {
+  for (int a = 0; a < 3; a++) y[a] = dadd(dadd(dscale(x[0], IO[a][0]), dscale(x[1], IO[a][1])), dscale(x[2], IO[a][2]));
+}
+/* spatial inertia times motion: [IO w + h × v ; m v − h × w] */
+static void kk_inertia_mul(int j, dual* ang, dual* lin, const dual* w, const dual* v) {
+  double h[3], IO[3][3];
+  kk_body(j, h, IO);
+  dual t[3], hx[3];
+  kk_symv(t, IO, w);
+  kk_cross_cd(hx, h, v);
+  for (int a = 0; a < 3; a++) ang[a] = dadd(t[a], hx[a]);
+  kk_cross_cd(hx, h, w);
+  for (int a = 0; a < 3; a++) lin[a] = dsub(dscale(v[a], KK_MASS[j]), hx[a]);
+}
+
+/* dynamics_bias (RNEA, v̇ = 0) into tau[7]; also the per-joint cos/sin for reuse */
+static void kk_bias(dual* tau, dual* cq, dual* sq, const dual* q, const dual* qd) {
+  dual w[3], v[3], al[3], ln[3]; /* parent body: angular/linear velocity, acceleration */
+  dual nf[7][3], ff[7][3];
+  for (int a = 0; a < 3; a++) {
+    w[a] = dc(0.0);
+    v[a] = dc(0.0);
+    al[a] = dc(0.0);
+    ln[a] = dc(0.0);
+  }
+  ln[2] = dc(TOG_KUKA_GRAVITY); /* base acceleration −g, g = (0, 0, −9.81) */
+  for (int j = 0; j < 7; j++) {
+    const double* r = KK_P[j];
+    cq[j] = dcos(q[j]);
+    sq[j] = dsin(q[j]);
+    dual t[3], tv[3], wj[3], vj[3], aj[3], lj[3];
+    kk_cross_dc(t, w, r);
+    for (int a = 0; a < 3; a++) tv[a] = dadd(v[a], t[a]);
+    kk_E(j, cq[j], sq[j], wj, w);
+    kk_E(j, cq[j], sq[j], vj, tv);
+    wj[2] = dadd(wj[2], qd[j]);
+    kk_cross_dc(t, al, r);
+    for (int a = 0; a < 3; a++) tv[a] = dadd(ln[a], t[a]);
+    kk_E(j, cq[j], sq[j], aj, al);
+    kk_E(j, cq[j], sq[j], lj, tv);
+    /* + v_j ×ₘ (S q̇_j), S = angular z */
+    aj[0] = dadd(aj[0], dmul(wj[1], qd[j]));
+    aj[1] = dsub(aj[1], dmul(wj[0], qd[j]));
+    lj[0] = dadd(lj[0], dmul(vj[1], qd[j]));
+    lj[1] = dsub(lj[1], dmul(vj[0], qd[j]));
+    /* f = I a + v ×* (I v) */
+    dual hva[3], hvl[3], iaa[3], ial[3], c1[3], c2[3];
+    kk_inertia_mul(j, hva, hvl, wj, vj);
+    kk_inertia_mul(j, iaa, ial, aj, lj);
+    kk_cross(c1, wj, hva);
+    kk_cross(c2, vj, hvl);
+    for (int a = 0; a < 3; a++) nf[j][a] = dadd(iaa[a], dadd(c1[a], c2[a]));
+    kk_cross(c1, wj, hvl);
+    for (int a = 0; a < 3; a++) ff[j][a] = dadd(ial[a], c1[a]);
+    for (int a = 0; a < 3; a++) {
+      w[a] = wj[a];
+      v[a] = vj[a];
+      al[a] = aj[a];
+      ln[a] = lj[a];
+    }
+  }
+  for (int j = 6; j >= 0; j--) {
+    tau[j] = nf[j][2];
+    if (j > 0) {
+      dual fp[3], np[3], rx[3];
+      kk_Et(j, cq[j], sq[j], fp, ff[j]);
+      kk_Et(j, cq[j], sq[j], np, nf[j]);
+      kk_cross_cd(rx, KK_P[j], fp);
+      for (int a = 0; a < 3; a++) {
+        np[a] = dadd(np[a], rx[a]);
+        nf[j - 1][a] = dadd(nf[j - 1][a], np[a]);
+        ff[j - 1][a] = dadd(ff[j - 1][a], fp[a]);
+      }
+    }
+  }
+}
+
+/* mass_matrix! by CRBA: lower triangle M[i][j], i >= j */
+static void kk_mass(dual M[7][7], const dual* cq, const dual* sq) {
+  double mc = KK_MASS[6], h0[3], IO0[3][3];
+  dual hc[3], Ic[3][3];
+  kk_body(6, h0, IO0);
+  for (int a = 0; a < 3; a++) {
+    hc[a] = dc(h0[a]);
+    for (int b = 0; b < 3; b++) Ic[a][b] = dc(IO0[a][b]);
+  }
+  for (int j = 6; j >= 0; j--) {
+    dual Fa[3], Fl[3];
+    for (int a = 0; a < 3; a++) Fa[a] = Ic[a][2];
+    Fl[0] = dneg(hc[1]);
+    Fl[1] = hc[0];
+    Fl[2] = dc(0.0);
+    M[j][j] = Fa[2];
+    for (int k = j; k >= 1; k--) {
+      dual fl[3], fa[3], rx[3];
+      kk_Et(k, cq[k], sq[k], fl, Fl);
+      kk_Et(k, cq[k], sq[k], fa, Fa);
+      kk_cross_cd(rx, KK_P[k], fl);
+      for (int a = 0; a < 3; a++) {
+        Fa[a] = dadd(fa[a], rx[a]);
+        Fl[a] = fl[a];
+      }
+      M[j][k - 1] = Fa[2];
+    }
+    if (j > 0) {
+      const double* r = KK_P[j];
+      dual hr[3], W[3][3], col[3], row[3], Ir[3][3];
+      kk_Et(j, cq[j], sq[j], hr, hc);
+      for (int b = 0; b < 3; b++) { /* W = Eᵀ Ic (columns) */
+        for (int a = 0; a < 3; a++) col[a] = Ic[a][b];
+        kk_Et(j, cq[j], sq[j], row, col);
+        for (int a = 0; a < 3; a++) W[a][b] = row[a];
+      }
+      for (int a = 0; a < 3; a++) { /* Ir = W E (rows) */
+        kk_Et(j, cq[j], sq[j], row, W[a]);
+        for (int b = 0; b < 3; b++) Ir[a][b] = row[b];
+      }
+      const double rr = (r[0] * r[0] + r[1] * r[1]) + r[2] * r[2];
+      dual dot = dadd(dadd(dscale(hr[0], r[0]), dscale(hr[1], r[1])), dscale(hr[2], r[2]));
+      dual sh = daddc(dscale(dot, 2.0), mc * rr);
+      double hb[3], IOb[3][3];
+      kk_body(j - 1, hb, IOb);
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) {
+          dual t = dsub(Ir[a][b], dadd(dscale(hr[a], r[b]), dscale(hr[b], r[a])));
+          t = daddc(t, -((mc * r[a]) * r[b]));
+          if (a == b) t = dadd(t, sh);
+          Ic[a][b] = daddc(t, IOb[a][b]);
+        }
+      for (int a = 0; a < 3; a++) hc[a] = daddc(daddc(hr[a], mc * r[a]), hb[a]);
+      mc = mc + KK_MASS[j - 1];
+    }
+  }
+}
+
+static void f_kuka(dual* xd, const dual* x, const dual* u) {
+  const dual* q = x;
+  const dual* qd = x + 7;
+  dual tau[7], cq[7], sq[7], M[7][7], L[7][7], y[7];
+  kk_bias(tau, cq, sq, q, qd);
+  kk_mass(M, cq, sq);
+  for (int j = 0; j < 7; j++) { /* Cholesky M = L Lᵀ */
+    dual s = M[j][j];
+    for (int k = 0; k < j; k++) s = dsub(s, dmul(L[j][k], L[j][k]));
+    L[j][j] = dsqrt(s);
+    for (int i = j + 1; i < 7; i++) {
+      dual t = M[i][j];
+      for (int k = 0; k < j; k++) t = dsub(t, dmul(L[i][k], L[j][k]));
+      L[i][j] = ddiv(t, L[j][j]);
+    }
+  }
+  for (int i = 0; i < 7; i++) {
+    dual t = dsub(u[i], tau[i]);
+    for (int k = 0; k < i; k++) t = dsub(t, dmul(L[i][k], y[k]));
+    y[i] = ddiv(t, L[i][i]);
+  }
+  for (int i = 6; i >= 0; i--) {
+    dual t = y[i];
+    for (int k = i + 1; k < 7; k++) t = dsub(t, dmul(L[k][i], xd[7 + k]));
+    xd[7 + i] = ddiv(t, L[i][i]);
+  }
+  for (int i = 0; i < 7; i++) xd[i] = qd[i];
+}
+
+/* dynamics_bias(state) at (q, v): the hold torque of dynamics/kuka.jl:117-132 (v = 0) */
+OC_EXPORT void oc_kuka_bias(double* tau, const double* q, const double* v) {
+  int save = g_nd;
+  g_nd = 0;
+  dual Q[7], V[7], T[7], c[7], s[7];
+  for (int i = 0; i < 7; i++) {
+    Q[i].v = q[i];
+    V[i].v = v[i];
+  }
+  kk_bias(T, c, s, Q, V);
+  for (int i = 0; i < 7; i++) tau[i] = T[i].v;
+  g_nd = save;
+}
+/* mass_matrix(state) (full, symmetric) for tests */
+OC_EXPORT void oc_kuka_mass(double* Mout, const double* q) {
+  int save = g_nd;
+  g_nd = 0;
+  dual Q[7], c[7], s[7], M[7][7];
+  for (int i = 0; i < 7; i++) {
+    Q[i].v = q[i];
+    c[i] = dcos(Q[i]);
+    s[i] = dsin(Q[i]);
+  }
+  kk_mass(M, c, s);
+  for (int i = 0; i < 7; i++)
+    for (int j = 0; j <= i; j++) Mout[i + 7 * j] = Mout[j + 7 * i] = M[i][j].v;
+  g_nd = save;
+}
+
 static void model_f(int model, dual* xd, const dual* x, const dual* u) {
   switch (model) {
     case TOG_MODEL_DOUBLE_INTEGRATOR: f_double_integrator(xd, x, u); break;
@@ -283,6 +553,7 @@ static void model_f(int model, dual* xd, const dual* x, const dual* u) {
     case TOG_MODEL_QUADROTOR: f_quadrotor(xd, x, u); break;
     case TOG_MODEL_CAR: f_car(xd, x, u); break;
     case TOG_MODEL_PENDULUM: f_pendulum(xd, x, u); break;
+    case TOG_MODEL_KUKA: f_kuka(xd, x, u); break;
   }
 }
 

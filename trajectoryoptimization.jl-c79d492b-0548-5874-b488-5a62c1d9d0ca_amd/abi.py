@@ -19,8 +19,8 @@ LIB_PATH = PKG_DIR / "csrc" / "libtog.so"
 TOG_ABI_VERSION = 1
 
 # models (include/tog.h tog_model_id)
-MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM = range(5)
-MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1)}
+MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM, MODEL_KUKA = range(6)
+MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1), 5: (14, 7)}
 # status codes (include/tog.h tog_status_code)
 OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 
@@ -223,12 +223,13 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_profile.argtypes = [vp, C.c_int32]
     lib.tog_profile_read.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     lib.tog_last_error.restype = C.c_char_p
+    lib.tog_dynamics_bias.argtypes = [C.c_int32, _dp, _dp]
     for name in ("tog_create", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
                  "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
-                 "tog_profile_read"):
+                 "tog_profile_read", "tog_dynamics_bias"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -243,7 +244,7 @@ EXPORTED_SYMBOLS = (
     "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
     "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
-    "tog_last_error",
+    "tog_last_error", "tog_dynamics_bias",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
 NKERNELS = 3

@@ -12,10 +12,11 @@
 
 #include "../../include/tog.h"
 #include "../../include/tog_math.h"
+#include "../../include/tog_kuka.h"
 
 namespace tog {
 
-constexpr int NMAX = 16;  // max states (Kuka n=14 is "next")
+constexpr int NMAX = 16;  // max states (Kuka n=14)
 constexpr int MMAX = 8;   // max controls
 
 // ---------------------------------------------------------------------------------------------
@@ -407,12 +408,268 @@ struct Quadrotor {  // dynamics/quadrotor.jl:10-71, params :1-7
   }
 };
 
+
+// Kuka iiwa 7-DoF arm (BASELINE config 5): Model(urdf) src/model.jl:394-431 over RigidBodyDynamics
+// v2.1.0 dynamics!: q̇ = v, v̇ = M(q)⁻¹(τ − c(q,v)), τ = I₇·u. RNEA bias (v̇ = 0, base at −g), CRBA
+// mass matrix, Cholesky solve, spatial quantities in body coordinates. Tables from the reference's
+// URDF (include/tog_kuka.h). Same operation sequence as the oracle's f_kuka (oracle/tog_oracle.c),
+// operand for operand, so rollouts and dual Jacobians are bit-identical to it.
+struct Kuka {
+  static constexpr int n = 14, m = 7, id = TOG_MODEL_KUKA;
+  static constexpr double R0[7][9] = TOG_KUKA_R0;
+  static constexpr double P[7][3] = TOG_KUKA_P;
+  static constexpr double MASS[7] = TOG_KUKA_MASS;
+  static constexpr double COM[7][3] = TOG_KUKA_COM;
+  static constexpr double IC[7][6] = TOG_KUKA_IC;
+
+  __host__ __device__ static constexpr double h_(int j, int a) { return MASS[j] * COM[j][a]; }
+  __host__ __device__ static constexpr double icm_(int j, int a, int b) {
+    return (a == 0) ? (b == 0 ? IC[j][0] : b == 1 ? IC[j][1] : IC[j][2])
+         : (a == 1) ? (b == 0 ? IC[j][1] : b == 1 ? IC[j][3] : IC[j][4])
+                    : (b == 0 ? IC[j][2] : b == 1 ? IC[j][4] : IC[j][5]);
+  }
+  // inertia about the body origin: Ic + m(|c|²1 − c cᵀ)
+  __host__ __device__ static constexpr double io_(int j, int a, int b) {
+    return icm_(j, a, b) +
+           MASS[j] * ((a == b ? (COM[j][0] * COM[j][0] + COM[j][1] * COM[j][1]) + COM[j][2] * COM[j][2] : 0.0) -
+                      COM[j][a] * COM[j][b]);
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void r0t(int j, T* y, const T* x) {  // R0ᵀ x
+#pragma unroll
+    for (int a = 0; a < 3; a++) y[a] = (x[0] * R0[j][a] + x[1] * R0[j][3 + a]) + x[2] * R0[j][6 + a];
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void r0(int j, T* y, const T* x) {  // R0 x
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+      y[a] = (x[0] * R0[j][3 * a] + x[1] * R0[j][3 * a + 1]) + x[2] * R0[j][3 * a + 2];
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void E(int j, const T& c, const T& s, T* y, const T* x) {
+    T t[3];
+    r0t(j, t, x);
+    y[0] = c * t[0] + s * t[1];
+    y[1] = c * t[1] - s * t[0];
+    y[2] = t[2];
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void Et(int j, const T& c, const T& s, T* y, const T* x) {
+    T t[3];
+    t[0] = c * x[0] - s * x[1];
+    t[1] = s * x[0] + c * x[1];
+    t[2] = x[2];
+    r0(j, y, t);
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void cross(T* y, const T* a, const T* b) {
+    y[0] = a[1] * b[2] - a[2] * b[1];
+    y[1] = a[2] * b[0] - a[0] * b[2];
+    y[2] = a[0] * b[1] - a[1] * b[0];
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void cross_dc(T* y, const T* a, const double* r) {
+    y[0] = a[1] * r[2] - a[2] * r[1];
+    y[1] = a[2] * r[0] - a[0] * r[2];
+    y[2] = a[0] * r[1] - a[1] * r[0];
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void cross_cd(T* y, const double* r, const T* b) {
+    y[0] = b[2] * r[1] - b[1] * r[2];
+    y[1] = b[0] * r[2] - b[2] * r[0];
+    y[2] = b[1] * r[0] - b[0] * r[1];
+  }
+  template <class T>
+  __host__ __device__ __forceinline__ static void inertia_mul(int j, T* ang, T* lin, const T* w, const T* v) {
+    const double h[3] = {h_(j, 0), h_(j, 1), h_(j, 2)};
+    T hx[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) ang[a] = (w[0] * io_(j, a, 0) + w[1] * io_(j, a, 1)) + w[2] * io_(j, a, 2);
+    cross_cd(hx, h, v);
+#pragma unroll
+    for (int a = 0; a < 3; a++) ang[a] = ang[a] + hx[a];
+    cross_cd(hx, h, w);
+#pragma unroll
+    for (int a = 0; a < 3; a++) lin[a] = v[a] * MASS[j] - hx[a];
+  }
+
+  // dynamics_bias: RNEA with v̇ = 0 -> tau; also cos/sin of q for the mass matrix
+  template <class T>
+  __host__ __device__ __forceinline__ static void bias(T* tau, T* cq, T* sq, const T* q, const T* qd) {
+    const T z = cst_(0.0, q[0]);
+    T w[3] = {z, z, z}, v[3] = {z, z, z}, al[3] = {z, z, z}, ln[3] = {z, z, cst_(TOG_KUKA_GRAVITY, q[0])};
+    T nf[7][3], ff[7][3];
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      cq[j] = cos_(q[j]);
+      sq[j] = sin_(q[j]);
+      T t[3], tv[3], wj[3], vj[3], aj[3], lj[3];
+      cross_dc(t, w, P[j]);
+#pragma unroll
+      for (int a = 0; a < 3; a++) tv[a] = v[a] + t[a];
+      E(j, cq[j], sq[j], wj, w);
+      E(j, cq[j], sq[j], vj, tv);
+      wj[2] = wj[2] + qd[j];
+      cross_dc(t, al, P[j]);
+#pragma unroll
+      for (int a = 0; a < 3; a++) tv[a] = ln[a] + t[a];
+      E(j, cq[j], sq[j], aj, al);
+      E(j, cq[j], sq[j], lj, tv);
+      aj[0] = aj[0] + wj[1] * qd[j];
+      aj[1] = aj[1] - wj[0] * qd[j];
+      lj[0] = lj[0] + vj[1] * qd[j];
+      lj[1] = lj[1] - vj[0] * qd[j];
+      T hva[3], hvl[3], iaa[3], ial[3], c1[3], c2[3];
+      inertia_mul(j, hva, hvl, wj, vj);
+      inertia_mul(j, iaa, ial, aj, lj);
+      cross(c1, wj, hva);
+      cross(c2, vj, hvl);
+#pragma unroll
+      for (int a = 0; a < 3; a++) nf[j][a] = iaa[a] + (c1[a] + c2[a]);
+      cross(c1, wj, hvl);
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        ff[j][a] = ial[a] + c1[a];
+        w[a] = wj[a];
+        v[a] = vj[a];
+        al[a] = aj[a];
+        ln[a] = lj[a];
+      }
+    }
+#pragma unroll
+    for (int j = 6; j >= 0; j--) {
+      tau[j] = nf[j][2];
+      if (j > 0) {
+        T fp[3], np[3], rx[3];
+        Et(j, cq[j], sq[j], fp, ff[j]);
+        Et(j, cq[j], sq[j], np, nf[j]);
+        cross_cd(rx, P[j], fp);
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+          np[a] = np[a] + rx[a];
+          nf[j - 1][a] = nf[j - 1][a] + np[a];
+          ff[j - 1][a] = ff[j - 1][a] + fp[a];
+        }
+      }
+    }
+  }
+
+  // mass_matrix by CRBA; lower triangle M[i][j], i >= j
+  template <class T>
+  __host__ __device__ __forceinline__ static void mass(T (*M)[7], const T* cq, const T* sq) {
+    double mc = MASS[6];
+    T hc[3], Ic[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      hc[a] = cst_(h_(6, a), cq[0]);
+#pragma unroll
+      for (int b = 0; b < 3; b++) Ic[a][b] = cst_(io_(6, a, b), cq[0]);
+    }
+#pragma unroll
+    for (int j = 6; j >= 0; j--) {
+      T Fa[3], Fl[3];
+#pragma unroll
+      for (int a = 0; a < 3; a++) Fa[a] = Ic[a][2];
+      Fl[0] = -hc[1];
+      Fl[1] = hc[0];
+      Fl[2] = cst_(0.0, cq[0]);
+      M[j][j] = Fa[2];
+#pragma unroll
+      for (int k = j; k >= 1; k--) {
+        T fl[3], fa[3], rx[3];
+        Et(k, cq[k], sq[k], fl, Fl);
+        Et(k, cq[k], sq[k], fa, Fa);
+        cross_cd(rx, P[k], fl);
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+          Fa[a] = fa[a] + rx[a];
+          Fl[a] = fl[a];
+        }
+        M[j][k - 1] = Fa[2];
+      }
+      if (j > 0) {
+        const double* r = P[j];
+        T hr[3], W[3][3], col[3], row[3], Ir[3][3];
+        Et(j, cq[j], sq[j], hr, hc);
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+#pragma unroll
+          for (int a = 0; a < 3; a++) col[a] = Ic[a][b];
+          Et(j, cq[j], sq[j], row, col);
+#pragma unroll
+          for (int a = 0; a < 3; a++) W[a][b] = row[a];
+        }
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+          Et(j, cq[j], sq[j], row, W[a]);
+#pragma unroll
+          for (int b = 0; b < 3; b++) Ir[a][b] = row[b];
+        }
+        const double rr = (r[0] * r[0] + r[1] * r[1]) + r[2] * r[2];
+        const T dot = (hr[0] * r[0] + hr[1] * r[1]) + hr[2] * r[2];
+        const T sh = dot * 2.0 + mc * rr;
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+          for (int b = 0; b < 3; b++) {
+            T t = Ir[a][b] - (hr[a] * r[b] + hr[b] * r[a]);
+            t = t + (-((mc * r[a]) * r[b]));
+            if (a == b) t = t + sh;
+            Ic[a][b] = t + io_(j - 1, a, b);
+          }
+#pragma unroll
+        for (int a = 0; a < 3; a++) hc[a] = (hr[a] + mc * r[a]) + h_(j - 1, a);
+        mc = mc + MASS[j - 1];
+      }
+    }
+  }
+
+  template <class T>
+  __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    const T* q = x;
+    const T* qd = x + 7;
+    T tau[7], cq[7], sq[7], M[7][7], L[7][7], y[7];
+    bias(tau, cq, sq, q, qd);
+    mass(M, cq, sq);
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      T s = M[j][j];
+#pragma unroll
+      for (int k = 0; k < j; k++) s = s - L[j][k] * L[j][k];
+      L[j][j] = sqrt_(s);
+#pragma unroll
+      for (int i = j + 1; i < 7; i++) {
+        T t = M[i][j];
+#pragma unroll
+        for (int k = 0; k < j; k++) t = t - L[i][k] * L[j][k];
+        L[i][j] = t / L[j][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      T t = u[i] - tau[i];
+#pragma unroll
+      for (int k = 0; k < i; k++) t = t - L[i][k] * y[k];
+      y[i] = t / L[i][i];
+    }
+#pragma unroll
+    for (int i = 6; i >= 0; i--) {
+      T t = y[i];
+#pragma unroll
+      for (int k = i + 1; k < 7; k++) t = t - L[k][i] * xd[7 + k];
+      xd[7 + i] = t / L[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; i++) xd[i] = qd[i];
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Explicit Runge-Kutta discretisation with runtime dt (src/integration.jl:115-158). Running-sum
 // form keeps the reference's left-to-right association: RK4 ((k1 + 2k2) + 2k3) + k4,
 // RK3 (k1 + 4k2) + k3, with RK3's third stage at (x - k1) + 2k2.
 template <class M, int INTEG, class T>
-__device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, double dt) {
+__host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, double dt) {
   constexpr int n = M::n;
   T k[n], s[n], t[n];
   M::f(k, x, u);

@@ -1604,7 +1604,9 @@ struct ModelLaunch {
 #ifndef TOG_JW
 #define TOG_JW 4
 #endif
-  static constexpr int JW = (M::n + M::m) <= 6 ? (M::n + M::m) : TOG_JW;
+  // (the Kuka RBD step keeps per-joint force and mass-matrix arrays live: one partial per thread
+  // holds its scratch to ~4 KB/lane against ~12 KB with 4)
+  static constexpr int JW = (M::n + M::m) <= 6 ? (M::n + M::m) : (M::id == TOG_MODEL_KUKA ? 1 : TOG_JW);
   static unsigned grid(long long total, int blk) { return (unsigned)((total + blk - 1) / blk); }
   static void init(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, hipStream_t st) {
     if (integ == TOG_RK4)

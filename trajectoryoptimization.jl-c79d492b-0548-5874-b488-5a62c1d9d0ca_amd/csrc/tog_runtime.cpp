@@ -21,6 +21,7 @@ const ModelOps* ops_cartpole();
 const ModelOps* ops_quadrotor();
 const ModelOps* ops_car();
 const ModelOps* ops_pendulum();
+const ModelOps* ops_kuka();
 }  // namespace tog
 
 static thread_local std::string g_err;
@@ -94,6 +95,7 @@ static const ModelOps* ops_for(int model) {
     case TOG_MODEL_QUADROTOR: return ops_quadrotor();
     case TOG_MODEL_CAR: return ops_car();
     case TOG_MODEL_PENDULUM: return ops_pendulum();
+    case TOG_MODEL_KUKA: return ops_kuka();
   }
   return nullptr;
 }
@@ -244,6 +246,16 @@ __global__ void k_reset_state(TrajState* st, long long B, double mu0) {
 extern "C" {
 
 int32_t tog_version(void) { return TOG_ABI_VERSION; }
+
+// dynamics_bias(state) of an RBD model at x = [q; v] (RigidBodyDynamics, used by
+// hold_trajectory dynamics/kuka.jl:117-132): host evaluation of the same model code the kernels run.
+int tog_dynamics_bias(int32_t model, const double* x, double* tau) {
+  if (!x || !tau) return TOG_ERR_ARG;
+  if (model != TOG_MODEL_KUKA) return TOG_ERR_UNSUPPORTED;
+  double c[7], s[7];
+  Kuka::bias<double>(tau, c, s, x, x + 7);
+  return TOG_OK;
+}
 
 int32_t tog_device_count(void) {
   int c = 0;
@@ -436,7 +448,7 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   b.sdbg = nullptr;
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
   if (b.nc < 1) b.nc = 1;
-  // reference constructor state: X = NaN, U = 0, K = d = 0, λ = 0, μ = μ_init (=1),
+  // reference constructor state: X = NaN, U = 0, K = d = 0, λ = 0, μ = opts.penalty_initial,
   // ρ = dρ = 0 (ilqr_solver.jl:118-144, augmented_lagrangian_solver.jl:143-169)
   fill(h, b.x0, B * n, 0.0);
   fill(h, b.X, B * N * n, NAN);
@@ -447,9 +459,9 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   fill(h, b.K, B * (N - 1) * m * n, 0.0);
   fill(h, b.d, B * (N - 1) * m, 0.0);
   fill(h, b.lam, B * N * P1, 0.0);
-  fill(h, b.mu, B * N * P1, 1.0);
+  fill(h, b.mu, B * N * P1, h->opts.penalty_initial);  // init_constraint_trajectories
   fill(h, b.C, B * N * P1, 0.0);
-  hipLaunchKernelGGL(k_reset_state, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, h->stream, b.st, (long long)B, 1.0);
+  hipLaunchKernelGGL(k_reset_state, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, h->stream, b.st, (long long)B, h->opts.penalty_initial);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(h->stream));
   *out = h;

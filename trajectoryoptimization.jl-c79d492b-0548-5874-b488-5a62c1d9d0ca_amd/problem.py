@@ -72,6 +72,8 @@ class Dynamics:
     quadrotor = Model(abi.MODEL_QUADROTOR, 13, 4, "quadrotor")  # dynamics/quadrotor.jl:10-71
     car = Model(abi.MODEL_CAR, 3, 2, "car")  # dynamics/car.jl:3-8
     pendulum = Model(abi.MODEL_PENDULUM, 2, 1, "pendulum")  # dynamics/pendulum.jl:3-12
+    # Model(urdf_kuka) dynamics/kuka.jl:137 -> src/model.jl:394-447 (RBD, tables include/tog_kuka.h)
+    kuka = Model(abi.MODEL_KUKA, 14, 7, "kuka")
 
 
 # ----------------------------------------------------------------------------- costs

@@ -192,6 +192,61 @@ def car_parallel_park(U0=None):
 
 # ---------------------------------------------------------------------------- BASELINE configs
 
+def dynamics_bias(model, x):
+    """``RigidBodyDynamics.dynamics_bias(state)`` at x = [q; v] (the libtog host evaluation of the
+    same model code the kernels run; RBD models only)."""
+    from . import abi
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    if x.shape != (model.n,):
+        raise ValueError(f"x must have length {model.n}")
+    tau = np.zeros(model.m)
+    lib = abi.load_library()
+    abi.check(lib, lib.tog_dynamics_bias(model.model_id, x.ctypes.data_as(abi._dp), tau.ctypes.data_as(abi._dp)))
+    return tau
+
+
+def hold_trajectory(n, m, N, model, q):
+    """dynamics/kuka.jl:117-132: U0[:, k] = dynamics_bias at configuration q, zero velocity.
+    Returns (N, m) like the reference's m x N matrix (only the first N-1 columns are used)."""
+    q = np.asarray(q, dtype=np.float64)
+    nq = model.n // 2
+    if len(q) > m:
+        raise ValueError(f"system must be fully actuated to hold an arbitrary position ({len(q)} should be > {m})")
+    x = np.zeros(model.n)
+    x[:nq] = q[:nq]
+    return np.tile(dynamics_bias(model, x), (N, 1))
+
+
+def kuka(x0=None, U0=None, N=51, tf=5.0):
+    """examples/kuka_iiwa/Kuka iiwa.ipynb cells 7-15: x0 = 0, xf[1:2] = pi/2, Q = diag(1x7, 100x7),
+    Qf = 1000 I, R = 1e-2 I, N = 51, tf = 5, rk3, terminal goal constraint, U0 = hold trajectory."""
+    model_d = rk3(Dynamics.kuka)
+    n, m = 14, 7
+    if x0 is None:
+        x0 = np.zeros(n)
+    xf = np.zeros(n)
+    xf[0] = math.pi / 2
+    xf[1] = math.pi / 2
+    Q = np.diag(np.r_[np.ones(7), 100.0 * np.ones(7)])
+    Qf = 1000.0 * np.eye(n)
+    R = 1e-2 * np.eye(m)
+    dt = tf / (N - 1)
+    if U0 is None:
+        U0 = hold_trajectory(n, m, N, Dynamics.kuka, np.asarray(x0)[:7])[: N - 1]
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    cons = Constraints(N)
+    cons[N - 1] += goal_constraint(xf)
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+
+
+def kuka_options():
+    """The notebook's solver options (Kuka iiwa.ipynb cell 11)."""
+    opts_ilqr = iLQRSolverOptions(iterations=300)
+    return AugmentedLagrangianSolverOptions(opts_uncon=opts_ilqr, iterations=20, cost_tolerance=1.0e-6,
+                                            cost_tolerance_intermediate=1.0e-5, constraint_tolerance=1.0e-3,
+                                            penalty_scaling=50.0, penalty_initial=0.01)
+
+
 def _per_traj_rng(seed0, B, fn):
     return np.stack([fn(np.random.default_rng(seed0 + b)) for b in range(B)])
 
@@ -241,6 +296,19 @@ def config_quad_maze(B=8192, offset=0, N=201):
     Z = _per_traj_rng(3000 + offset, B, gen)
     prob = quad_obs(N=N, x0=Z[:, :n], U0=Z[:, n:].reshape(B, N - 1, m))
     return prob, AugmentedLagrangianSolverOptions()
+
+
+def config_kuka(B=4096, offset=0):
+    """Config 5: Kuka iiwa (n=14, m=7, N=51), AL-iLQR with the terminal goal and the notebook's options;
+    x0[1:7] ~ U(-0.2, 0.2) (seed 4000+b), U0 = the hold trajectory at x0 (the notebook's own
+    initialisation, Kuka iiwa.ipynb cell 15). SURVEY §8(d) proposed hold + 0.1 N(0,1): with link 7's
+    3e-4 kg m^2 inertia that open-loop rollout diverges within ~10 knots, so the batch differs by x0."""
+    N, n, m = 51, 14, 7
+    x0 = np.zeros((B, n))
+    for b in range(B):
+        x0[b, :7] = np.random.default_rng(4000 + offset + b).uniform(-0.2, 0.2, 7)
+    U0 = np.stack([hold_trajectory(n, m, N, Dynamics.kuka, x0[b, :7])[: N - 1] for b in range(B)])
+    return kuka(x0=x0, U0=U0, N=N), kuka_options()
 
 
 def config_doubleintegrator(B=1):
