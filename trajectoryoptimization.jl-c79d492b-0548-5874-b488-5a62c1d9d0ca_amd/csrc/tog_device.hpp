@@ -97,6 +97,8 @@ struct DevBuffers {
   double* lsJ;  // (NC, B) speculative line-search trial costs
   int* lsok;    // (NC, B) speculative line-search trial rollout status
   int nc;       // candidates evaluated per trajectory per launch (<= 64)
+  int* ls_list;   // (2, B) ping-pong lists of trajectories still undecided after a speculative round
+  int* ls_count;  // [LS_MAX_ROUNDS] list lengths, zeroed at the start of every forward pass
   int bwd_stride;     // k_bwd_team: per-team LDS stride (doubles) of the launch
   int bwd_shmem;      // k_bwd_team: dynamic LDS bytes per block of the launch
   int bwd_stride2[2]; // [std, sqrt] strides

@@ -1183,6 +1183,8 @@ attempt:
 // replayed once more, writing the new trajectory in place. One round covers iterations_linesearch=20.
 // =============================================================================================
 constexpr int FTEAM = 32;
+constexpr int LS_MAX_ROUNDS = 2;  // speculative line-search rounds per forward pass
+constexpr int LS_FIRST = 8;       // width of the first round
 
 __device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS traffic within the wave
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1461,27 +1463,60 @@ __device__ __forceinline__ bool ls_decided_within(const tog_options& o, const De
   }
 }
 
-// speculative trials: one lane per (trajectory, trial j), α_j = 2^-j, cost only. Trials [lo, lo+cnt);
-// a launch with lo > 0 only runs for trajectories the earlier trials did not settle (the step-level
-// path passes its J_prev through Jprev_in).
+// speculative trials: one lane per (trajectory, trial j), α_j = 2^-j, cost only. Trials [lo, lo+cnt).
+// The first round covers every trajectory; later rounds only the trajectories listed by
+// k_ls_compact (list != nullptr, length *count) — the earlier trials did not settle them. Lanes past
+// the list's end exit at once, so whole waves retire (the step-level path passes its J_prev through
+// Jprev_in).
 template <class M, int INTEG>
 __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
-                                                 int cnt, int bookkeeping, const double* Jprev_in) {
+                                                 int cnt, const int* __restrict__ list, const int* __restrict__ count) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nb = list ? (long long)*count : P->B;
+  if ((long long)blockIdx.x * blockDim.x >= nb * cnt) return;  // block past the list: retire before LDS work
   extern __shared__ double spec_lds[];
   const RowTables RT =
       (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, spec_lds) : global_row_tables(P);
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int NC = Bf.nc;
-  if (t >= P->B * cnt) return;
-  const long long b = t / cnt;
+  if (t >= nb * cnt) return;
+  const long long i = t / cnt;
+  const long long b = list ? (long long)list[i] : i;
   const int j = lo + (int)(t % cnt);
   const TrajState& st = Bf.st[b];
   if (!st.active) return;
-  if (lo > 0 && ls_decided_within(P->o, Bf, b, NC, bookkeeping ? st.J : Jprev_in[b], st.dV0, st.dV1, lo)) return;
   double Jj = INFINITY;
   const bool ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
   Bf.lsJ[b * NC + j] = Jj;
   Bf.lsok[b * NC + j] = ok ? 1 : 0;
+}
+
+// After trials [0, hi): list the active trajectories the acceptance logic has not settled yet
+// (input: every trajectory when in_list == nullptr, else in_list[0, *in_count)). One thread per
+// entry; a wave reserves its slots with one atomic (ballot + popcount). The list order varies from
+// run to run, the per-trajectory results do not. (Templated on the model only to give every model's
+// translation unit its own instance.)
+template <class M>
+__global__ void __launch_bounds__(256) k_ls_compact(const DevProblem* __restrict__ P, DevBuffers Bf, int hi,
+                                                    int bookkeeping, const double* __restrict__ Jprev_in,
+                                                    const int* __restrict__ in_list, const int* __restrict__ in_count,
+                                                    int* __restrict__ out_list, int* __restrict__ out_count) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nb = in_list ? (long long)*in_count : P->B;
+  bool und = false;
+  long long b = 0;
+  if (t < nb) {
+    b = in_list ? (long long)in_list[t] : t;
+    const TrajState& st = Bf.st[b];
+    und = st.active && !ls_decided_within(P->o, Bf, b, Bf.nc, bookkeeping ? st.J : Jprev_in[b], st.dV0, st.dV1, hi);
+  }
+  const unsigned long long mask = __ballot(und);
+  if (mask == 0) return;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int leader = __ffsll((long long)mask) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(out_count, __popcll(mask));
+  base = __shfl(base, leader);
+  if (und) out_list[base + __popcll(mask & ((1ull << lane) - 1))] = (int)b;
 }
 
 // decision (sequential acceptance logic replayed over the speculative trials, forward_pass.jl:19-65),
@@ -1657,19 +1692,33 @@ struct ModelLaunch {
   }
   static void forward(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, int bk,
                       const double* Jp, double* Jo, hipStream_t st) {
-    // speculative line search in two rounds: trials [0, R1) for every trajectory (settles ~98% of
-    // them on the benchmark configs), then [R1, nc) only where still undecided
-    constexpr int R1 = 8;
-    const int r1 = Bf.nc < R1 ? Bf.nc : R1;
+    // speculative line search in two rounds: trials [0, 8) for every trajectory (settles ~98% of them
+    // on configs 2, 3 and 5), then [8, nc) only for the trajectories the first round left undecided
+    // (k_ls_compact lists them, so the second round's waves are dense). Narrower first rounds were
+    // measured slower: 8 lanes sharing one trajectory's K/X/U per load is what keeps the rollouts
+    // coalesced, and the Kuka's heavy lanes need the width to fill the SIMDs.
     const unsigned sm = (unsigned)Bf.rows_shmem;
-    for (int round = 0; round < 2; round++) {
-      const int lo = round ? r1 : 0, cnt = round ? Bf.nc - r1 : r1;
-      if (cnt <= 0) continue;
-      const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial)
+    (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_MAX_ROUNDS, st);
+    int lo = 0, round = 0;
+    const int* list = nullptr;
+    const int* count = nullptr;
+    while (lo < Bf.nc) {
+      const int hi = (round + 1 < LS_MAX_ROUNDS) ? (lo == 0 ? LS_FIRST : 2 * lo) : Bf.nc;
+      const int cnt = (hi < Bf.nc ? hi : Bf.nc) - lo;
+      if (round > 0) {  // list the trajectories trials [0, lo) did not settle
+        int* out = Bf.ls_list + (size_t)(round & 1) * B;
+        hipLaunchKernelGGL((k_ls_compact<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, lo, bk, Jp,
+                           list, count, out, Bf.ls_count + round);
+        list = out;
+        count = Bf.ls_count + round;
+      }
+      const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
       if (integ == TOG_RK4)
-        hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, bk, Jp);
+        hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
       else
-        hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, bk, Jp);
+        hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
+      lo += cnt;
+      round++;
     }
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_ls_commit<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);

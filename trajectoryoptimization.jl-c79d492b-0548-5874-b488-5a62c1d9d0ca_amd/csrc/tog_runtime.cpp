@@ -440,7 +440,8 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
       (rc = dalloc(h, &b.Qscr, B * N * h->nq)) || (rc = dalloc(h, &b.st, B)) ||
       (rc = dalloc(h, &h->d_scratch, B)) || (rc = dalloc(h, &h->d_scratch2, B)) ||
       (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4)) ||
-      (rc = dalloc(h, &b.lsJ, B * 64)) || (rc = dalloc(h, &b.lsok, B * 64))) {
+      (rc = dalloc(h, &b.lsJ, B * 64)) || (rc = dalloc(h, &b.lsok, B * 64)) ||
+      (rc = dalloc(h, &b.ls_list, 2 * B)) || (rc = dalloc(h, &b.ls_count, LS_MAX_ROUNDS))) {
     tog_destroy(h);
     return rc;
   }
