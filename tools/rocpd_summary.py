@@ -52,24 +52,30 @@ def main(d):
     return traffic(d)
 
 
-GROUPS = {"backward": ("k_bwd_team", "k_backward"), "forward": ("k_ls_spec", "k_ls_commit"),
+GROUPS = {"backward": ("k_bwd_team", "k_backward"), "forward": ("k_ls_spec", "k_ls_compact", "k_ls_commit"),
           "jacobian": ("k_jacobian",)}
 
 
 def traffic(d):
-    """Per-launch HBM bytes of each bench kernel group: 2 x FETCH_SIZE + WRITE_SIZE (guide §HBM)."""
+    """Per-step HBM bytes of each bench kernel group (one bench "launch" of a group = all its
+    dispatches in one step, e.g. forward = 2 x k_ls_spec + k_ls_compact + k_ls_commit): the group's
+    summed 2 x FETCH_SIZE + WRITE_SIZE (guide §HBM) over all dispatches, divided by the dispatch count
+    of its least frequent kernel (once per step)."""
     res = {}
     for ctr, sym, corr in (("fetch", "FETCH_SIZE", 2.0), ("write", "WRITE_SIZE", 1.0)):
         dbs = list((d / ctr).glob("*.db"))
         if not dbs:
             return None
         c = sqlite3.connect(dbs[0])
-        for name, n, avg in c.execute("select kernel_name, count(*), avg(value) from counters_collection "
-                                      f"where counter_name='{sym}' group by kernel_name"):
+        tot, cnt = {}, {}
+        for name, n, sm in c.execute("select kernel_name, count(*), sum(value) from counters_collection "
+                                     f"where counter_name='{sym}' group by kernel_name"):
             for g, keys in GROUPS.items():
                 if any(k + "<" in name for k in keys):
-                    res.setdefault(g, {}).setdefault(ctr, 0.0)
-                    res[g][ctr] += avg * 1024.0 * corr
+                    tot[g] = tot.get(g, 0.0) + sm * 1024.0 * corr
+                    cnt[g] = min(cnt.get(g, n), n)
+        for g in tot:
+            res.setdefault(g, {})[ctr] = tot[g] / max(1, cnt[g])
     for g in res:
         res[g]["traffic_bytes"] = res[g].get("fetch", 0.0) + res[g].get("write", 0.0)
     return res
