@@ -416,36 +416,53 @@ struct Quadrotor {  // dynamics/quadrotor.jl:10-71, params :1-7
 // mass matrix, Cholesky solve, spatial quantities in body coordinates. Tables from the reference's
 // URDF (include/tog_kuka.h). Same operation sequence as the oracle's f_kuka (oracle/tog_oracle.c),
 // operand for operand, so rollouts and dual Jacobians are bit-identical to it.
+// Joint tables with the derived per-body inertia terms, built at compile time from include/tog_kuka.h.
+struct KukaTab {
+  double R0[7][9], P[7][3], M[7], H[7][3], IO[7][9];
+  constexpr KukaTab() : R0{}, P{}, M{}, H{}, IO{} {
+    constexpr double r0[7][9] = TOG_KUKA_R0, pp[7][3] = TOG_KUKA_P, mass[7] = TOG_KUKA_MASS,
+                     com[7][3] = TOG_KUKA_COM, ic[7][6] = TOG_KUKA_IC;
+    for (int j = 0; j < 7; j++) {
+      for (int e = 0; e < 9; e++) R0[j][e] = r0[j][e];
+      const double* c = com[j];
+      const double cc = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+      const double icm[3][3] = {{ic[j][0], ic[j][1], ic[j][2]}, {ic[j][1], ic[j][3], ic[j][4]},
+                                {ic[j][2], ic[j][4], ic[j][5]}};
+      M[j] = mass[j];
+      for (int a = 0; a < 3; a++) {
+        P[j][a] = pp[j][a];
+        H[j][a] = mass[j] * c[a];  // first moment m·c
+        // inertia about the body origin: Ic + m(|c|²1 − c cᵀ)
+        for (int b = 0; b < 3; b++) IO[j][3 * a + b] = icm[a][b] + mass[j] * ((a == b ? cc : 0.0) - c[a] * c[b]);
+      }
+    }
+  }
+};
+
 struct Kuka {
   static constexpr int n = 14, m = 7, id = TOG_MODEL_KUKA;
-  static constexpr double R0[7][9] = TOG_KUKA_R0;
-  static constexpr double P[7][3] = TOG_KUKA_P;
-  static constexpr double MASS[7] = TOG_KUKA_MASS;
-  static constexpr double COM[7][3] = TOG_KUKA_COM;
-  static constexpr double IC[7][6] = TOG_KUKA_IC;
-
-  __host__ __device__ static constexpr double h_(int j, int a) { return MASS[j] * COM[j][a]; }
-  __host__ __device__ static constexpr double icm_(int j, int a, int b) {
-    return (a == 0) ? (b == 0 ? IC[j][0] : b == 1 ? IC[j][1] : IC[j][2])
-         : (a == 1) ? (b == 0 ? IC[j][1] : b == 1 ? IC[j][3] : IC[j][4])
-                    : (b == 0 ? IC[j][2] : b == 1 ? IC[j][4] : IC[j][5]);
+  static constexpr KukaTab KT{};
+  // Joint index laundered through an SGPR at each use: the tables are then read from constant memory
+  // (scalar loads) where they are used, instead of ~200 fp64 literals being materialised once and
+  // kept live in VGPRs across the three RK stages (which spilled 4 KB/lane in the Jacobian).
+  __host__ __device__ __forceinline__ static int lj(int j) {
+#ifdef __HIP_DEVICE_COMPILE__
+    asm volatile("" : "+s"(j));
+#endif
+    return j;
   }
-  // inertia about the body origin: Ic + m(|c|²1 − c cᵀ)
-  __host__ __device__ static constexpr double io_(int j, int a, int b) {
-    return icm_(j, a, b) +
-           MASS[j] * ((a == b ? (COM[j][0] * COM[j][0] + COM[j][1] * COM[j][1]) + COM[j][2] * COM[j][2] : 0.0) -
-                      COM[j][a] * COM[j][b]);
-  }
+  __host__ __device__ __forceinline__ static double h_(int j, int a) { return KT.H[j][a]; }
+  __host__ __device__ __forceinline__ static double io_(int j, int a, int b) { return KT.IO[j][3 * a + b]; }
   template <class T>
   __host__ __device__ __forceinline__ static void r0t(int j, T* y, const T* x) {  // R0ᵀ x
 #pragma unroll
-    for (int a = 0; a < 3; a++) y[a] = (x[0] * R0[j][a] + x[1] * R0[j][3 + a]) + x[2] * R0[j][6 + a];
+    for (int a = 0; a < 3; a++) y[a] = (x[0] * KT.R0[j][a] + x[1] * KT.R0[j][3 + a]) + x[2] * KT.R0[j][6 + a];
   }
   template <class T>
   __host__ __device__ __forceinline__ static void r0(int j, T* y, const T* x) {  // R0 x
 #pragma unroll
     for (int a = 0; a < 3; a++)
-      y[a] = (x[0] * R0[j][3 * a] + x[1] * R0[j][3 * a + 1]) + x[2] * R0[j][3 * a + 2];
+      y[a] = (x[0] * KT.R0[j][3 * a] + x[1] * KT.R0[j][3 * a + 1]) + x[2] * KT.R0[j][3 * a + 2];
   }
   template <class T>
   __host__ __device__ __forceinline__ static void E(int j, const T& c, const T& s, T* y, const T* x) {
@@ -492,7 +509,7 @@ struct Kuka {
     for (int a = 0; a < 3; a++) ang[a] = ang[a] + hx[a];
     cross_cd(hx, h, w);
 #pragma unroll
-    for (int a = 0; a < 3; a++) lin[a] = v[a] * MASS[j] - hx[a];
+    for (int a = 0; a < 3; a++) lin[a] = v[a] * KT.M[j] - hx[a];
   }
 
   // dynamics_bias: RNEA with v̇ = 0 -> tau; also cos/sin of q for the mass matrix
@@ -503,27 +520,28 @@ struct Kuka {
     T nf[7][3], ff[7][3];
 #pragma unroll
     for (int j = 0; j < 7; j++) {
+      const int jl = Kuka::lj(j);
       cq[j] = cos_(q[j]);
       sq[j] = sin_(q[j]);
       T t[3], tv[3], wj[3], vj[3], aj[3], lj[3];
-      cross_dc(t, w, P[j]);
+      cross_dc(t, w, KT.P[jl]);
 #pragma unroll
       for (int a = 0; a < 3; a++) tv[a] = v[a] + t[a];
-      E(j, cq[j], sq[j], wj, w);
-      E(j, cq[j], sq[j], vj, tv);
+      E(jl, cq[j], sq[j], wj, w);
+      E(jl, cq[j], sq[j], vj, tv);
       wj[2] = wj[2] + qd[j];
-      cross_dc(t, al, P[j]);
+      cross_dc(t, al, KT.P[jl]);
 #pragma unroll
       for (int a = 0; a < 3; a++) tv[a] = ln[a] + t[a];
-      E(j, cq[j], sq[j], aj, al);
-      E(j, cq[j], sq[j], lj, tv);
+      E(jl, cq[j], sq[j], aj, al);
+      E(jl, cq[j], sq[j], lj, tv);
       aj[0] = aj[0] + wj[1] * qd[j];
       aj[1] = aj[1] - wj[0] * qd[j];
       lj[0] = lj[0] + vj[1] * qd[j];
       lj[1] = lj[1] - vj[0] * qd[j];
       T hva[3], hvl[3], iaa[3], ial[3], c1[3], c2[3];
-      inertia_mul(j, hva, hvl, wj, vj);
-      inertia_mul(j, iaa, ial, aj, lj);
+      inertia_mul(jl, hva, hvl, wj, vj);
+      inertia_mul(jl, iaa, ial, aj, lj);
       cross(c1, wj, hva);
       cross(c2, vj, hvl);
 #pragma unroll
@@ -543,9 +561,10 @@ struct Kuka {
       tau[j] = nf[j][2];
       if (j > 0) {
         T fp[3], np[3], rx[3];
-        Et(j, cq[j], sq[j], fp, ff[j]);
-        Et(j, cq[j], sq[j], np, nf[j]);
-        cross_cd(rx, P[j], fp);
+        const int jl = Kuka::lj(j);
+        Et(jl, cq[j], sq[j], fp, ff[j]);
+        Et(jl, cq[j], sq[j], np, nf[j]);
+        cross_cd(rx, KT.P[jl], fp);
 #pragma unroll
         for (int a = 0; a < 3; a++) {
           np[a] = np[a] + rx[a];
@@ -559,7 +578,7 @@ struct Kuka {
   // mass_matrix by CRBA; lower triangle M[i][j], i >= j
   template <class T>
   __host__ __device__ __forceinline__ static void mass(T (*M)[7], const T* cq, const T* sq) {
-    double mc = MASS[6];
+    double mc = KT.M[6];
     T hc[3], Ic[3][3];
 #pragma unroll
     for (int a = 0; a < 3; a++) {
@@ -579,9 +598,10 @@ struct Kuka {
 #pragma unroll
       for (int k = j; k >= 1; k--) {
         T fl[3], fa[3], rx[3];
-        Et(k, cq[k], sq[k], fl, Fl);
-        Et(k, cq[k], sq[k], fa, Fa);
-        cross_cd(rx, P[k], fl);
+        const int kl = Kuka::lj(k);
+        Et(kl, cq[k], sq[k], fl, Fl);
+        Et(kl, cq[k], sq[k], fa, Fa);
+        cross_cd(rx, KT.P[kl], fl);
 #pragma unroll
         for (int a = 0; a < 3; a++) {
           Fa[a] = fa[a] + rx[a];
@@ -590,20 +610,21 @@ struct Kuka {
         M[j][k - 1] = Fa[2];
       }
       if (j > 0) {
-        const double* r = P[j];
+        const int jl = Kuka::lj(j), jp = Kuka::lj(j - 1);
+        const double* r = KT.P[jl];
         T hr[3], W[3][3], col[3], row[3], Ir[3][3];
-        Et(j, cq[j], sq[j], hr, hc);
+        Et(jl, cq[j], sq[j], hr, hc);
 #pragma unroll
         for (int b = 0; b < 3; b++) {
 #pragma unroll
           for (int a = 0; a < 3; a++) col[a] = Ic[a][b];
-          Et(j, cq[j], sq[j], row, col);
+          Et(jl, cq[j], sq[j], row, col);
 #pragma unroll
           for (int a = 0; a < 3; a++) W[a][b] = row[a];
         }
 #pragma unroll
         for (int a = 0; a < 3; a++) {
-          Et(j, cq[j], sq[j], row, W[a]);
+          Et(jl, cq[j], sq[j], row, W[a]);
 #pragma unroll
           for (int b = 0; b < 3; b++) Ir[a][b] = row[b];
         }
@@ -617,11 +638,11 @@ struct Kuka {
             T t = Ir[a][b] - (hr[a] * r[b] + hr[b] * r[a]);
             t = t + (-((mc * r[a]) * r[b]));
             if (a == b) t = t + sh;
-            Ic[a][b] = t + io_(j - 1, a, b);
+            Ic[a][b] = t + io_(jp, a, b);
           }
 #pragma unroll
-        for (int a = 0; a < 3; a++) hc[a] = (hr[a] + mc * r[a]) + h_(j - 1, a);
-        mc = mc + MASS[j - 1];
+        for (int a = 0; a < 3; a++) hc[a] = (hr[a] + mc * r[a]) + h_(jp, a);
+        mc = mc + KT.M[jp];
       }
     }
   }
@@ -630,18 +651,19 @@ struct Kuka {
   __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
     const T* q = x;
     const T* qd = x + 7;
-    T tau[7], cq[7], sq[7], M[7][7], L[7][7], y[7];
+    T tau[7], cq[7], sq[7], L[7][7], y[7];
     bias(tau, cq, sq, q, qd);
-    mass(M, cq, sq);
+    mass(L, cq, sq);
+    // Cholesky M = L Lᵀ in place (entry (i,j) of M is read once, before L[i][j] replaces it)
 #pragma unroll
     for (int j = 0; j < 7; j++) {
-      T s = M[j][j];
+      T s = L[j][j];
 #pragma unroll
       for (int k = 0; k < j; k++) s = s - L[j][k] * L[j][k];
       L[j][j] = sqrt_(s);
 #pragma unroll
       for (int i = j + 1; i < 7; i++) {
-        T t = M[i][j];
+        T t = L[i][j];
 #pragma unroll
         for (int k = 0; k < j; k++) t = t - L[i][k] * L[j][k];
         L[i][j] = t / L[j][j];
