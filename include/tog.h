@@ -81,7 +81,20 @@ enum tog_constraint_type {
   TOG_CON_CIRCLES = 2,
   /* `count` sphere_constraint rows (src/utils.jl:150-156) on x[1..3]:
      c = -((x1-x0)^2 + (x2-y0)^2 + (x3-z0)^2 - r^2). data = [x0,y0,z0,r]*count. */
-  TOG_CON_SPHERES = 3
+  TOG_CON_SPHERES = 3,
+  /* infeasible_constraints(n, m), src/constraints.jl:306-314: the n slack controls of an
+     infeasible-start problem must vanish, c = u[m_model + i] (stage equality, n rows, no data).
+     Only valid in a TOG_PROB_INFEASIBLE problem. */
+  TOG_CON_INFEASIBLE = 4
+};
+
+/* problem flags (tog_problem_desc.flags) */
+enum tog_problem_flag {
+  /* infeasible_problem(prob, R_inf) (src/solvers/altro/infeasible.jl:2-33): the model is
+     add_slack_controls(model) (src/model.jl:761-779), x+ = f_d(x, u[1:m]) + u[m+1:m+n], so
+     desc.m = m_model + n and R, H, r, the bound data are given for the augmented controls
+     (R = blockdiag(R, R_inf I / dt), H and r zero-padded). */
+  TOG_PROB_INFEASIBLE = 1
 };
 
 typedef struct tog_constraint {
@@ -105,8 +118,8 @@ typedef struct tog_constraint_set {
 typedef struct tog_problem_desc {
   int32_t model;      /* tog_model_id                       */
   int32_t integrator; /* tog_integrator                     */
-  int32_t n, m, N;    /* must match the model's n, m        */
-  int32_t reserved0;
+  int32_t n, m, N;    /* must match the model's n, m (m + n with TOG_PROB_INFEASIBLE) */
+  int32_t flags;      /* tog_problem_flag bits (0 = plain problem) */
   int64_t batch;      /* B                                  */
   double dt;          /* prob.dt (tf > 0; min-time is out of scope) */
   /* stage QuadraticCost: 1/2 x'Qx + 1/2 u'Ru + q'x + r'u + c + u'Hx, times dt */
@@ -266,6 +279,12 @@ int32_t tog_backward_pass(tog_handle* h, int32_t sqrt, int32_t al, int32_t flags
 int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double* J_out);
 /* rollout!(prob, solver, α) (src/rollout.jl:2-23) for every trajectory; ok_out (B) int32 or NULL */
 int32_t tog_rollout(tog_handle* h, double alpha, int32_t* ok_out);
+
+/* slack_controls(prob) (src/solvers/altro/infeasible.jl:63-80) for a TOG_PROB_INFEASIBLE handle:
+   from x0, the state trajectory X and the model controls U[1:m], writes the slack controls
+   U[m+1:m+n] that make X dynamically feasible (x_{k+1} = f_d(x_k, u_k) + s_k). Device side, in
+   place; TOG_ERR_ARG on a plain handle. */
+int32_t tog_slack_controls(tog_handle* h);
 
 /* ---- solve level ---- */
 /* initialise the per-trajectory solve state machine (reset!, λ=0, μ=μ0, initial rollout, J) */

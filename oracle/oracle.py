@@ -46,6 +46,7 @@ def lib():
         L.oc_set.argtypes = [vp, C.c_int, dp]
         L.oc_pmax.argtypes = [vp]
         L.oc_rollout_open_loop.argtypes = [vp]
+        L.oc_slack_controls.argtypes = [vp]
         L.oc_rollout.argtypes = [vp, C.c_double]
         L.oc_jacobians.argtypes = [vp]
         L.oc_cost_expansion.argtypes = [vp, C.c_int, C.c_int]
@@ -167,6 +168,9 @@ class OracleSolver:
     def rollout(self, alpha):
         return bool(lib().oc_rollout(self.s, alpha))
 
+    def slack_controls(self):
+        lib().oc_slack_controls(self.s)
+
     def jacobians(self):
         lib().oc_jacobians(self.s)
 
@@ -212,3 +216,25 @@ def solve_batch(prob, opts, nthreads=1, B=None):
     U0 = np.ascontiguousarray(prob._U[:B])
     return int(lib().oc_solve_batch(C.byref(desc.desc), C.byref(o), abi.MODE_AL if al else abi.MODE_ILQR,
                                     _dp(x0), _dp(U0), B, nthreads))
+
+
+def solve_altro_infeasible(prob, opts, b=0):
+    """Oracle restatement of ``solve!(prob, ::ALTROSolverOptions)`` from a given X
+    (altro_methods.jl:2-124, infeasible.jl:2-99) for trajectory ``b``; returns (X, U, solver_inf,
+    solver_feasible or None). Mirrors ``solvers._solve_altro_infeasible`` step for step."""
+    m = prob.model.m
+    pinf = _pkg.infeasible_problem(prob, opts.R_inf)
+    si = OracleSolver(pinf, opts, b)
+    si.slack_controls()
+    si.solve()
+    X = si.get("X")
+    U = si.get("U")[:, :m].copy()
+    sf = None
+    if opts.resolve_feasible_problem:
+        p2 = prob.copy()
+        p2._X[b] = np.nan if opts.dynamically_feasible_projection else X
+        p2._U[b] = U
+        sf = OracleSolver(p2, opts.opts_al, b)
+        sf.solve()
+        X, U = sf.get("X"), sf.get("U")
+    return X, U, si, sf

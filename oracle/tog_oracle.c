@@ -31,7 +31,8 @@
 #include "../include/tog_math.h"
 #include "../include/tog_kuka.h"
 
-#define DMAX 24 /* max partials: n+m+1 */
+#define DMAX 24 /* max partials: n+m+1 of a model (slack columns are never dual) */
+#define OM 32   /* max controls, including the n slack controls of an infeasible problem */
 #define OC_EXPORT __attribute__((visibility("default")))
 
 /* =====================================================================
@@ -595,7 +596,7 @@ OC_EXPORT void oc_discrete_f(int model, int integ, double* xn, const double* x, 
   int n = model_n[model], m = model_m[model];
   int save = g_nd;
   g_nd = 0;
-  dual X[16], U[8], XN[16];
+  dual X[16], U[OM], XN[16];
   for (int i = 0; i < n; i++) X[i].v = x[i];
   for (int i = 0; i < m; i++) U[i].v = u[i];
   dual DT;
@@ -609,7 +610,7 @@ OC_EXPORT void oc_discrete_f(int model, int integ, double* xn, const double* x, 
 OC_EXPORT void oc_continuous_f(int model, double* xd, const double* x, const double* u) {
   int n = model_n[model], m = model_m[model];
   g_nd = 0;
-  dual X[16], U[8], XD[16];
+  dual X[16], U[OM], XD[16];
   for (int i = 0; i < n; i++) X[i].v = x[i];
   for (int i = 0; i < m; i++) U[i].v = u[i];
   model_f(model, XD, X, U);
@@ -622,7 +623,7 @@ OC_EXPORT void oc_discrete_jacobian(int model, int integ, double* S, const doubl
   int n = model_n[model], m = model_m[model];
   int L = n + m + 1;
   g_nd = L;
-  dual X[16], U[8], XN[16], DT;
+  dual X[16], U[OM], XN[16], DT;
   for (int i = 0; i < n; i++) {
     X[i] = dc(x[i]);
     X[i].p[i] = 1.0;
@@ -827,7 +828,7 @@ static void lu_solve(const double* Ain, int n, double* B, int nrhs) {
 
 /* singular values of a small n x n matrix by one-sided Jacobi; returns cond = smax/smin (cond(A)) */
 static double cond2(const double* Ain, int n) {
-  double A[64], V[64];
+  double A[OM * OM], V[OM * OM];
   memcpy(A, Ain, sizeof(double) * n * n);
   for (int sweep = 0; sweep < 60; sweep++) {
     double off = 0.0;
@@ -877,7 +878,7 @@ OC_EXPORT void oc_qr_R(double* R, double* P, int rows, int cols) { qr_R(R, P, ro
    lowrankdowndate!(C, B[i,:]) per row (Julia 1.1 LinearAlgebra cholesky.jl). Returns 0 or
    PosDefException index. */
 static int chol_minus(double* Uo, const double* A, int n, const double* B, int nb) {
-  double U[64], v[8];
+  double U[OM * OM], v[OM];
   memcpy(U, A, sizeof(double) * n * n);
   for (int r = 0; r < nb; r++) {
     for (int j = 0; j < n; j++) v[j] = B[IDX(r, j, nb)];
@@ -907,8 +908,8 @@ typedef struct {
   int inequality;
   int p_stage, p_term;
   /* bound */
-  double x_max[16], x_min[16], u_max[8], u_min[8];
-  int ax_max[16], ax_min[16], au_max[8], au_min[8];
+  double x_max[16], x_min[16], u_max[OM], u_min[OM];
+  int ax_max[16], ax_min[16], au_max[OM], au_min[OM];
   /* goal */
   double xf[16];
   /* obstacles */
@@ -924,6 +925,7 @@ typedef struct {
 
 typedef struct oc_solver {
   int model, integ, n, m, N;
+  int slack, mb; /* infeasible problem: slack = n slack controls after the mb model controls */
   double dt;
   double *Q, *R, *H, *q, *r, c, *Qf, *qf, cf;
   int nsets;
@@ -998,6 +1000,11 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
       oc->inequality = 1;
       oc->p_stage = tc->count;
       oc->p_term = 0;
+      break;
+    case TOG_CON_INFEASIBLE: /* infeasible_constraints(n, m) src/constraints.jl:306-314 */
+      oc->inequality = 0;
+      oc->p_stage = n;
+      oc->p_term = 0; /* :stage only */
       break;
   }
 }
@@ -1074,6 +1081,17 @@ static int con_eval(const oc_con* oc, int n, int m, const double* x, const doubl
         }
       }
       break;
+    case TOG_CON_INFEASIBLE:
+      /* inf_con(v, x, u) = copyto!(v, u[m+1:m+n]); ∇inf = [0 0 I] (src/constraints.jl:306-314) */
+      if (!term) {
+        int mb = m - n;
+        for (int i = 0; i < n; i++) {
+          v[r] = u[mb + i];
+          if (Ju) Ju[r + ldj * (mb + i)] = 1.0;
+          r++;
+        }
+      }
+      break;
     case TOG_CON_SPHERES:
       if (!term) {
         for (int o = 0; o < oc->count; o++) {
@@ -1124,6 +1142,8 @@ static void desc_load(oc_solver* s, const tog_problem_desc* d) {
   s->m = d->m;
   s->N = d->N;
   s->dt = d->dt;
+  s->slack = (d->flags & TOG_PROB_INFEASIBLE) ? d->n : 0;
+  s->mb = d->m - s->slack;
   int n = s->n, m = s->m, N = s->N;
   s->Q = malloc(sizeof(double) * n * n);
   memcpy(s->Q, d->Q, sizeof(double) * n * n);
@@ -1194,7 +1214,7 @@ OC_EXPORT oc_solver* oc_create(const tog_problem_desc* d, const tog_options* o) 
   s->ineq = calloc((size_t)P * N, sizeof(int));
   for (int k = 0; k < N; k++) {
     double cbuf[256];
-    double xz[16] = {0}, uz[8] = {0};
+    double xz[16] = {0}, uz[OM] = {0};
     set_eval(s, k, xz, k < N - 1 ? uz : NULL, cbuf, NULL, NULL, s->ineq + (size_t)k * P);
   }
   s->trace = calloc(6 * 4096, sizeof(double));
@@ -1320,6 +1340,47 @@ OC_EXPORT double oc_cost_bar(oc_solver* s, int al) { return cost(s, al, s->Xb, s
 /* =====================================================================
  * Rollouts (src/rollout.jl)
  * ===================================================================== */
+/* evaluate!(x+, model, x, u, dt) of the solver's model. For an infeasible problem this is
+   add_slack_controls (src/model.jl:761-779): f!(x+, x, u[1:m], dt) then x+ .+= u[m+1:m+n]. */
+static void traj_f(const oc_solver* s, double* xn, const double* x, const double* u) {
+  oc_discrete_f(s->model, s->integ, xn, x, u, s->dt);
+  for (int i = 0; i < s->slack; i++) xn[i] += u[s->mb + i];
+}
+
+/* ∇f!(Z, x, u, dt) of the solver's model into F (n x (n+m+1)): the model's jacobian in
+   columns [x; u[1:m]] and dt, and Diagonal(1.0I, n) in the slack columns (src/model.jl:771-774). */
+static void traj_jacobian(const oc_solver* s, double* F, const double* x, const double* u) {
+  int n = s->n, mb = s->mb, m = s->m;
+  if (!s->slack) {
+    oc_discrete_jacobian(s->model, s->integ, F, x, u, s->dt);
+    return;
+  }
+  double Z[16 * (16 + OM + 1)];
+  oc_discrete_jacobian(s->model, s->integ, Z, x, u, s->dt); /* n x (n+mb+1) */
+  memcpy(F, Z, sizeof(double) * n * (n + mb));
+  for (int j = 0; j < n; j++)
+    for (int i = 0; i < n; i++) F[i + n * (n + mb + j)] = (i == j) ? 1.0 : 0.0;
+  memcpy(F + (size_t)n * (n + m), Z + (size_t)n * (n + mb), sizeof(double) * n);
+}
+
+/* slack_controls(prob) (src/solvers/altro/infeasible.jl:63-80), run on the original model
+   with x[k+1] = f(x[k], U[k]); s_k = X[k+1] - x[k+1]; x[k+1] += s_k. Writes U[m+1:m+n]. */
+OC_EXPORT void oc_slack_controls(oc_solver* s) {
+  int n = s->n, m = s->m, N = s->N;
+  if (!s->slack) return;
+  double x[16], xn[16];
+  memcpy(x, s->x0, sizeof(double) * n);
+  for (int k = 0; k < N - 1; k++) {
+    double* u = s->U + (size_t)k * m;
+    oc_discrete_f(s->model, s->integ, xn, x, u, s->dt);
+    const double* Xn = s->X + (size_t)(k + 1) * n;
+    for (int i = 0; i < n; i++) {
+      u[s->mb + i] = Xn[i] - xn[i];
+      x[i] = xn[i] + u[s->mb + i];
+    }
+  }
+}
+
 /* rollout!(prob) src/rollout.jl:25-38: open loop only if any X non-finite */
 OC_EXPORT void oc_rollout_open_loop(oc_solver* s) {
   int n = s->n, m = s->m, N = s->N;
@@ -1329,7 +1390,7 @@ OC_EXPORT void oc_rollout_open_loop(oc_solver* s) {
   if (finite) return;
   memcpy(s->X, s->x0, sizeof(double) * n);
   for (int k = 0; k < N - 1; k++)
-    oc_discrete_f(s->model, s->integ, s->X + (size_t)(k + 1) * n, s->X + (size_t)k * n, s->U + (size_t)k * m, s->dt);
+    traj_f(s, s->X + (size_t)(k + 1) * n, s->X + (size_t)k * n, s->U + (size_t)k * m);
 }
 
 /* rollout!(prob, solver, alpha) src/rollout.jl:2-23 */
@@ -1350,7 +1411,7 @@ OC_EXPORT int oc_rollout(oc_solver* s, double alpha) {
       for (int j = 0; j < n; j++) t = fma(Kk[IDX(i, j, m)], dx[j], t);
       ub[i] = (s->U[(size_t)(k - 1) * m + i] + t) + alpha * dk[i];
     }
-    oc_discrete_f(s->model, s->integ, s->Xb + (size_t)k * n, xb, ub, s->dt);
+    traj_f(s, s->Xb + (size_t)k * n, xb, ub);
     double nx = 0, nu = 0;
     int bad = 0;
     for (int i = 0; i < n; i++) {
@@ -1374,7 +1435,7 @@ OC_EXPORT int oc_rollout(oc_solver* s, double alpha) {
 OC_EXPORT void oc_jacobians(oc_solver* s) {
   int n = s->n, m = s->m, N = s->N, L = n + m + 1;
   for (int k = 0; k < N - 1; k++)
-    oc_discrete_jacobian(s->model, s->integ, s->F + (size_t)k * n * L, Xk(s, k), Uk(s, k), s->dt);
+    traj_jacobian(s, s->F + (size_t)k * n * L, Xk(s, k), Uk(s, k));
 }
 
 /* =====================================================================
@@ -1422,7 +1483,7 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
   for (int k = 0; k < N - 1; k++) {
     expansion_stage(s, k);
     if (sq) { /* objective.jl:70-86 */
-      double U[256];
+      double U[OM * OM];
       if (chol_upper(U, s->Qxx + (size_t)k * n * n, n)) return -1;
       memcpy(s->Qxx + (size_t)k * n * n, U, sizeof(double) * n * n);
       if (chol_upper(U, s->Quu + (size_t)k * m * m, m)) return -1;
@@ -1431,13 +1492,13 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
   }
   expansion_terminal(s);
   if (sq) {
-    double U[256];
+    double U[OM * OM];
     if (chol_upper(U, s->Qxx + (size_t)(N - 1) * n * n, n)) return -1;
     memcpy(s->Qxx + (size_t)(N - 1) * n * n, U, sizeof(double) * n * n);
   }
   if (!al) return 0;
   /* AL terms */
-  double cx[64 * 16], cu[64 * 8], cval[64];
+  double cx[64 * 16], cu[64 * OM], cval[64];
   for (int k = 0; k < N; k++) {
     int p = s->p[k];
     if (p == 0) continue;
@@ -1483,7 +1544,7 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
       }
     } else {
       /* chol_plus!(Q.xx, Iμ_sqrt*cx) ; chol_plus!(Q.uu, Iμ_sqrt*cu)  (no ux term, A.5) */
-      double M[64 * 16], R[256];
+      double M[64 * OM], R[OM * OM];
       for (int j = 0; j < n; j++)
         for (int r = 0; r < p; r++) M[r + p * j] = ws[r] * cx[r + p * j];
       chol_plus(R, Qxx, n, M, p, n);
@@ -1540,7 +1601,7 @@ static void backward_std(oc_solver* s) {
   memcpy(Sx + (size_t)(N - 1) * n, s->Qx + (size_t)(N - 1) * n, sizeof(double) * n);
   s->dV[0] = s->dV[1] = 0.0;
   s->bp_restarts = 0;
-  double AtS[256], T[256], Quu_reg[64], Qux_reg[128], Kk[128], dk[8], tmp[256];
+  double AtS[256], T[OM * OM], Quu_reg[OM * OM], Qux_reg[OM * 16], Kk[OM * 16], dk[OM], tmp[OM * OM];
   int k = N - 2;
   while (k >= 0) {
     const double* Fk = s->F + (size_t)k * n * L;
@@ -1563,7 +1624,7 @@ static void backward_std(oc_solver* s) {
     matmul(T, AtS, n, n, A, n);
     for (int i = 0; i < n * n; i++) Qxx[i] += T[i];
     /* Q[k].uu .+= fdu'*S*fdu */
-    double BtS[128];
+    double BtS[OM * 16];
     matTmul(BtS, B, n, m, S1, n);
     matmul(T, BtS, m, n, B, m);
     for (int i = 0; i < m * m; i++) Quu[i] += T[i];
@@ -1572,7 +1633,7 @@ static void backward_std(oc_solver* s) {
     for (int i = 0; i < m * n; i++) Qux[i] += T[i];
 
     if (s->opts.bp_reg_type == 1) { /* :state */
-      double BtB[64], BtA[128];
+      double BtB[OM * OM], BtA[OM * 16];
       matTmul(BtB, B, n, m, B, m);
       matTmul(BtA, B, n, m, A, n);
       for (int i = 0; i < m * m; i++) Quu_reg[i] = Quu[i] + s->rho * BtB[i];
@@ -1601,7 +1662,7 @@ static void backward_std(oc_solver* s) {
     memcpy(s->K + (size_t)k * m * n, Kk, sizeof(double) * m * n);
     memcpy(s->d + (size_t)k * m, dk, sizeof(double) * m);
     /* S[k].x = Q.x + K'*Q.uu*d + K'*Q.u + Q.ux'*d */
-    double KtQuu[128];
+    double KtQuu[OM * 16];
     matTmul(KtQuu, Kk, m, n, Quu, m); /* n x m */
     double* Sk = Sxx + (size_t)k * n * n;
     double* sk = Sx + (size_t)k * n;
@@ -1649,7 +1710,7 @@ static void backward_sqrt(oc_solver* s) {
   memcpy(Sx + (size_t)(N - 1) * n, s->Qx + (size_t)(N - 1) * n, sizeof(double) * n);
   s->dV[0] = s->dV[1] = 0.0;
   s->bp_restarts = 0;
-  double tmp_x[256], tmp_u[128], R[256], Quu_reg[64], Qux_reg[128], Kk[128], dk[8], t[256];
+  double tmp_x[256], tmp_u[OM * 16], R[OM * OM], Quu_reg[OM * OM], Qux_reg[OM * 16], Kk[OM * 16], dk[OM], t[OM * OM];
   int k = N - 2;
   while (k >= 0) {
     const double* Fk = s->F + (size_t)k * n * L;
@@ -1676,13 +1737,13 @@ static void backward_sqrt(oc_solver* s) {
     for (int i = 0; i < m * n; i++) Qux[i] += t[i];
 
     if (s->opts.bp_reg_type == 1) { /* :state: chol_plus(Q.uu, sqrt(ρ)*fdu) */
-      double Bs[128], BtA[128];
+      double Bs[OM * 16], BtA[OM * 16];
       for (int i = 0; i < n * m; i++) Bs[i] = sqrt(s->rho) * B[i];
       chol_plus(Quu_reg, Quu, m, Bs, n, m);
       matTmul(BtA, B, n, m, A, n);
       for (int i = 0; i < m * n; i++) Qux_reg[i] = Qux[i] + s->rho * BtA[i];
     } else {
-      double D[64];
+      double D[OM * OM];
       memset(D, 0, sizeof(D));
       for (int i = 0; i < m; i++) D[i + m * i] = sqrt(s->rho);
       chol_plus(Quu_reg, Quu, m, D, m, m);
@@ -1698,7 +1759,7 @@ static void backward_sqrt(oc_solver* s) {
       continue;
     }
     /* K = -Quu_reg\(Quu_reg'\Qux_reg) ; d = -Quu_reg\(Quu_reg'\Q.u) */
-    double RT[64];
+    double RT[OM * OM];
     for (int j = 0; j < m; j++)
       for (int i = 0; i < m; i++) RT[IDX(i, j, m)] = Quu_reg[IDX(j, i, m)];
     memcpy(Kk, Qux_reg, sizeof(double) * m * n);
@@ -1714,7 +1775,7 @@ static void backward_sqrt(oc_solver* s) {
     /* S[k].x = Q.x + (K'*Q.uu')*(Q.uu*d) + K'*Q.u + Q.ux'*d */
     double* sk = Sx + (size_t)k * n;
     {
-      double KtUt[128], Ud[8], a[16], b[16], c[16];
+      double KtUt[OM * 16], Ud[OM], a[16], b[16], c[16];
       for (int j = 0; j < m; j++) /* K'*Quu' : n x m, (K'Quu')[i,j] = Σ_l K[l,i] Quu[j,l] */
         for (int i = 0; i < n; i++) {
           double acc = 0;
@@ -1728,7 +1789,7 @@ static void backward_sqrt(oc_solver* s) {
       for (int i = 0; i < n; i++) sk[i] = ((Qx[i] + a[i]) + b[i]) + c[i];
     }
     /* tmp1 = (Q.xx')\Q.ux'  (n x m) */
-    double tmp1[128], QxxT[256];
+    double tmp1[OM * 16], QxxT[256];
     for (int j = 0; j < n; j++)
       for (int i = 0; i < n; i++) QxxT[IDX(i, j, n)] = Qxx[IDX(j, i, n)];
     int singular = 0;
@@ -1739,14 +1800,14 @@ static void backward_sqrt(oc_solver* s) {
     if (singular) s->flags |= TOG_TRAJ_SINGULAR;
     lu_solve(QxxT, n, tmp1, m);
     /* tmp2 = chol_minus(Q.uu, tmp1) */
-    double tmp2[64];
+    double tmp2[OM * OM];
     if (chol_minus(tmp2, Quu, m, tmp1, n)) {
       s->flags |= TOG_TRAJ_SQRT_PD_FAIL;
       memcpy(tmp2, Quu, sizeof(double) * m * m); /* the reference throws here */
     }
     /* S[k].xx = chol_plus(Q.xx + tmp1*K, tmp2*K) */
     {
-      double top[256], bot[128];
+      double top[256], bot[OM * 16];
       matmul(top, tmp1, n, m, Kk, n);
       for (int i = 0; i < n * n; i++) top[i] = Qxx[i] + top[i];
       matmul(bot, tmp2, m, m, Kk, n);
@@ -1754,7 +1815,7 @@ static void backward_sqrt(oc_solver* s) {
     }
     /* ΔV */
     {
-      double a = 0.0, Ud[8], b = 0.0;
+      double a = 0.0, Ud[OM], b = 0.0;
       for (int i = 0; i < m; i++) a = fma(dk[i], Qu[i], a);
       matmul(Ud, Quu, m, m, dk, 1);
       for (int i = 0; i < m; i++) b = fma(Ud[i], Ud[i], b);

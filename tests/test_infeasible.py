@@ -1,0 +1,266 @@
+"""Infeasible start: ``infeasible_problem`` + slack controls + the ALTRO
+infeasible-start flow (src/solvers/altro/infeasible.jl:2-99, altro_methods.jl:2-124,
+src/model.jl:761-779, src/constraints.jl:306-314).
+
+CPU tests pin the oracle on the reference's own assertions (test/infeasible_tests.jl,
+test/constraint_tests.jl:189-194); the ``gpu`` tests hold libtog.so (Infeasible<M> kernels, through
+the C ABI) bit-for-bit to the oracle, and solves to the north-star 1e-6 with equal iteration counts.
+"""
+import numpy as np
+import pytest
+
+TOL_SOLVE = 1e-6
+TOL_STEP = 1e-13
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=float)
+    b = np.asarray(b, dtype=float)
+    scale = max(1.0, float(np.max(np.abs(b)))) if b.size else 1.0
+    return float(np.max(np.abs(a - b))) / scale if b.size else 0.0
+
+
+def pendulum_opts(tog, resolve):
+    """test/infeasible_tests.jl:11-19."""
+    opts_ilqr = tog.iLQRSolverOptions()
+    opts_al = tog.AugmentedLagrangianSolverOptions(constraint_tolerance=1e-5, cost_tolerance=1e-5,
+                                                   cost_tolerance_intermediate=1e-5, opts_uncon=opts_ilqr,
+                                                   iterations=30, penalty_scaling=10.0)
+    return tog.ALTROSolverOptions(opts_al=opts_al, R_inf=1.0, resolve_feasible_problem=resolve)
+
+
+def pendulum_line(tog, constrained_variant=False):
+    """test/infeasible_tests.jl:21-45: Problems.pendulum with X0 = line_trajectory(x0, xf, N)."""
+    prob = tog.Problems.pendulum()
+    if constrained_variant:  # Constraints([bnd], N); constraints[N] += goal
+        n, m, N = 2, 1, prob.N
+        bnd = tog.BoundConstraint(n, m, u_min=-3.0, u_max=3.0)
+        cons = tog.Constraints([bnd], N)
+        cons[N - 1] = cons[N - 1] + tog.goal_constraint(prob.xf)
+        prob = tog.Problem(prob.model, prob.obj, prob.U, constraints=cons, x0=prob.x0[0], xf=prob.xf, N=N,
+                           dt=prob.dt)
+    prob.X = tog.line_trajectory(prob.x0[0], prob.xf, prob.N)
+    return prob
+
+
+def quad_line_batch(tog, B=3, N=31, seed=7):
+    """Quadrotor (test/quadrotor_tests.jl:4-35 model and costs, u in [0, 15] + goal), N shortened,
+    batched random starts with a straight-line state guess per trajectory (the quadrotor_maze
+    initial-guess path, problems/quadrotor_maze.jl:107-114, with line_trajectory)."""
+    p0 = tog.Problems.quadrotor_test("goal+bounds")
+    n, m = 13, 4
+    rng = np.random.default_rng(seed)
+    x0 = np.tile(p0.x0[0], (B, 1))
+    x0[:, 0:3] += rng.standard_normal((B, 3))
+    U0 = 0.5 * 9.81 / 4 + 0.1 * rng.standard_normal((B, N - 1, m))
+    xf = p0.xf
+    cons = tog.Constraints(N)
+    bnd = tog.BoundConstraint(n, m, u_min=0.0, u_max=15.0)
+    for k in range(N - 1):
+        cons[k] += bnd
+    cons[N - 1] += tog.goal_constraint(xf)
+    obj = tog.LQRObjective(p0.obj.stage.Q, p0.obj.stage.R, p0.obj.terminal.Q, xf, N)
+    prob = tog.Problem(p0.model, obj, U0, x0=x0, xf=xf, N=N, dt=0.05, constraints=cons)
+    prob.X = np.stack([tog.line_trajectory(x0[b], xf, N) for b in range(B)])
+    return prob
+
+
+# ----------------------------------------------------------------------------- CPU: host + oracle
+
+
+def test_infeasible_constraint_kat(tog):
+    """test/constraint_tests.jl:189-194: con_inf.c(v, x, u_inf[inds[2]]) == [5, -5, 10]."""
+    n, m = 3, 2
+    con = tog.infeasible_constraints(n, m)
+    u_inf = np.concatenate([[0.3, -0.7], [5.0, -5.0, 10.0]])
+    assert np.array_equal(con.evaluate(np.zeros(n), u_inf), [5.0, -5.0, 10.0])
+    assert con.length("stage") == n and con.length("terminal") == 0 and not con.inequality
+    J = con.jacobian(np.zeros(n), u_inf)
+    assert J.shape == (n, 2 * n + m) and np.array_equal(J[:, n + m:], np.eye(n)) and not J[:, :n + m].any()
+    # C_inf = [..., bnd, con_inf]: the stage vector is the plain one followed by the slacks (:196-202)
+    bnd = tog.BoundConstraint(n, m, u_min=-1.0, u_max=1.0, x_max=2.0)
+    x = np.array([0.5, 3.0, -1.0])
+    v_stage = bnd.evaluate(x, u_inf[:m])
+    v_inf = np.concatenate([bnd.evaluate(x, u_inf), con.evaluate(x, u_inf)])
+    assert np.array_equal(v_inf, np.concatenate([v_stage, [5.0, -5.0, 10.0]]))
+
+
+def test_infeasible_problem_structure(tog):
+    """infeasible_problem (infeasible.jl:2-33): augmented R, zero-padded H/r, bounds moved after the
+    other constraints (update_constraint_set_jacobians, constraint_sets.jl:135-150), slack
+    equality appended at the stage knots only, controls [U; 0]."""
+    prob = tog.Problems.quad_obs(N=21)
+    n, m, N = 13, 4, prob.N
+    prob.X = np.zeros((N, n))
+    pinf = tog.infeasible_problem(prob, 0.5)
+    assert pinf.model.m == m + n and pinf.model.slack == n and pinf.model.model_id == prob.model.model_id
+    R = pinf.obj.stage.R
+    assert np.array_equal(R[:m, :m], prob.obj.stage.R)
+    assert np.array_equal(R[m:, m:], 0.5 * np.eye(n) / prob.dt) and not R[:m, m:].any()
+    assert pinf.obj.stage.H.shape == (m + n, n) and not pinf.obj.stage.H[m:].any()
+    for k in range(N - 1):
+        kinds = [type(c).__name__ for c in pinf.constraints[k]]
+        assert kinds[-1] == "InfeasibleConstraint"
+        nb = [i for i, t in enumerate(kinds) if t == "BoundConstraint"]
+        assert all(i > j for i in nb for j, t in enumerate(kinds[:-1]) if t != "BoundConstraint")
+    assert all(type(c).__name__ != "InfeasibleConstraint" for c in pinf.constraints[N - 1])
+    assert np.array_equal(pinf.U[:, :m], prob.U) and not pinf.U[:, m:].any()
+    d = pinf.build_desc().desc
+    assert d.flags == tog.abi.PROB_INFEASIBLE and d.m == m + n
+
+
+def test_line_trajectory(tog):
+    """line_trajectory (infeasible.jl:82-90): t = range(0, N, length=N), slope (xf-x0)/N."""
+    X = tog.line_trajectory([0.0, 0.0], [np.pi, 0.0], 31)
+    assert X.shape == (31, 2) and np.array_equal(X[0], [0, 0]) and np.array_equal(X[-1], [np.pi, 0])
+    t = np.linspace(0, 31, 31)
+    assert np.allclose(X[1:-1, 0], (np.pi / 31) * t[1:-1], rtol=0, atol=1e-15)
+
+
+def test_oracle_slack_controls_and_jacobian(tog, oracle):
+    """slack_controls (infeasible.jl:63-80) and the slack model (src/model.jl:761-779) in the oracle
+    against a numpy restatement over the oracle's plain model."""
+    prob = pendulum_line(tog)
+    pinf = tog.infeasible_problem(prob, 1.0)
+    o = oracle.OracleSolver(pinf, pendulum_opts(tog, False))
+    o.slack_controls()
+    U = o.get("U")
+    X = prob.X
+    x = prob.x0[0].copy()
+    for k in range(prob.N - 1):
+        xn = oracle.discrete_f(tog.abi.MODEL_PENDULUM, tog.abi.RK3, x, prob.U[k], prob.dt)
+        s = X[k + 1] - xn
+        assert np.array_equal(U[k, 1:], s), k
+        assert np.array_equal(U[k, :1], prob.U[k])
+        x = xn + s
+    # the open-loop rollout of the slack model reproduces X (to rounding of x + (X - x))
+    o.set("X", np.full((prob.N, 2), np.nan))
+    o.rollout_open_loop()
+    assert np.allclose(o.get("X"), X, rtol=0, atol=1e-14)
+    o.jacobians()
+    A, Bm = o.get("A"), o.get("B")
+    for k in range(prob.N - 1):
+        S = oracle.discrete_jacobian(tog.abi.MODEL_PENDULUM, tog.abi.RK3, o.get("X")[k], U[k, :1], prob.dt)
+        assert np.array_equal(A[k], S[:, :2])
+        assert np.array_equal(Bm[k][:, :1], S[:, 2:3])
+        assert np.array_equal(Bm[k][:, 1:], np.eye(2))
+
+
+@pytest.mark.parametrize("variant", [False, True])
+def test_reference_infeasible_pendulum_oracle(tog, oracle, variant):
+    """test/infeasible_tests.jl:23-55 on the oracle: ‖X_N − xf‖ < 1e-3 (first case),
+    max_violation < constraint_tolerance (second), resolve ≈ no resolve to 1e-5."""
+    Xend = {}
+    for resolve in (False, True):
+        prob = pendulum_line(tog, variant)
+        opts = pendulum_opts(tog, resolve)
+        X, U, si, sf = oracle.solve_altro_infeasible(prob, opts)
+        Xend[resolve] = X[-1]
+        if not variant:
+            assert np.linalg.norm(X[-1] - prob.xf) < 1e-3
+        else:
+            p = prob.copy()
+            p.X, p.U = X, U
+            assert tog.max_violation(p) < opts.opts_al.constraint_tolerance
+    assert np.linalg.norm(Xend[False] - Xend[True]) < 1e-5
+
+
+# ----------------------------------------------------------------------------- GPU parity
+
+
+@pytest.mark.gpu
+def test_gpu_slack_controls_and_rollout(tog, oracle, gpu):
+    """tog_slack_controls + Infeasible<Quadrotor> rollout / Jacobians vs the oracle, bitwise."""
+    prob = quad_line_batch(tog, B=4, N=21)
+    pinf = tog.infeasible_problem(prob, 1.0)
+    opts = tog.ALTROSolverOptions()
+    solver = tog.ALTROSolver(pinf, opts)
+    h = solver.handle
+    h.slack_controls()
+    U = h.get(tog.abi.FIELD_U)
+    for b in range(prob.B):
+        o = oracle.OracleSolver(pinf, opts, b)
+        o.slack_controls()
+        assert rel(U[b], o.get("U")) == 0.0, b
+    pinf._U[...] = U
+    pinf._X[...] = np.nan
+    h.upload_state(pinf)
+    h.rollout_open_loop()
+    h.jacobians()
+    X, A, Bm = h.get(tog.abi.FIELD_X), h.get(tog.abi.FIELD_A), h.get(tog.abi.FIELD_B)
+    for b in range(prob.B):
+        o = oracle.OracleSolver(pinf, opts, b)
+        o.rollout_open_loop()
+        o.jacobians()
+        assert rel(X[b], o.get("X")) < TOL_STEP, b
+        assert rel(A[b], o.get("A")) < TOL_STEP, b
+        assert rel(Bm[b], o.get("B")) < TOL_STEP, b
+        assert np.array_equal(Bm[b][:, :, 4:], np.broadcast_to(np.eye(13), (20, 13, 13)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sqrt", [False, True])
+def test_gpu_infeasible_backward_pass(tog, oracle, gpu, sqrt):
+    """cost_expansion! + backwardpass! of the infeasible quadrotor under AL (slack equality rows,
+    m = 17: the LDS backward kernel) vs the oracle."""
+    prob = quad_line_batch(tog, B=3, N=21, seed=3)
+    pinf = tog.infeasible_problem(prob, 1.0)
+    il = tog.iLQRSolverOptions(square_root=sqrt)
+    opts = tog.AugmentedLagrangianSolverOptions(opts_uncon=il)
+    solver = tog.AugmentedLagrangianSolver(pinf, opts)
+    h = solver.handle
+    h.slack_controls()
+    h.update_constraints()
+    h.jacobians()
+    dV = h.backward_pass(sqrt=sqrt, al=True)
+    K, d = h.get(tog.abi.FIELD_K), h.get(tog.abi.FIELD_D)
+    U = h.get(tog.abi.FIELD_U)
+    for b in range(prob.B):
+        p = pinf.copy()
+        p._U[b] = U[b]
+        o = oracle.OracleSolver(p, opts, b)
+        o.update_constraints()
+        o.jacobians()
+        assert o.cost_expansion(sqrt, True) == 0
+        dVo, _ = o.backward(sqrt)
+        assert rel(K[b], o.get("K")) < TOL_STEP, b
+        assert rel(d[b], o.get("d")) < TOL_STEP, b
+        assert rel(dV[b], dVo) < TOL_STEP, b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [False, True])
+def test_gpu_reference_infeasible_pendulum(tog, oracle, gpu, variant):
+    """test/infeasible_tests.jl through solve_b(prob, ALTROSolverOptions) on the device: the
+    reference's thresholds, and the same X, U and iteration counts as the oracle."""
+    Xend = {}
+    for resolve in (False, True):
+        prob = pendulum_line(tog, variant)
+        opts = pendulum_opts(tog, resolve)
+        ref = prob.copy()
+        solver = tog.solve_b(prob, opts)
+        Xo, Uo, si, sf = oracle.solve_altro_infeasible(ref, opts)
+        assert rel(prob.X, Xo) < TOL_SOLVE and rel(prob.U, Uo) < TOL_SOLVE
+        assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+        Xend[resolve] = prob.X[-1]
+        if not variant:
+            assert np.linalg.norm(prob.X[-1] - prob.xf) < 1e-3
+        else:
+            assert tog.max_violation(prob) < opts.opts_al.constraint_tolerance
+    assert np.linalg.norm(Xend[False] - Xend[True]) < 1e-5
+
+
+@pytest.mark.gpu
+def test_gpu_infeasible_quadrotor_batch(tog, oracle, gpu):
+    """A batch of infeasible-start quadrotor solves (resolve + projection) vs the oracle per
+    trajectory: final X, U within 1e-6 and equal iteration counts in both phases."""
+    prob = quad_line_batch(tog, B=3, N=31, seed=11)
+    opts = tog.ALTROSolverOptions()
+    ref = prob.copy()
+    solver = tog.solve_b(prob, opts)
+    for b in range(prob.B):
+        Xo, Uo, si, sf = oracle.solve_altro_infeasible(ref, opts, b)
+        assert rel(prob._X[b], Xo) < TOL_SOLVE, b
+        assert rel(prob._U[b], Uo) < TOL_SOLVE, b
+        assert int(solver.stats["iterations_total"][b]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS]), b
+        assert int(solver.stats_feasible["iterations_total"][b]) == int(sf.get("stats")[tog.abi.STAT_TOTAL_STEPS]), b

@@ -25,7 +25,8 @@ MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1), 5: (14, 7)}
 OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 
 RK3, RK4 = 0, 1
-CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES = range(4)
+CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE = range(5)
+PROB_INFEASIBLE = 1  # tog_problem_flag
 MODE_ILQR, MODE_AL = 0, 1
 
 (FIELD_X, FIELD_U, FIELD_XBAR, FIELD_UBAR, FIELD_K, FIELD_D, FIELD_A, FIELD_B, FIELD_S, FIELD_SX,
@@ -63,7 +64,7 @@ class tog_constraint_set(C.Structure):
 class tog_problem_desc(C.Structure):
     _fields_ = [
         ("model", C.c_int32), ("integrator", C.c_int32), ("n", C.c_int32), ("m", C.c_int32),
-        ("N", C.c_int32), ("reserved0", C.c_int32), ("batch", C.c_int64), ("dt", C.c_double),
+        ("N", C.c_int32), ("flags", C.c_int32), ("batch", C.c_int64), ("dt", C.c_double),
         ("Q", _dp), ("R", _dp), ("H", _dp), ("q", _dp), ("r", _dp), ("c", C.c_double),
         ("Qf", _dp), ("qf", _dp), ("cf", C.c_double),
         ("n_sets", C.c_int32), ("reserved1", C.c_int32),
@@ -136,7 +137,7 @@ class DescBuilder:
     """
 
     def __init__(self, model, integrator, n, m, N, dt, Q, R, H, q, r, c, Qf, qf, cf, sets, knot_set,
-                 batch=1):
+                 batch=1, flags=0):
         self._keep = []
 
         def arr(x, shape):
@@ -147,6 +148,7 @@ class DescBuilder:
         d = tog_problem_desc()
         d.model, d.integrator, d.n, d.m, d.N = int(model), int(integrator), int(n), int(m), int(N)
         d.batch = int(batch)
+        d.flags = int(flags)
         d.dt = float(dt)
         d.Q = as_dp(arr(Q, (n, n)))
         d.R = as_dp(arr(R, (m, m)))
@@ -224,12 +226,13 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_profile_read.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     lib.tog_last_error.restype = C.c_char_p
     lib.tog_dynamics_bias.argtypes = [C.c_int32, _dp, _dp]
+    lib.tog_slack_controls.argtypes = [vp]
     for name in ("tog_create", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
                  "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
-                 "tog_profile_read", "tog_dynamics_bias"):
+                 "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -244,7 +247,7 @@ EXPORTED_SYMBOLS = (
     "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
     "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
-    "tog_last_error", "tog_dynamics_bias",
+    "tog_last_error", "tog_dynamics_bias", "tog_slack_controls",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
 NKERNELS = 3

@@ -17,7 +17,7 @@
 namespace tog {
 
 constexpr int NMAX = 16;  // max states (Kuka n=14)
-constexpr int MMAX = 8;   // max controls
+constexpr int MMAX = 32;  // max controls (an infeasible problem adds n slack controls)
 
 // ---------------------------------------------------------------------------------------------
 // Constraint rows. A ConstraintSet (src/constraint_sets.jl) is flattened on the host into rows in
@@ -30,7 +30,8 @@ enum RowType : int {
   ROW_UMIN = 3,  // c = a - u[i]
   ROW_GOAL = 4,  // c = x[i] - a            (equality, goal_constraint src/constraints.jl:299-304)
   ROW_CIRCLE = 5,  // c = -((x1-a)^2 + (x2-b)^2 - r^2)            src/utils.jl:140-144
-  ROW_SPHERE = 6   // c = -((x1-a)^2 + (x2-b)^2 + (x3-c)^2 - r^2)  src/utils.jl:150-156
+  ROW_SPHERE = 6,  // c = -((x1-a)^2 + (x2-b)^2 + (x3-c)^2 - r^2)  src/utils.jl:150-156
+  ROW_USLACK = 7   // c = u[i]  (equality; infeasible_constraints, src/constraints.jl:306-314)
 };
 
 struct ConRow {
@@ -689,11 +690,40 @@ struct Kuka {
 };
 
 // ---------------------------------------------------------------------------------------------
+// add_slack_controls(model) (src/model.jl:761-779): the infeasible-start model. Controls are
+// [u (Mb::m); s (Mb::n)], x+ = f_d(x, u) + s. Kernels see it as a model with m = Mb::m + Mb::n;
+// discrete_step adds the slacks after the base model's RK step, k_jacobian writes the identity
+// slack block directly (the reference's ∇f! copies Diagonal(1.0I, n), it is never differentiated).
+template <class Mb>
+struct Infeasible {
+  using Base = Mb;
+  static constexpr int n = Mb::n, m = Mb::m + Mb::n, id = Mb::id;
+  static constexpr int slack = Mb::n;
+};
+
+template <class M>
+struct ModelTraits {
+  using Base = M;
+  static constexpr int slack = 0;
+};
+template <class Mb>
+struct ModelTraits<Infeasible<Mb>> {
+  using Base = Mb;
+  static constexpr int slack = Mb::n;
+};
+
+// ---------------------------------------------------------------------------------------------
 // Explicit Runge-Kutta discretisation with runtime dt (src/integration.jl:115-158). Running-sum
 // form keeps the reference's left-to-right association: RK4 ((k1 + 2k2) + 2k3) + k4,
 // RK3 (k1 + 4k2) + k3, with RK3's third stage at (x - k1) + 2k2.
 template <class M, int INTEG, class T>
 __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, double dt) {
+  if constexpr (ModelTraits<M>::slack > 0) {
+    using Mb = typename ModelTraits<M>::Base;
+    discrete_step<Mb, INTEG, T>(xn, x, u, dt);  // model.f(x+, x, u[idx.u], dt)
+#pragma unroll
+    for (int i = 0; i < Mb::n; i++) xn[i] = xn[i] + u[Mb::m + i];  // x+ .+= u[idx.inf]
+  } else {
   constexpr int n = M::n;
   T k[n], s[n], t[n];
   M::f(k, x, u);
@@ -741,6 +771,7 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
       s[i] = s[i] + k[i];
       xn[i] = x[i] + s[i] / 6.0;
     }
+  }
   }
 }
 
@@ -809,6 +840,7 @@ __device__ __forceinline__ double row_value(const ConRow& r, const double* x, co
     case ROW_XMIN: return r.a - x[r.idx];
     case ROW_UMIN: return r.a - u[r.idx];
     case ROW_GOAL: return x[r.idx] - r.a;
+    case ROW_USLACK: return u[r.idx];
     case ROW_CIRCLE: {
       const double dx = x[0] - r.a, dy = x[1] - r.b;
       return -((dx * dx + dy * dy) - r.r * r.r);
@@ -819,7 +851,7 @@ __device__ __forceinline__ double row_value(const ConRow& r, const double* x, co
     }
   }
 }
-__device__ __forceinline__ bool row_inequality(const ConRow& r) { return r.type != ROW_GOAL; }
+__device__ __forceinline__ bool row_inequality(const ConRow& r) { return r.type != ROW_GOAL && r.type != ROW_USLACK; }
 
 // The same row seen by every lane of a wave (lanes iterate knots and rows in lockstep over the
 // shared row table): make its type and index wave-uniform so that the switch is a scalar branch
@@ -839,6 +871,7 @@ __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n,
     case ROW_XMIN: idx[0] = r.idx; v[0] = -1.0; return 1;
     case ROW_UMIN: idx[0] = n + r.idx; v[0] = -1.0; return 1;
     case ROW_GOAL: idx[0] = r.idx; v[0] = 1.0; return 1;
+    case ROW_USLACK: idx[0] = n + r.idx; v[0] = 1.0; return 1;
     case ROW_CIRCLE:
       idx[0] = 0; v[0] = -(2.0 * (x[0] - r.a));
       idx[1] = 1; v[1] = -(2.0 * (x[1] - r.b));

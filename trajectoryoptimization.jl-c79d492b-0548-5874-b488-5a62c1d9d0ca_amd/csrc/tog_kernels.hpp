@@ -22,6 +22,9 @@
 namespace tog {
 
 constexpr int PCAP = 32;  // max constraint rows per knot handled by the LDS layout
+constexpr int PCAP_SLACK = 64;  // infeasible problems: the n slack rows come on top (quadrotor_maze: 63)
+template <class M>
+__host__ __device__ constexpr int pcap_of() { return ModelTraits<M>::slack > 0 ? PCAP_SLACK : PCAP; }
 constexpr int WAVE = 64;
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroups: s_barrier is ~free
@@ -323,7 +326,10 @@ template <class M, int INTEG, int W>
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TOG_JAC_WAVES)))
 k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
-  constexpr int n = M::n, m = M::m, L = n + m, NCH = (L + W - 1) / W;
+  // an infeasible model (ModelTraits<M>::slack) differentiates its base model only; its slack
+  // columns are the identity (src/model.jl:771-774)
+  using Mb = typename ModelTraits<M>::Base;
+  constexpr int n = M::n, m = M::m, L = n + m, mb = Mb::m, Lb = n + mb, NCH = (Lb + W - 1) / W;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int N = P->N;
@@ -334,7 +340,7 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   if (!Bf.st[b].active) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
-  Dual<W> xd[n], ud[m], xn[n];
+  Dual<W> xd[n], ud[mb], xn[n];
 #pragma unroll
   for (int i = 0; i < n; i++) {
     xd[i].v = x[i];
@@ -342,20 +348,25 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
     for (int w = 0; w < W; w++) xd[i].g[w] = (i == c * W + w) ? 1.0 : 0.0;
   }
 #pragma unroll
-  for (int i = 0; i < m; i++) {
+  for (int i = 0; i < mb; i++) {
     ud[i].v = u[i];
 #pragma unroll
     for (int w = 0; w < W; w++) ud[i].g[w] = (n + i == c * W + w) ? 1.0 : 0.0;
   }
-  discrete_step<M, INTEG>(xn, xd, ud, P->dt);
+  discrete_step<Mb, INTEG>(xn, xd, ud, P->dt);
   double* out = Bf.AB + ((size_t)b * (N - 1) + k) * n * L;
 #pragma unroll
   for (int w = 0; w < W; w++) {
     const int col = c * W + w;
-    if (col < L) {
+    if (col < Lb) {
 #pragma unroll
       for (int i = 0; i < n; i++) out[i + n * col] = xn[i].g[w];
     }
+  }
+  if constexpr (ModelTraits<M>::slack > 0) {
+    for (int j = c; j < n; j += NCH)
+#pragma unroll
+      for (int i = 0; i < n; i++) out[i + n * (Lb + j)] = (i == j) ? 1.0 : 0.0;
   }
 }
 
@@ -427,7 +438,8 @@ __device__ void wqr(double* A, int rows, double* wv) {
 template <class M, bool SQRT>
 struct BwdLds {
   static constexpr int n = M::n, m = M::m, L = n + m;
-  static constexpr int WR = n + (n > PCAP ? n : PCAP);  // QR workspace rows
+  static constexpr int PC = pcap_of<M>();
+  static constexpr int WR = n + (n > PC ? n : PC);  // QR workspace rows
   double S[n * n];
   double s[n];
   double AB[n * L];
@@ -446,9 +458,9 @@ struct BwdLds {
   double Wq[WR * n];   // QR workspace
   double xk[n];
   double uk[m];
-  double cval[PCAP], wv[PCAP], wsv[PCAP], gv[PCAP];
-  double cx[PCAP * n];
-  double cu[PCAP * m];
+  double cval[PC], wv[PC], wsv[PC], gv[PC];
+  double cx[PC * n];
+  double cu[PC * m];
   double red[WAVE];
   // lane-0 serial scratch (kept in LDS: private arrays with runtime indexing spill to scratch memory)
   double G[m * m];
@@ -1615,8 +1627,37 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
 #include "tog_bwd_team.hpp"
 namespace tog {
 
+// slack_controls(prob) (src/solvers/altro/infeasible.jl:63-80), one thread per trajectory:
+// x_1 = x0; x_{k+1} = f_d(x_k, u_k) on the base model; s_k = X_{k+1} - x_{k+1}; x_{k+1} += s_k.
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_slack_controls(const DevProblem* __restrict__ P, DevBuffers Bf) {
+  using Mb = typename ModelTraits<M>::Base;
+  constexpr int n = M::n, m = M::m;
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P->B) return;
+  const int N = P->N;
+  const double* X = Bf.X + (size_t)b * N * n;
+  double* U = Bf.U + (size_t)b * (N - 1) * m;
+  double x[n], xn[n];
+#pragma unroll
+  for (int i = 0; i < n; i++) x[i] = Bf.x0[(size_t)b * n + i];
+  for (int k = 0; k < N - 1; k++) {
+    double* u = U + (size_t)k * m;
+    discrete_step<Mb, INTEG>(xn, x, u, P->dt);
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      const double sl = X[(size_t)(k + 1) * n + i] - xn[i];
+      u[Mb::m + i] = sl;
+      x[i] = xn[i] + sl;
+    }
+  }
+}
+
 struct ModelOps {
   int n, m;
+  int slack;  // n for an infeasible model (add_slack_controls), else 0
+  int pcap;   // max constraint rows per knot of the backward kernels' LDS layout
+  void (*slack_controls)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*init)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, hipStream_t);
   void (*rollout_open)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*jacobian)(const DevProblem*, const DevBuffers&, long long B, int N, int integ, hipStream_t);
@@ -1641,7 +1682,8 @@ struct ModelLaunch {
 #endif
   // (the Kuka RBD step keeps per-joint force and mass-matrix arrays live: one partial per thread
   // holds its scratch to ~4 KB/lane against ~12 KB with 4)
-  static constexpr int JW = (M::n + M::m) <= 6 ? (M::n + M::m) : (M::id == TOG_MODEL_KUKA ? 1 : TOG_JW);
+  using Mb = typename ModelTraits<M>::Base;  // the differentiated model (infeasible: without slacks)
+  static constexpr int JW = (Mb::n + Mb::m) <= 6 ? (Mb::n + Mb::m) : (Mb::id == TOG_MODEL_KUKA ? 1 : TOG_JW);
   static unsigned grid(long long total, int blk) { return (unsigned)((total + blk - 1) / blk); }
   static void init(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, hipStream_t st) {
     if (integ == TOG_RK4)
@@ -1656,7 +1698,7 @@ struct ModelLaunch {
       hipLaunchKernelGGL((k_rollout_open<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
   }
   static void jacobian(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int integ, hipStream_t st) {
-    constexpr int NCH = (M::n + M::m + JW - 1) / JW;
+    constexpr int NCH = (Mb::n + Mb::m + JW - 1) / JW;
     const long long total = B * (long long)(N - 1) * NCH;
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_jacobian<M, TOG_RK4, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
@@ -1665,6 +1707,7 @@ struct ModelLaunch {
   }
   static void backward(const DevProblem* P, const DevBuffers& Bf, long long B, int sq, int al, int flags, int team,
                        hipStream_t st) {
+    if constexpr (M::m <= M::n && M::n + 1 <= 16) {
     if (team) {  // column-per-lane teams, TPW trajectories per wave (tog_bwd_team.hpp)
       constexpr int TPW = TeamCfg<M>::TPW;
       const dim3 g((unsigned)((B + TPW - 1) / TPW)), blk(64);
@@ -1680,6 +1723,7 @@ struct ModelLaunch {
         else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, sm, st, P, Bl, flags);
       }
       return;
+    }
     }
     const dim3 g((unsigned)B), blk(64);
     if (sq) {
@@ -1736,6 +1780,14 @@ struct ModelLaunch {
     else
       hipLaunchKernelGGL((k_rollout<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
   }
+  static void slack_controls(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, hipStream_t st) {
+    if constexpr (ModelTraits<M>::slack > 0) {
+      if (integ == TOG_RK4)
+        hipLaunchKernelGGL((k_slack_controls<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+      else
+        hipLaunchKernelGGL((k_slack_controls<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+    }
+  }
   static void update_constraints(const DevProblem* P, const DevBuffers& Bf, long long B, hipStream_t st) {
     hipLaunchKernelGGL((k_update_constraints<M>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
   }
@@ -1743,6 +1795,9 @@ struct ModelLaunch {
     ModelOps o;
     o.n = M::n;
     o.m = M::m;
+    o.slack = ModelTraits<M>::slack;
+    o.pcap = pcap_of<M>();
+    o.slack_controls = slack_controls;
     o.init = init;
     o.rollout_open = rollout_open;
     o.jacobian = jacobian;

@@ -22,6 +22,12 @@ const ModelOps* ops_quadrotor();
 const ModelOps* ops_car();
 const ModelOps* ops_pendulum();
 const ModelOps* ops_kuka();
+// add_slack_controls(model) variants (infeasible start, src/model.jl:761-779)
+const ModelOps* ops_inf_double_integrator();
+const ModelOps* ops_inf_cartpole();
+const ModelOps* ops_inf_quadrotor();
+const ModelOps* ops_inf_car();
+const ModelOps* ops_inf_pendulum();
 }  // namespace tog
 
 static thread_local std::string g_err;
@@ -88,7 +94,17 @@ static void timed(tog_handle* h, int kind, F&& fn) {
   h->ev_kind.push_back(kind);
 }
 
-static const ModelOps* ops_for(int model) {
+static const ModelOps* ops_for(int model, bool infeasible) {
+  if (infeasible) {
+    switch (model) {
+      case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_inf_double_integrator();
+      case TOG_MODEL_CARTPOLE: return ops_inf_cartpole();
+      case TOG_MODEL_QUADROTOR: return ops_inf_quadrotor();
+      case TOG_MODEL_CAR: return ops_inf_car();
+      case TOG_MODEL_PENDULUM: return ops_inf_pendulum();
+    }
+    return nullptr;  // the Kuka infeasible variant is not built
+  }
   switch (model) {
     case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_double_integrator();
     case TOG_MODEL_CARTPOLE: return ops_cartpole();
@@ -119,8 +135,8 @@ static bool host_chol_upper(const double* A, int n, double* U) {
 }
 
 // Flatten the ordered constraint sets into per-knot rows (src/constraint_sets.jl:64-131).
-static int build_rows(const tog_problem_desc* d, std::vector<ConRow>& rows, std::vector<int>& off,
-                      std::vector<int>& cnt) {
+static int build_rows(const tog_problem_desc* d, int slack, int pcap, std::vector<ConRow>& rows,
+                      std::vector<int>& off, std::vector<int>& cnt) {
   const int n = d->n, m = d->m, N = d->N;
   off.assign(N, 0);
   cnt.assign(N, 0);
@@ -163,12 +179,18 @@ static int build_rows(const tog_problem_desc* d, std::vector<ConRow>& rows, std:
             for (int o = 0; o < con.count; o++)
               rows.push_back({ROW_SPHERE, 0, D[4 * o], D[4 * o + 1], D[4 * o + 2], D[4 * o + 3]});
           break;
+        case TOG_CON_INFEASIBLE:
+          // infeasible_constraints(n, m) (src/constraints.jl:306-314): c = u[m+1:m+n], stage only
+          if (!slack) return fail(TOG_ERR_ARG, "TOG_CON_INFEASIBLE needs a TOG_PROB_INFEASIBLE problem");
+          if (!term)
+            for (int i = 0; i < slack; i++) rows.push_back({ROW_USLACK, m - slack + i, 0.0, 0.0, 0.0, 0.0});
+          break;
         default:
           return fail(TOG_ERR_ARG, "unknown constraint type");
       }
     }
     cnt[k] = (int)rows.size() - off[k];
-    if (cnt[k] > PCAP) return fail(TOG_ERR_UNSUPPORTED, "more than PCAP constraint rows at one knot");
+    if (cnt[k] > pcap) return fail(TOG_ERR_UNSUPPORTED, "too many constraint rows at one knot (PCAP)");
     // knots with the same rows share one copy (stage knots of one ConstraintSet): the table stays
     // small enough for the backward kernel to cache it in LDS
     for (int j = 0; j < k; j++) {
@@ -312,7 +334,8 @@ int32_t tog_destroy(tog_handle* h) {
 int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t device, tog_handle** out) {
   if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
   *out = nullptr;
-  const ModelOps* ops = ops_for(d->model);
+  if (d->flags & ~(int32_t)TOG_PROB_INFEASIBLE) return fail(TOG_ERR_ARG, "unknown problem flags");
+  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0);
   if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
   if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
   if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
@@ -339,7 +362,7 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
 
   std::vector<ConRow> rows;
   std::vector<int> off, cnt;
-  int rc = build_rows(d, rows, off, cnt);
+  int rc = build_rows(d, ops->slack, ops->pcap, rows, off, cnt);
   if (rc) {
     tog_destroy(h);
     return rc;
@@ -652,6 +675,15 @@ int32_t tog_rollout_open_loop(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
   HIPCHECK(hipSetDevice(h->device));
   h->ops->rollout_open(h->dP, h->buf, h->B, h->integ, h->stream);
+  HIPCHECK(hipGetLastError());
+  return TOG_OK;
+}
+
+int32_t tog_slack_controls(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (!h->ops->slack) return fail(TOG_ERR_ARG, "slack_controls needs a TOG_PROB_INFEASIBLE handle");
+  HIPCHECK(hipSetDevice(h->device));
+  h->ops->slack_controls(h->dP, h->buf, h->B, h->integ, h->stream);
   HIPCHECK(hipGetLastError());
   return TOG_OK;
 }

@@ -88,6 +88,10 @@ class BatchHandle:
     def rollout_open_loop(self):
         abi.check(self.lib, self.lib.tog_rollout_open_loop(self.h))
 
+    def slack_controls(self):
+        """``slack_controls(prob)`` into U[m+1:m+n] (infeasible handles, infeasible.jl:63-80)."""
+        abi.check(self.lib, self.lib.tog_slack_controls(self.h))
+
     def jacobians(self):
         abi.check(self.lib, self.lib.tog_jacobians(self.h))
 

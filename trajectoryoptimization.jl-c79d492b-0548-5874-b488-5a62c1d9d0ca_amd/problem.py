@@ -40,6 +40,7 @@ class Model:
     m: int
     name: str
     integration: int | None = None  # None = Continuous; abi.RK3 / abi.RK4 = Discrete
+    slack: int = 0  # add_slack_controls: the last `slack` (= n) controls are infeasible slacks
 
     @property
     def discrete(self) -> bool:
@@ -54,6 +55,17 @@ def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) ->
     if key not in ("rk3", "rk4"):
         raise ValueError(f"integration {discretizer!r} is not built (rk3, rk4 only; SURVEY.md §2)")
     return Model(model.model_id, model.n, model.m, model.name, abi.RK3 if key == "rk3" else abi.RK4)
+
+
+def add_slack_controls(model: Model) -> Model:
+    """``add_slack_controls(model)`` (src/model.jl:761-779): a discrete model with n extra controls,
+    x+ = f_d(x, u[1:m]) + u[m+1:m+n]; its Jacobian is [∇f | I]. The device evaluates it as
+    ``Infeasible<M>`` (csrc/tog_device.hpp)."""
+    if not model.discrete:
+        raise ValueError("add_slack_controls needs a discrete model")
+    if model.slack:
+        raise ValueError("model already has slack controls")
+    return Model(model.model_id, model.n, model.m + model.n, model.name + "_inf", model.integration, model.n)
 
 
 def rk3(model: Model, dt: float = 1.0) -> Model:
@@ -235,7 +247,7 @@ class BoundConstraint(_Constraint):
         x = np.asarray(x, dtype=np.float64)
         if u is None:
             return np.concatenate([(x - self.x_max)[a["x_max"]], (self.x_min - x)[a["x_min"]]])
-        u = np.asarray(u, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)[: self.m]  # u[con.inds[2]] (constraint_sets.jl:106-110)
         return np.concatenate([(x - self.x_max)[a["x_max"]], (u - self.u_max)[a["u_max"]],
                                (self.x_min - x)[a["x_min"]], (self.u_min - u)[a["u_min"]]])
 
@@ -249,9 +261,43 @@ class BoundConstraint(_Constraint):
         sel = np.concatenate([a["x_max"], a["u_max"], a["x_min"], a["u_min"]])
         return jac[sel]
 
-    def to_abi(self):
-        data = np.concatenate([self.x_max, self.x_min, self.u_max, self.u_min])
+    def to_abi(self, m=None):
+        # an infeasible problem's controls are [u; slack]: the slack entries are unbounded
+        # (trimmed), so the rows are those of the model controls (constraint_sets.jl:135-150)
+        pad = np.full(0 if m is None else m - self.m, np.inf)
+        data = np.concatenate([self.x_max, self.x_min, self.u_max, pad, self.u_min, -pad])
         return (abi.CON_BOUND, 0, data)
+
+
+class InfeasibleConstraint(_Constraint):
+    """``infeasible_constraints(n, m)`` (src/constraints.jl:306-314): Constraint{Equality} on the
+    slack controls, c = u[m+1:m+n], ∇c = [0 0 I]. Stage only."""
+
+    inequality = False
+    label = "infeasible"
+
+    def __init__(self, n, m):
+        self.n, self.m = n, m
+
+    def length(self, kind="stage"):
+        return self.n if kind == "stage" else 0
+
+    def evaluate(self, x, u=None):
+        if u is None:
+            return np.zeros(0)
+        return np.asarray(u, dtype=np.float64)[self.m: self.m + self.n].copy()
+
+    def jacobian(self, x, u=None):
+        J = np.zeros((self.n, 2 * self.n + self.m))
+        J[:, self.n + self.m:] = np.eye(self.n)
+        return J
+
+    def to_abi(self, m=None):
+        return (abi.CON_INFEASIBLE, 0, np.zeros(1))
+
+
+def infeasible_constraints(n, m):
+    return InfeasibleConstraint(n, m)
 
 
 def _validate_bounds(mx, mn, n):  # src/constraints.jl:276-296
@@ -500,11 +546,13 @@ class Problem:
             key = tuple(id(c) for c in cs) + (k == N - 1,)
             if key not in keys:
                 keys[key] = len(sets)
-                sets.append([c.to_abi() for c in cs])
+                sets.append([c.to_abi(m) if isinstance(c, (BoundConstraint, InfeasibleConstraint)) else c.to_abi()
+                             for c in cs])
             knot_set.append(keys[key])
         R = stage.R if stage.R.size else np.zeros((m, m))
         return abi.DescBuilder(self.model.model_id, self.model.integration, n, m, N, self.dt, stage.Q, R, stage.H,
-                               stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B)
+                               stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B,
+                               flags=abi.PROB_INFEASIBLE if self.model.slack else 0)
 
 
 def _validate_time(N, tf, dt):
@@ -583,3 +631,60 @@ def max_violation(prob: Problem) -> float:
                 c_max = max(c_max, max(max_e, max_i))
         out.append(c_max)
     return out[0] if not prob.batched else np.array(out)
+
+
+# ----------------------------------------------------------------------------- infeasible start
+
+
+def infeasible_problem(prob: Problem, R_inf: float = 1.0) -> Problem:
+    """``infeasible_problem(prob, R_inf)`` (src/solvers/altro/infeasible.jl:2-33).
+
+    Slack controls u_inf (n per knot) make any state trajectory dynamically feasible:
+    the model becomes ``add_slack_controls`` (x+ = f_d(x,u) + u_inf), the stage cost gets
+    ``R_inf*I/dt`` on u_inf (zero-padded r and H), and every stage constraint set becomes
+    ``update_constraint_set_jacobians`` order — non-bound constraints first, then the bounds
+    (constraint_sets.jl:135-150) — followed by ``infeasible_constraints`` (u_inf = 0).
+    The terminal set is kept. The state trajectory X is kept; the slack controls are filled on
+    the device by ``slack_controls`` (infeasible.jl:63-80) when the solver is set up.
+    """
+    n, m, N = prob.model.n, prob.model.m, prob.N
+    stage, term = prob.obj.stage, prob.obj.terminal
+    R = np.zeros((m + n, m + n))
+    R[:m, :m] = stage.R
+    R[m:, m:] = R_inf * np.eye(n) / prob.dt
+    H = np.vstack([stage.H, np.zeros((n, n))])
+    r = np.concatenate([stage.r, np.zeros(n)])
+    cost_inf = QuadraticCost(stage.Q, R, H, stage.q, r, stage.c)
+    obj = Objective(cost_inf, term.copy(), N=N)
+    con_inf = infeasible_constraints(n, m)
+    cons = Constraints(N)
+    constrained = prob.is_constrained()
+    memo = {}
+    for k in range(N - 1):
+        cs = prob.constraints[k]
+        key = tuple(id(c) for c in cs)
+        if key not in memo:  # knots sharing a set keep sharing one (same rows, one device copy)
+            others = [c for c in cs if not isinstance(c, BoundConstraint)] if constrained else []
+            bnds = [c for c in cs if isinstance(c, BoundConstraint)] if constrained else []
+            memo[key] = ConstraintSet(others + bnds + [con_inf])
+        cons.C[k] = memo[key]
+    cons.C[N - 1] = ConstraintSet(prob.constraints[N - 1]) if constrained else ConstraintSet()
+    p = Problem(add_slack_controls(prob.model), obj, constraints=cons, x0=prob.x0 if prob.batched else prob.x0[0],
+                xf=prob.xf, N=N, dt=prob.dt)
+    p._U[:, :, :m] = prob._U
+    p._U[:, :, m:] = 0.0
+    p._X[...] = prob._X
+    return p
+
+
+def line_trajectory(x0, xf, N):
+    """``line_trajectory(x0, xf, N)`` (src/solvers/altro/infeasible.jl:82-90): (N, n) with
+    x_k = (xf - x0)/N * t_k, t = range(0, N, length=N), first/last rows pinned to x0/xf."""
+    x0 = np.asarray(x0, dtype=np.float64)
+    xf = np.asarray(xf, dtype=np.float64)
+    t = np.linspace(0.0, N, N)
+    slope = (xf - x0) / N
+    X = np.array([slope * t[k] for k in range(N)])
+    X[0] = x0
+    X[-1] = xf
+    return X

@@ -19,6 +19,7 @@ import numpy as np
 
 from . import abi
 from .device import BatchHandle
+from .problem import infeasible_problem
 
 
 # ----------------------------------------------------------------------------- options
@@ -85,9 +86,9 @@ class AugmentedLagrangianSolverOptions:
 
 @dataclass
 class ALTROSolverOptions:
-    """src/solvers/altro/altro_solver.jl:6-65. With ``projected_newton=false`` (default), a NaN
-    initial state trajectory and ``tf > 0`` ALTRO reduces to the AL solve (altro_methods.jl:98-124);
-    the infeasible-start, minimum-time and projected-Newton phases are SURVEY.md §8(f) "next"."""
+    """src/solvers/altro/altro_solver.jl:6-65. With a NaN initial state trajectory ALTRO is the AL
+    solve; with a given X it is the infeasible-start solve (altro_methods.jl:98-124, infeasible.jl).
+    The minimum-time and projected-Newton phases are SURVEY.md §8(f) "next" (not built)."""
 
     verbose: bool = False
     opts_al: AugmentedLagrangianSolverOptions = field(default_factory=AugmentedLagrangianSolverOptions)
@@ -251,8 +252,53 @@ def AbstractSolverFor(prob, opts, **kw):
 def _altro_check(prob, opts):
     if opts.projected_newton:
         raise NotImplementedError("ALTRO projected-Newton phase is SURVEY.md §8(f) 'next' (not built)")
-    if np.isfinite(prob._X).all():
-        raise NotImplementedError("infeasible-start ALTRO (X0 given) is SURVEY.md §8(f) 'next' (not built)")
+
+
+def _altro_infeasible(prob) -> bool:
+    """``!all(isnan, prob.X[1])`` (altro_methods.jl:101): the whole batch must agree."""
+    given = ~np.isnan(prob._X[:, 0, :]).all(axis=1)
+    if given.any() and not given.all():
+        raise ValueError("infeasible start: X must be given for every trajectory of the batch or for none")
+    return bool(given.all())
+
+
+def _solve_altro_infeasible(prob, opts, max_steps, device):
+    """``solve!(prob, ::ALTROSolverOptions)`` with an initial state trajectory
+    (altro_methods.jl:2-124):
+
+    1. ``infeasible_problem(prob, R_inf)`` and its AL solve from the given X, with the slack controls
+       from ``slack_controls`` (computed on the device, infeasible.jl:63-80);
+    2. ``process_results!``: X and the model controls U[1:m] go back to ``prob``;
+    3. with ``resolve_feasible_problem``, the feasible problem is solved again by AL (iLQR when it
+       is unconstrained, augmented_lagrangian_methods.jl:33-36) from those controls. With
+       ``dynamically_feasible_projection`` it starts from ``projection!``'s trajectory. In this
+       snapshot ``projection!`` runs ``backwardpass!`` on a freshly constructed iLQR solver: ∇F and
+       the Q expansion are zero, so after one regularisation restart K = d = -0.0 and the α = 0
+       rollout is the open-loop rollout of U from x0 (ilqr_methods.jl:179-190, backward_pass.jl:9-85,
+       DESIGN.md §8). The device does exactly that: X = NaN triggers ``rollout!(prob)``.
+    Without resolve, ``prob`` keeps the infeasible solve's X (the projection is discarded).
+    """
+    m = prob.model.m
+    prob_inf = infeasible_problem(prob, opts.R_inf)
+    solver = ALTROSolver(prob_inf, opts, device=device)
+    h = solver.handle
+    h.slack_controls()
+    o = to_tog_options(opts)
+    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None
+            else int(o.iterations) * int(o.al_iterations) + 1)
+    h.download_state(prob_inf)
+    solver.stats = h.stats_dict()
+    solver.prob_infeasible = prob_inf
+    prob._X[...] = prob_inf._X
+    prob._U[...] = prob_inf._U[:, :, :m]
+    if np.any(solver.stats["flags"] & abi.TRAJ_COST_INCREASED):
+        raise RuntimeError("Error: Cost increased during Forward Pass")
+    if opts.resolve_feasible_problem:
+        if opts.dynamically_feasible_projection:
+            prob._X[...] = np.nan
+        feasible = solve_b(prob, opts.opts_al, max_steps=max_steps, device=device)
+        solver.stats_feasible = feasible.stats
+    return solver
 
 
 def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int = 0):
@@ -263,6 +309,10 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
         solver.handle.upload_state(prob)
     else:
         opts = solver_or_opts
+        if isinstance(opts, ALTROSolverOptions):
+            _altro_check(prob, opts)
+            if _altro_infeasible(prob):
+                return _solve_altro_infeasible(prob, opts, max_steps, device)
         if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
             # solve!(prob, ::AugmentedLagrangianSolverOptions) on an unconstrained problem
             # falls back to the unconstrained solver (augmented_lagrangian_methods.jl:33-36)
