@@ -45,8 +45,9 @@ def pendulum_line(tog, constrained_variant=False):
 
 def quad_line_batch(tog, B=3, N=31, seed=7):
     """Quadrotor (test/quadrotor_tests.jl:4-35 model and costs, u in [0, 15] + goal), N shortened,
-    batched random starts with a straight-line state guess per trajectory (the quadrotor_maze
-    initial-guess path, problems/quadrotor_maze.jl:107-114, with line_trajectory)."""
+    batched random starts with a straight-line state guess x0 -> xf per trajectory (the
+    quadrotor_maze initial-guess path, problems/quadrotor_maze.jl:107-114). Not line_trajectory:
+    that one is slope*t without the x0 offset (infeasible.jl:82-90), which zeroes the quaternion."""
     p0 = tog.Problems.quadrotor_test("goal+bounds")
     n, m = 13, 4
     rng = np.random.default_rng(seed)
@@ -61,7 +62,8 @@ def quad_line_batch(tog, B=3, N=31, seed=7):
     cons[N - 1] += tog.goal_constraint(xf)
     obj = tog.LQRObjective(p0.obj.stage.Q, p0.obj.stage.R, p0.obj.terminal.Q, xf, N)
     prob = tog.Problem(p0.model, obj, U0, x0=x0, xf=xf, N=N, dt=0.05, constraints=cons)
-    prob.X = np.stack([tog.line_trajectory(x0[b], xf, N) for b in range(B)])
+    t = np.linspace(0.0, 1.0, N)[None, :, None]
+    prob.X = x0[:, None, :] + (xf - x0)[:, None, :] * t
     return prob
 
 
