@@ -66,7 +66,8 @@ enum tog_model_id {
 
 enum tog_integrator {
   TOG_RK3 = 0, /* src/integration.jl:149-158 */
-  TOG_RK4 = 1  /* src/integration.jl:115-125 */
+  TOG_RK4 = 1, /* src/integration.jl:115-125 */
+  TOG_MIDPOINT = 2 /* explicit midpoint, src/integration.jl:26-33 (discretize_model(model, :midpoint)) */
 };
 
 /* ---------------------------------------------------------------- constraints */

@@ -561,6 +561,15 @@ static void model_f(int model, dual* xd, const dual* x, const dual* u) {
 /* rk4: src/integration.jl:115-125 ; rk3: src/integration.jl:149-158 (dt is a Dual input) */
 static void discrete_f_dual(int model, int integ, int n, dual* xn, const dual* x, const dual* u, dual dt) {
   dual k1[16], k2[16], k3[16], k4[16], t[16];
+  if (integ == TOG_MIDPOINT) { /* src/integration.jl:26-33 */
+    model_f(model, k1, x, u);
+    dual h = ddivc(dt, 2.0); /* xdot .*= dt/2. */
+    for (int i = 0; i < n; i++) k1[i] = dmul(k1[i], h);
+    for (int i = 0; i < n; i++) t[i] = dadd(x[i], k1[i]);
+    model_f(model, k2, t, u); /* f!(xdot, x + xdot, u) */
+    for (int i = 0; i < n; i++) xn[i] = dadd(x[i], dmul(k2[i], dt)); /* x + xdot*dt */
+    return;
+  }
   model_f(model, k1, x, u);
   for (int i = 0; i < n; i++) k1[i] = dmul(k1[i], dt);
   for (int i = 0; i < n; i++) t[i] = dadd(x[i], ddivc(k1[i], 2.0));

@@ -24,7 +24,7 @@ def rel(a, b):
 def lqr_problem(tog, model, integ, N=21, dt=0.05, B=4, seed=0, constraints=None):
     rng = np.random.default_rng(seed)
     n, m = model.n, model.m
-    md = tog.rk4(model) if integ == "rk4" else tog.rk3(model)
+    md = tog.discretize_model(model, integ)
     xf = rng.standard_normal(n)
     if model.name == "quadrotor":
         xf[3:7] = [1, 0, 0, 0]
@@ -38,7 +38,8 @@ def lqr_problem(tog, model, integ, N=21, dt=0.05, B=4, seed=0, constraints=None)
 
 
 MODELS = [("doubleintegrator", "rk3"), ("cartpole", "rk3"), ("quadrotor", "rk4"), ("quadrotor", "rk3"),
-          ("car", "rk4"), ("pendulum", "rk3")]
+          ("car", "rk4"), ("pendulum", "rk3"), ("quadrotor", "midpoint"), ("cartpole", "midpoint")]
+INTEG = {"rk3": 0, "rk4": 1, "midpoint": 2}
 
 
 @pytest.mark.parametrize("name,integ", MODELS)
@@ -54,7 +55,7 @@ def test_jacobian_parity(tog, oracle, gpu, name, integ):
     tog.jacobian_b(prob, solver)
     A = solver.handle.get(tog.abi.FIELD_A)
     Bm = solver.handle.get(tog.abi.FIELD_B)
-    ig = tog.abi.RK4 if integ == "rk4" else tog.abi.RK3
+    ig = INTEG[integ]
     for b in range(prob.B):
         for k in range(prob.N - 1):
             S = oracle.discrete_jacobian(model.model_id, ig, prob._X[b, k], prob._U[b, k], prob.dt)
@@ -255,3 +256,17 @@ def test_batch_stats_and_status(tog, gpu):
     assert h.total_steps() == 48
     flags = h.status()
     assert np.all(flags & tog.abi.TRAJ_ACTIVE)
+
+
+@pytest.mark.parametrize("integ", ["midpoint", "rk3"])
+def test_solve_pendulum_altro(tog, oracle, gpu, integ):
+    """pendulum_tests.jl:23-27 over the explicit schemes: the device AL solve equals the oracle's
+    and meets the reference's max_violation < constraint_tolerance."""
+    ilqr = tog.iLQRSolverOptions()
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=ilqr, iterations=50, penalty_scaling=10.0)
+    opts = tog.ALTROSolverOptions(opts_al=al)
+    prob = tog.Problems.pendulum(integ)
+    _solve_and_compare(tog, oracle, prob, opts)
+    gp = prob.copy()
+    tog.solve_b(gp, opts)
+    assert tog.max_violation(gp) < al.constraint_tolerance

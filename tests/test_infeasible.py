@@ -266,3 +266,38 @@ def test_gpu_infeasible_quadrotor_batch(tog, oracle, gpu):
         assert rel(prob._U[b], Uo) < TOL_SOLVE, b
         assert int(solver.stats["iterations_total"][b]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS]), b
         assert int(solver.stats_feasible["iterations_total"][b]) == int(sf.get("stats")[tog.abi.STAT_TOTAL_STEPS]), b
+
+
+def maze_opts(tog, resolve=False):
+    """test/infeasible_tests.jl:57-76 (the reference's commented-out maze case)."""
+    il = tog.iLQRSolverOptions(iterations=300)
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=il, iterations=40, cost_tolerance=1e-5,
+                                              cost_tolerance_intermediate=1e-4, constraint_tolerance=1e-3,
+                                              penalty_scaling=10.0, penalty_initial=1.0)
+    return tog.ALTROSolverOptions(resolve_feasible_problem=resolve, opts_al=al, R_inf=0.001)
+
+
+def test_quadrotor_maze_problem(tog):
+    """problems/quadrotor_maze.jl: 44 cylinders (+ r_quad), bnd1 at knot 1, bnd2 + maze at 2..N-1,
+    bnd_xf at N; the interpolated state guess starts at x0, ends at xf and keeps q = q0."""
+    p = tog.Problems.quadrotor_maze()
+    nc = p.constraints.num_constraints()
+    assert nc[0] == 8 and all(c == 56 for c in nc[1:-1]) and nc[-1] == 18
+    assert np.allclose(p.X[0], p.x0[0]) and np.allclose(p.X[-1], p.xf)
+    assert np.allclose(p.X[:, 3:7], [1, 0, 0, 0])
+    pinf = tog.infeasible_problem(p, 0.001)
+    nci = pinf.constraints.num_constraints()
+    assert nci[0] == 8 + 13 and all(c == 56 + 13 for c in nci[1:-1]) and nci[-1] == 18
+
+
+@pytest.mark.gpu
+def test_gpu_quadrotor_maze_infeasible(tog, oracle, gpu):
+    """The quadrotor_maze infeasible-start AL solve (69 rows per knot: the LDS backward kernel)
+    on the device equals the oracle: X, U and the iteration count."""
+    p = tog.Problems.quadrotor_maze()
+    opts = maze_opts(tog, resolve=False)
+    ref = p.copy()
+    solver = tog.solve_b(p, opts)
+    Xo, Uo, si, _ = oracle.solve_altro_infeasible(ref, opts)
+    assert rel(p.X, Xo) < TOL_SOLVE and rel(p.U, Uo) < TOL_SOLVE
+    assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])

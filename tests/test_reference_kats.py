@@ -271,9 +271,9 @@ def test_car_parallel_park(tog, oracle):
     assert np.linalg.norm(s.get("X")[-1] - prob.xf) < 1e-3
 
 
-@pytest.mark.parametrize("integ", ["rk3", "rk4"])
+@pytest.mark.parametrize("integ", ["midpoint", "rk3", "rk4"])
 def test_pendulum_altro(tog, oracle, integ):
-    """pendulum_tests.jl:23-27 (the rk3/rk4 schemes in scope): AL (ALTRO phase 1) with
+    """pendulum_tests.jl:23-27 (the explicit schemes :midpoint, :rk3, :rk4): AL (ALTRO phase 1) with
     penalty_scaling=10, 50 outer iterations reaches max_violation < constraint_tolerance."""
     ilqr = tog.iLQRSolverOptions()
     al = tog.AugmentedLagrangianSolverOptions(opts_uncon=ilqr, iterations=50, penalty_scaling=10.0)
@@ -287,3 +287,31 @@ def test_doubleintegrator_altro(tog, oracle):
     prob, opts = tog.Problems.config_doubleintegrator()
     s = _solve(tog, oracle, prob, opts)
     assert s.max_violation() < opts.opts_al.constraint_tolerance
+
+
+def test_undefined_integration_raises(tog):
+    """pendulum_tests.jl:30: Problem(model, obj, integration=:bogus) throws ArgumentError."""
+    prob = tog.Problems.pendulum()
+    with pytest.raises(ValueError):
+        tog.Problem(tog.Dynamics.pendulum, prob.obj, integration="bogus", N=prob.N, dt=prob.dt)
+    with pytest.raises(NotImplementedError):
+        tog.discretize_model(tog.Dynamics.pendulum, "midpoint_implicit")
+
+
+def test_midpoint_jacobian_matches_central_differences(tog, oracle):
+    """The dual-number midpoint Jacobian (src/integration.jl:26-33 under ForwardDiff) equals
+    central differences of the oracle's midpoint step, for every model."""
+    rng = np.random.default_rng(5)
+    for mid in range(tog.abi.MODEL_KUKA):
+        n, m = tog.abi.MODEL_NM[mid]
+        x, u = 0.3 * rng.standard_normal(n), 0.3 * rng.standard_normal(m)
+        if mid == tog.abi.MODEL_QUADROTOR:
+            x[3:7] = [1, 0.1, -0.2, 0.05]
+        S = oracle.discrete_jacobian(mid, tog.abi.MIDPOINT, x, u, 0.05)
+        z = np.concatenate([x, u])
+        for j in range(n + m):
+            e = np.zeros(n + m)
+            e[j] = 1e-6
+            fp = oracle.discrete_f(mid, tog.abi.MIDPOINT, (z + e)[:n], (z + e)[n:], 0.05)
+            fm = oracle.discrete_f(mid, tog.abi.MIDPOINT, (z - e)[:n], (z - e)[n:], 0.05)
+            assert np.allclose(S[:, j], (fp - fm) / 2e-6, rtol=1e-6, atol=1e-7), (mid, j)

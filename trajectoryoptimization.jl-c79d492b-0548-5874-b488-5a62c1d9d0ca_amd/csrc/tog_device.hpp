@@ -725,6 +725,18 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
     for (int i = 0; i < Mb::n; i++) xn[i] = xn[i] + u[Mb::m + i];  // x+ .+= u[idx.inf]
   } else {
   constexpr int n = M::n;
+  if constexpr (INTEG == TOG_MIDPOINT) {
+    // midpoint (src/integration.jl:26-33): ẋ = f(x,u); ẋ .*= dt/2; ẋ = f(x + ẋ, u); x+ = x + ẋ*dt
+    T k[n], t[n];
+    M::f(k, x, u);
+    const double h = dt / 2.0;
+#pragma unroll
+    for (int i = 0; i < n; i++) t[i] = x[i] + k[i] * h;
+    M::f(k, t, u);
+#pragma unroll
+    for (int i = 0; i < n; i++) xn[i] = x[i] + k[i] * dt;
+    return;
+  } else {
   T k[n], s[n], t[n];
   M::f(k, x, u);
 #pragma unroll
@@ -771,6 +783,7 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
       s[i] = s[i] + k[i];
       xn[i] = x[i] + s[i] / 6.0;
     }
+  }
   }
   }
 }

@@ -21,10 +21,11 @@
 
 namespace tog {
 
-constexpr int PCAP = 32;  // max constraint rows per knot handled by the LDS layout
-constexpr int PCAP_SLACK = 64;  // infeasible problems: the n slack rows come on top (quadrotor_maze: 63)
+// max constraint rows per knot in the LDS backward kernel's layout (problems/quadrotor_maze.jl:
+// 12 bound rows + 44 cylinders per stage knot, + 13 slack rows in its infeasible-start problem)
+constexpr int PCAP = 72;
 template <class M>
-__host__ __device__ constexpr int pcap_of() { return ModelTraits<M>::slack > 0 ? PCAP_SLACK : PCAP; }
+__host__ __device__ constexpr int pcap_of() { return PCAP; }
 constexpr int WAVE = 64;
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroups: s_barrier is ~free
@@ -1688,12 +1689,16 @@ struct ModelLaunch {
   static void init(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, hipStream_t st) {
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_init<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
+    else if (integ == TOG_MIDPOINT)
+      hipLaunchKernelGGL((k_init<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
     else
       hipLaunchKernelGGL((k_init<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
   }
   static void rollout_open(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, hipStream_t st) {
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_rollout_open<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+    else if (integ == TOG_MIDPOINT)
+      hipLaunchKernelGGL((k_rollout_open<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
     else
       hipLaunchKernelGGL((k_rollout_open<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
   }
@@ -1759,6 +1764,8 @@ struct ModelLaunch {
       const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
       if (integ == TOG_RK4)
         hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
+      else if (integ == TOG_MIDPOINT)
+        hipLaunchKernelGGL((k_ls_spec<M, TOG_MIDPOINT>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
       else
         hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
       lo += cnt;
@@ -1766,6 +1773,8 @@ struct ModelLaunch {
     }
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_ls_commit<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);
+    else if (integ == TOG_MIDPOINT)
+      hipLaunchKernelGGL((k_ls_commit<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);
     else
       hipLaunchKernelGGL((k_ls_commit<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);
   }
@@ -1777,6 +1786,8 @@ struct ModelLaunch {
                       hipStream_t st) {
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_rollout<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
+    else if (integ == TOG_MIDPOINT)
+      hipLaunchKernelGGL((k_rollout<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
     else
       hipLaunchKernelGGL((k_rollout<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
   }
@@ -1784,6 +1795,8 @@ struct ModelLaunch {
     if constexpr (ModelTraits<M>::slack > 0) {
       if (integ == TOG_RK4)
         hipLaunchKernelGGL((k_slack_controls<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+      else if (integ == TOG_MIDPOINT)
+        hipLaunchKernelGGL((k_slack_controls<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
       else
         hipLaunchKernelGGL((k_slack_controls<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
     }

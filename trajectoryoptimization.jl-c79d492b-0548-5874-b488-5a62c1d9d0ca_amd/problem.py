@@ -52,9 +52,17 @@ def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) ->
     if model.discrete:
         raise ValueError("model is already discrete")
     key = discretizer.lstrip(":")
-    if key not in ("rk3", "rk4"):
-        raise ValueError(f"integration {discretizer!r} is not built (rk3, rk4 only; SURVEY.md §2)")
-    return Model(model.model_id, model.n, model.m, model.name, abi.RK3 if key == "rk3" else abi.RK4)
+    if key in ("rk3_implicit", "midpoint_implicit"):
+        raise NotImplementedError(f"implicit integration {discretizer!r} is not built (SURVEY.md §8(f))")
+    if key not in ("rk3", "rk4", "midpoint"):
+        raise ValueError(f"Integration not defined: {discretizer!r}")  # src/model.jl:659
+    integ = {"rk3": abi.RK3, "rk4": abi.RK4, "midpoint": abi.MIDPOINT}[key]
+    return Model(model.model_id, model.n, model.m, model.name, integ)
+
+
+def midpoint(model: Model, dt: float = 1.0) -> Model:
+    """``midpoint(model)`` (src/model.jl:642, src/integration.jl:26-33)."""
+    return discretize_model(model, "midpoint", dt)
 
 
 def add_slack_controls(model: Model) -> Model:

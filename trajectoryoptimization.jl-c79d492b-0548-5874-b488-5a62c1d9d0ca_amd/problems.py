@@ -8,6 +8,7 @@ import math
 import numpy as np
 
 from .problem import (BoundConstraint, CircleConstraints, Constraints, Dynamics, LQRObjective, Problem,
+                      discretize_model,
                       SphereConstraints, goal_constraint, rk3, rk4)
 from .solvers import ALTROSolverOptions, AugmentedLagrangianSolverOptions, iLQRSolverOptions
 
@@ -160,7 +161,7 @@ def car_sqrt_bp(constrained=False):
 def pendulum(integration="rk3", U0=None):
     """problems/pendulum.jl:1-35: rk3, N=31, dt=0.15, Q=R=Qf=1e-3 I, xf=[π,0], |u|<=3 at
     k<N, goal at N, U=ones."""
-    model_d = rk4(Dynamics.pendulum) if integration == "rk4" else rk3(Dynamics.pendulum)
+    model_d = discretize_model(Dynamics.pendulum, integration)
     n, m = 2, 1
     Q, R = 1e-3 * np.eye(n), 1e-3 * np.eye(m)
     x0, xf = np.zeros(n), np.array([math.pi, 0.0])
@@ -315,3 +316,81 @@ def config_doubleintegrator(B=1):
     """Config 1: double integrator block move, ALTRO defaults."""
     prob = doubleintegrator()
     return prob, ALTROSolverOptions()
+
+
+def interp_rows(N, tf, X):
+    """``interp_rows(N, tf, X)`` (src/utils.jl:5-15): each row of X (n, N1) through a cubic spline
+    on range(0, tf, N1), sampled on range(0, tf, N). The reference uses Interpolations.jl's
+    ``CubicSplineInterpolation`` (BSpline(Cubic(Line(OnGrid())))) — not installed here; its Line
+    boundary condition is the natural spline (zero second derivative at both ends), restated with
+    scipy. Used only to build initial guesses."""
+    from scipy.interpolate import CubicSpline
+
+    X = np.asarray(X, dtype=np.float64)
+    t1 = np.linspace(0.0, tf, X.shape[1])
+    t2 = np.linspace(0.0, tf, N)
+    return np.stack([CubicSpline(t1, X[i], bc_type="natural")(t2) for i in range(X.shape[0])])
+
+
+def quadrotor_maze(N=101):
+    """problems/quadrotor_maze.jl:1-114: quadrotor (rk3) through 38 cylinders, u in [0, 50],
+    x/z box, terminal box on position/velocity; initial controls hover, initial *state* guess
+    interp_rows of 7 way-points — an infeasible start (ALTRO solves it via slack controls)."""
+    model_d = rk3(Dynamics.quadrotor)
+    n, m = 13, 4
+    q0 = np.array([1.0, 0.0, 0.0, 0.0])
+    x0 = np.zeros(n)
+    x0[0:3] = [0.0, 0.0, 10.0]
+    x0[3:7] = q0
+    xf = np.zeros(n)
+    xf[0:3] = [0.0, 60.0, 10.0]
+    xf[3:7] = q0
+    Q = 1e-3 * np.eye(n)
+    Q[3:7, 3:7] = 1e-2 * np.eye(4)
+    R = 1e-4 * np.eye(m)
+    Qf = 1000.0 * np.eye(n)
+    r_quad, r_cyl = 2.0, 2.0
+    cyl = []
+    for i in np.linspace(-25, -10, 5):
+        cyl.append((i, 10.0, r_cyl))
+    for i in np.linspace(10, 25, 5):
+        cyl.append((i, 10.0, r_cyl))
+    for i in np.linspace(-5, 5, 4):
+        cyl.append((i, 30.0, r_cyl))
+    for i in np.linspace(-25, -10, 5):
+        cyl.append((i, 50.0, r_cyl))
+    for i in np.linspace(10, 25, 5):
+        cyl.append((i, 50.0, r_cyl))
+    for i in np.linspace(10 + 2 * r_cyl, 50 - 2 * r_cyl, 10):
+        cyl.append((-25.0, i, r_cyl))
+    for i in np.linspace(10 + 2 * r_cyl, 50 - 2 * r_cyl, 10):
+        cyl.append((25.0, i, r_cyl))
+    maze = CircleConstraints(n, m, [(cx, cy, r + r_quad) for (cx, cy, r) in cyl], "maze")
+    x_max = np.full(n, np.inf)
+    x_min = np.full(n, -np.inf)
+    x_max[0:3] = [25.0, np.inf, 20.0]
+    x_min[0:3] = [-25.0, -np.inf, 0.0]
+    bnd1 = BoundConstraint(n, m, u_min=0.0, u_max=50.0)
+    bnd2 = BoundConstraint(n, m, u_min=0.0, u_max=50.0, x_min=x_min, x_max=x_max)
+    xU, xL = xf.copy(), xf.copy()
+    xU[3:7], xL[3:7] = np.inf, -np.inf
+    xU[7:10], xL[7:10] = 0.0, 0.0
+    bnd_xf = BoundConstraint(n, m, x_min=xL, x_max=xU)
+    tf = 5.0
+    dt = tf / (N - 1)
+    cons = Constraints(N)
+    cons[0] += bnd1
+    stage = bnd2 + maze
+    for k in range(1, N - 1):
+        cons[k] = stage
+    cons[N - 1] += bnd_xf
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    U0 = HOVER * np.ones((N - 1, m))
+    prob = Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
+    Xg = np.zeros((n, 7))
+    Xg[:, 0] = x0
+    Xg[:, 6] = xf
+    Xg[0:3, 1:6] = [[0, -12.5, -20, -12.5, 0], [15, 20, 30, 40, 45], [10, 10, 10, 10, 10]]
+    Xg[3:7, :] = q0[:, None]
+    prob.X = interp_rows(N, tf, Xg).T
+    return prob
