@@ -33,6 +33,7 @@
 
 #define DMAX 24 /* max partials: n+m+1 of a model (slack columns are never dual) */
 #define OM 32   /* max controls, including the n slack controls of an infeasible problem */
+#define OP 128  /* max constraint rows per knot (quadrotor_maze infeasible: 69) */
 #define OC_EXPORT __attribute__((visibility("default")))
 
 /* =====================================================================
@@ -1507,7 +1508,7 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
   }
   if (!al) return 0;
   /* AL terms */
-  double cx[64 * 16], cu[64 * OM], cval[64];
+  double cx[OP * 16], cu[OP * OM], cval[OP];
   for (int k = 0; k < N; k++) {
     int p = s->p[k];
     if (p == 0) continue;
@@ -1516,7 +1517,7 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
     const double* c = s->C + (size_t)k * P; /* obj.C[k] (last evaluated, A.10) */
     const double* lam = s->lam + (size_t)k * P;
     const double* mu = s->mu + (size_t)k * P;
-    double w[64], g[64], ws[64];
+    double w[OP], g[OP], ws[OP];
     for (int i = 0; i < p; i++) {
       /* a = active_set(c, λ) */
       int ineq = s->ineq[(size_t)k * P + i];
@@ -1553,7 +1554,7 @@ OC_EXPORT int oc_cost_expansion(oc_solver* s, int sq, int al) {
       }
     } else {
       /* chol_plus!(Q.xx, Iμ_sqrt*cx) ; chol_plus!(Q.uu, Iμ_sqrt*cu)  (no ux term, A.5) */
-      double M[64 * OM], R[OM * OM];
+      double M[OP * OM], R[OM * OM];
       for (int j = 0; j < n; j++)
         for (int r = 0; r < p; r++) M[r + p * j] = ws[r] * cx[r + p * j];
       chol_plus(R, Qxx, n, M, p, n);

@@ -301,3 +301,32 @@ def test_gpu_quadrotor_maze_infeasible(tog, oracle, gpu):
     Xo, Uo, si, _ = oracle.solve_altro_infeasible(ref, opts)
     assert rel(p.X, Xo) < TOL_SOLVE and rel(p.U, Uo) < TOL_SOLVE
     assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sqrt", [False, True])
+def test_gpu_quadrotor_maze_step_level(tog, oracle, gpu, sqrt):
+    """One AL step of the maze's infeasible problem (69 rows per knot, more than a wave's lanes;
+    the sqrt expansion's [Q.uu; √Iμ cu] QR is 86 x 17): constraint values, AL cost, Jacobians,
+    gains and ΔV bit-identical to the oracle, then the forward pass picks the same α and J."""
+    p = tog.Problems.quadrotor_maze()
+    pinf = tog.infeasible_problem(p, 0.001)
+    opts = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(square_root=sqrt))
+    h = tog.AugmentedLagrangianSolver(pinf, opts).handle
+    o = oracle.OracleSolver(pinf, opts)
+    h.slack_controls()
+    o.slack_controls()
+    h.update_constraints()
+    o.update_constraints()
+    assert rel(h.get(tog.abi.FIELD_C)[0], o.get("C")) == 0.0
+    J0 = o.cost(True)
+    assert h.cost(al=True)[0] == J0
+    h.jacobians()
+    o.jacobians()
+    dV = h.backward_pass(sqrt=sqrt, al=True)[0]
+    assert o.cost_expansion(sqrt, True) == 0
+    dVo, _ = o.backward(sqrt)
+    assert rel(h.get(tog.abi.FIELD_K)[0], o.get("K")) < TOL_STEP
+    assert rel(h.get(tog.abi.FIELD_D)[0], o.get("d")) < TOL_STEP
+    assert rel(dV, dVo) < TOL_STEP
+    assert h.forward_pass(J0, al=True)[0] == o.forward(J0, True)

@@ -6,14 +6,18 @@ sys.path.insert(0, str(ROOT))
 import __graft_entry__ as g
 tog = g.load_package(); orc = g.load_oracle(); abi = tog.abi
 
-def trace(prob, opts, b=0, nsteps=200):
+def trace(prob, opts, b=0, nsteps=200, slack=False):
     o = orc.OracleSolver(prob, opts, b=b)
+    if slack:
+        o.slack_controls()
     steps = o.solve()
     tr = o.trace()
     p1 = prob.copy(); p1.x0 = prob.x0[b:b+1].copy(); p1._X = prob._X[b:b+1].copy(); p1._U = prob._U[b:b+1].copy(); p1.batched = True
     s = tog.AbstractSolverFor(p1, opts)
     h = s.handle
-    mode = abi.MODE_AL if isinstance(opts, tog.AugmentedLagrangianSolverOptions) and prob.is_constrained() else abi.MODE_ILQR
+    mode = abi.MODE_AL if isinstance(opts, (tog.AugmentedLagrangianSolverOptions, tog.ALTROSolverOptions)) and prob.is_constrained() else abi.MODE_ILQR
+    if slack:
+        h.slack_controls()
     h.solve_init(mode)
     rows = []
     for i in range(min(nsteps, len(tr))):
@@ -38,3 +42,11 @@ if which == "quad":
 elif which == "obs":
     prob, opts = tog.Problems.config_quad_maze(B=2, N=101)
     trace(prob, opts, b=0)
+elif which == "maze_inf":
+    prob = tog.Problems.quadrotor_maze()
+    il = tog.iLQRSolverOptions(iterations=300)
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=il, iterations=40, cost_tolerance=1e-5,
+                                              cost_tolerance_intermediate=1e-4, constraint_tolerance=1e-3,
+                                              penalty_scaling=10.0, penalty_initial=1.0)
+    opts = tog.ALTROSolverOptions(resolve_feasible_problem=False, opts_al=al, R_inf=0.001)
+    trace(tog.infeasible_problem(prob, opts.R_inf), opts, b=0, slack=True)

@@ -440,7 +440,9 @@ template <class M, bool SQRT>
 struct BwdLds {
   static constexpr int n = M::n, m = M::m, L = n + m;
   static constexpr int PC = pcap_of<M>();
-  static constexpr int WR = n + (n > PC ? n : PC);  // QR workspace rows
+  static constexpr int WR = n + (n > PC ? n : PC);  // QR workspace rows ([Q.xx; Iμ cx])
+  // QR workspace: [Q.xx; √Iμ cx] (WR x n) and [Q.uu; √Iμ cu] ((m + PC) x m; larger when m > n)
+  static constexpr int WQ = WR * n > (m + PC) * m ? WR * n : (m + PC) * m;
   double S[n * n];
   double s[n];
   double AB[n * L];
@@ -456,7 +458,7 @@ struct BwdLds {
   double KtQ[n * m];
   double tmp1[n * m];
   double tmp2[m * m];
-  double Wq[WR * n];   // QR workspace
+  double Wq[WQ];       // QR workspace
   double xk[n];
   double uk[m];
   double cval[PC], wv[PC], wsv[PC], gv[PC];
@@ -525,8 +527,7 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
   for (int e = lane; e < p * n; e += WAVE) sh.cx[e] = 0.0;
   for (int e = lane; e < p * m; e += WAVE) sh.cu[e] = 0.0;
   wsync();
-  if (lane < p) {
-    const int r = lane;
+  for (int r = lane; r < p; r += WAVE) {  // p may exceed the wave (PCAP > 64)
     const double c = row_value(rows[r], sh.xk, term ? nullptr : sh.uk);
     const double l = lam[r];
     const bool a = row_inequality(rows[r]) ? ((c >= 0.0) || (l > 0.0)) : true;
