@@ -301,6 +301,8 @@ def test_gpu_quadrotor_maze_infeasible(tog, oracle, gpu):
     Xo, Uo, si, _ = oracle.solve_altro_infeasible(ref, opts)
     assert rel(p.X, Xo) < TOL_SOLVE and rel(p.U, Uo) < TOL_SOLVE
     assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+    # the reference's (commented-out) assertion, infeasible_tests.jl:69-70
+    assert tog.max_violation(p) < opts.opts_al.constraint_tolerance
 
 
 @pytest.mark.gpu
