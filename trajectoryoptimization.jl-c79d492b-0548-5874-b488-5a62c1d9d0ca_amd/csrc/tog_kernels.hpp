@@ -1708,6 +1708,8 @@ struct ModelLaunch {
     const long long total = B * (long long)(N - 1) * NCH;
     if (integ == TOG_RK4)
       hipLaunchKernelGGL((k_jacobian<M, TOG_RK4, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+    else if (integ == TOG_MIDPOINT)
+      hipLaunchKernelGGL((k_jacobian<M, TOG_MIDPOINT, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
     else
       hipLaunchKernelGGL((k_jacobian<M, TOG_RK3, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
   }
