@@ -245,6 +245,14 @@ void tog_default_options(tog_options* opts);
    augmented_lagrangian_solver.jl:120-140. Allocates every device buffer. */
 int32_t tog_create(const tog_problem_desc* desc, const tog_options* opts, int32_t device,
                    tog_handle** out);
+/* One handle over several devices (one process driving ndev GPUs, e.g. the single Julia process):
+   the batch is split into ndev contiguous slices, one device each (sizes differ by at most one,
+   earlier devices take the remainder). Every entry point fans out over the slices and host arrays
+   are split/gathered along the batch axis; tog_batch_stats reduces over devices. The per-device
+   pointers of tog_get_device_ptr / tog_batch_stats_device and tog_set_stream are
+   TOG_ERR_UNSUPPORTED on such a handle. devices may repeat (several slices on one GPU). */
+int32_t tog_create_multi(const tog_problem_desc* desc, const tog_options* opts, const int32_t* devices,
+                         int32_t ndev, tog_handle** out);
 int32_t tog_destroy(tog_handle* h);
 /* use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream */
 int32_t tog_set_stream(tog_handle* h, void* hip_stream);

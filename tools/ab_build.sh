@@ -7,7 +7,7 @@ src="$(cd "$(dirname "$0")/.." && pwd)/trajectoryoptimization.jl-c79d492b-0548-5
 out="$(cd "$(dirname "$0")/.." && pwd)/build_ab/$name"
 mkdir -p "$out"
 cd "$out"
-for f in tog_runtime.cpp k_double_integrator.hip k_cartpole.hip k_quadrotor.hip k_car.hip k_pendulum.hip k_kuka.hip; do
+for f in tog_runtime.cpp $(cd "$src" && ls k_*.hip); do
   x=""; [ "$f" = tog_runtime.cpp ] && x="-x hip"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function $flags $x -c "$src/$f" -o "${f%.*}.o" &
 done

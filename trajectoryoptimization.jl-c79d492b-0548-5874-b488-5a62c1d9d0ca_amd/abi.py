@@ -200,6 +200,8 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_device_count.restype = C.c_int32
     lib.tog_default_options.argtypes = [C.POINTER(tog_options)]
     lib.tog_create.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_options), C.c_int32, C.POINTER(vp)]
+    lib.tog_create_multi.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_options), _ip, C.c_int32,
+                                     C.POINTER(vp)]
     lib.tog_destroy.argtypes = [vp]
     lib.tog_set_stream.argtypes = [vp, vp]
     lib.tog_synchronize.argtypes = [vp]
@@ -227,7 +229,7 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_last_error.restype = C.c_char_p
     lib.tog_dynamics_bias.argtypes = [C.c_int32, _dp, _dp]
     lib.tog_slack_controls.argtypes = [vp]
-    for name in ("tog_create", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
+    for name in ("tog_create", "tog_create_multi", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
@@ -242,7 +244,8 @@ def load_library(path: os.PathLike | None = None):
 
 
 EXPORTED_SYMBOLS = (
-    "tog_version", "tog_device_count", "tog_default_options", "tog_create", "tog_destroy", "tog_set_stream",
+    "tog_version", "tog_device_count", "tog_default_options", "tog_create", "tog_create_multi", "tog_destroy",
+    "tog_set_stream",
     "tog_synchronize", "tog_set_state", "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims",
     "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",

@@ -1198,7 +1198,10 @@ attempt:
 // =============================================================================================
 constexpr int FTEAM = 32;
 constexpr int LS_MAX_ROUNDS = 2;  // speculative line-search rounds per forward pass
-constexpr int LS_FIRST = 8;       // width of the first round
+#ifndef TOG_LS_FIRST
+#define TOG_LS_FIRST 8
+#endif
+constexpr int LS_FIRST = TOG_LS_FIRST;  // width of the first round
 
 __device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS traffic within the wave
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

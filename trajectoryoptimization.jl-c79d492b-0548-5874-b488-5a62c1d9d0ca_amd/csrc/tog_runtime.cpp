@@ -69,6 +69,10 @@ struct tog_handle {
   std::vector<hipEvent_t> ev_pool;
   std::vector<int> ev_kind;  // kernel id per recorded (start, end) pair
   size_t ev_used = 0;
+  // tog_create_multi: a handle over several devices owns one plain handle per device, each with a
+  // contiguous slice [part_off[i], part_off[i+1]) of the batch; every entry point fans out
+  std::vector<tog_handle*> parts;
+  std::vector<long long> part_off;
 };
 
 static hipEvent_t next_event(tog_handle* h) {
@@ -320,8 +324,53 @@ void tog_default_options(tog_options* o) {
 
 const char* tog_last_error(void) { return g_err.c_str(); }
 
+
+// =============================================================================================
+// Multi-device handles (tog_create_multi): the batch is split into
+// contiguous slices, one plain handle (device buffers + stream) per device. Trajectories are
+// independent (§8(e)), so every step-level and solve-level call is the same call on each slice;
+// launches are asynchronous per device, so the devices run concurrently. Host arrays are split
+// and gathered along the batch axis, which is the outermost axis of every field.
+// =============================================================================================
+static bool is_multi(const tog_handle* h) { return h && !h->parts.empty(); }
+
+// doubles per trajectory of a host-side field array (tog_get / tog_set layouts)
+static size_t per_traj(const tog_handle* h, int field) {
+  const size_t n = h->n, m = h->m, N = h->N, P1 = h->pmax > 0 ? h->pmax : 1;
+  switch (field) {
+    case TOG_FIELD_X: case TOG_FIELD_XBAR: return N * n;
+    case TOG_FIELD_U: case TOG_FIELD_UBAR: case TOG_FIELD_D: return (N - 1) * m;
+    case TOG_FIELD_K: return (N - 1) * m * n;
+    case TOG_FIELD_A: return (N - 1) * n * n;
+    case TOG_FIELD_B: return (N - 1) * n * m;
+    case TOG_FIELD_S: return N * n * n;
+    case TOG_FIELD_SX: return N * n;
+    case TOG_FIELD_DV: case TOG_FIELD_RHO: return 2;
+    case TOG_FIELD_LAMBDA: case TOG_FIELD_MU: case TOG_FIELD_C: return N * P1;
+    case TOG_FIELD_X0: return n;
+    case TOG_FIELD_STATS: return TOG_NSTATS;
+  }
+  return 0;
+}
+
+extern "C++" {
+template <class F>
+static int32_t each_part(tog_handle* h, F&& fn) {
+  for (size_t i = 0; i < h->parts.size(); i++) {
+    int32_t rc = fn(h->parts[i], (size_t)h->part_off[i]);
+    if (rc) return rc;
+  }
+  return TOG_OK;
+}
+}  // extern "C++"
+
 int32_t tog_destroy(tog_handle* h) {
   if (!h) return TOG_OK;
+  if (is_multi(h)) {
+    for (tog_handle* p : h->parts) tog_destroy(p);
+    delete h;
+    return TOG_OK;
+  }
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : h->allocs) (void)hipFree(p);
@@ -493,8 +542,47 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   return TOG_OK;
 }
 
+int32_t tog_create_multi(const tog_problem_desc* d, const tog_options* opts, const int32_t* devices,
+                         int32_t ndev, tog_handle** out) {
+  if (!d || !opts || !devices || !out) return fail(TOG_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (ndev < 1) return fail(TOG_ERR_ARG, "ndev must be >= 1");
+  if (d->batch < ndev) return fail(TOG_ERR_ARG, "batch must be >= ndev");
+  tog_handle* h = new tog_handle();
+  const long long B = d->batch, base = B / ndev, rem = B % ndev;
+  long long off = 0;
+  for (int i = 0; i < ndev; i++) {
+    tog_problem_desc di = *d;
+    di.batch = base + (i < rem ? 1 : 0);
+    tog_handle* p = nullptr;
+    int32_t rc = tog_create(&di, opts, devices[i], &p);
+    if (rc) {
+      const std::string msg = g_err;
+      tog_destroy(h);
+      return fail(rc, "device " + std::to_string(devices[i]) + ": " + msg);
+    }
+    h->parts.push_back(p);
+    h->part_off.push_back(off);
+    off += di.batch;
+  }
+  h->part_off.push_back(off);
+  tog_handle* p0 = h->parts[0];
+  h->device = p0->device;
+  h->model = p0->model;
+  h->integ = p0->integ;
+  h->n = p0->n;
+  h->m = p0->m;
+  h->N = p0->N;
+  h->pmax = p0->pmax;
+  h->B = B;
+  h->opts = *opts;
+  *out = h;
+  return TOG_OK;
+}
+
 int32_t tog_set_stream(tog_handle* h, void* s) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return fail(TOG_ERR_UNSUPPORTED, "tog_set_stream: a multi-device handle owns one stream per device");
   HIPCHECK(hipSetDevice(h->device));
   HIPCHECK(hipStreamSynchronize(h->stream));
   if (h->own_stream) HIPCHECK(hipStreamDestroy(h->stream));
@@ -510,6 +598,7 @@ int32_t tog_set_stream(tog_handle* h, void* s) {
 
 int32_t tog_synchronize(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_synchronize(p); });
   HIPCHECK(hipSetDevice(h->device));
   HIPCHECK(hipStreamSynchronize(h->stream));
   return TOG_OK;
@@ -549,6 +638,7 @@ static size_t field_count(tog_handle* h, int field, double** dptr) {
 
 int32_t tog_get_device_ptr(tog_handle* h, int32_t field, void** dptr) {
   if (!h || !dptr) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) return fail(TOG_ERR_UNSUPPORTED, "device pointers are per device: use the per-device handles");
   double* p = nullptr;
   field_count(h, field, &p);
   if (field == TOG_FIELD_STATS) {
@@ -574,6 +664,11 @@ static int put_states(tog_handle* h, const std::vector<TrajState>& st) {
 
 int32_t tog_get(tog_handle* h, int32_t field, double* out) {
   if (!h || !out) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    const size_t w = per_traj(h, field);
+    if (!w) return fail(TOG_ERR_ARG, "unknown field");
+    return each_part(h, [&](tog_handle* p, size_t o) { return tog_get(p, field, out + o * w); });
+  }
   HIPCHECK(hipSetDevice(h->device));
   const size_t n = h->n, m = h->m, N = h->N, B = h->B;
   DevBuffers& b = h->buf;
@@ -628,6 +723,11 @@ int32_t tog_get(tog_handle* h, int32_t field, double* out) {
 
 int32_t tog_set(tog_handle* h, int32_t field, const double* in) {
   if (!h || !in) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    const size_t w = per_traj(h, field);
+    if (!w) return fail(TOG_ERR_ARG, "unknown field");
+    return each_part(h, [&](tog_handle* p, size_t o) { return tog_set(p, field, in + o * w); });
+  }
   HIPCHECK(hipSetDevice(h->device));
   if (field == TOG_FIELD_DV || field == TOG_FIELD_RHO) {
     std::vector<TrajState> st;
@@ -656,6 +756,12 @@ int32_t tog_set(tog_handle* h, int32_t field, const double* in) {
 
 int32_t tog_set_state(tog_handle* h, const double* x0, const double* U, const double* X) {
   if (!h || !x0 || !U) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    const size_t n = h->n, m = h->m, N = h->N;
+    return each_part(h, [&](tog_handle* p, size_t o) {
+      return tog_set_state(p, x0 + o * n, U + o * (N - 1) * m, X ? X + o * N * n : nullptr);
+    });
+  }
   HIPCHECK(hipSetDevice(h->device));
   const size_t n = h->n, m = h->m, N = h->N, B = h->B;
   HIPCHECK(hipMemcpyAsync(h->buf.x0, x0, sizeof(double) * B * n, hipMemcpyHostToDevice, h->stream));
@@ -674,6 +780,7 @@ int32_t tog_set_state(tog_handle* h, const double* x0, const double* U, const do
 // ------------------------------------------------------------------------------ step level
 int32_t tog_rollout_open_loop(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_rollout_open_loop(p); });
   HIPCHECK(hipSetDevice(h->device));
   h->ops->rollout_open(h->dP, h->buf, h->B, h->integ, h->stream);
   HIPCHECK(hipGetLastError());
@@ -682,6 +789,7 @@ int32_t tog_rollout_open_loop(tog_handle* h) {
 
 int32_t tog_slack_controls(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_slack_controls(p); });
   if (!h->ops->slack) return fail(TOG_ERR_ARG, "slack_controls needs a TOG_PROB_INFEASIBLE handle");
   HIPCHECK(hipSetDevice(h->device));
   h->ops->slack_controls(h->dP, h->buf, h->B, h->integ, h->stream);
@@ -691,6 +799,7 @@ int32_t tog_slack_controls(tog_handle* h) {
 
 int32_t tog_jacobians(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_jacobians(p); });
   HIPCHECK(hipSetDevice(h->device));
   h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream);
   HIPCHECK(hipGetLastError());
@@ -699,6 +808,7 @@ int32_t tog_jacobians(tog_handle* h) {
 
 int32_t tog_update_constraints(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_update_constraints(p); });
   HIPCHECK(hipSetDevice(h->device));
   h->ops->update_constraints(h->dP, h->buf, h->B, h->stream);
   HIPCHECK(hipGetLastError());
@@ -707,6 +817,8 @@ int32_t tog_update_constraints(tog_handle* h) {
 
 int32_t tog_cost(tog_handle* h, int32_t al, double* J_out) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h))
+    return each_part(h, [&](tog_handle* p, size_t o) { return tog_cost(p, al, J_out ? J_out + o : nullptr); });
   HIPCHECK(hipSetDevice(h->device));
   h->ops->cost(h->dP, h->buf, h->B, al, 0, h->d_scratch, h->stream);
   HIPCHECK(hipGetLastError());
@@ -719,6 +831,10 @@ int32_t tog_cost(tog_handle* h, int32_t al, double* J_out) {
 
 int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, double* dV_out) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h))
+    return each_part(h, [&](tog_handle* p, size_t o) {
+      return tog_backward_pass(p, sq, al, flags, dV_out ? dV_out + 2 * o : nullptr);
+    });
   HIPCHECK(hipSetDevice(h->device));
   if (sq && !h->hostP.sqrt_ok) return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass");
   if ((flags & TOG_BP_STORE_S) && !h->buf.Sdbg) {
@@ -734,6 +850,10 @@ int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, 
 
 int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double* J_out) {
   if (!h || !J_prev) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h))
+    return each_part(h, [&](tog_handle* p, size_t o) {
+      return tog_forward_pass(p, al, J_prev + o, J_out ? J_out + o : nullptr);
+    });
   HIPCHECK(hipSetDevice(h->device));
   HIPCHECK(hipMemcpyAsync(h->d_scratch, J_prev, sizeof(double) * h->B, hipMemcpyHostToDevice, h->stream));
   h->ops->forward(h->dP, h->buf, h->B, h->integ, al ? TOG_MODE_AL : TOG_MODE_ILQR, 0, h->d_scratch, h->d_scratch2,
@@ -748,6 +868,8 @@ int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double
 
 int32_t tog_rollout(tog_handle* h, double alpha, int32_t* ok_out) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h))
+    return each_part(h, [&](tog_handle* p, size_t o) { return tog_rollout(p, alpha, ok_out ? ok_out + o : nullptr); });
   HIPCHECK(hipSetDevice(h->device));
   h->ops->rollout(h->dP, h->buf, h->B, h->integ, alpha, h->d_iscratch, h->stream);
   HIPCHECK(hipGetLastError());
@@ -761,6 +883,10 @@ int32_t tog_rollout(tog_handle* h, double alpha, int32_t* ok_out) {
 // ------------------------------------------------------------------------------ solve level
 int32_t tog_solve_init(tog_handle* h, int32_t mode) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) {
+    h->mode = mode;
+    return each_part(h, [&](tog_handle* p, size_t) { return tog_solve_init(p, mode); });
+  }
   if (mode != TOG_MODE_ILQR && mode != TOG_MODE_AL) return fail(TOG_ERR_ARG, "mode");
   HIPCHECK(hipSetDevice(h->device));
   h->mode = mode;
@@ -771,6 +897,7 @@ int32_t tog_solve_init(tog_handle* h, int32_t mode) {
 
 int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t) { return tog_solve_step(p, nsteps); });
   HIPCHECK(hipSetDevice(h->device));
   const int al = (h->mode == TOG_MODE_AL);
   for (int i = 0; i < nsteps; i++) {
@@ -786,6 +913,7 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
 
 int32_t tog_batch_stats_device(tog_handle* h, void* dptr3) {
   if (!h || !dptr3) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) return fail(TOG_ERR_UNSUPPORTED, "device pointers are per device: use tog_batch_stats");
   HIPCHECK(hipSetDevice(h->device));
   hipLaunchKernelGGL(k_batch_stats, dim3(1), dim3(1024), 0, h->stream, h->buf.st, (long long)h->B, (double*)dptr3);
   HIPCHECK(hipGetLastError());
@@ -794,6 +922,24 @@ int32_t tog_batch_stats_device(tog_handle* h, void* dptr3) {
 
 int32_t tog_batch_stats(tog_handle* h, double* out3) {
   if (!h || !out3) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    // queue every device's reduction first, then gather: [Σ n_active, Σ J, max c_max]
+    for (tog_handle* p : h->parts) {
+      int32_t rc = tog_batch_stats_device(p, p->d_stats);
+      if (rc) return rc;
+    }
+    out3[0] = 0.0, out3[1] = 0.0, out3[2] = 0.0;
+    for (tog_handle* p : h->parts) {
+      double v[3];
+      HIPCHECK(hipSetDevice(p->device));
+      HIPCHECK(hipMemcpyAsync(v, p->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, p->stream));
+      HIPCHECK(hipStreamSynchronize(p->stream));
+      out3[0] += v[0];
+      out3[1] += v[1];
+      out3[2] = v[2] > out3[2] ? v[2] : out3[2];
+    }
+    return TOG_OK;
+  }
   int rc = tog_batch_stats_device(h, h->d_stats);
   if (rc) return rc;
   HIPCHECK(hipMemcpyAsync(out3, h->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, h->stream));
@@ -803,6 +949,17 @@ int32_t tog_batch_stats(tog_handle* h, double* out3) {
 
 int32_t tog_total_steps(tog_handle* h, int64_t* out) {
   if (!h || !out) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    int64_t t = 0;
+    int32_t rc = each_part(h, [&](tog_handle* p, size_t) {
+      int64_t v = 0;
+      int32_t r = tog_total_steps(p, &v);
+      t += v;
+      return r;
+    });
+    *out = t;
+    return rc;
+  }
   std::vector<TrajState> st;
   int rc = get_states(h, st);
   if (rc) return rc;
@@ -829,6 +986,7 @@ int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps) {
 
 int32_t tog_profile(tog_handle* h, int32_t enable) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t) { return tog_profile(p, enable); });
   HIPCHECK(hipSetDevice(h->device));
   if (enable) {
     HIPCHECK(hipStreamSynchronize(h->stream));
@@ -841,6 +999,19 @@ int32_t tog_profile(tog_handle* h, int32_t enable) {
 
 int32_t tog_profile_read(tog_handle* h, double* total_ms, int64_t* launches) {
   if (!h || !total_ms || !launches) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {  // summed over devices
+    double ms[TOG_NKERNELS] = {0};
+    int64_t ln[TOG_NKERNELS] = {0};
+    int32_t rc = each_part(h, [&](tog_handle* p, size_t) {
+      double a[TOG_NKERNELS];
+      int64_t b[TOG_NKERNELS];
+      int32_t r = tog_profile_read(p, a, b);
+      for (int i = 0; i < TOG_NKERNELS; i++) ms[i] += a[i], ln[i] += b[i];
+      return r;
+    });
+    for (int i = 0; i < TOG_NKERNELS; i++) total_ms[i] = ms[i], launches[i] = ln[i];
+    return rc;
+  }
   HIPCHECK(hipSetDevice(h->device));
   HIPCHECK(hipStreamSynchronize(h->stream));
   for (int i = 0; i < TOG_NKERNELS; i++) {
@@ -858,6 +1029,7 @@ int32_t tog_profile_read(tog_handle* h, double* total_ms, int64_t* launches) {
 
 int32_t tog_status(tog_handle* h, int32_t* flags_out) {
   if (!h || !flags_out) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t o) { return tog_status(p, flags_out + o); });
   std::vector<TrajState> st;
   int rc = get_states(h, st);
   if (rc) return rc;

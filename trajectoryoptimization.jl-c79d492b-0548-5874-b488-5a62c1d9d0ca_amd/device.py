@@ -11,13 +11,21 @@ from . import abi
 
 
 class BatchHandle:
-    def __init__(self, prob, opts: abi.tog_options, device: int = 0, stream=None):
+    def __init__(self, prob, opts: abi.tog_options, device: int = 0, stream=None, devices=None):
+        """``devices``: a list of HIP device ids for one handle over several GPUs
+        (tog_create_multi: the batch is split into contiguous slices, one per entry)."""
         self.lib = abi.load_library()
         self.desc_builder = prob.build_desc()
         self.opts = opts
         h = C.c_void_p()
-        abi.check(self.lib, self.lib.tog_create(C.byref(self.desc_builder.desc), C.byref(opts), int(device),
-                                                C.byref(h)))
+        if devices is not None:
+            devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
+            abi.check(self.lib, self.lib.tog_create_multi(C.byref(self.desc_builder.desc), C.byref(opts),
+                                                          devs.ctypes.data_as(C.POINTER(C.c_int32)), len(devs),
+                                                          C.byref(h)))
+        else:
+            abi.check(self.lib, self.lib.tog_create(C.byref(self.desc_builder.desc), C.byref(opts), int(device),
+                                                    C.byref(h)))
         self.h = h
         dims = (C.c_int64 * 6)()
         abi.check(self.lib, self.lib.tog_dims(self.h, dims))

@@ -175,10 +175,10 @@ class AbstractSolver:
 
     mode = abi.MODE_ILQR
 
-    def __init__(self, prob, opts, device: int = 0, stream=None):
+    def __init__(self, prob, opts, device: int = 0, stream=None, devices=None):
         self.opts = opts
         self.stats: dict = {}
-        self.handle = BatchHandle(prob, to_tog_options(opts), device=device, stream=stream)
+        self.handle = BatchHandle(prob, to_tog_options(opts), device=device, stream=stream, devices=devices)
         self.n, self.m, self.N = prob.model.n, prob.model.m, prob.N
 
     def size(self):
