@@ -93,9 +93,15 @@ def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
         steps2 = orc.solve_batch(prob, opts, nthreads=threads)
         dt2 = time.perf_counter() - t
         steps, dt, B = steps + steps2, dt + dt2, B + B2
+    # single-thread rate next to the reference's published per-core figures
+    p1, o1 = pkg.Problems.config_quadrotor(B=1, offset=300000)
+    t1 = time.perf_counter()
+    s1 = orc.solve_batch(p1, o1, nthreads=1)
+    d1 = time.perf_counter() - t1
     return {"value": steps / dt, "unit": "iLQR iterations/s", "cores": threads, "kind": "port",
             "sample": f"{B} config-3 trajectories solved to AL convergence ({steps} iLQR steps, "
-                      f"{dt:.1f} s) by oracle/tog_oracle.c, OpenMP over trajectories"}
+                      f"{dt:.1f} s) by oracle/tog_oracle.c, OpenMP over trajectories",
+            "single_thread": {"value": s1 / d1, "sample": f"1 trajectory, {s1} iLQR steps, {d1:.1f} s"}}
 
 
 def main():
@@ -106,7 +112,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU (default: the config's)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="quadrotor")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

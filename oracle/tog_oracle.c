@@ -44,7 +44,7 @@ typedef struct {
   double p[DMAX];
 } dual;
 
-static int g_nd = 0; /* number of active partials (0 => primal evaluation) */
+static _Thread_local int g_nd = 0; /* number of active partials (0 => primal evaluation); per thread: oc_solve_batch runs trajectories on OpenMP threads */
 
 static inline dual dc(double v) {
   dual r;
