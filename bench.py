@@ -40,6 +40,10 @@ WORKLOADS = {
     "quad_maze": ("config_quad_maze", 8192, True,
                   "quad_obs maze N=201, AL-iLQR, bounds + 4 cylinders + 3 spheres (BASELINE.json configs[3], per-GPU shard)",
                   "synthetic (seeded x0[1:3] ~ U([-5,5]x[-3,0]x[8,12]), U0 = hover + 0.1 N(0,1))"),
+    "maze_infeasible": ("config_quadrotor_maze_infeasible", 1024, True,
+                        "quadrotor_maze infeasible-start AL phase (SURVEY.md §8(f) row 1): m = 4 + 13 slack controls, "
+                        "69 constraint rows per knot, N=101",
+                        "synthetic (seeded maze way-points + N(0, 0.5^2), hover U0, slack controls from the guess)"),
     "kuka": ("config_kuka", 4096, True,
              "Kuka iiwa 7-DoF (RBD), AL-iLQR, terminal goal, notebook options (BASELINE.json configs[4])",
              "synthetic (seeded x0[1:7] ~ U(-0.2,0.2), U0 = hold torque at x0)"),
@@ -154,6 +158,8 @@ def main():
         abi.check(h.lib, h.lib.tog_batch_stats_device(h.h, ctypes.c_void_p(stats_t.data_ptr())))
         pkg.distributed.reduce_stats(stats_t, gathered, dist)
 
+    if prob.model.slack:  # infeasible start: slack_controls(prob) before the solve (infeasible.jl:63-80)
+        h.slack_controls()
     h.solve_init(abi.MODE_AL if al_mode else abi.MODE_ILQR)
     h.solve_step(args.warmup)
     h.synchronize()

@@ -8,7 +8,7 @@ import math
 import numpy as np
 
 from .problem import (BoundConstraint, CircleConstraints, Constraints, Dynamics, LQRObjective, Problem,
-                      discretize_model,
+                      discretize_model, infeasible_problem,
                       SphereConstraints, goal_constraint, rk3, rk4)
 from .solvers import ALTROSolverOptions, AugmentedLagrangianSolverOptions, iLQRSolverOptions
 
@@ -332,7 +332,7 @@ def interp_rows(N, tf, X):
     return np.stack([CubicSpline(t1, X[i], bc_type="natural")(t2) for i in range(X.shape[0])])
 
 
-def quadrotor_maze(N=101):
+def quadrotor_maze(N=101, waypoints=None):
     """problems/quadrotor_maze.jl:1-114: quadrotor (rk3) through 38 cylinders, u in [0, 50],
     x/z box, terminal box on position/velocity; initial controls hover, initial *state* guess
     interp_rows of 7 way-points — an infeasible start (ALTRO solves it via slack controls)."""
@@ -387,10 +387,43 @@ def quadrotor_maze(N=101):
     obj = LQRObjective(Q, R, Qf, xf, N)
     U0 = HOVER * np.ones((N - 1, m))
     prob = Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
-    Xg = np.zeros((n, 7))
+    prob.X = _maze_guess(N, tf, x0, xf, waypoints)
+    return prob
+
+
+_MAZE_WAYPOINTS = np.array([[0, -12.5, -20, -12.5, 0], [15, 20, 30, 40, 45], [10, 10, 10, 10, 10]], dtype=float)
+
+
+def _maze_guess(N, tf, x0, xf, waypoints=None):
+    """X_guess of problems/quadrotor_maze.jl:107-114 through interp_rows: (N, n)."""
+    Xg = np.zeros((len(x0), 7))
     Xg[:, 0] = x0
     Xg[:, 6] = xf
-    Xg[0:3, 1:6] = [[0, -12.5, -20, -12.5, 0], [15, 20, 30, 40, 45], [10, 10, 10, 10, 10]]
-    Xg[3:7, :] = q0[:, None]
-    prob.X = interp_rows(N, tf, Xg).T
-    return prob
+    Xg[0:3, 1:6] = _MAZE_WAYPOINTS if waypoints is None else waypoints
+    Xg[3:7, :] = np.array([1.0, 0.0, 0.0, 0.0])[:, None]
+    return interp_rows(N, tf, Xg).T
+
+
+def maze_altro_options():
+    """test/infeasible_tests.jl:57-76 (the reference's quadrotor_maze case)."""
+    il = iLQRSolverOptions(iterations=300)
+    al = AugmentedLagrangianSolverOptions(opts_uncon=il, iterations=40, cost_tolerance=1e-5,
+                                          cost_tolerance_intermediate=1e-4, constraint_tolerance=1e-3,
+                                          penalty_scaling=10.0, penalty_initial=1.0)
+    return ALTROSolverOptions(resolve_feasible_problem=False, opts_al=al, R_inf=0.001)
+
+
+def config_quadrotor_maze_infeasible(B=1024, offset=0):
+    """The quadrotor_maze infeasible-start AL phase (ALTRO with a state guess) as a batch: the five
+    interior way-points of problems/quadrotor_maze.jl jittered by N(0, 0.5^2) per coordinate (seed
+    5000+b), hover controls; returns the *infeasible* problem (slack controls still to be filled
+    by ``slack_controls``) and the ALTRO options."""
+    p0 = quadrotor_maze()
+    N = p0.N
+    Xs = _per_traj_rng(5000 + offset, B, lambda r: _maze_guess(
+        N, 5.0, p0.x0[0], p0.xf, _MAZE_WAYPOINTS + 0.5 * r.standard_normal(_MAZE_WAYPOINTS.shape)).ravel())
+    p0b = Problem(p0.model, p0.obj, np.broadcast_to(p0.U, (B, N - 1, 4)).copy(), constraints=p0.constraints,
+                  x0=np.tile(p0.x0[0], (B, 1)), xf=p0.xf, N=N, dt=p0.dt)
+    p0b.X = Xs.reshape(B, N, 13)
+    opts = maze_altro_options()
+    return infeasible_problem(p0b, opts.R_inf), opts
