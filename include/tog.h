@@ -203,7 +203,11 @@ enum tog_field {
   TOG_FIELD_C = 13,     /* (pmax,N,B)     constraint values at (X,U)           */
   TOG_FIELD_X0 = 14,    /* (n,B)                                               */
   TOG_FIELD_STATS = 15, /* (TOG_NSTATS,B) see tog_stat                         */
-  TOG_FIELD_RHO = 16    /* (2,B)          [ρ, dρ]                              */
+  TOG_FIELD_RHO = 16,   /* (2,B)          [ρ, dρ]                              */
+  TOG_FIELD_Q = 17      /* (nq,N,B)       cost expansion Q[k] from tog_cost_expansion, per knot
+                           [Q.x (n); Q.u (m); Q.xx (n,n); Q.uu (m,m); Q.ux (m,n)], nq = n+m+n²+m²+mn;
+                           the terminal knot has Q.u = Q.uu = Q.ux = 0. Valid until the next
+                           backward pass (the buffer doubles as its restart-replay scratch). */
 };
 
 /* per-trajectory statistics row (TOG_FIELD_STATS), all stored as double */
@@ -283,6 +287,17 @@ int32_t tog_cost(tog_handle* h, int32_t al, double* J_out);
    sqrt selects _backwardpass_sqrt!; al selects the AL objective; flags = tog_bp_flag.
    Uses and updates the per-trajectory ρ, dρ. dV_out: (2,B) host or NULL. */
 int32_t tog_backward_pass(tog_handle* h, int32_t sqrt, int32_t al, int32_t flags, double* dV_out);
+/* cost_expansion!(prob, solver) (ilqr_methods.jl:55-62 -> objective.jl:51-94, cost.jl:183-198; AL:
+   augmented_lagrangian_methods.jl:186-276) at (X, U) into TOG_FIELD_Q, for inspection and for
+   tests that call it apart from the backward pass (test/sqrt_bp_tests.jl:27-37). sqrt selects
+   cost_expansion_sqrt (Q.xx, Q.uu hold upper Cholesky factors); al adds the AL terms from the
+   constraint values C last evaluated (tog_update_constraints / a cost evaluation). tog_backward_pass
+   performs the same expansion fused, knot by knot, and does not read this field. */
+int32_t tog_cost_expansion(tog_handle* h, int32_t sqrt, int32_t al);
+/* solve!(prob, iLQRSolver) / solve!(prob, AugmentedLagrangianSolver) to completion:
+   tog_solve(h, TOG_MODE_ILQR | TOG_MODE_AL, iterations (x al_iterations) + 1) */
+int32_t tog_solve_ilqr(tog_handle* h);
+int32_t tog_solve_al(tog_handle* h);
 /* forwardpass! (forward_pass.jl:5-85) from the stored ΔV; J_prev (B) host pointer;
    J_out (B) host or NULL. Writes X̄, Ū. */
 int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double* J_out);

@@ -28,7 +28,7 @@ _lib = None
 FIELDS = {"X": abi.FIELD_X, "U": abi.FIELD_U, "Xbar": abi.FIELD_XBAR, "Ubar": abi.FIELD_UBAR, "K": abi.FIELD_K,
           "d": abi.FIELD_D, "A": abi.FIELD_A, "B": abi.FIELD_B, "S": abi.FIELD_S, "Sx": abi.FIELD_SX,
           "dV": abi.FIELD_DV, "lambda": abi.FIELD_LAMBDA, "mu": abi.FIELD_MU, "C": abi.FIELD_C,
-          "x0": abi.FIELD_X0, "stats": abi.FIELD_STATS, "rho": abi.FIELD_RHO}
+          "x0": abi.FIELD_X0, "stats": abi.FIELD_STATS, "rho": abi.FIELD_RHO, "Q": abi.FIELD_Q}
 
 
 def lib():
@@ -145,7 +145,7 @@ class OracleSolver:
         return {"X": (N, n), "U": (N - 1, m), "Xbar": (N, n), "Ubar": (N - 1, m), "K": (N - 1, n, m),
                 "d": (N - 1, m), "A": (N - 1, n, n), "B": (N - 1, m, n), "S": (N, n, n), "Sx": (N, n),
                 "dV": (2,), "lambda": (N, P), "mu": (N, P), "C": (N, P), "x0": (n,), "stats": (abi.NSTATS,),
-                "rho": (2,)}[name]
+                "rho": (2,), "Q": (N, n + m + n * n + m * m + m * n)}[name]
 
     def get(self, name):
         out = np.empty(self.shape(name))

@@ -2096,6 +2096,21 @@ OC_EXPORT void oc_get(oc_solver* s, int field, double* out) {
     case TOG_FIELD_C: memcpy(out, s->C, sizeof(double) * P * N); break;
     case TOG_FIELD_X0: memcpy(out, s->x0, sizeof(double) * n); break;
     case TOG_FIELD_RHO: out[0] = s->rho; out[1] = s->drho; break;
+    case TOG_FIELD_Q: { /* per knot [Q.x; Q.u; Q.xx; Q.uu; Q.ux] (terminal: u parts 0) */
+      size_t nq = (size_t)n + m + n * n + m * m + m * n;
+      memset(out, 0, sizeof(double) * nq * N);
+      for (int k = 0; k < N; k++) {
+        double* q = out + (size_t)k * nq;
+        memcpy(q, s->Qx + (size_t)k * n, sizeof(double) * n);
+        memcpy(q + n + m, s->Qxx + (size_t)k * n * n, sizeof(double) * n * n);
+        if (k < N - 1) {
+          memcpy(q + n, s->Qu + (size_t)k * m, sizeof(double) * m);
+          memcpy(q + n + m + n * n, s->Quu + (size_t)k * m * m, sizeof(double) * m * m);
+          memcpy(q + n + m + n * n + m * m, s->Qux + (size_t)k * m * n, sizeof(double) * m * n);
+        }
+      }
+      break;
+    }
     case TOG_FIELD_STATS:
       memset(out, 0, sizeof(double) * TOG_NSTATS);
       out[TOG_STAT_J] = s->J;

@@ -30,7 +30,7 @@ PROB_INFEASIBLE = 1  # tog_problem_flag
 MODE_ILQR, MODE_AL = 0, 1
 
 (FIELD_X, FIELD_U, FIELD_XBAR, FIELD_UBAR, FIELD_K, FIELD_D, FIELD_A, FIELD_B, FIELD_S, FIELD_SX,
- FIELD_DV, FIELD_LAMBDA, FIELD_MU, FIELD_C, FIELD_X0, FIELD_STATS, FIELD_RHO) = range(17)
+ FIELD_DV, FIELD_LAMBDA, FIELD_MU, FIELD_C, FIELD_X0, FIELD_STATS, FIELD_RHO, FIELD_Q) = range(18)
 
 (STAT_J, STAT_DJ, STAT_GRADIENT, STAT_ITERATIONS, STAT_ZERO_COUNT, STAT_ALPHA, STAT_Z, STAT_C_MAX,
  STAT_AL_ITER, STAT_TOTAL_STEPS, STAT_LS_TRIALS, STAT_BP_RESTARTS, STAT_FLAGS, STAT_PENALTY_MAX) = range(14)
@@ -229,12 +229,16 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_last_error.restype = C.c_char_p
     lib.tog_dynamics_bias.argtypes = [C.c_int32, _dp, _dp]
     lib.tog_slack_controls.argtypes = [vp]
+    lib.tog_cost_expansion.argtypes = [vp, C.c_int32, C.c_int32]
+    lib.tog_solve_ilqr.argtypes = [vp]
+    lib.tog_solve_al.argtypes = [vp]
     for name in ("tog_create", "tog_create_multi", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
                  "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
-                 "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls"):
+                 "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
+                 "tog_solve_ilqr", "tog_solve_al"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -250,7 +254,8 @@ EXPORTED_SYMBOLS = (
     "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
     "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
-    "tog_last_error", "tog_dynamics_bias", "tog_slack_controls",
+    "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
+    "tog_solve_al",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
 NKERNELS = 3

@@ -1658,11 +1658,194 @@ __global__ void __launch_bounds__(64) k_slack_controls(const DevProblem* __restr
   }
 }
 
+// =============================================================================================
+// k_cost_expansion: cost_expansion!(prob, solver) on its own (the backward kernels fuse it knot by
+// knot), one thread per (trajectory, knot) into Q (nq, N, B) = [Q.x; Q.u; Q.xx; Q.uu; Q.ux].
+// ilqr_methods.jl:55-62 -> objective.jl:51-94, cost.jl:183-198; AL terms
+// augmented_lagrangian_methods.jl:186-276 with the constraint values last evaluated (A.10).
+// Same operation order as oc_cost_expansion (oracle/tog_oracle.c). Inspection path: the dense
+// per-thread row Jacobians and QR workspace live in scratch memory.
+// =============================================================================================
+__device__ inline bool dev_chol_upper(double* U, const double* A, int n) {  // dpotrf 'U', A read-only
+  for (int i = 0; i < n * n; i++) U[i] = 0.0;
+  for (int j = 0; j < n; j++) {
+    double s = A[j + n * j];
+    for (int k = 0; k < j; k++) s -= U[k + n * j] * U[k + n * j];
+    if (!(s > 0.0)) return false;
+    const double ujj = sqrt(s);
+    U[j + n * j] = ujj;
+    for (int c = j + 1; c < n; c++) {
+      double t = A[j + n * c];
+      for (int k = 0; k < j; k++) t -= U[k + n * j] * U[k + n * c];
+      U[j + n * c] = t / ujj;
+    }
+  }
+  return true;
+}
+
+// R (cols x cols) of qr(Pm) for Pm (rows x cols), LAPACK dgeqr2/dlarfg as oracle qr_R
+__device__ inline void dev_qr_R(double* R, double* Pm, int rows, int cols) {
+  const int kmax = rows < cols ? rows : cols;
+  for (int j = 0; j < kmax; j++) {
+    const double alpha = Pm[j + rows * j];
+    double ss = 0.0;
+    for (int i = j + 1; i < rows; i++) ss = fma(Pm[i + rows * j], Pm[i + rows * j], ss);
+    const double xnorm = sqrt(ss);
+    if (xnorm == 0.0) continue;
+    const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+    const double tau = (beta - alpha) / beta;
+    const double sc = 1.0 / (alpha - beta);
+    for (int i = j + 1; i < rows; i++) Pm[i + rows * j] *= sc;
+    Pm[j + rows * j] = beta;
+    for (int c = j + 1; c < cols; c++) {
+      double w = Pm[j + rows * c];
+      for (int i = j + 1; i < rows; i++) w = fma(Pm[i + rows * j], Pm[i + rows * c], w);
+      w *= tau;
+      Pm[j + rows * c] -= w;
+      for (int i = j + 1; i < rows; i++) Pm[i + rows * c] = fma(-Pm[i + rows * j], w, Pm[i + rows * c]);
+    }
+  }
+  for (int j = 0; j < cols; j++)
+    for (int i = 0; i < cols; i++) R[i + cols * j] = (i <= j && i < rows) ? Pm[i + rows * j] : 0.0;
+}
+
+template <class M>
+__global__ void __launch_bounds__(64) k_cost_expansion(const DevProblem* __restrict__ P, DevBuffers Bf, int sq,
+                                                       int al, int* fail) {
+  constexpr int n = M::n, m = M::m, NQ = nq_of<M>(), PC = pcap_of<M>(), W = n > m ? n : m;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = P->N;
+  if (t >= P->B * (long long)N) return;
+  const int k = (int)(t % N);
+  const long long b = t / N;
+  const bool term = (k == N - 1);
+  double* q = Bf.Qscr + ((size_t)b * N + k) * NQ;
+  double* Qx = q;
+  double* Qu = q + n;
+  double* Qxx = q + n + m;
+  double* Quu = Qxx + n * n;
+  double* Qux = Quu + m * m;
+  for (int i = 0; i < NQ; i++) q[i] = 0.0;
+  const double* x = Bf.X + ((size_t)b * N + k) * n;
+  const double* u = term ? nullptr : Bf.U + ((size_t)b * (N - 1) + k) * m;
+  const double dt = P->dt;
+  if (!term) {  // cost.jl:183-198
+    for (int i = 0; i < n; i++) {
+      double a = 0.0, c = 0.0;
+      for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], x[j], a);
+      for (int j = 0; j < m; j++) c = fma(P->H[j + m * i], u[j], c);
+      Qx[i] = ((a + P->q[i]) + c) * dt;
+    }
+    for (int i = 0; i < m; i++) {
+      double a = 0.0, c = 0.0;
+      for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], u[j], a);
+      for (int j = 0; j < n; j++) c = fma(P->H[i + m * j], x[j], c);
+      Qu[i] = ((a + P->r[i]) + c) * dt;
+    }
+    for (int i = 0; i < n * n; i++) Qxx[i] = P->Q[i] * dt;
+    for (int i = 0; i < m * m; i++) Quu[i] = P->R[i] * dt;
+    for (int i = 0; i < m * n; i++) Qux[i] = P->H[i] * dt;
+  } else {
+    for (int i = 0; i < n * n; i++) Qxx[i] = P->Qf[i];
+    for (int i = 0; i < n; i++) {
+      double a = 0.0;
+      for (int j = 0; j < n; j++) a = fma(P->Qf[i + n * j], x[j], a);
+      Qx[i] = a + P->qf[i];
+    }
+  }
+  double Wk[(W + PC) * W];  // Cholesky / QR workspace
+  if (sq) {  // objective.jl:70-86
+    if (!dev_chol_upper(Wk, Qxx, n)) { fail[b] = 1; return; }
+    for (int i = 0; i < n * n; i++) Qxx[i] = Wk[i];
+    if (!term) {
+      if (!dev_chol_upper(Wk, Quu, m)) { fail[b] = 1; return; }
+      for (int i = 0; i < m * m; i++) Quu[i] = Wk[i];
+    }
+  }
+  const int p = P->knot_cnt[k];
+  if (!al || p == 0) return;
+  const ConRow* rows = P->rows + P->knot_off[k];
+  const int pmax = P->pmax;
+  const double* c = Bf.C + ((size_t)b * N + k) * pmax;
+  const double* lam = Bf.lam + ((size_t)b * N + k) * pmax;
+  const double* mu = Bf.mu + ((size_t)b * N + k) * pmax;
+  double cx[PC * n], cu[PC * m], w[PC], ws[PC], g[PC];
+  for (int i = 0; i < p * n; i++) cx[i] = 0.0;
+  for (int i = 0; i < p * m; i++) cu[i] = 0.0;
+  for (int r = 0; r < p; r++) {
+    const ConRow row = rows[r];
+    int idx[3];
+    double v[3];
+    const int nz = row_grad(row, x, n, idx, v);
+    for (int z = 0; z < nz; z++) {
+      if (idx[z] < n) cx[r + p * idx[z]] = v[z];
+      else if (!term) cu[r + p * (idx[z] - n)] = v[z];
+    }
+    const bool a = row_inequality(row) ? ((c[r] >= 0.0) || (lam[r] > 0.0)) : true;
+    w[r] = a ? mu[r] : 0.0;
+    ws[r] = a ? sqrt(mu[r]) : 0.0;
+    g[r] = w[r] * c[r] + lam[r];
+  }
+  if (!sq) {
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < n; i++) {
+        double s = 0.0;
+        for (int r = 0; r < p; r++) s = fma(cx[r + p * i] * w[r], cx[r + p * j], s);
+        Qxx[i + n * j] += s;
+      }
+    if (!term) {
+      for (int j = 0; j < m; j++)
+        for (int i = 0; i < m; i++) {
+          double s = 0.0;
+          for (int r = 0; r < p; r++) s = fma(cu[r + p * i] * w[r], cu[r + p * j], s);
+          Quu[i + m * j] += s;
+        }
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < m; i++) {
+          double s = 0.0;
+          for (int r = 0; r < p; r++) s = fma(cu[r + p * i] * w[r], cx[r + p * j], s);
+          Qux[i + m * j] += s;
+        }
+    }
+  } else {  // chol_plus!(Q.xx, √Iμ cx), chol_plus!(Q.uu, √Iμ cu): qr([Q; √Iμ c]).R (no ux term, A.5)
+    double R[W * W];
+    const int rx = n + p;
+    for (int j = 0; j < n; j++) {
+      for (int i = 0; i < n; i++) Wk[i + rx * j] = Qxx[i + n * j];
+      for (int r = 0; r < p; r++) Wk[n + r + rx * j] = ws[r] * cx[r + p * j];
+    }
+    dev_qr_R(R, Wk, rx, n);
+    for (int i = 0; i < n * n; i++) Qxx[i] = R[i];
+    if (!term) {
+      const int ru = m + p;
+      for (int j = 0; j < m; j++) {
+        for (int i = 0; i < m; i++) Wk[i + ru * j] = Quu[i + m * j];
+        for (int r = 0; r < p; r++) Wk[m + r + ru * j] = ws[r] * cu[r + p * j];
+      }
+      dev_qr_R(R, Wk, ru, m);
+      for (int i = 0; i < m * m; i++) Quu[i] = R[i];
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    double s = 0.0;
+    for (int r = 0; r < p; r++) s = fma(cx[r + p * i], g[r], s);
+    Qx[i] += s;
+  }
+  if (!term)
+    for (int i = 0; i < m; i++) {
+      double s = 0.0;
+      for (int r = 0; r < p; r++) s = fma(cu[r + p * i], g[r], s);
+      Qu[i] += s;
+    }
+}
+
 struct ModelOps {
   int n, m;
   int slack;  // n for an infeasible model (add_slack_controls), else 0
   int pcap;   // max constraint rows per knot of the backward kernels' LDS layout
   void (*slack_controls)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
+  void (*cost_expansion)(const DevProblem*, const DevBuffers&, long long B, int N, int sqrt, int al, int* fail,
+                         hipStream_t);
   void (*init)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, hipStream_t);
   void (*rollout_open)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*jacobian)(const DevProblem*, const DevBuffers&, long long B, int N, int integ, hipStream_t);
@@ -1807,6 +1990,11 @@ struct ModelLaunch {
         hipLaunchKernelGGL((k_slack_controls<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
     }
   }
+  static void cost_expansion(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int sq, int al,
+                             int* fail, hipStream_t st) {
+    hipLaunchKernelGGL((k_cost_expansion<M>), dim3(grid(B * (long long)N, 64)), dim3(64), 0, st, P, Bf, sq, al,
+                       fail);
+  }
   static void update_constraints(const DevProblem* P, const DevBuffers& Bf, long long B, hipStream_t st) {
     hipLaunchKernelGGL((k_update_constraints<M>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
   }
@@ -1817,6 +2005,7 @@ struct ModelLaunch {
     o.slack = ModelTraits<M>::slack;
     o.pcap = pcap_of<M>();
     o.slack_controls = slack_controls;
+    o.cost_expansion = cost_expansion;
     o.init = init;
     o.rollout_open = rollout_open;
     o.jacobian = jacobian;

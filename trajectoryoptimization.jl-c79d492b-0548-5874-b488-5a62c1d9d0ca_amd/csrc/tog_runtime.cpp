@@ -349,6 +349,7 @@ static size_t per_traj(const tog_handle* h, int field) {
     case TOG_FIELD_LAMBDA: case TOG_FIELD_MU: case TOG_FIELD_C: return N * P1;
     case TOG_FIELD_X0: return n;
     case TOG_FIELD_STATS: return TOG_NSTATS;
+    case TOG_FIELD_Q: return N * (size_t)h->nq;
   }
   return 0;
 }
@@ -574,6 +575,7 @@ int32_t tog_create_multi(const tog_problem_desc* d, const tog_options* opts, con
   h->m = p0->m;
   h->N = p0->N;
   h->pmax = p0->pmax;
+  h->nq = p0->nq;
   h->B = B;
   h->opts = *opts;
   *out = h;
@@ -631,6 +633,7 @@ static size_t field_count(tog_handle* h, int field, double** dptr) {
     case TOG_FIELD_X0: *dptr = b.x0; return B * n;
     case TOG_FIELD_S: *dptr = b.Sdbg; return B * N * n * n;
     case TOG_FIELD_SX: *dptr = b.sdbg; return B * N * n;
+    case TOG_FIELD_Q: *dptr = b.Qscr; return B * N * (size_t)h->nq;
   }
   *dptr = nullptr;
   return 0;
@@ -827,6 +830,31 @@ int32_t tog_cost(tog_handle* h, int32_t al, double* J_out) {
     HIPCHECK(hipStreamSynchronize(h->stream));
   }
   return TOG_OK;
+}
+
+int32_t tog_cost_expansion(tog_handle* h, int32_t sq, int32_t al) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t) { return tog_cost_expansion(p, sq, al); });
+  HIPCHECK(hipSetDevice(h->device));
+  HIPCHECK(hipMemsetAsync(h->d_iscratch, 0, sizeof(int) * h->B, h->stream));
+  h->ops->cost_expansion(h->dP, h->buf, h->B, h->N, sq, al, h->d_iscratch, h->stream);
+  HIPCHECK(hipGetLastError());
+  std::vector<int> f(h->B);
+  HIPCHECK(hipMemcpyAsync(f.data(), h->d_iscratch, sizeof(int) * h->B, hipMemcpyDeviceToHost, h->stream));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  for (int v : f)
+    if (v) return fail(TOG_ERR_ARG, "PosDefException: cost Hessian not positive definite (objective.jl:70-86)");
+  return TOG_OK;
+}
+
+int32_t tog_solve_ilqr(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  return tog_solve(h, TOG_MODE_ILQR, h->opts.iterations + 1);
+}
+
+int32_t tog_solve_al(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  return tog_solve(h, TOG_MODE_AL, h->opts.iterations * h->opts.al_iterations + 1);
 }
 
 int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, double* dV_out) {

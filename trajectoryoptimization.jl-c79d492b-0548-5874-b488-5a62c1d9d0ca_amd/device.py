@@ -52,6 +52,7 @@ class BatchHandle:
             abi.FIELD_SX: (B, N, n), abi.FIELD_DV: (B, 2), abi.FIELD_LAMBDA: (B, N, P),
             abi.FIELD_MU: (B, N, P), abi.FIELD_C: (B, N, P), abi.FIELD_X0: (B, n),
             abi.FIELD_STATS: (B, abi.NSTATS), abi.FIELD_RHO: (B, 2),
+            abi.FIELD_Q: (B, N, n + m + n * n + m * m + m * n),
         }[field]
 
     def get(self, field, raw=False):
@@ -99,6 +100,10 @@ class BatchHandle:
     def slack_controls(self):
         """``slack_controls(prob)`` into U[m+1:m+n] (infeasible handles, infeasible.jl:63-80)."""
         abi.check(self.lib, self.lib.tog_slack_controls(self.h))
+
+    def cost_expansion(self, sqrt=False, al=False):
+        """``cost_expansion!`` into FIELD_Q (ilqr_methods.jl:55-62)."""
+        abi.check(self.lib, self.lib.tog_cost_expansion(self.h, int(sqrt), int(al)))
 
     def jacobians(self):
         abi.check(self.lib, self.lib.tog_jacobians(self.h))
