@@ -125,14 +125,14 @@ __device__ __forceinline__ void team_rows(const DevBuffers& Bf, long long b, int
     bool isx = false, isu = false;
     if (r < p) {
       const ConRow row = cr[r];
-      const double c = row_value(row, x, u);
+      const double c = row_value<false>(row, x, u);
       const double l = lam[r];
-      const bool a = row_inequality(row) ? ((c >= 0.0) || (l > 0.0)) : true;
+      const bool a = row_inequality<false>(row) ? ((c >= 0.0) || (l > 0.0)) : true;
       RowInfo ri;
       ri.w = a ? mu[r] : 0.0;
       ri.ws = a ? sqrt(mu[r]) : 0.0;
       ri.g = ri.w * c + l;
-      ri.nnz = row_grad(row, x, n, ri.idx, ri.v);
+      ri.nnz = row_grad<false>(row, x, n, ri.idx, ri.v);
       rows[r] = ri;
       isu = (row.type == ROW_UMAX || row.type == ROW_UMIN);
       isx = !isu;

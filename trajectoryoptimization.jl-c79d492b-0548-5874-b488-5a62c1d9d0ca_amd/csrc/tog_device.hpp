@@ -846,14 +846,17 @@ __device__ __forceinline__ double terminal_cost(const DevProblem* P, const doubl
 }
 
 // constraint row value (u == nullptr at the terminal knot: only x rows exist there)
+// SLACK = false compiles the infeasible-start slack row out (plain models never have it; the extra
+// case costs the team backward kernel registers)
+template <bool SLACK = true>
 __device__ __forceinline__ double row_value(const ConRow& r, const double* x, const double* u) {
+  if (SLACK && r.type == ROW_USLACK) return u[r.idx];
   switch (r.type) {
     case ROW_XMAX: return x[r.idx] - r.a;
     case ROW_UMAX: return u[r.idx] - r.a;
     case ROW_XMIN: return r.a - x[r.idx];
     case ROW_UMIN: return r.a - u[r.idx];
     case ROW_GOAL: return x[r.idx] - r.a;
-    case ROW_USLACK: return u[r.idx];
     case ROW_CIRCLE: {
       const double dx = x[0] - r.a, dy = x[1] - r.b;
       return -((dx * dx + dy * dy) - r.r * r.r);
@@ -864,7 +867,10 @@ __device__ __forceinline__ double row_value(const ConRow& r, const double* x, co
     }
   }
 }
-__device__ __forceinline__ bool row_inequality(const ConRow& r) { return r.type != ROW_GOAL && r.type != ROW_USLACK; }
+template <bool SLACK = true>
+__device__ __forceinline__ bool row_inequality(const ConRow& r) {
+  return r.type != ROW_GOAL && (!SLACK || r.type != ROW_USLACK);
+}
 
 // The same row seen by every lane of a wave (lanes iterate knots and rows in lockstep over the
 // shared row table): make its type and index wave-uniform so that the switch is a scalar branch
@@ -877,14 +883,19 @@ __device__ __forceinline__ ConRow uniform_row(const ConRow& r) {
 }
 
 // d c / d [x; u] of a row: writes up to 3 (index, value) pairs, index in [0, n+m)
+template <bool SLACK = true>
 __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n, int* idx, double* v) {
+  if (SLACK && r.type == ROW_USLACK) {
+    idx[0] = n + r.idx;
+    v[0] = 1.0;
+    return 1;
+  }
   switch (r.type) {
     case ROW_XMAX: idx[0] = r.idx; v[0] = 1.0; return 1;
     case ROW_UMAX: idx[0] = n + r.idx; v[0] = 1.0; return 1;
     case ROW_XMIN: idx[0] = r.idx; v[0] = -1.0; return 1;
     case ROW_UMIN: idx[0] = n + r.idx; v[0] = -1.0; return 1;
     case ROW_GOAL: idx[0] = r.idx; v[0] = 1.0; return 1;
-    case ROW_USLACK: idx[0] = n + r.idx; v[0] = 1.0; return 1;
     case ROW_CIRCLE:
       idx[0] = 0; v[0] = -(2.0 * (x[0] - r.a));
       idx[1] = 1; v[1] = -(2.0 * (x[1] - r.b));

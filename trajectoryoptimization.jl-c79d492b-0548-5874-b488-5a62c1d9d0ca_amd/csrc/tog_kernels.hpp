@@ -42,6 +42,7 @@ __host__ __device__ constexpr int nq_of() {
 // AL terms λ'c + ½ c'Iμ c of one knot (augmented_lagrangian_methods.jl:298-313), rows in order. The
 // multipliers are loaded four rows at a time so their global loads overlap instead of serialising
 // one round trip per row. Ck (constraint values out) may be null.
+template <bool SLACK>
 __device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const double* lamk, const double* muk,
                                               const double* x, const double* u, double& lc, double& cIc,
                                               double* Ck) {
@@ -56,9 +57,9 @@ __device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const
     for (int q = 0; q < 4; q++) {
       if (base + q < cnt) {
         const ConRow r = uniform_row(rows[base + q]);
-        const double c = row_value(r, x, u);
+        const double c = row_value<SLACK>(r, x, u);
         const double l = lv[q];
-        const bool a = row_inequality(r) ? ((c >= 0.0) || (l > 0.0)) : true;
+        const bool a = row_inequality<SLACK>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
         const double w = a ? mv[q] : 0.0;
         lc = fma(l, c, lc);
         cIc = fma(c * w, c, cIc);
@@ -88,7 +89,7 @@ __device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& 
     const double* x = Xs + (size_t)k * n;
     const double* u = (k < N - 1) ? Us + (size_t)k * m : nullptr;
     double lc = 0.0, cIc = 0.0;
-    al_knot_terms(rows, cnt, lam + (size_t)k * pmax, mu + (size_t)k * pmax, x, u, lc, cIc,
+    al_knot_terms<(ModelTraits<M>::slack > 0)>(rows, cnt, lam + (size_t)k * pmax, mu + (size_t)k * pmax, x, u, lc, cIc,
                   Cout ? Cout + (size_t)k * pmax : nullptr);
     Jc += lc + 0.5 * cIc;
   }
@@ -1335,16 +1336,16 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
         for (int q = 0; q < RB; q++) {
           if (q < cnt) {
             const ConRow r = uniform_row(rows[q]);
-            const double c = row_value(r, xb, ub);
+            const double c = row_value<(ModelTraits<M>::slack > 0)>(r, xb, ub);
             const double l = lk[q];
-            const bool a = row_inequality(r) ? ((c >= 0.0) || (l > 0.0)) : true;
+            const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
             const double w = a ? mk[q] : 0.0;
             lc = fma(l, c, lc);
             cIc = fma(c * w, c, cIc);
           }
         }
         if (cnt > RB)
-          al_knot_terms(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB, mu + (size_t)(k - 1) * pmax + RB, xb,
+          al_knot_terms<(ModelTraits<M>::slack > 0)>(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB, mu + (size_t)(k - 1) * pmax + RB, xb,
                         ub, lc, cIc, nullptr);
         Jc += lc + 0.5 * cIc;
       }
@@ -1376,7 +1377,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     if (cnt) {
       const ConRow* rows = RT.rows + RT.koff[N - 1];
       double lc = 0.0, cIc = 0.0;
-      al_knot_terms(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax, xb, nullptr, lc, cIc,
+      al_knot_terms<(ModelTraits<M>::slack > 0)>(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax, xb, nullptr, lc, cIc,
                     nullptr);
       Jc += lc + 0.5 * cIc;
     }
