@@ -123,7 +123,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # TOG_BENCH_DIST=1 takes the torch.distributed (RCCL) path even at world size 1, to exercise the
+    # multi-rank code (stream interop, stats all-gather, job rate) on a one-GPU box
+    if world > 1 or os.environ.get("TOG_BENCH_DIST") == "1":
         import torch
         import torch.distributed as dist
 
@@ -140,7 +142,11 @@ def main():
     if dist is not None:
         import torch
 
-        stream = torch.cuda.current_stream().cuda_stream  # libtog and RCCL share one stream
+        # libtog, the stats reduction and RCCL share one stream. A dedicated stream, not torch's
+        # default: its handle is 0 (the null stream), which tog_set_stream reads as "own stream".
+        tstream = torch.cuda.Stream(device=local_rank)
+        torch.cuda.set_stream(tstream)
+        stream = tstream.cuda_stream
     solver = pkg.AbstractSolverFor(prob, opts, device=local_rank, stream=stream)
     h = solver.handle
     n, m, N = prob.model.n, prob.model.m, prob.N
