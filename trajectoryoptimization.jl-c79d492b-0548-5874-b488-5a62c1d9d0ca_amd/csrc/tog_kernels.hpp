@@ -1540,15 +1540,26 @@ __global__ void __launch_bounds__(256) k_ls_compact(const DevProblem* __restrict
 // decision (sequential acceptance logic replayed over the speculative trials, forward_pass.jl:19-65),
 // commit (in-place replay of the accepted α, or the max-iterations fallback) and bookkeeping.
 // One thread per trajectory.
+// phase 0: every active trajectory. phase 1: only those the trials [0, hi) settle (ls_decided_within);
+// phase 2: only the listed ones (k_ls_compact's list after trials [0, hi)). Phases 1 and 2 partition
+// the active trajectories, so phase 1 can run on a second stream while the second speculative round
+// evaluates the listed trajectories.
 template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
-                                                  int bookkeeping, const double* Jprev_in, double* Jout) {
+                                                  int bookkeeping, const double* Jprev_in, double* Jout, int phase,
+                                                  int hi, const int* __restrict__ list, const int* __restrict__ count) {
   extern __shared__ double commit_lds[];
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nb = (phase == 2) ? (long long)*count : P->B;
+  if ((long long)blockIdx.x * blockDim.x >= nb) return;  // whole block past the list: retire early
   const RowTables RT =
       (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, commit_lds) : global_row_tables(P);
-  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= P->B) return;
+  if (t >= nb) return;
+  const long long b = (phase == 2) ? (long long)list[t] : t;
   if (!Bf.st[b].active) return;
+  if (phase == 1 && !ls_decided_within(P->o, Bf, b, Bf.nc, bookkeeping ? Bf.st[b].J : Jprev_in[b], Bf.st[b].dV0,
+                                       Bf.st[b].dV1, hi))
+    return;
   constexpr int n = M::n, m = M::m;
   const tog_options& o = P->o;
   const bool al = (mode == TOG_MODE_AL);
@@ -1840,6 +1851,12 @@ __global__ void __launch_bounds__(64) k_cost_expansion(const DevProblem* __restr
     }
 }
 
+// a second stream on the handle's device and the fork/join events that overlap work on it
+struct StreamPair {
+  hipStream_t st2;
+  hipEvent_t fork, join;
+};
+
 struct ModelOps {
   int n, m;
   int slack;  // n for an infeasible model (add_slack_controls), else 0
@@ -1853,7 +1870,7 @@ struct ModelOps {
   void (*backward)(const DevProblem*, const DevBuffers&, long long B, int sqrt, int al, int flags, int team,
                    hipStream_t);
   void (*forward)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, int bookkeeping,
-                  const double* Jprev, double* Jout, hipStream_t);
+                  const double* Jprev, double* Jout, hipStream_t, const StreamPair* sp);
   void (*cost)(const DevProblem*, const DevBuffers&, long long B, int al, int use_bar, double* J, hipStream_t);
   void (*rollout)(const DevProblem*, const DevBuffers&, long long B, int integ, double alpha, int* ok, hipStream_t);
   void (*update_constraints)(const DevProblem*, const DevBuffers&, long long B, hipStream_t);
@@ -1929,15 +1946,45 @@ struct ModelLaunch {
       else hipLaunchKernelGGL((k_backward<M, 0, 0>), g, blk, 0, st, P, Bf, flags);
     }
   }
-  static void forward(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, int bk,
-                      const double* Jp, double* Jo, hipStream_t st) {
+  template <int INTEG>
+  static void spec(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int lo, int cnt, const int* list,
+                   const int* count, hipStream_t st) {
+    const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
+    hipLaunchKernelGGL((k_ls_spec<M, INTEG>), dim3(gs), dim3(256), (unsigned)Bf.rows_shmem, st, P, Bf, mode, lo, cnt,
+                       list, count);
+  }
+  template <int INTEG>
+  static void commit(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
+                     double* Jo, int phase, int hi, const int* list, const int* count, hipStream_t st) {
+    hipLaunchKernelGGL((k_ls_commit<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
+                       bk, Jp, Jo, phase, hi, list, count);
+  }
+  template <int INTEG>
+  static void forward_i(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
+                        double* Jo, hipStream_t st, const StreamPair* sp) {
     // speculative line search in two rounds: trials [0, 8) for every trajectory (settles ~98% of them
     // on configs 2, 3 and 5), then [8, nc) only for the trajectories the first round left undecided
     // (k_ls_compact lists them, so the second round's waves are dense). Narrower first rounds were
     // measured slower: 8 lanes sharing one trajectory's K/X/U per load is what keeps the rollouts
     // coalesced, and the Kuka's heavy lanes need the width to fill the SIMDs.
-    const unsigned sm = (unsigned)Bf.rows_shmem;
     (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_MAX_ROUNDS, st);
+    if (sp && LS_MAX_ROUNDS == 2 && Bf.nc > LS_FIRST) {
+      // the decided trajectories' commit (phase 1) overlaps the second round on a second stream;
+      // both kernels are latency bound at low occupancy
+      spec<INTEG>(P, Bf, B, mode, 0, LS_FIRST, nullptr, nullptr, st);
+      int* list = Bf.ls_list + (size_t)B;
+      int* count = Bf.ls_count + 1;
+      hipLaunchKernelGGL((k_ls_compact<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, LS_FIRST, bk, Jp, nullptr,
+                         nullptr, list, count);
+      (void)hipEventRecord(sp->fork, st);
+      (void)hipStreamWaitEvent(sp->st2, sp->fork, 0);
+      commit<INTEG>(P, Bf, B, mode, bk, Jp, Jo, 1, LS_FIRST, nullptr, nullptr, sp->st2);
+      spec<INTEG>(P, Bf, B, mode, LS_FIRST, Bf.nc - LS_FIRST, list, count, st);
+      commit<INTEG>(P, Bf, B, mode, bk, Jp, Jo, 2, LS_FIRST, list, count, st);
+      (void)hipEventRecord(sp->join, sp->st2);
+      (void)hipStreamWaitEvent(st, sp->join, 0);
+      return;
+    }
     int lo = 0, round = 0;
     const int* list = nullptr;
     const int* count = nullptr;
@@ -1951,22 +1998,17 @@ struct ModelLaunch {
         list = out;
         count = Bf.ls_count + round;
       }
-      const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
-      if (integ == TOG_RK4)
-        hipLaunchKernelGGL((k_ls_spec<M, TOG_RK4>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
-      else if (integ == TOG_MIDPOINT)
-        hipLaunchKernelGGL((k_ls_spec<M, TOG_MIDPOINT>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
-      else
-        hipLaunchKernelGGL((k_ls_spec<M, TOG_RK3>), dim3(gs), dim3(256), sm, st, P, Bf, mode, lo, cnt, list, count);
+      spec<INTEG>(P, Bf, B, mode, lo, cnt, list, count, st);
       lo += cnt;
       round++;
     }
-    if (integ == TOG_RK4)
-      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);
-    else if (integ == TOG_MIDPOINT)
-      hipLaunchKernelGGL((k_ls_commit<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);
-    else
-      hipLaunchKernelGGL((k_ls_commit<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), sm, st, P, Bf, mode, bk, Jp, Jo);
+    commit<INTEG>(P, Bf, B, mode, bk, Jp, Jo, 0, 0, nullptr, nullptr, st);
+  }
+  static void forward(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, int bk,
+                      const double* Jp, double* Jo, hipStream_t st, const StreamPair* sp) {
+    if (integ == TOG_RK4) forward_i<TOG_RK4>(P, Bf, B, mode, bk, Jp, Jo, st, sp);
+    else if (integ == TOG_MIDPOINT) forward_i<TOG_MIDPOINT>(P, Bf, B, mode, bk, Jp, Jo, st, sp);
+    else forward_i<TOG_RK3>(P, Bf, B, mode, bk, Jp, Jo, st, sp);
   }
   static void cost(const DevProblem* P, const DevBuffers& Bf, long long B, int al, int bar, double* J,
                    hipStream_t st) {

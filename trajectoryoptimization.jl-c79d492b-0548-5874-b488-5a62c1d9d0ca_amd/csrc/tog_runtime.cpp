@@ -73,6 +73,9 @@ struct tog_handle {
   // contiguous slice [part_off[i], part_off[i+1]) of the batch; every entry point fans out
   std::vector<tog_handle*> parts;
   std::vector<long long> part_off;
+  // second stream + fork/join events: the forward pass overlaps the decided trajectories' commit
+  // with the second speculative round (tog_kernels.hpp forward_i)
+  StreamPair sp = {nullptr, nullptr, nullptr};
 };
 
 static hipEvent_t next_event(tog_handle* h) {
@@ -376,6 +379,9 @@ int32_t tog_destroy(tog_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->sp.st2) (void)hipStreamDestroy(h->sp.st2);
+  if (h->sp.fork) (void)hipEventDestroy(h->sp.fork);
+  if (h->sp.join) (void)hipEventDestroy(h->sp.join);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   delete h;
   return TOG_OK;
@@ -400,6 +406,9 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   HIPCHECK(hipSetDevice(device));
   HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   h->own_stream = true;
+  HIPCHECK(hipStreamCreateWithFlags(&h->sp.st2, hipStreamNonBlocking));
+  HIPCHECK(hipEventCreateWithFlags(&h->sp.fork, hipEventDisableTiming));
+  HIPCHECK(hipEventCreateWithFlags(&h->sp.join, hipEventDisableTiming));
   h->model = d->model;
   h->integ = d->integrator;
   h->n = d->n;
@@ -885,7 +894,7 @@ int32_t tog_forward_pass(tog_handle* h, int32_t al, const double* J_prev, double
   HIPCHECK(hipSetDevice(h->device));
   HIPCHECK(hipMemcpyAsync(h->d_scratch, J_prev, sizeof(double) * h->B, hipMemcpyHostToDevice, h->stream));
   h->ops->forward(h->dP, h->buf, h->B, h->integ, al ? TOG_MODE_AL : TOG_MODE_ILQR, 0, h->d_scratch, h->d_scratch2,
-                  h->stream);
+                  h->stream, nullptr);
   HIPCHECK(hipGetLastError());
   if (J_out) {
     HIPCHECK(hipMemcpyAsync(J_out, h->d_scratch2, sizeof(double) * h->B, hipMemcpyDeviceToHost, h->stream));
@@ -933,7 +942,10 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
     timed(h, TOG_KERNEL_BACKWARD,
           [&] { h->ops->backward(h->dP, h->buf, h->B, h->opts.square_root, al, 0, h->bwd_team, h->stream); });
     timed(h, TOG_KERNEL_FORWARD,
-          [&] { h->ops->forward(h->dP, h->buf, h->B, h->integ, h->mode, 1, nullptr, nullptr, h->stream); });
+          [&] {
+            h->ops->forward(h->dP, h->buf, h->B, h->integ, h->mode, 1, nullptr, nullptr, h->stream,
+                            getenv("TOG_NO_OVERLAP") ? nullptr : &h->sp);
+          });
   }
   HIPCHECK(hipGetLastError());
   return TOG_OK;
