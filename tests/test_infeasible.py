@@ -332,3 +332,21 @@ def test_gpu_quadrotor_maze_step_level(tog, oracle, gpu, sqrt):
     assert rel(h.get(tog.abi.FIELD_D)[0], o.get("d")) < TOL_STEP
     assert rel(dV, dVo) < TOL_STEP
     assert h.forward_pass(J0, al=True)[0] == o.forward(J0, True)
+
+
+@pytest.mark.gpu
+def test_gpu_infeasible_error_paths(tog, gpu):
+    """slack_controls on a plain handle, a slack constraint in a plain problem and the unbuilt Kuka
+    slack variant fail loudly through the ABI (no silent fallback)."""
+    prob, opts = tog.Problems.config_quadrotor(B=2)
+    h = tog.AugmentedLagrangianSolver(prob, opts).handle
+    with pytest.raises(RuntimeError, match="TOG_PROB_INFEASIBLE"):
+        h.slack_controls()
+    bad = prob.copy()
+    bad.constraints[0] = bad.constraints[0] + tog.infeasible_constraints(13, 4)
+    with pytest.raises(RuntimeError, match="TOG_CON_INFEASIBLE"):
+        tog.AugmentedLagrangianSolver(bad, opts)
+    pk, ok = tog.Problems.config_kuka(B=1)
+    pk.X = np.zeros((pk.N, 14))
+    with pytest.raises(RuntimeError, match="model not built"):
+        tog.ALTROSolver(tog.infeasible_problem(pk, 1.0), tog.ALTROSolverOptions(opts_al=ok))
