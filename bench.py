@@ -49,6 +49,8 @@ WORKLOADS = {
              "synthetic (seeded x0[1:7] ~ U(-0.2,0.2), U0 = hold torque at x0)"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6  # MI355X public spec, fp64 vector (the local guide has no fp64 row):
+#                          256 CU x 4 SIMD x 16 lanes x 2 FLOP x 2.4 GHz
 
 
 def kernel_bytes(n, m, N, p_stage, p_term, trials):
@@ -62,6 +64,27 @@ def kernel_bytes(n, m, N, p_stage, p_term, trials):
                + 2 * K * (n + m)                                # accept: copy X̄,Ū -> X,U
                + trials * 3 * (K * p_stage + p_term))           # λ, μ read, C written per trial
     return {"jacobian": jac, "backward": bwd, "forward": fwd}
+
+
+def bwd_flops(n, m, N, p_x, p_u, sqrt=True):
+    """Useful fp64 FLOPs of one trajectory's square-root backward pass (per backward launch), counted
+    from the operation sequence of backward_pass.jl:87-169 (the oracle's): per knot
+      Q.x/Q.u += [A B]ᵀs                2n(n+m)
+      S·[A B], S upper-triangular        (n+m)·n(n+1)
+      chol_plus QR [Q.xx; S A]           Σ_j 4(n+1)(n-1-j) + 3n   (structured: R top block)
+      chol_plus QR [Q.uu; S B; AL rows]  Σ_j 4(n+1+p_u)(m-1-j) + 3(n+p_u)
+      AL state rows QR on Q.xx           Σ_j 4(p_x+1)(n-1-j)
+      Q.ux += (S B)ᵀ(S A)                2nmn
+      Quu_reg QR, two triangular solves  4m³ + 2·2m²(n+1)
+      tmp1 = Q.xxᵀ \ Q.uxᵀ, chol_minus   n²m + 6nm²
+      S-update operands + QR             2n²m + 2m²n + Σ_j 4(m+1)(n-1-j)
+    Divisions and square roots count as one FLOP each. (The std pass is within ~10 % of this.)"""
+    tri = lambda rows, cols: sum(4 * (rows + 1) * (cols - 1 - j) for j in range(cols))  # noqa: E731
+    per_knot = (2 * n * (n + m) + (n + m) * n * (n + 1) + tri(n, n) + 3 * n
+                + tri(n + p_u, m) + 3 * (n + p_u) + (tri(p_x, n) if p_x else 0)
+                + 2 * n * m * n + 4 * m ** 3 + 4 * m * m * (n + 1)
+                + n * n * m + 6 * n * m * m + 2 * n * n * m + 2 * m * m * n + tri(m, n))
+    return per_knot * (N - 1)
 
 
 def measured_traffic(kernel):
@@ -80,31 +103,70 @@ def measured_traffic(kernel):
     return round(t["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
 
 
+def host_cpu_info():
+    """Host CPU facts for the baseline line: nproc (what the OS shows), the CPUs this process may run
+    on (affinity), the cgroup CPU quota (a GPU box's share of a big host) and the model name."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "cpu_model": None}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
 def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
     """The C oracle ("port" of the reference algorithm) on the host cores: full AL-iLQR solves of
-    config-3 trajectories, OpenMP over trajectories. Bounded sample (~`seconds` of work)."""
-    threads = threads or min(16, len(os.sched_getaffinity(0)))
-    B = 2 * threads
-    prob, opts = pkg.Problems.config_quadrotor(B=B, offset=100000)
+    config-3 trajectories, OpenMP over trajectories (threads pinned, OMP_PROC_BIND=close). Every
+    CPU this process may use takes part: the affinity set, capped by the cgroup quota when one
+    is set (a GPU box's share of a larger host: oversubscribing the quota only adds contention).
+    Bounded sample (~`seconds` of work per run); runs repeat until two consecutive runs agree within
+    10 % (at most 4) and the last pair's mean is reported."""
+    info = host_cpu_info()
+    avail = info["affinity"]
+    if info["cgroup_quota_cpus"]:
+        avail = max(1, min(avail, int(info["cgroup_quota_cpus"])))
+    threads = threads or avail
+    # calibration: 2 trajectories per thread, then size the sample to ~`seconds`
+    prob, opts = pkg.Problems.config_quadrotor(B=2 * threads, offset=100000)
     t = time.perf_counter()
-    steps = orc.solve_batch(prob, opts, nthreads=threads)
-    dt = time.perf_counter() - t
-    if dt < seconds:  # scale the sample up to ~`seconds`
-        B2 = int(min(4096, B * max(1.0, (seconds - dt) / max(dt, 1e-3))))
-        B2 = max(threads, B2 - B2 % threads)
-        prob, opts = pkg.Problems.config_quadrotor(B=B2, offset=200000)
+    orc.solve_batch(prob, opts, nthreads=threads)
+    dt = max(time.perf_counter() - t, 1e-3)
+    B = int(min(16384, 2 * threads * max(1.0, seconds / dt)))
+    B = max(threads, B - B % threads)
+    runs = []
+    for r in range(4):
+        prob, opts = pkg.Problems.config_quadrotor(B=B, offset=200000 + r * B)
         t = time.perf_counter()
-        steps2 = orc.solve_batch(prob, opts, nthreads=threads)
-        dt2 = time.perf_counter() - t
-        steps, dt, B = steps + steps2, dt + dt2, B + B2
+        steps = orc.solve_batch(prob, opts, nthreads=threads)
+        runs.append((steps, time.perf_counter() - t))
+        if len(runs) >= 2:
+            a, b = (x[0] / x[1] for x in runs[-2:])
+            if abs(a - b) <= 0.1 * max(a, b):
+                break
+    rates = [x[0] / x[1] for x in runs]
+    value = 0.5 * (rates[-1] + rates[-2]) if len(rates) >= 2 else rates[-1]
     # single-thread rate next to the reference's published per-core figures (SURVEY.md §6, §8(d))
     p1, o1 = pkg.Problems.config_quadrotor(B=1, offset=300000)
     t1 = time.perf_counter()
     s1 = orc.solve_batch(p1, o1, nthreads=1)
     d1 = time.perf_counter() - t1
-    return {"value": steps / dt, "unit": "iLQR iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{B} config-3 trajectories solved to AL convergence ({steps} iLQR steps, "
-                      f"{dt:.1f} s) by oracle/tog_oracle.c, OpenMP over trajectories",
+    return {"value": value, "unit": "iLQR iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{B} config-3 trajectories per run solved to AL convergence by oracle/tog_oracle.c, "
+                      f"OpenMP over trajectories; runs (steps, s): "
+                      + ", ".join(f"({x[0]}, {x[1]:.1f})" for x in runs),
+            "run_rates": [round(x, 1) for x in rates],
+            "nproc": info["nproc"], "affinity_cpus": info["affinity"],
+            "cgroup_quota_cpus": info["cgroup_quota_cpus"], "cpu_model": info["cpu_model"],
             "single_thread": {"value": s1 / d1, "sample": f"1 trajectory, {s1} iLQR steps, {d1:.1f} s"}}
 
 
@@ -116,12 +178,15 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU (default: the config's)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="quadrotor")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-solve-leg", action="store_true", help="skip the full-solve timing leg")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("OMP_PROC_BIND", "close")  # the CPU-baseline leg's OpenMP threads are pinned
+    os.environ.setdefault("OMP_PLACES", "cores")
     dist = None
     # TOG_BENCH_DIST=1 takes the torch.distributed (RCCL) path even at world size 1, to exercise the
     # multi-rank code (stream interop, stats all-gather, job rate) on a one-GPU box
@@ -135,6 +200,7 @@ def main():
     pkg = __graft_entry__.load_package()
     abi = pkg.abi
     cfg_fn, B_default, al_mode, wl_desc, wl_data = WORKLOADS[args.workload]
+    mode = abi.MODE_AL if al_mode else abi.MODE_ILQR
     B = args.batch or B_default
     offset, count = pkg.distributed.shard(B * world, rank, world)  # weak scaling: B trajectories per GPU
     prob, opts = getattr(pkg.Problems, cfg_fn)(B=count, offset=offset)
@@ -160,35 +226,39 @@ def main():
         # batch statistics [n_active, Σ cost, max c_max] of every shard: written on-device by
         # k_batch_stats and exchanged with ONE RCCL collective, stream-ordered (no host sync)
         if dist is None:
-            return
+            return None
         abi.check(h.lib, h.lib.tog_batch_stats_device(h.h, ctypes.c_void_p(stats_t.data_ptr())))
-        pkg.distributed.reduce_stats(stats_t, gathered, dist)
+        return pkg.distributed.reduce_stats(stats_t, gathered, dist)
 
+    def barrier_sync():
+        h.synchronize()
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    # ---------------------------------------------------------------- leg 1: step window
     if prob.model.slack:  # infeasible start: slack_controls(prob) before the solve (infeasible.jl:63-80)
         h.slack_controls()
-    h.solve_init(abi.MODE_AL if al_mode else abi.MODE_ILQR)
+    h.solve_init(mode)
     h.solve_step(args.warmup)
     h.synchronize()
     steps0 = h.total_steps()
-    if dist is not None:
-        dist.barrier()
-    h.synchronize()
+    active0 = int(h.batch_stats()[0])
+    barrier_sync()
     h.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         h.solve_step(1)
         allreduce_stats()
-    h.synchronize()
-    if dist is not None:
-        import torch
-
-        torch.cuda.synchronize()
-        dist.barrier()
+    barrier_sync()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     ms, launches = h.profile_read()
     h.profile(False)
     steps_done = h.total_steps() - steps0
+    active1 = int(h.batch_stats()[0])
     St = h.get(abi.FIELD_STATS)
     trials = float(np.mean(St[:, abi.STAT_LS_TRIALS][St[:, abi.STAT_LS_TRIALS] > 0])) if np.any(
         St[:, abi.STAT_LS_TRIALS] > 0) else 1.0
@@ -211,10 +281,36 @@ def main():
     alg_bytes = kb[names[dom]] * per_launch_traj
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     traffic, tsrc = measured_traffic(names[dom]) if args.workload == "quadrotor" else (None, None)
+    # whole step: Σ per-kernel algorithmic bytes of every trajectory-step of the job ÷ the window's wall
+    # time, against the job's aggregate HBM peak (world x 8 TB/s)
+    step_gbs = sum(kb.values()) * steps_all / elapsed / 1e9 / world
+    # backward kernel's useful fp64 FLOP rate against the fp64 vector peak
+    p_u = 2 * m if al_mode else 0  # control-bound rows of the stage constraints
+    p_x = max(0, p_stage - p_u) if al_mode else 0
+    bwd_i = names.index("backward")
+    bwd_avg_ms = ms[bwd_i] / max(1, launches[bwd_i])
+    bwd_traj = steps_done / max(1, launches[bwd_i])
+    flops = bwd_flops(n, m, N, p_x, p_u) * bwd_traj
+    flop_rate = flops / (bwd_avg_ms * 1e-3) / 1e12
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_source": (f"{tsrc} (committed PMC passes of this command; not measured in this run)"
+                                   if tsrc else None),
                 "algorithmic_bytes_per_launch": round(alg_bytes), "kernel": names[dom],
-                "kernel_ms": {nm_: round(float(ms[i] / max(1, launches[i])), 4) for i, nm_ in enumerate(names)}}
+                "kernel_ms": {nm_: round(float(ms[i] / max(1, launches[i])), 4) for i, nm_ in enumerate(names)},
+                "step_achieved": round(step_gbs, 2),
+                "step_frac": round(step_gbs / HBM_PEAK_GBS, 5),
+                "step_bytes_per_traj_iter": int(sum(kb.values())),
+                "flop_kernel": "backward",
+                "flop_achieved_tflops": round(flop_rate, 3),
+                "flop_peak_tflops": FP64_PEAK_TFLOPS,
+                "flop_frac": round(flop_rate / FP64_PEAK_TFLOPS, 5),
+                "flops_per_traj_iter": int(bwd_flops(n, m, N, p_x, p_u))}
+
+    # ---------------------------------------------------------------- leg 2: the whole solve
+    solve_leg = None
+    if not args.no_solve_leg:
+        solve_leg = time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_rank, pkg)
 
     if rank == 0:
         cpu = None
@@ -229,13 +325,55 @@ def main():
             "data": wl_data,
             "config": {"workload": wl_desc, "n": n, "m": m, "N": N,
                        "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"batch-shard x{world}",
-                       "mean_line_search_trials": round(trials, 3)},
+                       "mean_line_search_trials": round(trials, 3),
+                       "timed_window": {"solve_steps": [args.warmup + 1, args.warmup + args.steps],
+                                        "active_at_start": active0, "active_at_end": active1,
+                                        "note": "value = trajectory-iterations in this window of the solve "
+                                                "/ its wall time; solve_rate below times the whole solve"}},
+            "solve_rate": solve_leg,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_rank, pkg, chunk=4, max_steps=10000):
+    """The whole solve, SURVEY.md §8(d): from tog_solve_init (initial rollout + cost) until no
+    trajectory of the job is active, including the batch-level stopping check every `chunk` steps
+    (a host readback of [n_active, Σ J, max c_max]; over RCCL for several ranks). Same trajectories
+    as the window leg (re-initialised from the same U0). Returns Σ steps ÷ max-over-ranks wall time."""
+    h.upload_state(prob)
+    if prob.model.slack:
+        h.slack_controls()
+    barrier_sync()
+    t0 = time.perf_counter()
+    h.solve_init(mode)
+    done = 0
+    while done < max_steps:
+        h.solve_step(chunk)
+        done += chunk
+        red = allreduce_stats()
+        n_active = float(red[0].item()) if red is not None else float(h.batch_stats()[0])
+        if n_active == 0.0:
+            break
+    barrier_sync()
+    wall = time.perf_counter() - t0
+    steps = h.total_steps()  # k_init (tog_solve_init) zeroes the per-trajectory counters
+    St = h.get(abi.FIELD_STATS)
+    conv = int(np.count_nonzero(St[:, abi.STAT_FLAGS].astype(np.int64) &
+                                (abi.TRAJ_AL_CONVERGED | abi.TRAJ_CONVERGED)))
+    if dist is not None:
+        rate, steps_all, wall_all = pkg.distributed.job_rate(steps, wall, dist, device=f"cuda:{local_rank}")
+    else:
+        rate, steps_all, wall_all = steps / wall, float(steps), wall
+    it = St[:, abi.STAT_TOTAL_STEPS]
+    return {"value": round(rate, 2), "unit": "iLQR iterations/s", "steps": int(steps_all),
+            "wall_s": round(wall_all, 4), "batch_steps": done,
+            "traj_iterations": {"min": int(it.min()), "mean": round(float(it.mean()), 2), "max": int(it.max())},
+            "converged": conv, "batch": int(prob.B),
+            "note": "tog_solve_init .. last trajectory finished, stopping check every 4 steps included"}
 
 
 if __name__ == "__main__":

@@ -50,8 +50,17 @@ enum tog_traj_flag {
   TOG_TRAJ_SQRT_PD_FAIL = 1 << 6,    /* lowrankdowndate!/cholesky PosDefException (sqrt BP)     */
   TOG_TRAJ_AL_CONVERGED = 1 << 7,    /* c_max < constraint_tolerance                            */
   TOG_TRAJ_AL_MAX_ITERS = 1 << 8,    /* AL outer loop exhausted                                 */
-  TOG_TRAJ_SINGULAR = 1 << 9         /* SingularException path (pinv fallback) hit in sqrt BP   */
+  TOG_TRAJ_SINGULAR = 1 << 9,        /* SingularException path (pinv fallback) hit in sqrt BP   */
+  TOG_TRAJ_BP_ABORTED = 1 << 10      /* more than TOG_BP_MAX_RESTARTS regularisation restarts in
+                                        one backward pass: the trajectory stops (with MAX_REG).
+                                        The reference would keep restarting (backward_pass.jl:52-62,
+                                        125-136), e.g. forever on a NaN expansion.              */
 };
+
+/* Regularisation restarts one backward pass may take before the trajectory is stopped with
+ * TOG_TRAJ_BP_ABORTED | TOG_TRAJ_MAX_REG (same cap in the oracle and every device kernel). The
+ * trajectory keeps its X, U; K, d, ΔV of the aborted pass are not used. */
+#define TOG_BP_MAX_RESTARTS 1000
 
 /* ---------------------------------------------------------------- models */
 enum tog_model_id {

@@ -78,4 +78,11 @@ TOG_HD double tog_cos(double x) {
   }
 }
 
+/* Julia's max/min on floats (Base.max, Base.min): NaN in either argument propagates, unlike C's
+ * fmax/fmin, which drop it. The AL bookkeeping uses them where the reference calls max/min/maximum/
+ * norm(., Inf) (augmented_lagrangian_methods.jl:107-118, 171-184), so a NaN constraint value is
+ * reported as a NaN violation on both sides instead of reading as feasible. */
+TOG_HD double tog_jlmax(double a, double b) { return (a != a) ? a : ((b != b) ? b : fmax(a, b)); }
+TOG_HD double tog_jlmin(double a, double b) { return (a != a) ? a : ((b != b) ? b : fmin(a, b)); }
+
 #endif /* TOG_MATH_H */

@@ -1659,7 +1659,10 @@ static void backward_std(oc_solver* s) {
       s->bp_restarts++;
       k = N - 2;
       s->dV[0] = s->dV[1] = 0.0;
-      if (s->bp_restarts > 2000) return;
+      if (s->bp_restarts > TOG_BP_MAX_RESTARTS) { /* restart cap: stop the trajectory (tog.h) */
+        s->flags |= TOG_TRAJ_MAX_REG | TOG_TRAJ_BP_ABORTED;
+        return; /* no :decrease, ΔV = 0 */
+      }
       continue;
     }
     /* K = -(Quu_reg\Qux_reg) ; d = -(Quu_reg\Q.u) */
@@ -1765,7 +1768,10 @@ static void backward_sqrt(oc_solver* s) {
       s->bp_restarts++;
       k = N - 2;
       s->dV[0] = s->dV[1] = 0.0;
-      if (s->bp_restarts > 2000) return;
+      if (s->bp_restarts > TOG_BP_MAX_RESTARTS) { /* restart cap: stop the trajectory (tog.h) */
+        s->flags |= TOG_TRAJ_MAX_REG | TOG_TRAJ_BP_ABORTED;
+        return; /* no :decrease, ΔV = 0 */
+      }
       continue;
     }
     /* K = -Quu_reg\(Quu_reg'\Qux_reg) ; d = -Quu_reg\(Quu_reg'\Q.u) */
@@ -1946,6 +1952,7 @@ static int ilqr_iterate(oc_solver* s, int al, double cost_tol, double grad_tol) 
   oc_jacobians(s);
   if (oc_cost_expansion(s, s->opts.square_root, al)) s->flags |= TOG_TRAJ_SQRT_PD_FAIL;
   oc_backward(s, s->opts.square_root, NULL);
+  if (s->flags & TOG_TRAJ_BP_ABORTED) return 1; /* restart cap hit: the trajectory stops here */
   double J = oc_forward(s, al, s->J);
   s->total_steps++;
   if (s->trace_len < 4096) {
@@ -2006,12 +2013,12 @@ static double max_violation(oc_solver* s) {
       size_t j = (size_t)k * P + i;
       if (s->ineq[j]) {
         ni++;
-        if (s->C[j] > im) im = s->C[j];
-      } else if (fabs(s->C[j]) > e)
-        e = fabs(s->C[j]);
+        im = tog_jlmax(im, s->C[j]); /* maximum(C.inequality): NaN propagates */
+      } else
+        e = tog_jlmax(e, fabs(s->C[j])); /* norm(C.equality, Inf) */
     }
-    c_max = fmax(e, c_max);
-    if (ni > 0) c_max = fmax(fmax(0.0, im), c_max);
+    c_max = tog_jlmax(e, c_max);
+    if (ni > 0) c_max = tog_jlmax(tog_jlmax(0.0, im), c_max);
   }
   return c_max;
 }
@@ -2037,14 +2044,15 @@ OC_EXPORT int oc_solve_al(oc_solver* s) {
     double ct = (i != o->al_iterations) ? o->al_cost_tolerance_intermediate : o->al_cost_tolerance;
     double gt = (i != o->al_iterations) ? o->al_gradient_norm_tolerance_intermediate : o->al_gradient_norm_tolerance;
     ilqr_solve(s, 1, ct, gt);
+    if (s->flags & TOG_TRAJ_BP_ABORTED) break; /* stopped by the restart cap (tog.h) */
     (void)al_cost(s, s->X, s->U); /* J = cost(prob) */
     /* dual_update! (:107-118) */
     for (int k = 0; k < N; k++)
       for (int j = 0; j < s->p[k]; j++) {
         size_t q = (size_t)k * P + j;
         double l = s->lam[q] + s->mu[q] * s->C[q];
-        l = fmax(o->dual_min, fmin(o->dual_max, l));
-        if (s->ineq[q]) l = fmax(0.0, l);
+        l = tog_jlmax(o->dual_min, tog_jlmin(o->dual_max, l));
+        if (s->ineq[q]) l = tog_jlmax(0.0, l);
         s->lam[q] = l;
       }
     update_active_set(s);

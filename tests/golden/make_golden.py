@@ -103,9 +103,29 @@ def solves():
     np.savez_compressed(HERE / "solves.npz", **out)
 
 
+def quad_maze_n201():
+    """BASELINE config 4 at its own horizon (quad_obs, N=201, dt=0.025): the first 4 seeded starts
+    of ``config_quad_maze`` (seeds 3000+b) solved by AL-iLQR. Two converge, two exhaust the AL
+    iterations (c_max > 1), which pins the failure path too. Stats: J, c_max, total steps, flags."""
+    prob, opts = tog.Problems.config_quad_maze(B=4, N=201)
+    Xs, Us, st = [], [], []
+    for b in range(prob.B):
+        s = oracle.OracleSolver(prob, opts, b)
+        s.solve()
+        Xs.append(s.get("X"))
+        Us.append(s.get("U"))
+        st.append(s.get("stats"))
+    np.savez_compressed(HERE / "quad_maze_n201.npz", x0=prob.x0, U0=prob._U, X=np.array(Xs), U=np.array(Us),
+                        stats=np.array(st))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["quad_maze"]:
+        quad_maze_n201()
+        sys.exit(0)
     jacobians()
     backward_passes()
     solves()
+    quad_maze_n201()
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)

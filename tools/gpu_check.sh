@@ -5,7 +5,10 @@ cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=${STEPS:-10}
-timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+{ echo "nproc: $(nproc)"; echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)";
+  python3 -c 'import os; print("affinity:", len(os.sched_getaffinity(0)))';
+  grep -m1 "model name" /proc/cpuinfo; } > gpurun_out/hostinfo.txt 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout ${PER_TEST_TIMEOUT:-300} --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 tail -30 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest exit $rc: stopping"; exit $rc; fi

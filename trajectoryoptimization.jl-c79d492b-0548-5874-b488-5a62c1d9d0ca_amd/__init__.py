@@ -16,10 +16,10 @@ from .problem import (BoundConstraint, CircleConstraints, Constraints, Constrain
                       SphereConstraints, circle_constraint, discretize_model, goal_constraint, initial_controls_b,
                       initial_states_b, max_violation, midpoint, rk3, rk4, set_x0_b, sphere_constraint, add_slack_controls,
                       InfeasibleConstraint, infeasible_constraints, infeasible_problem, line_trajectory)
-from .solvers import (AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
+from .solvers import (Expansion, AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
                       AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, solve, solve_b, solver_name,
                       to_tog_options)
-from .steps import backwardpass_b, cost, cost_expansion_b, forwardpass_b, jacobian_b, rollout_b
+from .steps import backwardpass_b, cost, cost_expansion_b, forwardpass_b, jacobian_b, rollout_b, update_constraints_b
 from . import problems as Problems
 from . import distributed
 
@@ -30,7 +30,7 @@ __all__ = [
     "initial_states_b", "max_violation", "midpoint", "rk3", "rk4", "set_x0_b", "sphere_constraint", "AbstractSolver",
     "AbstractSolverFor", "ALTROSolver", "ALTROSolverOptions", "AugmentedLagrangianSolver",
     "AugmentedLagrangianSolverOptions", "iLQRSolver", "iLQRSolverOptions", "solve", "solve_b", "solver_name",
-    "to_tog_options", "backwardpass_b", "cost", "cost_expansion_b", "forwardpass_b", "jacobian_b", "rollout_b",
+    "to_tog_options", "Expansion", "backwardpass_b", "cost", "cost_expansion_b", "update_constraints_b", "forwardpass_b", "jacobian_b", "rollout_b",
     "Problems", "add_slack_controls", "InfeasibleConstraint", "infeasible_constraints", "infeasible_problem",
     "line_trajectory",
 ]

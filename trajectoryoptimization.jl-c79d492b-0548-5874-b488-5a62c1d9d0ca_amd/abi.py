@@ -46,6 +46,8 @@ TRAJ_SQRT_PD_FAIL = 1 << 6
 TRAJ_AL_CONVERGED = 1 << 7
 TRAJ_AL_MAX_ITERS = 1 << 8
 TRAJ_SINGULAR = 1 << 9
+TRAJ_BP_ABORTED = 1 << 10
+BP_MAX_RESTARTS = 1000  # TOG_BP_MAX_RESTARTS
 
 BP_STORE_S = 1
 
@@ -125,7 +127,9 @@ def default_options() -> tog_options:
 
 
 def as_dp(a: np.ndarray):
-    assert a.dtype == np.float64 and a.flags["F_CONTIGUOUS"] or a.flags["C_CONTIGUOUS"]
+    if not (a.dtype == np.float64 and (a.flags["F_CONTIGUOUS"] or a.flags["C_CONTIGUOUS"])):
+        raise TypeError(f"C ABI buffers must be contiguous float64 arrays, got {a.dtype} "
+                        f"(C={a.flags['C_CONTIGUOUS']}, F={a.flags['F_CONTIGUOUS']})")
     return a.ctypes.data_as(_dp)
 
 

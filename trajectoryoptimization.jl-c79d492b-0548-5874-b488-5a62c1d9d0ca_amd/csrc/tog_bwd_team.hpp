@@ -1053,8 +1053,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       } else {
         reg_increase(P, s);
         restarts++;
-        if (restarts > 1000) {
-          s.flags |= TOG_TRAJ_MAX_REG;
+        if (restarts > TOG_BP_MAX_RESTARTS) {  // restart cap (tog.h): the trajectory stops
+          s.flags |= TOG_TRAJ_MAX_REG | TOG_TRAJ_BP_ABORTED;
           done = true;
         }
       }
@@ -1409,15 +1409,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   BPROF(11)
   BPROF_FLUSH
   if (!live) return;
-  reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
+  const bool aborted = (s.flags & TOG_TRAJ_BP_ABORTED) != 0;
+  if (!aborted) reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
   if (tl == 0) {
     TrajState& g = Bf.st[b];
     g.rho = s.rho;
     g.drho = s.drho;
     g.flags = s.flags;
-    g.dV0 = dV0;
-    g.dV1 = dV1;
+    g.dV0 = aborted ? 0.0 : dV0;
+    g.dV1 = aborted ? 0.0 : dV1;
     g.bp_restarts = restarts + (faithful ? 1 : 0);
+    if (aborted) g.active = 0;  // no forward pass, no bookkeeping: the trajectory is finished
   }
 }
 #undef Xg

@@ -215,13 +215,13 @@ __device__ inline double traj_max_violation(const DevProblem* __restrict__ P, co
       const double c = C[(size_t)k * pmax + i];
       if (row_inequality(rows[i])) {
         ni++;
-        im = fmax(im, c);
+        im = tog_jlmax(im, c);  // maximum(C.inequality): NaN propagates (Julia max)
       } else {
-        e = fmax(e, fabs(c));
+        e = tog_jlmax(e, fabs(c));  // norm(C.equality, Inf)
       }
     }
-    c_max = fmax(e, c_max);
-    if (ni > 0) c_max = fmax(fmax(0.0, im), c_max);
+    c_max = tog_jlmax(e, c_max);
+    if (ni > 0) c_max = tog_jlmax(tog_jlmax(0.0, im), c_max);
   }
   return c_max;
 }
@@ -960,8 +960,8 @@ attempt:
       }
       reg_increase(P, s);
       restarts++;
-      if (restarts > 1000) {
-        s.flags |= TOG_TRAJ_MAX_REG;
+      if (restarts > TOG_BP_MAX_RESTARTS) {  // restart cap (tog.h): the trajectory stops
+        s.flags |= TOG_TRAJ_MAX_REG | TOG_TRAJ_BP_ABORTED;
         break;
       }
       wsync();
@@ -1175,15 +1175,17 @@ attempt:
       if (lane < n) Bf.sdbg[((size_t)b * N + k) * n + lane] = sh.s[lane];
     }
   }
-  reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
+  const bool aborted = (s.flags & TOG_TRAJ_BP_ABORTED) != 0;
+  if (!aborted) reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:82 / :166)
   if (lane == 0) {
     TrajState& g = Bf.st[b];
     g.rho = s.rho;
     g.drho = s.drho;
     g.flags = s.flags;
-    g.dV0 = dV0;
-    g.dV1 = dV1;
+    g.dV0 = aborted ? 0.0 : dV0;
+    g.dV1 = aborted ? 0.0 : dV1;
     g.bp_restarts = restarts + (faithful ? 1 : 0);
+    if (aborted) g.active = 0;  // no forward pass, no bookkeeping: the trajectory is finished
   }
 }
 
@@ -1435,8 +1437,8 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
     for (int i = 0; i < cnt; i++) {
       const size_t q = (size_t)k * pmax + i;
       double l = lam[q] + mu[q] * C[q];  // dual_update! (:107-118)
-      l = fmax(o.dual_min, fmin(o.dual_max, l));
-      if (row_inequality(rows[i])) l = fmax(0.0, l);
+      l = tog_jlmax(o.dual_min, tog_jlmin(o.dual_max, l));
+      if (row_inequality(rows[i])) l = tog_jlmax(0.0, l);
       lam[q] = l;
       mu[q] = fmax(0.0, fmin(o.penalty_max, o.penalty_scaling * mu[q]));  // penalty_update! (:121-126)
       mumax = fmax(mumax, mu[q]);

@@ -231,7 +231,7 @@ static __global__ void __launch_bounds__(1024) k_batch_stats(const TrajState* __
   for (long long b = t; b < B; b += blockDim.x) {
     a += st[b].active ? 1.0 : 0.0;
     j += st[b].J;
-    c = fmax(c, st[b].c_max);
+    c = tog_jlmax(c, st[b].c_max);  // a NaN violation propagates (Julia max), never reads as feasible
   }
   sa[t] = a;
   sj[t] = j;
@@ -241,7 +241,7 @@ static __global__ void __launch_bounds__(1024) k_batch_stats(const TrajState* __
     if (t < w) {
       sa[t] += sa[t + w];
       sj[t] += sj[t + w];
-      sc[t] = fmax(sc[t], sc[t + w]);
+      sc[t] = tog_jlmax(sc[t], sc[t + w]);
     }
     __syncthreads();
   }
@@ -387,21 +387,10 @@ int32_t tog_destroy(tog_handle* h) {
   return TOG_OK;
 }
 
-int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t device, tog_handle** out) {
-  if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
-  *out = nullptr;
-  if (d->flags & ~(int32_t)TOG_PROB_INFEASIBLE) return fail(TOG_ERR_ARG, "unknown problem flags");
-  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0);
-  if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
-  if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
-  if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
-  if (d->batch < 1) return fail(TOG_ERR_ARG, "batch must be >= 1");
-  if (!(d->dt > 0)) return fail(TOG_ERR_ARG, "dt must be strictly positive");  // src/problem.jl:66-68
-  if (d->integrator != TOG_RK3 && d->integrator != TOG_RK4 && d->integrator != TOG_MIDPOINT)
-    return fail(TOG_ERR_UNSUPPORTED, "integrator");
-  int ndev = tog_device_count();
-  if (device < 0 || device >= ndev) return fail(TOG_ERR_DEVICE, "no such HIP device");
-  tog_handle* h = new tog_handle();
+// Body of tog_create after argument validation: every early return (HIPCHECK, allocation, build_rows)
+// leaves the partially built handle to the caller, which destroys it (streams, events, allocations).
+static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog_options* opts,
+                             const ModelOps* ops, int32_t device) {
   h->device = device;
   HIPCHECK(hipSetDevice(device));
   HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
@@ -423,10 +412,7 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   std::vector<ConRow> rows;
   std::vector<int> off, cnt;
   int rc = build_rows(d, ops->slack, ops->pcap, rows, off, cnt);
-  if (rc) {
-    tog_destroy(h);
-    return rc;
-  }
+  if (rc) return rc;
   h->nrows = (int)rows.size();
   h->pmax = 0;
   for (int k = 0; k < N; k++) h->pmax = cnt[k] > h->pmax ? cnt[k] : h->pmax;
@@ -481,17 +467,14 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
       if (std::signbit(P.H[i])) pz = false;
     P.diag_cost = diag ? (pz ? 2 : 1) : 0;
     if (opts->square_root && !ok) {
-      tog_destroy(h);
       return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
     }
   }
   P.o = *opts;
   const size_t B = (size_t)h->B, P1 = (size_t)(h->pmax > 0 ? h->pmax : 1);
   if ((rc = dalloc(h, &h->d_knot_off, N)) || (rc = dalloc(h, &h->d_knot_cnt, N)) ||
-      (rc = dalloc(h, &h->d_rows, rows.size() + 1)) || (rc = dalloc(h, &h->dP, 1))) {
-    tog_destroy(h);
+      (rc = dalloc(h, &h->d_rows, rows.size() + 1)) || (rc = dalloc(h, &h->dP, 1)))
     return rc;
-  }
   HIPCHECK(hipMemcpy(h->d_knot_off, off.data(), sizeof(int) * N, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(h->d_knot_cnt, cnt.data(), sizeof(int) * N, hipMemcpyHostToDevice));
   if (!rows.empty()) HIPCHECK(hipMemcpy(h->d_rows, rows.data(), sizeof(ConRow) * rows.size(), hipMemcpyHostToDevice));
@@ -524,10 +507,8 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
       (rc = dalloc(h, &h->d_scratch, B)) || (rc = dalloc(h, &h->d_scratch2, B)) ||
       (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4)) ||
       (rc = dalloc(h, &b.lsJ, B * 64)) || (rc = dalloc(h, &b.lsok, B * 64)) ||
-      (rc = dalloc(h, &b.ls_list, 2 * B)) || (rc = dalloc(h, &b.ls_count, LS_MAX_ROUNDS))) {
-    tog_destroy(h);
+      (rc = dalloc(h, &b.ls_list, 2 * B)) || (rc = dalloc(h, &b.ls_count, LS_MAX_ROUNDS)))
     return rc;
-  }
   b.Sdbg = nullptr;
   b.sdbg = nullptr;
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
@@ -548,6 +529,29 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   hipLaunchKernelGGL(k_reset_state, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, h->stream, b.st, (long long)B, h->opts.penalty_initial);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(h->stream));
+  return TOG_OK;
+}
+
+int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t device, tog_handle** out) {
+  if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (d->flags & ~(int32_t)TOG_PROB_INFEASIBLE) return fail(TOG_ERR_ARG, "unknown problem flags");
+  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0);
+  if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
+  if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
+  if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
+  if (d->batch < 1) return fail(TOG_ERR_ARG, "batch must be >= 1");
+  if (!(d->dt > 0)) return fail(TOG_ERR_ARG, "dt must be strictly positive");  // src/problem.jl:66-68
+  if (d->integrator != TOG_RK3 && d->integrator != TOG_RK4 && d->integrator != TOG_MIDPOINT)
+    return fail(TOG_ERR_UNSUPPORTED, "integrator");
+  int ndev = tog_device_count();
+  if (device < 0 || device >= ndev) return fail(TOG_ERR_DEVICE, "no such HIP device");
+  tog_handle* h = new tog_handle();
+  const int32_t rc = create_single(h, d, opts, ops, device);
+  if (rc) {
+    tog_destroy(h);
+    return rc;
+  }
   *out = h;
   return TOG_OK;
 }
@@ -976,7 +980,7 @@ int32_t tog_batch_stats(tog_handle* h, double* out3) {
       HIPCHECK(hipStreamSynchronize(p->stream));
       out3[0] += v[0];
       out3[1] += v[1];
-      out3[2] = v[2] > out3[2] ? v[2] : out3[2];
+      out3[2] = tog_jlmax(out3[2], v[2]);
     }
     return TOG_OK;
   }

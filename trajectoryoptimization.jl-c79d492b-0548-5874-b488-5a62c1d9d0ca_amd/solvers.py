@@ -170,6 +170,29 @@ def solver_name(opts) -> str:
 
 # ----------------------------------------------------------------------------- solvers
 
+@dataclass
+class Expansion:
+    """``Expansion{T}`` (src/cost.jl:5-33): x, u, xx, uu, ux, batched over (B, N)."""
+
+    x: np.ndarray
+    u: np.ndarray
+    xx: np.ndarray
+    uu: np.ndarray
+    ux: np.ndarray
+
+    @classmethod
+    def from_flat(cls, q, n, m):
+        """Split TOG_FIELD_Q's per-knot record [x; u; xx; uu; ux] (matrices column-major)."""
+        lead = q.shape[:-1]
+        o = n + m
+        xx = q[..., o:o + n * n].reshape(lead + (n, n)).swapaxes(-1, -2)
+        o += n * n
+        uu = q[..., o:o + m * m].reshape(lead + (m, m)).swapaxes(-1, -2)
+        o += m * m
+        ux = q[..., o:o + m * n].reshape(lead + (n, m)).swapaxes(-1, -2)
+        return cls(q[..., :n].copy(), q[..., n:n + m].copy(), np.ascontiguousarray(xx), np.ascontiguousarray(uu),
+                   np.ascontiguousarray(ux))
+
 class AbstractSolver:
     """``AbstractSolver{T}`` (src/solvers.jl:7). Holds ``opts``, ``stats`` and the device handle."""
 
@@ -207,6 +230,13 @@ class AbstractSolver:
     @property
     def rho(self):
         return self.handle.get(abi.FIELD_RHO)
+
+    @property
+    def Q(self):
+        """``solver.Q``: the cost-to-go expansion of the last ``cost_expansion!`` (ilqr_solver.jl:
+        130-131), per knot ``Expansion(x, u, xx, uu, ux)`` as batched arrays (B, N, ...). The
+        terminal knot's u-parts are zero. With ``square_root`` xx and uu hold upper factors."""
+        return Expansion.from_flat(self.handle.get(abi.FIELD_Q), self.n, self.m)
 
 
 class iLQRSolver(AbstractSolver):

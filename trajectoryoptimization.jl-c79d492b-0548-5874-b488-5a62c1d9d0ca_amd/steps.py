@@ -35,10 +35,23 @@ def jacobian_b(prob, solver: AbstractSolver):
     solver.handle.jacobians()
 
 
+def update_constraints_b(prob, solver: AbstractSolver):
+    """``update_constraints!(C, constraints, X, U)`` + ``update_active_set!`` on the current X, U
+    (constraint_sets.jl:221-260; the AL expansion reads them, test/sqrt_bp_tests.jl:62-63)."""
+    solver.handle.update_constraints()
+
+
 def cost_expansion_b(prob, solver: AbstractSolver):
-    """``cost_expansion!(prob, solver)`` (ilqr_methods.jl:55-62). On the device the expansion is
-    fused into the backward-pass kernel, so this only validates the call order."""
-    solver._expansion_ready = True
+    """``cost_expansion!(prob, solver)`` (ilqr_methods.jl:55-62): ``reset!(solver.Q)`` then the
+    stage/terminal expansion of the objective at (X, U) — the square-root factors when
+    ``opts.square_root`` (objective.jl:51-94), plus the AL terms of the stored constraint values
+    and active set for an AL solver (augmented_lagrangian_methods.jl:186-276). Computed on the device
+    (``tog_cost_expansion``) into ``solver.Q``. The backward-pass kernels compute the same expansion
+    fused, so ``backwardpass_b`` does not need this call; it is the reference's step-level entry point
+    (test/sqrt_bp_tests.jl:27-37)."""
+    sq = bool(_opts_ilqr(solver).square_root)
+    solver.handle.cost_expansion(sqrt=sq, al=_al(solver))
+    return solver.Q
 
 
 def backwardpass_b(prob, solver: AbstractSolver, square_root: bool | None = None, store_S: bool = True):
