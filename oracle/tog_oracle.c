@@ -677,36 +677,35 @@ static void matmul(double* C, const double* A, int r, int k, const double* B, in
     }
 }
 
-/* dlapy2 */
-static double lapy2(double x, double y) {
-  double xa = fabs(x), ya = fabs(y);
-  double w = xa > ya ? xa : ya, z = xa < ya ? xa : ya;
-  if (z == 0.0 || w > 1.79e308) return w;
-  double t = z / w;
-  return w * sqrt(1.0 + t * t);
-}
-
 /* R factor of qr(P) for P (rows x cols), rows >= cols, LAPACK dgeqr2/dlarfg Householder.
-   Julia: qr(P).R (chol_plus, backward_pass.jl:172-183). Writes the cols x cols upper triangle to R. */
+   Julia: qr(P).R (chol_plus, backward_pass.jl:172-183). Writes the cols x cols upper triangle to R.
+   Arithmetic contract v2, shared bit for bit with the device QRs:
+   * sums over the rows below the diagonal (‖x‖², the reflector dot products) run in 4 interleaved
+     accumulators, term t = i-(j+1) into accumulator t & 3, combined as (a0 + a1) + (a2 + a3): the
+     dependent chain is a quarter as long (LAPACK's dnrm2 also reorders; the values agree to rounding);
+   * β = -sign(α)·sqrt(α² + ‖x‖²) with one fma and one sqrt (dlapy2's rescaling only matters near
+     overflow);
+   * τ = (β-α)/β and the scale 1/(α-β) as in dlarfg. */
+static double sum4(const double* a) { return (a[0] + a[1]) + (a[2] + a[3]); }
+
 static void qr_R(double* R, double* P, int rows, int cols) {
   int kmax = rows < cols ? rows : cols;
   for (int j = 0; j < kmax; j++) {
     double alpha = P[IDX(j, j, rows)];
-    /* ‖P[j+1:rows, j]‖ as a plain fma sum of squares (LAPACK's dnrm2 rescales to avoid overflow;
-       identical up to rounding for these magnitudes; DESIGN.md §3 arithmetic contract) */
-    double ss = 0.0;
-    for (int i = j + 1; i < rows; i++) ss = fma(P[IDX(i, j, rows)], P[IDX(i, j, rows)], ss);
-    double xnorm = sqrt(ss);
-    if (xnorm == 0.0) continue; /* tau = 0, H = I */
-    double beta = -copysign(lapy2(alpha, xnorm), alpha);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = j + 1; i < rows; i++) acc[(i - j - 1) & 3] = fma(P[IDX(i, j, rows)], P[IDX(i, j, rows)], acc[(i - j - 1) & 3]);
+    double ss = sum4(acc);
+    if (ss == 0.0) continue; /* tau = 0, H = I */
+    double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
     double tau = (beta - alpha) / beta;
     double sc = 1.0 / (alpha - beta);
     for (int i = j + 1; i < rows; i++) P[IDX(i, j, rows)] *= sc;
     P[IDX(j, j, rows)] = beta;
     /* apply H = I - tau v v' to P[j:rows, j+1:cols], v = [1; P[j+1:rows, j]] */
     for (int c = j + 1; c < cols; c++) {
-      double w = P[IDX(j, c, rows)];
-      for (int i = j + 1; i < rows; i++) w = fma(P[IDX(i, j, rows)], P[IDX(i, c, rows)], w);
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int i = j + 1; i < rows; i++) a4[(i - j - 1) & 3] = fma(P[IDX(i, j, rows)], P[IDX(i, c, rows)], a4[(i - j - 1) & 3]);
+      double w = P[IDX(j, c, rows)] + sum4(a4);
       w *= tau;
       P[IDX(j, c, rows)] -= w;
       for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] = fma(-P[IDX(i, j, rows)], w, P[IDX(i, c, rows)]);
@@ -714,6 +713,30 @@ static void qr_R(double* R, double* P, int rows, int cols) {
   }
   for (int j = 0; j < cols; j++)
     for (int i = 0; i < cols; i++) R[IDX(i, j, cols)] = (i <= j && i < rows) ? P[IDX(i, j, rows)] : 0.0;
+}
+
+/* Triangular solves of the square-root backward pass (contract v2): the diagonal reciprocals are
+   formed first (independent divisions) and every substitution step multiplies by them, so the
+   dependent chain per step is one multiply instead of one division (x_j = b_j·(1/U_jj)). */
+static void solve_upper_rcp(const double* A, int n, double* B, int nrhs) { /* A upper: A \ B */
+  double r[OM > 16 ? OM : 16];
+  for (int j = 0; j < n; j++) r[j] = 1.0 / A[IDX(j, j, n)];
+  for (int c = 0; c < nrhs; c++)
+    for (int j = n - 1; j >= 0; j--) {
+      double xj = B[IDX(j, c, n)] * r[j];
+      B[IDX(j, c, n)] = xj;
+      for (int i = j - 1; i >= 0; i--) B[IDX(i, c, n)] = fma(-A[IDX(i, j, n)], xj, B[IDX(i, c, n)]);
+    }
+}
+static void solve_uppert_rcp(const double* A, int n, double* B, int nrhs) { /* A upper: A' \ B */
+  double r[OM > 16 ? OM : 16];
+  for (int j = 0; j < n; j++) r[j] = 1.0 / A[IDX(j, j, n)];
+  for (int c = 0; c < nrhs; c++)
+    for (int j = 0; j < n; j++) {
+      double xj = B[IDX(j, c, n)] * r[j];
+      B[IDX(j, c, n)] = xj;
+      for (int i = j + 1; i < n; i++) B[IDX(i, c, n)] = fma(-A[IDX(j, i, n)], xj, B[IDX(i, c, n)]);
+    }
 }
 
 /* chol_plus(A, B) = qr([A; B]).R, A n1 x c, B n2 x c (backward_pass.jl:172-179) */
@@ -898,9 +921,10 @@ static int chol_minus(double* Uo, const double* A, int n, const double* B, int n
       double s2 = s * s;
       if (s2 > 1.0) return i + 1;
       double c = sqrt(1.0 - s2);
+      double rc = 1.0 / c; /* contract v2: one division per rotation, (U_ij - s v_j)·(1/c) */
       U[IDX(i, i, n)] = c * Aii;
       for (int j = i + 1; j < n; j++) {
-        double tmp = (U[IDX(i, j, n)] - s * v[j]) / c;
+        double tmp = (U[IDX(i, j, n)] - s * v[j]) * rc;
         v[j] = c * v[j] - s * tmp;
         U[IDX(i, j, n)] = tmp;
       }
@@ -1775,16 +1799,15 @@ static void backward_sqrt(oc_solver* s) {
       continue;
     }
     /* K = -Quu_reg\(Quu_reg'\Qux_reg) ; d = -Quu_reg\(Quu_reg'\Q.u) */
-    double RT[OM * OM];
-    for (int j = 0; j < m; j++)
-      for (int i = 0; i < m; i++) RT[IDX(i, j, m)] = Quu_reg[IDX(j, i, m)];
+    /* (Quu_reg' \ and Quu_reg \ are triangular solves: Julia's `\` dispatches them to
+       substitution; contract v2 multiplies by the diagonal reciprocals) */
     memcpy(Kk, Qux_reg, sizeof(double) * m * n);
-    lu_solve(RT, m, Kk, n);
-    lu_solve(Quu_reg, m, Kk, n);
+    solve_uppert_rcp(Quu_reg, m, Kk, n);
+    solve_upper_rcp(Quu_reg, m, Kk, n);
     for (int i = 0; i < m * n; i++) Kk[i] = -Kk[i];
     memcpy(dk, Qu, sizeof(double) * m);
-    lu_solve(RT, m, dk, 1);
-    lu_solve(Quu_reg, m, dk, 1);
+    solve_uppert_rcp(Quu_reg, m, dk, 1);
+    solve_upper_rcp(Quu_reg, m, dk, 1);
     for (int i = 0; i < m; i++) dk[i] = -dk[i];
     memcpy(s->K + (size_t)k * m * n, Kk, sizeof(double) * m * n);
     memcpy(s->d + (size_t)k * m, dk, sizeof(double) * m);
@@ -1805,16 +1828,14 @@ static void backward_sqrt(oc_solver* s) {
       for (int i = 0; i < n; i++) sk[i] = ((Qx[i] + a[i]) + b[i]) + c[i];
     }
     /* tmp1 = (Q.xx')\Q.ux'  (n x m) */
-    double tmp1[OM * 16], QxxT[256];
-    for (int j = 0; j < n; j++)
-      for (int i = 0; i < n; i++) QxxT[IDX(i, j, n)] = Qxx[IDX(j, i, n)];
+    double tmp1[OM * 16];
     int singular = 0;
     for (int i = 0; i < n; i++)
       if (Qxx[IDX(i, i, n)] == 0.0) singular = 1;
     for (int j = 0; j < m; j++)
       for (int i = 0; i < n; i++) tmp1[IDX(i, j, n)] = Qux[IDX(j, i, m)];
     if (singular) s->flags |= TOG_TRAJ_SINGULAR;
-    lu_solve(QxxT, n, tmp1, m);
+    solve_uppert_rcp(Qxx, n, tmp1, m); /* Q.xx upper-triangular: forward substitution */
     /* tmp2 = chol_minus(Q.uu, tmp1) */
     double tmp2[OM * OM];
     if (chol_minus(tmp2, Quu, m, tmp1, n)) {

@@ -20,7 +20,8 @@ lib = abi.load_library()
 read = lib.tog_bwd_prof_read
 read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-prob, opts = pkg.Problems.config_quadrotor(B=8192)
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+prob, opts = pkg.Problems.config_quadrotor(B=B)
 s = pkg.AbstractSolverFor(prob, opts)
 s.handle.solve_init(abi.MODE_AL)
 s.handle.solve_step(1)
@@ -31,5 +32,7 @@ s.handle.solve_step(steps)
 s.handle.synchronize()
 assert read(buf) == 20
 tot = sum(buf)
+waves = (B + 3) // 4
+print(f"B={B} steps={steps}: cycles per wave-knot = {tot / (waves * steps * (prob.N - 1)):.0f}")
 for nm, v in zip(NAMES, buf):
-    print(f"{nm:40s} {100.0 * v / tot:6.2f}%  {v / 1e9:10.3f} Gcyc")
+    print(f"{nm:40s} {100.0 * v / tot:6.2f}%  {v / 1e9:10.3f} Gcyc  {v / (waves * steps * (prob.N - 1)):9.0f} cyc/wave-knot")

@@ -201,14 +201,16 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
       constexpr int j = decltype(jc)::value;
       if (j < rows) {
         const bool me = (tl == j);
-        double ss = 0.0;
+        // contract v2 (oracle qr_R): 4 interleaved accumulators by position below the diagonal,
+        // β from one fma + one sqrt
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (TQ_LIVE(i, j)) ss = fma(a[i], a[i], ss);
-        const double xnorm = sqrt(ss);
+          if (TQ_LIVE(i, j)) acc[(i - j - 1) & 3] = fma(a[i], a[i], acc[(i - j - 1) & 3]);
+        const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         const double alpha = a[j];
-        const double beta = -copysign(lapy2(alpha, xnorm), alpha);
-        const bool refl = me && (xnorm != 0.0);
+        const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
+        const bool refl = me && (ss != 0.0);
         const double tau_l = refl ? (beta - alpha) / beta : 0.0;
         const double sc = refl ? 1.0 / (alpha - beta) : 1.0;
 #pragma unroll
@@ -221,10 +223,11 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
 #pragma unroll
           for (int i = j + 1; i < ROWS; i++)
             if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
-          double w = a[j];
+          double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int i = j + 1; i < ROWS; i++)
-            if (TQ_LIVE(i, j)) w = fma(v[i], a[i], w);
+            if (TQ_LIVE(i, j)) a4[(i - j - 1) & 3] = fma(v[i], a[i], a4[(i - j - 1) & 3]);
+          double w = a[j] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
           w *= tau;
           if (!(tl > j && tl < COLS)) w = 0.0;
           a[j] -= w;
@@ -240,15 +243,15 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
   for (int j = 0; j < COLS; j++) {
     if (j < rows) {
       if (tl == j) {
-        double ss = 0.0;
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (TQ_LIVE(i, j)) ss = fma(a[i], a[i], ss);
-        const double xnorm = sqrt(ss);
+          if (TQ_LIVE(i, j)) acc[(i - j - 1) & 3] = fma(a[i], a[i], acc[(i - j - 1) & 3]);
+        const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         double tau = 0.0;
-        if (xnorm != 0.0) {
+        if (ss != 0.0) {
           const double alpha = a[j];
-          const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+          const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
           tau = (beta - alpha) / beta;
           const double sc = 1.0 / (alpha - beta);
 #pragma unroll
@@ -264,10 +267,11 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
       team_sync();
       const double tau = bus[0];
       if (tau != 0.0 && tl > j && tl < COLS) {
-        double w = a[j];
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (TQ_LIVE(i, j)) w = fma(bus[i], a[i], w);
+          if (TQ_LIVE(i, j)) a4[(i - j - 1) & 3] = fma(bus[i], a[i], a4[(i - j - 1) & 3]);
+        double w = a[j] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
         w *= tau;
         a[j] -= w;
 #pragma unroll
@@ -1084,17 +1088,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         for (int i = 0; i < j; i++) col[i] = fma(-F[i][j], col[j], col[i]);
       }
     } else {
-      // K = -Quu_reg \ (Quu_reg' \ Qux_reg)
+      // K = -Quu_reg \ (Quu_reg' \ Qux_reg); contract v2: multiply by the diagonal reciprocals
+      double rF[m];
+#pragma unroll
+      for (int j = 0; j < m; j++) rF[j] = 1.0 / F[j][j];
 #pragma unroll
       for (int j = 0; j < m; j++) {
-        const double xj = col[j] / F[j][j];
+        const double xj = col[j] * rF[j];
         col[j] = xj;
 #pragma unroll
         for (int i = j + 1; i < m; i++) col[i] = fma(-F[j][i], xj, col[i]);
       }
 #pragma unroll
       for (int j = m - 1; j >= 0; j--) {
-        const double xj = col[j] / F[j][j];
+        const double xj = col[j] * rF[j];
         col[j] = xj;
 #pragma unroll
         for (int i = j - 1; i >= 0; i--) col[i] = fma(-F[i][j], xj, col[i]);
@@ -1236,12 +1243,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       double t1[m];
 #pragma unroll
       for (int i = 0; i < m; i++) t1[i] = Quxc[i];
+      // contract v2: x_j = b_j·(1/U_jj); lane j forms the reciprocal of its diagonal entry up front
+      double dgx = Qxc[0];
+#pragma unroll
+      for (int j = 1; j < n; j++)
+        if (tl == j) dgx = Qxc[j];
+      const double rdiag = 1.0 / dgx;
       if constexpr (TEAM == 16) {
         static_for<0, n>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
           if (tl == j) {
 #pragma unroll
-            for (int i = 0; i < m; i++) t1[i] = t1[i] / Qxc[j];
+            for (int i = 0; i < m; i++) t1[i] = t1[i] * rdiag;
           }
           double xj[m];
 #pragma unroll
@@ -1257,7 +1270,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           if (tl == j) {
 #pragma unroll
             for (int i = 0; i < m; i++) {
-              t1[i] = t1[i] / Qxc[j];
+              t1[i] = t1[i] * rdiag;
               bus[i] = t1[i];
             }
           }
@@ -1323,11 +1336,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
             const double s2 = sn * sn;
             if (s2 > 1.0) okd = false;
             const double cs = sqrt(1.0 - s2);
+            const double rcs = 1.0 / cs;  // contract v2: one division per rotation
 #pragma unroll
             for (int jj = 0; jj < m; jj++) {
               if (jj == tl) urow[jj] = cs * Aii;
               if (jj > tl) {
-                const double tmp = (urow[jj] - sn * v[jj]) / cs;
+                const double tmp = (urow[jj] - sn * v[jj]) * rcs;
                 v[jj] = cs * v[jj] - sn * tmp;
                 urow[jj] = tmp;
               }

@@ -401,15 +401,15 @@ __device__ void wqr(double* A, int rows, double* wv) {
   const int lane = threadIdx.x;
   const int kmax = rows < COLS ? rows : COLS;
   for (int j = 0; j < kmax; j++) {
-    double ss = 0.0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // contract v2: 4 interleaved accumulators (oracle qr_R)
     for (int i = j + 1; i < rows; i++) {
       const double a = A[i + rows * j];
-      ss = fma(a, a, ss);
+      acc[(i - j - 1) & 3] = fma(a, a, acc[(i - j - 1) & 3]);
     }
-    const double xnorm = sqrt(ss);
-    if (xnorm == 0.0) continue;  // tau = 0, H = I (uniform branch: every lane computed ss)
+    const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    if (ss == 0.0) continue;  // tau = 0, H = I (uniform branch: every lane computed ss)
     const double alpha = A[j + rows * j];
-    const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+    const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
     const double tau = (beta - alpha) / beta;
     const double sc = 1.0 / (alpha - beta);
     wsync();
@@ -417,8 +417,9 @@ __device__ void wqr(double* A, int rows, double* wv) {
     wsync();
     if (lane > j && lane < COLS) {
       const int c = lane;
-      double w = A[j + rows * c];
-      for (int i = j + 1; i < rows; i++) w = fma(A[i + rows * j], A[i + rows * c], w);
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int i = j + 1; i < rows; i++) a4[(i - j - 1) & 3] = fma(A[i + rows * j], A[i + rows * c], a4[(i - j - 1) & 3]);
+      double w = A[j + rows * c] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
       w *= tau;
       A[j + rows * c] -= w;
       wv[c] = w;
@@ -920,20 +921,23 @@ attempt:
             else v = (i - m == j) ? sqrt(s.rho) : 0.0;
             Wl[i + rows * j] = v;
           }
-        for (int j = 0; j < m; j++) {  // serial Householder (m x m, tiny)
-          double ss = 0.0;
-          for (int i = j + 1; i < rows; i++) ss = fma(Wl[i + rows * j], Wl[i + rows * j], ss);
-          const double xnorm = sqrt(ss);
-          if (xnorm == 0.0) continue;
+        for (int j = 0; j < m; j++) {  // serial Householder (m x m, tiny; contract v2 as qr_R)
+          double acc[4] = {0.0, 0.0, 0.0, 0.0};
+          for (int i = j + 1; i < rows; i++)
+            acc[(i - j - 1) & 3] = fma(Wl[i + rows * j], Wl[i + rows * j], acc[(i - j - 1) & 3]);
+          const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+          if (ss == 0.0) continue;
           const double alpha = Wl[j + rows * j];
-          const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+          const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
           const double tau = (beta - alpha) / beta;
           const double sc = 1.0 / (alpha - beta);
           for (int i = j + 1; i < rows; i++) Wl[i + rows * j] *= sc;
           Wl[j + rows * j] = beta;
           for (int c = j + 1; c < m; c++) {
-            double w = Wl[j + rows * c];
-            for (int i = j + 1; i < rows; i++) w = fma(Wl[i + rows * j], Wl[i + rows * c], w);
+            double a4[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int i = j + 1; i < rows; i++)
+              a4[(i - j - 1) & 3] = fma(Wl[i + rows * j], Wl[i + rows * c], a4[(i - j - 1) & 3]);
+            double w = Wl[j + rows * c] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
             w *= tau;
             Wl[j + rows * c] -= w;
             for (int i = j + 1; i < rows; i++) Wl[i + rows * c] = fma(-Wl[i + rows * j], w, Wl[i + rows * c]);
@@ -989,17 +993,21 @@ attempt:
       if (!SQRT) {
         lu_solve_col<m>(sh.F, sh.piv, col);
       } else {
-        // Quu_reg' \ col (forward substitution), then Quu_reg \ (back substitution)
+        // Quu_reg' \ col (forward substitution), then Quu_reg \ (back substitution); contract v2:
+        // multiply by the diagonal reciprocals
+        double rF[m];
+#pragma unroll
+        for (int j = 0; j < m; j++) rF[j] = 1.0 / sh.F[j + m * j];
 #pragma unroll
         for (int j = 0; j < m; j++) {
-          const double xj = col[j] / sh.F[j + m * j];
+          const double xj = col[j] * rF[j];
           col[j] = xj;
 #pragma unroll
           for (int i = j + 1; i < m; i++) col[i] = fma(-sh.F[j + m * i], xj, col[i]);
         }
 #pragma unroll
         for (int j = m - 1; j >= 0; j--) {
-          const double xj = col[j] / sh.F[j + m * j];
+          const double xj = col[j] * rF[j];
           col[j] = xj;
 #pragma unroll
           for (int i = j - 1; i >= 0; i--) col[i] = fma(-sh.F[i + m * j], xj, col[i]);
@@ -1082,9 +1090,12 @@ attempt:
         double col[n];
 #pragma unroll
         for (int i = 0; i < n; i++) col[i] = sh.Qux[c + m * i];
+        double rq[n];
+#pragma unroll
+        for (int j = 0; j < n; j++) rq[j] = 1.0 / sh.Qxx[j + n * j];
 #pragma unroll
         for (int j = 0; j < n; j++) {
-          const double xj = col[j] / sh.Qxx[j + n * j];
+          const double xj = col[j] * rq[j];
           col[j] = xj;
 #pragma unroll
           for (int i = j + 1; i < n; i++) col[i] = fma(-sh.Qxx[j + n * i], xj, col[i]);
@@ -1121,9 +1132,10 @@ attempt:
               break;
             }
             const double c = sqrt(1.0 - s2);
+            const double rc = 1.0 / c;
             U[i + m * i] = c * Aii;
             for (int j = i + 1; j < m; j++) {
-              const double tmp = (U[i + m * j] - sn * v[j]) / c;
+              const double tmp = (U[i + m * j] - sn * v[j]) * rc;
               v[j] = c * v[j] - sn * tmp;
               U[i + m * j] = tmp;
             }
@@ -1702,18 +1714,19 @@ __device__ inline void dev_qr_R(double* R, double* Pm, int rows, int cols) {
   const int kmax = rows < cols ? rows : cols;
   for (int j = 0; j < kmax; j++) {
     const double alpha = Pm[j + rows * j];
-    double ss = 0.0;
-    for (int i = j + 1; i < rows; i++) ss = fma(Pm[i + rows * j], Pm[i + rows * j], ss);
-    const double xnorm = sqrt(ss);
-    if (xnorm == 0.0) continue;
-    const double beta = -copysign(lapy2(alpha, xnorm), alpha);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // contract v2 (oracle qr_R)
+    for (int i = j + 1; i < rows; i++) acc[(i - j - 1) & 3] = fma(Pm[i + rows * j], Pm[i + rows * j], acc[(i - j - 1) & 3]);
+    const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    if (ss == 0.0) continue;
+    const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
     const double tau = (beta - alpha) / beta;
     const double sc = 1.0 / (alpha - beta);
     for (int i = j + 1; i < rows; i++) Pm[i + rows * j] *= sc;
     Pm[j + rows * j] = beta;
     for (int c = j + 1; c < cols; c++) {
-      double w = Pm[j + rows * c];
-      for (int i = j + 1; i < rows; i++) w = fma(Pm[i + rows * j], Pm[i + rows * c], w);
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int i = j + 1; i < rows; i++) a4[(i - j - 1) & 3] = fma(Pm[i + rows * j], Pm[i + rows * c], a4[(i - j - 1) & 3]);
+      double w = Pm[j + rows * c] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
       w *= tau;
       Pm[j + rows * c] -= w;
       for (int i = j + 1; i < rows; i++) Pm[i + rows * c] = fma(-Pm[i + rows * j], w, Pm[i + rows * c]);
