@@ -685,7 +685,10 @@ static void matmul(double* C, const double* A, int r, int k, const double* B, in
      dependent chain is a quarter as long (LAPACK's dnrm2 also reorders; the values agree to rounding);
    * β = -sign(α)·sqrt(α² + ‖x‖²) with one fma and one sqrt (dlapy2's rescaling only matters near
      overflow);
-   * τ = (β-α)/β and the scale 1/(α-β) as in dlarfg. */
+   contract v3: the reflector is kept unnormalised, v = [α-β; x] (dlarfg divides x by α-β and keeps
+   τ = (β-α)/β; H = I - τ v̂v̂' is the same matrix). With v'v = -2β(α-β), H y = y + v·(v'y)/(β(α-β)):
+   one reciprocal 1/(β(α-β)) per column, no scaling pass over the column, and every applied column
+   costs one fma per row for v'y and one for the update. */
 static double sum4(const double* a) { return (a[0] + a[1]) + (a[2] + a[3]); }
 
 static void qr_R(double* R, double* P, int rows, int cols) {
@@ -697,18 +700,16 @@ static void qr_R(double* R, double* P, int rows, int cols) {
     double ss = sum4(acc);
     if (ss == 0.0) continue; /* tau = 0, H = I */
     double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-    double tau = (beta - alpha) / beta;
-    double sc = 1.0 / (alpha - beta);
-    for (int i = j + 1; i < rows; i++) P[IDX(i, j, rows)] *= sc;
+    double vd = alpha - beta;
+    double rd = 1.0 / (beta * vd);
     P[IDX(j, j, rows)] = beta;
-    /* apply H = I - tau v v' to P[j:rows, j+1:cols], v = [1; P[j+1:rows, j]] */
+    /* apply H to P[j:rows, j+1:cols], v = [vd; P[j+1:rows, j]] */
     for (int c = j + 1; c < cols; c++) {
       double a4[4] = {0.0, 0.0, 0.0, 0.0};
       for (int i = j + 1; i < rows; i++) a4[(i - j - 1) & 3] = fma(P[IDX(i, j, rows)], P[IDX(i, c, rows)], a4[(i - j - 1) & 3]);
-      double w = P[IDX(j, c, rows)] + sum4(a4);
-      w *= tau;
-      P[IDX(j, c, rows)] -= w;
-      for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] = fma(-P[IDX(i, j, rows)], w, P[IDX(i, c, rows)]);
+      double p = fma(vd, P[IDX(j, c, rows)], sum4(a4)) * rd;
+      P[IDX(j, c, rows)] = fma(vd, p, P[IDX(j, c, rows)]);
+      for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] = fma(P[IDX(i, j, rows)], p, P[IDX(i, c, rows)]);
     }
   }
   for (int j = 0; j < cols; j++)

@@ -164,21 +164,24 @@ __device__ __forceinline__ T opaque(T v) {
   return v;
 }
 
-// Broadcast lane L's value to the 16 lanes of its DPP row (= its team when TEAM == 16): a register
-// move (v_mov_b32_dpp row_newbcast:L), no LDS round trip. All lanes of the team must be active.
+// Broadcast lane L's value to the 16 lanes of its DPP row (= its team when TEAM == 16): one 64-bit
+// register move (v_mov_b64_dpp row_newbcast:L, gfx90a+ DPP64), no LDS round trip. All lanes of the
+// team must be active (a disabled source lane is an invalid DPP source).
 template <int L>
 __device__ __forceinline__ double row_bcast(double v) {
-  const long long x = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(x & 0xffffffffll), 0x150 + L, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), 0x150 + L, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+  // (a frozen-poison `old` operand: every lane of the row has a valid source, so no copy of v is
+  // needed to seed the destination)
+  return __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(v), v, 0x150 + L, 0xF, 0xF, true);
 }
 
-// Lane i of each DPP row receives lane i-1's value (row_shr:1); lane 0 keeps `old`.
-__device__ __forceinline__ double row_shr1(double v, double old) {
-  const long long x = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
-  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(x & 0xffffffffll), 0x111, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(x >> 32), 0x111, 0xF, 0xF, false);
+// Lane i of each DPP row receives lane i-1's value (row_shr:1, two 32-bit DPP moves: 64-bit DPP
+// only has row_newbcast); lane 0 of the row receives 0.
+__device__ __forceinline__ double row_shr1(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(0), (int)(x & 0xffffffffll), 0x111,
+                                             0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(0), (int)(x >> 32), 0x111, 0xF, 0xF,
+                                             true);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
@@ -190,51 +193,45 @@ __device__ __forceinline__ double row_shr1(double v, double old) {
 // FULL: rows == ROWS is known at compile time (no per-entry liveness selects).
 template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16, bool FULL = false>
 __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus) {
-#define TQ_LIVE(i, j) ((FULL || (i) < rows) && !((i) > (j) && (i) < TOP))
+#define TQ_LIVE(i, j) ((FULL || TEAMW == 16 || (i) < rows) && !((i) > (j) && (i) < TOP))
   if constexpr (TEAMW == 16) {
     // Reflectors broadcast by DPP row_newbcast (the team is one DPP row). The lane-predicated parts
     // are written branch-free: every lane runs the reflector arithmetic on its own column (SIMT
     // issues it once either way) and lane j's results are selected once per step, and the update
     // uses w = 0 on lanes <= j, which leaves their live entries unchanged (x - 0, fma(v, 0, x)) and
     // only touches the dead reflector storage below their diagonals.
+    // Contract v3 (oracle qr_R): the reflector stays unnormalised, v = [α-β; x], and
+    // H y = y + v (v'y)/(β(α-β)). Per column j, lane j's pivot scalars and its column below the
+    // diagonal reach the team by 64-bit DPP row broadcasts; lanes c > j then spend one fma per row
+    // on v'y and one on the update. Rows past `rows` must be zero: they are inert (fma(0,0,s) == s,
+    // fma(0,p,0) == 0), so the loops run over the compile-time ROWS with no per-row liveness tests.
     static_for<0, COLS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      if (j < rows) {
-        const bool me = (tl == j);
-        // contract v2 (oracle qr_R): 4 interleaved accumulators by position below the diagonal,
-        // β from one fma + one sqrt
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int i = j + 1; i < ROWS; i++)
+        if (TQ_LIVE(i, j)) acc[(i - j - 1) & 3] = fma(a[i], a[i], acc[(i - j - 1) & 3]);
+      const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      const double alpha = a[j];
+      const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
+      const double vd = alpha - beta;
+      const double rd = (ss != 0.0) ? 1.0 / (beta * vd) : 0.0;  // 0: tau = 0, H = I
+      if (tl == j && ss != 0.0) a[j] = beta;
+      const double rdj = row_bcast<j>(rd), vdj = row_bcast<j>(vd);
+      double v[ROWS];
+#pragma unroll
+      for (int i = j + 1; i < ROWS; i++)
+        if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
+      if (tl > j && tl < COLS && rdj != 0.0) {
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (TQ_LIVE(i, j)) acc[(i - j - 1) & 3] = fma(a[i], a[i], acc[(i - j - 1) & 3]);
-        const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        const double alpha = a[j];
-        const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-        const bool refl = me && (ss != 0.0);
-        const double tau_l = refl ? (beta - alpha) / beta : 0.0;
-        const double sc = refl ? 1.0 / (alpha - beta) : 1.0;
+          if (TQ_LIVE(i, j)) a4[(i - j - 1) & 3] = fma(v[i], a[i], a4[(i - j - 1) & 3]);
+        const double p = fma(vdj, a[j], (a4[0] + a4[1]) + (a4[2] + a4[3])) * rdj;
+        a[j] = fma(vdj, p, a[j]);
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (TQ_LIVE(i, j)) a[i] *= sc;
-        if (refl) a[j] = beta;
-        const double tau = row_bcast<j>(tau_l);
-        if (tau != 0.0) {
-          double v[ROWS];
-#pragma unroll
-          for (int i = j + 1; i < ROWS; i++)
-            if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
-          double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int i = j + 1; i < ROWS; i++)
-            if (TQ_LIVE(i, j)) a4[(i - j - 1) & 3] = fma(v[i], a[i], a4[(i - j - 1) & 3]);
-          double w = a[j] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-          w *= tau;
-          if (!(tl > j && tl < COLS)) w = 0.0;
-          a[j] -= w;
-#pragma unroll
-          for (int i = j + 1; i < ROWS; i++)
-            if (TQ_LIVE(i, j)) a[i] = fma(-v[i], w, a[i]);
-        }
+          if (TQ_LIVE(i, j)) a[i] = fma(v[i], p, a[i]);
       }
     });
     return;
@@ -242,41 +239,39 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
 #pragma unroll
   for (int j = 0; j < COLS; j++) {
     if (j < rows) {
+      double vd = 0.0;
       if (tl == j) {
         double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
           if (TQ_LIVE(i, j)) acc[(i - j - 1) & 3] = fma(a[i], a[i], acc[(i - j - 1) & 3]);
         const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        double tau = 0.0;
+        double rd = 0.0;  // contract v3 (see the 16-lane path): 0 means tau = 0, H = I
         if (ss != 0.0) {
           const double alpha = a[j];
           const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-          tau = (beta - alpha) / beta;
-          const double sc = 1.0 / (alpha - beta);
+          vd = alpha - beta;
+          rd = 1.0 / (beta * vd);
 #pragma unroll
           for (int i = j + 1; i < ROWS; i++)
-            if (TQ_LIVE(i, j)) {
-              a[i] *= sc;
-              bus[i] = a[i];
-            }
+            if (TQ_LIVE(i, j)) bus[i] = a[i];
           a[j] = beta;
         }
-        bus[0] = tau;
+        bus[0] = rd;
       }
+      vd = __shfl(vd, (int)(threadIdx.x - tl) + j, WAVE);  // lane j's α-β (every lane active here)
       team_sync();
-      const double tau = bus[0];
-      if (tau != 0.0 && tl > j && tl < COLS) {
+      const double rd = bus[0];
+      if (rd != 0.0 && tl > j && tl < COLS) {
         double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
           if (TQ_LIVE(i, j)) a4[(i - j - 1) & 3] = fma(bus[i], a[i], a4[(i - j - 1) & 3]);
-        double w = a[j] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-        w *= tau;
-        a[j] -= w;
+        const double p = fma(vd, a[j], (a4[0] + a4[1]) + (a4[2] + a4[3])) * rd;
+        a[j] = fma(vd, p, a[j]);
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
-          if (TQ_LIVE(i, j)) a[i] = fma(-bus[i], w, a[i]);
+          if (TQ_LIVE(i, j)) a[i] = fma(bus[i], p, a[i]);
       }
       team_sync();
     }
@@ -284,34 +279,37 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
 #undef TQ_LIVE
 }
 
-// cond(R) > thresh for an upper-triangular m x m R held by every lane of the team (same decision
-// procedure and arithmetic as cond_exceeds; backward_pass.jl:129). R^-1 is formed one column at a
-// time (few live registers); the Jacobi SVD of the rare ambiguous band runs on lane 0 of the team
-// in LDS scratch `w` (m*m + 1 doubles) and its verdict is broadcast.
+// cond(R) > thresh for an upper-triangular m x m R held by every lane of the team (backward_pass.jl:129;
+// the oracle computes cond2 by one-sided Jacobi every time). The Frobenius bounds
+// cond2 <= cF = |R|_F |R^-1|_F <= m cond2 decide almost every call; they are only bounds, so R^-1 is
+// formed with the diagonal reciprocals rR (the gains solve reuses them) and the tests keep a 1e-12
+// relative margin, far above the rounding of cF: a verdict taken here is the oracle's verdict. The
+// Jacobi SVD of the ambiguous band runs on lane 0 of the team in LDS scratch `w` (m*m + 1 doubles)
+// with the oracle's arithmetic, and its verdict is broadcast.
 template <int m>
-__device__ __forceinline__ bool cond_exceeds_team(const double (&R)[m][m], double thresh, double* w, int tl) {
+__device__ __forceinline__ bool cond_exceeds_team(const double (&R)[m][m], const double (&rR)[m], double thresh,
+                                                  double* w, int tl) {
   double nr = 0.0, ni = 0.0;
 #pragma unroll
   for (int c = 0; c < m; c++) {
-    double ric[m];
+    double ric[m];  // column c of R^-1 (zero below row c)
+    ric[c] = rR[c];
 #pragma unroll
-    for (int i = 0; i < m; i++) ric[i] = (i == c) ? 1.0 : 0.0;
+    for (int j = c - 1; j >= 0; j--) {
+      double t = 0.0;
 #pragma unroll
-    for (int j = m - 1; j >= 0; j--) {
-      const double xj = ric[j] / R[j][j];
-      ric[j] = xj;
-#pragma unroll
-      for (int i = j - 1; i >= 0; i--) ric[i] -= R[i][j] * xj;
+      for (int l = j + 1; l <= c; l++) t = fma(R[j][l], ric[l], t);
+      ric[j] = -t * rR[j];
     }
 #pragma unroll
-    for (int i = 0; i < m; i++) {
-      nr += R[i][c] * R[i][c];
-      ni += ric[i] * ric[i];
+    for (int i = 0; i <= c; i++) {
+      nr = fma(R[i][c], R[i][c], nr);
+      ni = fma(ric[i], ric[i], ni);
     }
   }
-  const double cF = sqrt(nr) * sqrt(ni);
-  if (cF <= thresh) return false;
-  if (cF / m > thresh) return true;
+  const double cF = sqrt(nr * ni);
+  if (cF * (1.0 + 1e-12) <= thresh) return false;
+  if (cF * (1.0 - 1e-12) > thresh * m) return true;
   // ambiguous band (team-uniform): one-sided Jacobi singular values on lane 0
   if (tl == 0) {
     double* A = w;
@@ -607,13 +605,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
               a[i] = Quuc[i];
             } else if (i - m < nu) {
               const RowInfo& ri = rows[ur[i - m]];
-              a[i] = ri.ws * row_at(ri, n + cu);
+              // (control-bound rows: one gradient entry, ±1 at n + control)
+              a[i] = ri.ws * ((ri.idx[0] == n + cu) ? ri.v[0] : 0.0);
             } else {
               a[i] = 0.0;
             }
           }
           if (!term) BPROF(14)  // expand: chol_plus operand rows
-          if (nu == PU)  // every control bounded on both sides: the common case, no row selects
+          // (16-lane teams run every QR over the zero-padded compile-time rows; 8-lane teams
+          // specialise the common case, every control bounded on both sides)
+          if (TEAM == 16 || nu == PU)
             team_qr<m + PU, m, m, TEAM, true>(a, m + PU, tl, bus);
           else
             team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
@@ -910,7 +911,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
       for (int i = 0; i < m; i++) col[i] = Qu[i];
     }
-    double F[m][m];
+    double F[m][m], rF[m];
     bool ok = true;
     int piv[m];
     if (!SQRT) {
@@ -1043,7 +1044,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           for (int i = 0; i < m; i++) F[i][j] = bus[i + m * j];
         team_sync();
       }
-      ok = !cond_exceeds_team<m>(F, 1e8, bus2, tl);
+#pragma unroll
+      for (int j = 0; j < m; j++) rF[j] = 1.0 / F[j][j];
+      ok = !cond_exceeds_team<m>(F, rF, 1e8, bus2, tl);
     }
     BPROF(5)  // regularise + cond
     if (!ok) {
@@ -1089,9 +1092,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       }
     } else {
       // K = -Quu_reg \ (Quu_reg' \ Qux_reg); contract v2: multiply by the diagonal reciprocals
-      double rF[m];
-#pragma unroll
-      for (int j = 0; j < m; j++) rF[j] = 1.0 / F[j][j];
+      // (rF: the diagonal reciprocals formed for the cond test)
 #pragma unroll
       for (int j = 0; j < m; j++) {
         const double xj = col[j] * rF[j];
@@ -1293,63 +1294,56 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! by each row of tmp1 (backward_pass.jl:186-192).
       // Systolic schedule: lane i owns row i of the factor; the downdate of (row r, column i) needs
       // only (r, i-1) and (r-1, i), so step t runs (r = t - i, i) on every lane i < m: n+m-1 steps
-      // instead of n*m, each (r, i) with exactly the oracle's operations. x travels lane to lane
-      // through a double-buffered bus slot.
+      // instead of n*m, each (r, i) with exactly the oracle's operations. Lane i keeps its row and
+      // the travelling x in a frame shifted by i (u[k] = R[i][i+k], w[k] = x[i+k]; slots k >= m-i
+      // carry don't-care values), so the pivot is always u[0], w[0] with no per-lane selects, and
+      // lane i-1 hands lane i its w[1..] (DPP row_shr:1 on 16-lane teams).
       const double* U2p;  // tmp2 (column-major): the downdated factor, or Q.uu on failure
       {
-        double urow[m], v[m];
+        double u[m], w[m];
 #pragma unroll
-        for (int jj = 0; jj < m; jj++) {
-          urow[jj] = colu ? QU[cu + m * jj] : 0.0;
-          v[jj] = 0.0;
+        for (int k = 0; k < m; k++) {
+          u[k] = (colu && tl + k < m) ? QU[tl + m * (tl + k)] : 0.0;
+          w[k] = 0.0;
         }
         double* msg = bus2;  // [2][m][m] (8-lane teams)
         bool okd = true;
 #pragma unroll 1
         for (int t = 0; t < n + m - 1; t++) {
           const int r = t - tl;
-          double vin[m];
+          double win[m];
           if constexpr (TEAM == 16) {
 #pragma unroll
-            for (int jj = 0; jj < m; jj++) vin[jj] = row_shr1(v[jj], 0.0);  // lane i-1's x from step t-1
+            for (int k = 0; k + 1 < m; k++) win[k] = row_shr1(w[k + 1]);  // lane i-1's x from step t-1
           }
           if (colu && r >= 0 && r < n) {
             if (tl == 0) {
 #pragma unroll
-              for (int jj = 0; jj < m; jj++) v[jj] = bus[TB + r * m + jj];
+              for (int k = 0; k < m; k++) w[k] = bus[TB + r * m + k];
             } else if constexpr (TEAM == 16) {
 #pragma unroll
-              for (int jj = 0; jj < m; jj++) v[jj] = vin[jj];
+              for (int k = 0; k + 1 < m; k++) w[k] = win[k];
             } else {
               const double* in = msg + ((t - 1) & 1) * m * m + (tl - 1) * m;
 #pragma unroll
-              for (int jj = 0; jj < m; jj++) v[jj] = in[jj];
+              for (int k = 0; k + 1 < m; k++) w[k] = in[k + 1];
             }
-            double Aii = urow[0], vi = v[0];
-#pragma unroll
-            for (int ii = 1; ii < m; ii++)
-              if (ii == tl) {
-                Aii = urow[ii];
-                vi = v[ii];
-              }
-            const double sn = vi / Aii;
+            const double sn = w[0] / u[0];
             const double s2 = sn * sn;
             if (s2 > 1.0) okd = false;
             const double cs = sqrt(1.0 - s2);
             const double rcs = 1.0 / cs;  // contract v2: one division per rotation
+            u[0] = cs * u[0];
 #pragma unroll
-            for (int jj = 0; jj < m; jj++) {
-              if (jj == tl) urow[jj] = cs * Aii;
-              if (jj > tl) {
-                const double tmp = (urow[jj] - sn * v[jj]) * rcs;
-                v[jj] = cs * v[jj] - sn * tmp;
-                urow[jj] = tmp;
-              }
+            for (int k = 1; k < m; k++) {
+              const double tmp = (u[k] - sn * w[k]) * rcs;
+              w[k] = cs * w[k] - sn * tmp;
+              u[k] = tmp;
             }
             if constexpr (TEAM != 16) {
               double* out = msg + (t & 1) * m * m + tl * m;
 #pragma unroll
-              for (int jj = 0; jj < m; jj++) out[jj] = v[jj];
+              for (int k = 0; k < m; k++) out[k] = w[k];
             }
           }
           if constexpr (TEAM != 16) team_sync();
@@ -1358,7 +1352,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         const bool fail = (__ballot(!okd) & tmask) != 0ull;
         if (colu) {
 #pragma unroll
-          for (int jj = 0; jj < m; jj++) bus2[2 * m * m + tl + m * jj] = (jj >= tl) ? urow[jj] : 0.0;
+          for (int jj = 0; jj < m; jj++)
+            if (jj < tl) bus2[2 * m * m + tl + m * jj] = 0.0;
+#pragma unroll
+          for (int k = 0; k < m; k++)
+            if (tl + k < m) bus2[2 * m * m + tl + m * (tl + k)] = u[k];
         }
         team_sync();
         U2p = fail ? QU : bus2 + 2 * m * m;

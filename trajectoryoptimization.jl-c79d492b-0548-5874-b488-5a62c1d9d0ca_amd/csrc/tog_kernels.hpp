@@ -410,25 +410,23 @@ __device__ void wqr(double* A, int rows, double* wv) {
     if (ss == 0.0) continue;  // tau = 0, H = I (uniform branch: every lane computed ss)
     const double alpha = A[j + rows * j];
     const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-    const double tau = (beta - alpha) / beta;
-    const double sc = 1.0 / (alpha - beta);
-    wsync();
-    for (int i = j + 1 + lane; i < rows; i += WAVE) A[i + rows * j] *= sc;
+    // contract v3 (oracle qr_R): unnormalised reflector v = [α-β; x], H y = y + v (v'y)/(β(α-β))
+    const double vd = alpha - beta;
+    const double rd = 1.0 / (beta * vd);
     wsync();
     if (lane > j && lane < COLS) {
       const int c = lane;
       double a4[4] = {0.0, 0.0, 0.0, 0.0};
       for (int i = j + 1; i < rows; i++) a4[(i - j - 1) & 3] = fma(A[i + rows * j], A[i + rows * c], a4[(i - j - 1) & 3]);
-      double w = A[j + rows * c] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-      w *= tau;
-      A[j + rows * c] -= w;
-      wv[c] = w;
+      const double p = fma(vd, A[j + rows * c], (a4[0] + a4[1]) + (a4[2] + a4[3])) * rd;
+      A[j + rows * c] = fma(vd, p, A[j + rows * c]);
+      wv[c] = p;
     }
     wsync();
     const int nc = COLS - j - 1, nr = rows - j - 1;
     for (int e = lane; e < nc * nr; e += WAVE) {
       const int i = j + 1 + e % nr, c = j + 1 + e / nr;
-      A[i + rows * c] = fma(-A[i + rows * j], wv[c], A[i + rows * c]);
+      A[i + rows * c] = fma(A[i + rows * j], wv[c], A[i + rows * c]);
     }
     if (lane == 0) A[j + rows * j] = beta;
     wsync();
@@ -929,18 +927,16 @@ attempt:
           if (ss == 0.0) continue;
           const double alpha = Wl[j + rows * j];
           const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-          const double tau = (beta - alpha) / beta;
-          const double sc = 1.0 / (alpha - beta);
-          for (int i = j + 1; i < rows; i++) Wl[i + rows * j] *= sc;
+          const double vd = alpha - beta;  // contract v3 (oracle qr_R)
+          const double rd = 1.0 / (beta * vd);
           Wl[j + rows * j] = beta;
           for (int c = j + 1; c < m; c++) {
             double a4[4] = {0.0, 0.0, 0.0, 0.0};
             for (int i = j + 1; i < rows; i++)
               a4[(i - j - 1) & 3] = fma(Wl[i + rows * j], Wl[i + rows * c], a4[(i - j - 1) & 3]);
-            double w = Wl[j + rows * c] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-            w *= tau;
-            Wl[j + rows * c] -= w;
-            for (int i = j + 1; i < rows; i++) Wl[i + rows * c] = fma(-Wl[i + rows * j], w, Wl[i + rows * c]);
+            const double p = fma(vd, Wl[j + rows * c], (a4[0] + a4[1]) + (a4[2] + a4[3])) * rd;
+            Wl[j + rows * c] = fma(vd, p, Wl[j + rows * c]);
+            for (int i = j + 1; i < rows; i++) Wl[i + rows * c] = fma(Wl[i + rows * j], p, Wl[i + rows * c]);
           }
         }
         for (int j = 0; j < m; j++)
@@ -1719,17 +1715,15 @@ __device__ inline void dev_qr_R(double* R, double* Pm, int rows, int cols) {
     const double ss = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     if (ss == 0.0) continue;
     const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-    const double tau = (beta - alpha) / beta;
-    const double sc = 1.0 / (alpha - beta);
-    for (int i = j + 1; i < rows; i++) Pm[i + rows * j] *= sc;
+    const double vd = alpha - beta;  // contract v3 (oracle qr_R)
+    const double rd = 1.0 / (beta * vd);
     Pm[j + rows * j] = beta;
     for (int c = j + 1; c < cols; c++) {
       double a4[4] = {0.0, 0.0, 0.0, 0.0};
       for (int i = j + 1; i < rows; i++) a4[(i - j - 1) & 3] = fma(Pm[i + rows * j], Pm[i + rows * c], a4[(i - j - 1) & 3]);
-      double w = Pm[j + rows * c] + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-      w *= tau;
-      Pm[j + rows * c] -= w;
-      for (int i = j + 1; i < rows; i++) Pm[i + rows * c] = fma(-Pm[i + rows * j], w, Pm[i + rows * c]);
+      const double p = fma(vd, Pm[j + rows * c], (a4[0] + a4[1]) + (a4[2] + a4[3])) * rd;
+      Pm[j + rows * c] = fma(vd, p, Pm[j + rows * c]);
+      for (int i = j + 1; i < rows; i++) Pm[i + rows * c] = fma(Pm[i + rows * j], p, Pm[i + rows * c]);
     }
   }
   for (int j = 0; j < cols; j++)
