@@ -918,7 +918,7 @@ static int chol_minus(double* Uo, const double* A, int n, const double* B, int n
     for (int j = 0; j < n; j++) v[j] = B[IDX(r, j, nb)];
     for (int i = 0; i < n; i++) {
       double Aii = U[IDX(i, i, n)];
-      double s = v[i] / Aii;
+      double s = v[i] * (1.0 / Aii); /* contract v3: the reciprocal comes off the rotation's chain */
       double s2 = s * s;
       if (s2 > 1.0) return i + 1;
       double c = sqrt(1.0 - s2);

@@ -207,6 +207,9 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
     // fma(0,p,0) == 0), so the loops run over the compile-time ROWS with no per-row liveness tests.
     static_for<0, COLS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
+      // lane tests recomputed per column from an opaque lane id: hoisted, the per-column exec masks
+      // of every QR stay live across the knot loop as SGPR pairs and spill
+      const int tq = opaque(tl);
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int i = j + 1; i < ROWS; i++)
@@ -216,13 +219,13 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
       const double beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
       const double vd = alpha - beta;
       const double rd = (ss != 0.0) ? 1.0 / (beta * vd) : 0.0;  // 0: tau = 0, H = I
-      if (tl == j && ss != 0.0) a[j] = beta;
+      if (tq == j && ss != 0.0) a[j] = beta;
       const double rdj = row_bcast<j>(rd), vdj = row_bcast<j>(vd);
       double v[ROWS];
 #pragma unroll
       for (int i = j + 1; i < ROWS; i++)
         if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
-      if (tl > j && tl < COLS && rdj != 0.0) {
+      if (tq > j && tq < COLS && rdj != 0.0) {
         double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = j + 1; i < ROWS; i++)
@@ -734,7 +737,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         team_sync();
       }
     }
-    // [A B] columns on the bus (first region)
+    // [A B] columns on the bus (first region; the std path's products read them there)
     double* bus2 = bus + n * L;
     if (colx) {
 #pragma unroll
@@ -744,6 +747,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
       for (int i = 0; i < n; i++) bus[i + n * (n + tl)] = Bc[i];
     }
+    if (SQRT) team_sync();
     if (!SQRT) {
       // T1 = [A B]' S (L x n), then Q.xx += (A'S)A ; Q.uu += (B'S)B ; Q.ux += (B'S)A (backward_pass.jl:32-36)
       team_sync();
@@ -800,43 +804,54 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         TX[i] = 0.0;
         TU[i] = 0.0;
       }
+      // Column l of S is read from LDS in one burst (one wait per column, rolled loop: few live
+      // registers); dense as the oracle's operand (explicit zeros below the diagonal).
 #pragma unroll 1
       for (int l = 0; l < n; l++) {
-        const double al = bus[l + n * c];
-        const double bl = bus[l + n * (n + cu)];
-        const double* Sl = Sreg + n * l;  // column l, explicit zeros below the diagonal
+        double sl[n];
+        const double* Sl = Sreg + n * l;
+#pragma unroll
+        for (int i = 0; i < n; i++) sl[i] = Sl[i];
+        const double al = bus[l + n * c], bl = bus[l + n * (n + cu)];
+        TEAM_FENCE();
 #pragma unroll
         for (int i = 0; i < n; i++) {
-          TX[i] = fma(Sl[i], al, TX[i]);
-          TU[i] = fma(Sl[i], bl, TU[i]);
+          TX[i] = fma(sl[i], al, TX[i]);
+          TU[i] = fma(sl[i], bl, TU[i]);
         }
       }
-      team_sync();
-      // tmp_u columns (lanes < m) then the tmp_x columns, both in region 1 ([A B] is dead)
-      double* busx = bus + n * m;
-      if (colu) {
-#pragma unroll
-        for (int i = 0; i < n; i++) bus[i + n * tl] = TU[i];
-      }
-      if (colx) {
-#pragma unroll
-        for (int i = 0; i < n; i++) busx[i + n * tl] = TX[i];
-      }
-      team_sync();
+      // Q.ux += tmp_u' tmp_x: tmp_u columns (lanes < m) then tmp_x columns go to region 1 ([A B]
+      // is dead); per l one burst of reads, one wait. (A DPP form that skips the round trip makes the
+      // compiler hoist the broadcasts and spill.)
       {
+        team_sync();
+        double* busx = bus + n * m;
+        if (colu) {
+#pragma unroll
+          for (int i = 0; i < n; i++) bus[i + n * tl] = TU[i];
+        }
+        if (colx) {
+#pragma unroll
+          for (int i = 0; i < n; i++) busx[i + n * tl] = TX[i];
+        }
+        team_sync();
         double t[m];
 #pragma unroll
         for (int i = 0; i < m; i++) t[i] = 0.0;
 #pragma unroll 1
         for (int l = 0; l < n; l++) {
+          double tu[m];
           const double tx = busx[l + n * c];
 #pragma unroll
-          for (int i = 0; i < m; i++) t[i] = fma(bus[l + n * i], tx, t[i]);
+          for (int i = 0; i < m; i++) tu[i] = bus[l + n * i];
+          TEAM_FENCE();
+#pragma unroll
+          for (int i = 0; i < m; i++) t[i] = fma(tu[i], tx, t[i]);
         }
 #pragma unroll
         for (int i = 0; i < m; i++) Quxc[i] += t[i];
+        team_sync();
       }
-      team_sync();
       BPROF(2)  // S [A B], Q.ux
       {
         double a[m + n];
@@ -1300,12 +1315,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
       // lane i-1 hands lane i its w[1..] (DPP row_shr:1 on 16-lane teams).
       const double* U2p;  // tmp2 (column-major): the downdated factor, or Q.uu on failure
       {
-        double u[m], w[m];
+        double u[m], w[m], wn[m];
 #pragma unroll
         for (int k = 0; k < m; k++) {
           u[k] = (colu && tl + k < m) ? QU[tl + m * (tl + k)] : 0.0;
           w[k] = 0.0;
+          wn[k] = bus[TB + k];  // lane 0: row 0 of tmp1 (the other lanes ignore wn)
         }
+        double ru = 1.0 / u[0];  // contract v3: s = x_i·(1/R_ii), the reciprocal formed a step ahead
         double* msg = bus2;  // [2][m][m] (8-lane teams)
         bool okd = true;
 #pragma unroll 1
@@ -1319,7 +1336,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
           if (colu && r >= 0 && r < n) {
             if (tl == 0) {
 #pragma unroll
-              for (int k = 0; k < m; k++) w[k] = bus[TB + r * m + k];
+              for (int k = 0; k < m; k++) w[k] = wn[k];
+              const int rn = r + 1 < n ? r + 1 : r;  // prefetch the next row of tmp1
+#pragma unroll
+              for (int k = 0; k < m; k++) wn[k] = bus[TB + rn * m + k];
             } else if constexpr (TEAM == 16) {
 #pragma unroll
               for (int k = 0; k + 1 < m; k++) w[k] = win[k];
@@ -1328,12 +1348,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
 #pragma unroll
               for (int k = 0; k + 1 < m; k++) w[k] = in[k + 1];
             }
-            const double sn = w[0] / u[0];
+            const double sn = w[0] * ru;
             const double s2 = sn * sn;
             if (s2 > 1.0) okd = false;
             const double cs = sqrt(1.0 - s2);
             const double rcs = 1.0 / cs;  // contract v2: one division per rotation
             u[0] = cs * u[0];
+            ru = 1.0 / u[0];
 #pragma unroll
             for (int k = 1; k < m; k++) {
               const double tmp = (u[k] - sn * w[k]) * rcs;

@@ -1121,7 +1121,7 @@ attempt:
           for (int j = 0; j < m; j++) v[j] = sh.tmp1[r + n * j];
           for (int i = 0; i < m; i++) {
             const double Aii = U[i + m * i];
-            const double sn = v[i] / Aii;
+            const double sn = v[i] * (1.0 / Aii);  // contract v3 (oracle chol_minus)
             const double s2 = sn * sn;
             if (s2 > 1.0) {
               okd = false;
