@@ -336,6 +336,42 @@ int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps);
 /* per-trajectory tog_traj_flag bits; flags_out: (B) int32 */
 int32_t tog_status(tog_handle* h, int32_t* flags_out);
 
+/* ---- ALTRO phase 2: projected Newton (src/solvers/direct/projected_newton.jl) ---- */
+/* ProjectedNewtonSolverOptions (src/solvers/direct/direct_solvers.jl:14-30); tog_default_pn_options
+   fills the reference defaults. Only solve_type :feasible (the default) is built: newton_step!
+   returns after projection_solve! (projected_newton.jl:498-501). */
+typedef struct tog_pn_options {
+  int32_t n_steps;              /* 1                                                          */
+  int32_t solve_type;           /* 0 = :feasible (1 = :optimal -> TOG_ERR_UNSUPPORTED)        */
+  double active_set_tolerance;  /* 1e-3: inequality rows with c >= -tol are projected         */
+  double feasibility_tolerance; /* 1e-6                                                       */
+} tog_pn_options;
+void tog_default_pn_options(tog_pn_options* opts);
+
+/* per-trajectory projected-Newton statistics row (tog_solve_pn out), all double */
+enum tog_pn_stat {
+  TOG_PN_VIOL = 0,        /* last viol of projection_solve! (active rows incl. dynamics, Inf norm) */
+  TOG_PN_C_MAX = 1,       /* max_violation(prob) after the solve (record_iteration!)           */
+  TOG_PN_J = 2,           /* cost(prob) after the solve                                         */
+  TOG_PN_PROJECTIONS = 3, /* _projection_solve! calls                                           */
+  TOG_PN_LINESEARCHES = 4,/* _projection_linesearch! calls                                      */
+  TOG_PN_REFINEMENTS = 5, /* reg_solve refinement iterations, in total                          */
+  TOG_PN_STEPS = 6,       /* newton steps taken (solver.stats[:iterations])                     */
+  TOG_PN_NSTATS = 7
+};
+/* The reference's _projection_linesearch! evaluates `count += a` (Int + BitVector, a MethodError)
+   when its first trial does not reduce the violation (projected_newton.jl:273-277): such a
+   trajectory stops with this flag and keeps the last accepted iterate. */
+#define TOG_TRAJ_PN_ERROR (1 << 11)
+
+/* solve!(prob, ProjectedNewtonSolver(prob, opts)) (projected_newton.jl:6-20) on every trajectory's
+   current X, U (in place): n_steps newton steps of the feasible projection, each
+   projection_solve! -> _projection_solve! (Jacobians of the dynamics and of the active
+   constraints, S = Y H⁻¹ Yᵀ with H the diagonal of the cost Hessian, a block-tridiagonal Cholesky
+   of S + 1e-2 I, chord-method line searches with reg_solve refinement to |r| < 1e-8).
+   out: (TOG_PN_NSTATS, B) host pointer or NULL. */
+int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out);
+
 /* per-kernel timing with HIP events recorded on the handle's stream around every launch issued by
    tog_solve_step (used by bench.py for the live roofline). */
 enum tog_kernel_id {

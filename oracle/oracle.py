@@ -69,6 +69,7 @@ def lib():
         L.oc_cond2.argtypes = [dp, C.c_int]
         L.oc_cond2.restype = C.c_double
         L.oc_qr_R.argtypes = [dp, dp, C.c_int, C.c_int]
+        L.oc_solve_pn.argtypes = [vp, C.POINTER(abi.tog_pn_options), dp]
         L.oc_solve_batch.restype = C.c_int64
         L.oc_solve_batch.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp, dp,
                                      C.c_int64, C.c_int]
@@ -198,6 +199,15 @@ class OracleSolver:
 
     def max_violation(self):
         return lib().oc_max_violation(self.s)
+
+    def solve_pn(self, pn_opts):
+        """solve!(prob, ProjectedNewtonSolver) (projected_newton.jl:6-20) on this trajectory's X, U;
+        returns the TOG_PN_NSTATS statistics row."""
+        out = np.zeros(abi.PN_NSTATS)
+        rc = lib().oc_solve_pn(self.s, C.byref(_pkg.to_tog_pn_options(pn_opts)), _dp(out))
+        if rc != 0:
+            raise NotImplementedError("projected Newton solve_type :optimal is not built")
+        return out
 
     def trace(self):
         out = np.empty((4096, 6))

@@ -2207,3 +2207,6 @@ OC_EXPORT int64_t oc_solve_batch(const tog_problem_desc* d, const tog_options* o
   (void)nthreads;
   return total;
 }
+
+/* ALTRO phase 2: projected Newton feasible projection (oracle/tog_oracle_pn.c) */
+#include "tog_oracle_pn.c"

@@ -1,0 +1,185 @@
+"""ALTRO phase 2, the projected Newton feasible projection:
+src/solvers/direct/projected_newton.jl:6-303 with ProjectedNewtonSolverOptions
+(direct_solvers.jl:14-30), driven from ALTRO by altro_methods.jl:5-39.
+
+CPU tests pin the oracle (oracle/tog_oracle_pn.c) on the reference's own assertions
+(test/projected_newton_test.jl:111-120: after the projection ``max_violation < feasibility_tolerance``;
+test/altro_tests.jl:40-46,65: the 1e-10 polish after an AL phase stopped at 1e-2). The ``gpu`` tests
+hold libtog.so (k_pn_begin / k_pn_project / k_pn_finish, tog_pn.hpp, through the C ABI) bit for bit
+to the oracle from the same AL iterate: X, U and every statistic.
+"""
+import numpy as np
+import pytest
+
+TOL_STEP = 1e-13
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=float)
+    b = np.asarray(b, dtype=float)
+    scale = max(1.0, float(np.max(np.abs(b)))) if b.size else 1.0
+    return float(np.max(np.abs(a - b))) / scale if b.size else 0.0
+
+
+def car_al_opts(tog, tol=1e-3):
+    """test/projected_newton_test.jl:29-35 (AL phase before the projection)."""
+    return tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(), constraint_tolerance=tol,
+                                                constraint_tolerance_intermediate=1e-1)
+
+
+def car_batch(tog, B, seed=3):
+    """Problems.car_obstacles with B perturbed copies of the reference's U0 = ones."""
+    rng = np.random.default_rng(seed)
+    U0 = np.ones((B, 50, 2)) + 0.05 * rng.standard_normal((B, 50, 2))
+    U0[0] = 1.0
+    return tog.Problems.car_obstacles(U0=U0, B=B)
+
+
+def oracle_al_state(tog, oracle, prob, opts):
+    """AL-solve every trajectory on the oracle; returns a copy of prob holding the AL iterates."""
+    p = prob.copy()
+    for b in range(prob.B):
+        o = oracle.OracleSolver(prob, opts, b=b)
+        o.solve()
+        p._X[b] = o.get("X")
+        p._U[b] = o.get("U")
+    return p
+
+
+# ----------------------------------------------------------------------------- CPU: host + oracle
+
+
+def test_pn_options_defaults(tog):
+    """ProjectedNewtonSolverOptions defaults (direct_solvers.jl:14-30) on both sides of the ABI."""
+    o = tog.ProjectedNewtonSolverOptions()
+    assert (o.n_steps, o.solve_type, o.active_set_tolerance, o.feasibility_tolerance) == (1, "feasible", 1e-3, 1e-6)
+    c = tog.to_tog_pn_options(o)
+    assert (c.n_steps, c.solve_type, c.active_set_tolerance, c.feasibility_tolerance) == (1, 0, 1e-3, 1e-6)
+    lib = tog.abi.load_library()
+    d = tog.abi.tog_pn_options()
+    lib.tog_default_pn_options(d)
+    assert (d.n_steps, d.solve_type, d.active_set_tolerance, d.feasibility_tolerance) == (1, 0, 1e-3, 1e-6)
+    with pytest.raises(NotImplementedError):
+        tog.to_tog_pn_options(tog.ProjectedNewtonSolverOptions(solve_type="optimal"))
+    with pytest.raises(ValueError):
+        tog.to_tog_pn_options(tog.ProjectedNewtonSolverOptions(solve_type="fast"))
+
+
+def test_altro_pn_tolerances(tog):
+    """altro_methods.jl:5-13: projected_newton moves the AL phase's constraint tolerance."""
+    opts = tog.ALTROSolverOptions(projected_newton=True, projected_newton_tolerance=1e-2)
+    tog.solvers._altro_pn_tolerances(opts)
+    assert opts.opts_al.constraint_tolerance == 1e-2 and not opts.opts_al.kickout_max_penalty
+    opts = tog.ALTROSolverOptions(projected_newton=True, projected_newton_tolerance=-1.0)
+    tog.solvers._altro_pn_tolerances(opts)
+    assert opts.opts_al.constraint_tolerance == 0.0 and opts.opts_al.kickout_max_penalty
+    opts = tog.ALTROSolverOptions(projected_newton=False)
+    tol0 = opts.opts_al.constraint_tolerance
+    tog.solvers._altro_pn_tolerances(opts)
+    assert opts.opts_al.constraint_tolerance == tol0
+
+
+def test_pn_rejects_infeasible_start(tog):
+    prob = tog.Problems.pendulum()
+    prob.X = tog.line_trajectory(prob.x0[0], prob.xf, prob.N)
+    with pytest.raises(NotImplementedError):
+        tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
+
+
+@pytest.mark.parametrize("ft,at", [(1e-6, 1e-3), (1e-10, 1e-3), (1e-10, 1e-4)])
+def test_oracle_projection_reaches_tolerance(tog, oracle, ft, at):
+    """test/projected_newton_test.jl:111-120: after the projection every constraint is satisfied to
+    the feasibility tolerance (``max_violation(solver) < feasibility_tolerance``), and the AL iterate it
+    starts from is not (1e-3 AL tolerance)."""
+    prob = tog.Problems.car_obstacles()
+    o = oracle.OracleSolver(prob, car_al_opts(tog))
+    o.solve()
+    c0 = o.max_violation()
+    assert 1e-7 < c0 < 1e-3
+    J0 = o.cost()
+    out = o.solve_pn(tog.ProjectedNewtonSolverOptions(feasibility_tolerance=ft, active_set_tolerance=at, n_steps=3))
+    assert out[tog.abi.PN_C_MAX] < ft
+    assert out[tog.abi.PN_C_MAX] == o.max_violation()
+    assert out[tog.abi.PN_VIOL] < ft
+    assert out[tog.abi.PN_STEPS] >= 1 and out[tog.abi.PN_PROJECTIONS] >= 1
+    assert out[tog.abi.PN_LINESEARCHES] >= out[tog.abi.PN_PROJECTIONS]
+    # a feasibility projection: the cost moves by a small amount only
+    assert abs(out[tog.abi.PN_J] - J0) < 1e-2 * abs(J0)
+
+
+def test_oracle_projection_noop_when_feasible(tog, oracle):
+    """projection_solve!'s while loop (projected_newton.jl:198-210) does not run when viol <= eps;
+    solve! still records one iteration."""
+    prob = tog.Problems.car_obstacles()
+    o = oracle.OracleSolver(prob, car_al_opts(tog))
+    o.solve()
+    o.solve_pn(tog.ProjectedNewtonSolverOptions(feasibility_tolerance=1e-10))
+    X, U = o.get("X"), o.get("U")
+    out = o.solve_pn(tog.ProjectedNewtonSolverOptions(feasibility_tolerance=1e-2))
+    assert out[tog.abi.PN_PROJECTIONS] == 0 and out[tog.abi.PN_STEPS] == 1
+    assert np.array_equal(o.get("X"), X) and np.array_equal(o.get("U"), U)
+
+
+# ----------------------------------------------------------------------------- GPU: device vs oracle
+
+
+def _pn_compare(tog, oracle, prob, al_opts, pn_opts):
+    """Device projected Newton from the oracle's AL iterates vs the oracle from the same state."""
+    start = oracle_al_state(tog, oracle, prob, al_opts)
+    gp = start.copy()
+    solver = tog.ProjectedNewtonSolver(gp, pn_opts)
+    tog.solve_b(gp, solver)
+    st = solver.stats
+    for b in range(prob.B):
+        o = oracle.OracleSolver(start, al_opts, b=b)  # X given: PrimalDual(prob) from the AL iterate
+        out = o.solve_pn(pn_opts)
+        assert rel(gp._X[b], o.get("X")) < TOL_STEP and rel(gp._U[b], o.get("U")) < TOL_STEP, b
+        for key, idx in (("projections", tog.abi.PN_PROJECTIONS), ("linesearches", tog.abi.PN_LINESEARCHES),
+                         ("refinements", tog.abi.PN_REFINEMENTS), ("iterations", tog.abi.PN_STEPS)):
+            assert st[key][b] == out[idx], (b, key, st[key][b], out[idx])
+        assert abs(st["c_max"][b] - out[tog.abi.PN_C_MAX]) <= 1e-13 * max(1.0, abs(out[tog.abi.PN_C_MAX]))
+        assert rel(st["cost"][b], out[tog.abi.PN_J]) < TOL_STEP
+        assert rel(st["viol"][b], out[tog.abi.PN_VIOL]) < TOL_STEP
+    return gp, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ft,at", [(1e-6, 1e-3), (1e-10, 1e-4)])
+def test_gpu_pn_car_parity(tog, oracle, gpu, ft, at):
+    """Device vs oracle on the reference's projected Newton problem, 4 perturbed starts."""
+    prob = car_batch(tog, 4)
+    pn = tog.ProjectedNewtonSolverOptions(feasibility_tolerance=ft, active_set_tolerance=at, n_steps=3)
+    gp, st = _pn_compare(tog, oracle, prob, car_al_opts(tog), pn)
+    ok = (st["flags"] & tog.abi.TRAJ_PN_ERROR) == 0
+    assert np.all(st["c_max"][ok] < ft)
+
+
+@pytest.mark.gpu
+def test_gpu_altro_projected_newton(tog, oracle, gpu):
+    """ALTRO with projected_newton (test/altro_tests.jl:40-46,65): AL to 1e-2, then the polish to
+    1e-10 on the same device buffers; the oracle runs the same two phases."""
+    prob = car_batch(tog, 3, seed=11)
+    al = car_al_opts(tog, tol=1e-3)
+    opts = tog.ALTROSolverOptions(opts_al=al, projected_newton=True, projected_newton_tolerance=1e-2)
+    opts.opts_pn.feasibility_tolerance = 1e-10
+    opts.opts_pn.active_set_tolerance = 1e-4
+    gp = prob.copy()
+    solver = tog.solve_b(gp, opts)
+    assert opts.opts_al.constraint_tolerance == 1e-2
+    for b in range(prob.B):
+        o = oracle.OracleSolver(prob, opts.opts_al, b=b)
+        o.solve()
+        out = o.solve_pn(opts.opts_pn)
+        assert rel(gp._X[b], o.get("X")) < 1e-6 and rel(gp._U[b], o.get("U")) < 1e-6, b
+        assert solver.stats_pn["iterations"][b] == out[tog.abi.PN_STEPS]
+        if not solver.stats_pn["flags"][b] & tog.abi.TRAJ_PN_ERROR:
+            assert solver.stats_pn["c_max"][b] < 1e-10
+
+
+@pytest.mark.gpu
+def test_gpu_pn_quad_maze(tog, oracle, gpu):
+    """Config 4 constraint set (n + pmax = 32 rows per block, the largest the wave kernels take)
+    at a short horizon: device vs oracle from the oracle's AL iterates."""
+    prob, opts = tog.Problems.config_quad_maze(B=2, N=41)
+    pn = tog.ProjectedNewtonSolverOptions(feasibility_tolerance=1e-8, n_steps=2)
+    _pn_compare(tog, oracle, prob, opts, pn)

@@ -17,8 +17,8 @@ from .problem import (BoundConstraint, CircleConstraints, Constraints, Constrain
                       initial_states_b, max_violation, midpoint, rk3, rk4, set_x0_b, sphere_constraint, add_slack_controls,
                       InfeasibleConstraint, infeasible_constraints, infeasible_problem, line_trajectory)
 from .solvers import (Expansion, AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
-                      AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, solve, solve_b, solver_name,
-                      to_tog_options)
+                      AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, ProjectedNewtonSolver,
+                      ProjectedNewtonSolverOptions, solve, solve_b, solver_name, to_tog_options, to_tog_pn_options)
 from .steps import backwardpass_b, cost, cost_expansion_b, forwardpass_b, jacobian_b, rollout_b, update_constraints_b
 from . import problems as Problems
 from . import distributed
@@ -32,5 +32,5 @@ __all__ = [
     "AugmentedLagrangianSolverOptions", "iLQRSolver", "iLQRSolverOptions", "solve", "solve_b", "solver_name",
     "to_tog_options", "Expansion", "backwardpass_b", "cost", "cost_expansion_b", "update_constraints_b", "forwardpass_b", "jacobian_b", "rollout_b",
     "Problems", "add_slack_controls", "InfeasibleConstraint", "infeasible_constraints", "infeasible_problem",
-    "line_trajectory",
+    "line_trajectory", "ProjectedNewtonSolver", "ProjectedNewtonSolverOptions", "to_tog_pn_options",
 ]

@@ -47,6 +47,11 @@ TRAJ_AL_CONVERGED = 1 << 7
 TRAJ_AL_MAX_ITERS = 1 << 8
 TRAJ_SINGULAR = 1 << 9
 TRAJ_BP_ABORTED = 1 << 10
+TRAJ_PN_ERROR = 1 << 11
+
+# projected Newton statistics row (tog_pn_stat)
+PN_VIOL, PN_C_MAX, PN_J, PN_PROJECTIONS, PN_LINESEARCHES, PN_REFINEMENTS, PN_STEPS = range(7)
+PN_NSTATS = 7
 BP_MAX_RESTARTS = 1000  # TOG_BP_MAX_RESTARTS
 
 BP_STORE_S = 1
@@ -89,6 +94,12 @@ class tog_options(C.Structure):
         ("penalty_max", C.c_double), ("penalty_initial", C.c_double), ("penalty_scaling", C.c_double),
         ("al_iterations", C.c_int32), ("kickout_max_penalty", C.c_int32),
     ]
+
+
+class tog_pn_options(C.Structure):
+    """ProjectedNewtonSolverOptions (src/solvers/direct/direct_solvers.jl:14-30)."""
+    _fields_ = [("n_steps", C.c_int32), ("solve_type", C.c_int32), ("active_set_tolerance", C.c_double),
+                ("feasibility_tolerance", C.c_double)]
 
 
 def default_options() -> tog_options:
@@ -236,13 +247,15 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_cost_expansion.argtypes = [vp, C.c_int32, C.c_int32]
     lib.tog_solve_ilqr.argtypes = [vp]
     lib.tog_solve_al.argtypes = [vp]
+    lib.tog_default_pn_options.argtypes = [C.POINTER(tog_pn_options)]
+    lib.tog_solve_pn.argtypes = [vp, C.POINTER(tog_pn_options), _dp]
     for name in ("tog_create", "tog_create_multi", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
                  "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
                  "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
-                 "tog_solve_ilqr", "tog_solve_al"):
+                 "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -259,7 +272,7 @@ EXPORTED_SYMBOLS = (
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
     "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
     "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
-    "tog_solve_al",
+    "tog_solve_al", "tog_default_pn_options", "tog_solve_pn",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
 NKERNELS = 3

@@ -1652,6 +1652,7 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
 // =============================================================================================
 }  // namespace tog
 #include "tog_bwd_team.hpp"
+#include "tog_pn.hpp"
 namespace tog {
 
 // slack_controls(prob) (src/solvers/altro/infeasible.jl:63-80), one thread per trajectory:
@@ -1883,6 +1884,9 @@ struct ModelOps {
   void (*cost)(const DevProblem*, const DevBuffers&, long long B, int al, int use_bar, double* J, hipStream_t);
   void (*rollout)(const DevProblem*, const DevBuffers&, long long B, int integ, double alpha, int* ok, hipStream_t);
   void (*update_constraints)(const DevProblem*, const DevBuffers&, long long B, hipStream_t);
+  // projected Newton (tog_pn.hpp): phase 0 = k_pn_begin, 1 = k_pn_project, 2 = k_pn_finish; null for
+  // the infeasible (slack) models
+  void (*pn)(const DevProblem*, const DevBuffers&, const PNBuffers&, long long B, int integ, int phase, hipStream_t);
   int bwd_lds_bytes;
   int team_tpw;                    // trajectories per wave of k_bwd_team
   int (*team_stride)(int pmax, int sqrt);  // per-team LDS stride of k_bwd_team (doubles)
@@ -2050,6 +2054,25 @@ struct ModelLaunch {
   static void update_constraints(const DevProblem* P, const DevBuffers& Bf, long long B, hipStream_t st) {
     hipLaunchKernelGGL((k_update_constraints<M>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
   }
+  template <int INTEG>
+  static void pn_phase(const DevProblem* P, const DevBuffers& Bf, const PNBuffers& W, long long B, int phase,
+                       hipStream_t st) {
+    if (phase == 0)
+      hipLaunchKernelGGL((k_pn_begin<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+    else if (phase == 1)
+      hipLaunchKernelGGL((k_pn_project<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+    else
+      hipLaunchKernelGGL((k_pn_finish<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+  }
+  static void pn(const DevProblem* P, const DevBuffers& Bf, const PNBuffers& W, long long B, int integ, int phase,
+                 hipStream_t st) {
+    if (integ == TOG_RK4)
+      pn_phase<TOG_RK4>(P, Bf, W, B, phase, st);
+    else if (integ == TOG_MIDPOINT)
+      pn_phase<TOG_MIDPOINT>(P, Bf, W, B, phase, st);
+    else
+      pn_phase<TOG_RK3>(P, Bf, W, B, phase, st);
+  }
   static ModelOps ops() {
     ModelOps o;
     o.n = M::n;
@@ -2066,6 +2089,10 @@ struct ModelLaunch {
     o.cost = cost;
     o.rollout = rollout;
     o.update_constraints = update_constraints;
+    if constexpr (ModelTraits<M>::slack == 0)
+      o.pn = pn;
+    else
+      o.pn = nullptr;
     o.bwd_lds_bytes = (int)sizeof(BwdLds<M, true>);
     o.team_tpw = TeamCfg<M>::TPW;
     o.team_stride = bwd_team_stride<M>;

@@ -1,0 +1,494 @@
+// tog_pn.hpp — ALTRO phase 2: the projected Newton feasible projection, batched.
+//
+// Reference: src/solvers/direct/projected_newton.jl:6-303 (solve!, newton_step!, projection_solve!,
+// _projection_solve!, _projection_linesearch!, reg_solve) with ProjectedNewtonSolverOptions
+// (direct_solvers.jl:14-30), solve_type :feasible. The CPU restatement is oracle/tog_oracle_pn.c;
+// every value here is produced with its operations in its order, so the two agree
+// bit for bit.
+//
+// Mapping (MI355X): one wave (64-thread block) per trajectory. The dual vector is ordered as the
+// reference's (direct_solvers.jl:80-105): G_0 = x_1 - x0, G_b = [f(x_b,u_b) - x_{b+1}; active C_b],
+// G_N = active C_N. S = Y H⁻¹ Yᵀ is then block tridiagonal with blocks of n + p_active ≤ 32 rows.
+// The blocks are built in parallel over their entries (a lane per entry), the block Cholesky of
+// S + 1e-2 I sweeps the knots with the current and previous factor staged in LDS (a lane per row
+// for the off-diagonal solves, a lane per entry for the Schur updates), and the substitutions run a
+// row per lane with the pivot broadcast from lane to lane (__shfl). Factors and S live in a
+// per-trajectory HBM workspace (PNBuffers); the trial point goes to X̄, Ū.
+#pragma once
+
+namespace tog {
+
+constexpr int PN_SM_MAX = 32;  // largest block (n + pmax) of the wave kernels
+
+struct PNState {
+  double viol, c_max, J;
+  int count;     // _projection_solve! calls of the current projection_solve!
+  int finished;  // no further newton step (c_max <= tol after a step, or an error)
+  int error;     // TOG_TRAJ_PN_ERROR path
+  int steps, projections, linesearches, refinements, pad;
+};
+
+struct PNBuffers {
+  double *Sd, *So, *Ld, *Lo;        // (B, nb, SM, SM): S diagonal / sub-diagonal blocks, their factors
+  double *yv, *xv, *rv, *wv, *dv;   // (B, nb, SM)
+  double* yd;                       // (B, N, n) dynamics rows
+  double* Xs;                       // (B, N, n) the point S and H⁻¹Yᵀ were formed at (_projection_solve! start)
+  int *act, *na, *sz;               // (B, N, pmax) active rows, (B, N) counts, (B, nb) block sizes
+  PNState* st;                      // (B)
+  int SM, nb;
+  double atol, eps;                 // active_set_tolerance, feasibility_tolerance
+};
+
+// per-trajectory views of the workspace
+struct PNView {
+  double *Sd, *So, *Ld, *Lo, *yv, *xv, *rv, *wv, *dv, *yd, *Xs;
+  int *act, *na, *sz;
+  int SM;
+  __device__ double* M(double* A, int b) const { return A + (size_t)b * SM * SM; }
+  __device__ double* V(double* v, int b) const { return v + (size_t)b * SM; }
+};
+
+__device__ __forceinline__ PNView pn_view(const PNBuffers& W, const DevProblem* P, long long b) {
+  PNView v;
+  const size_t blk = (size_t)W.nb * W.SM * W.SM, vec = (size_t)W.nb * W.SM;
+  v.Sd = W.Sd + b * blk;
+  v.So = W.So + b * blk;
+  v.Ld = W.Ld + b * blk;
+  v.Lo = W.Lo + b * blk;
+  v.yv = W.yv + b * vec;
+  v.xv = W.xv + b * vec;
+  v.rv = W.rv + b * vec;
+  v.wv = W.wv + b * vec;
+  v.dv = W.dv + b * vec;
+  v.yd = W.yd + (size_t)b * P->N * P->n;
+  v.Xs = W.Xs + (size_t)b * P->N * P->n;
+  v.act = W.act + (size_t)b * P->N * P->pmax;
+  v.na = W.na + (size_t)b * P->N;
+  v.sz = W.sz + (size_t)b * W.nb;
+  v.SM = W.SM;
+  return v;
+}
+
+__device__ __forceinline__ void pn_sync() { __syncthreads(); }  // one-wave blocks: orders LDS traffic
+
+// H⁻¹ diagonal (Diagonal(solver.H): Q·dt, R·dt, terminal Qf; cost.jl:214-228)
+__device__ __forceinline__ double pn_wx(const DevProblem* P, int k, int i) {
+  const int n = P->n;
+  return 1.0 / (k < P->N - 1 ? P->Q[i + n * i] * P->dt : P->Qf[i + n * i]);
+}
+__device__ __forceinline__ double pn_wu(const DevProblem* P, int i) { return 1.0 / (P->R[i + P->m * i] * P->dt); }
+
+// dynamics_constraints! + update_constraints! at (X, U): dynamics rows into yd, constraint values
+// into C (projected_newton.jl:36-44,67-73). A lane per knot.
+template <class M, int INTEG>
+__device__ void pn_eval(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
+                        const double* U, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  double* C = Bf.C + (size_t)b * N * pmax;
+  const double* x0 = Bf.x0 + (size_t)b * n;
+  for (int k = lane; k < N; k += WAVE) {
+    const double* xk = X + (size_t)k * n;
+    if (k == 0)
+      for (int i = 0; i < n; i++) w.yd[i] = xk[i] - x0[i];
+    if (k < N - 1) {
+      double xn[n];
+      discrete_step<M, INTEG>(xn, xk, U + (size_t)k * m, P->dt);
+      for (int i = 0; i < n; i++) w.yd[(size_t)(k + 1) * n + i] = xn[i] - X[(size_t)(k + 1) * n + i];
+    }
+    const int cnt = P->knot_cnt[k];
+    const ConRow* rows = P->rows + P->knot_off[k];
+    for (int r = 0; r < cnt; r++) C[(size_t)k * pmax + r] = row_value(rows[r], xk, k < N - 1 ? U + (size_t)k * m : nullptr);
+  }
+  pn_sync();
+}
+
+// active_set! (projected_newton.jl:75-93) and the block sizes. A lane per knot.
+__device__ void pn_active_set(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, double tol,
+                              int nb, int lane) {
+  const int N = P->N, pmax = P->pmax, n = P->n;
+  const double* C = Bf.C + (size_t)b * N * pmax;
+  for (int k = lane; k < N; k += WAVE) {
+    const ConRow* rows = P->rows + P->knot_off[k];
+    int c = 0;
+    for (int i = 0; i < P->knot_cnt[k]; i++)
+      if (!row_inequality(rows[i]) || C[(size_t)k * pmax + i] >= -tol) w.act[k * pmax + c++] = i;
+    w.na[k] = c;
+  }
+  pn_sync();
+  for (int bb = lane; bb < nb; bb += WAVE) w.sz[bb] = (bb < N ? n : 0) + (bb >= 1 ? w.na[bb - 1] : 0);
+  pn_sync();
+}
+
+// y[a] into yv (block order) and its Inf norm (NaN propagates); every lane returns it
+__device__ double pn_gather_y(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, int nb,
+                              int lane) {
+  const int N = P->N, pmax = P->pmax, n = P->n;
+  const double* C = Bf.C + (size_t)b * N * pmax;
+  double viol = 0.0;
+  for (int bb = lane; bb < nb; bb += WAVE) {
+    double* y = w.V(w.yv, bb);
+    int r = 0;
+    if (bb < N)
+      for (int i = 0; i < n; i++) y[r++] = w.yd[(size_t)bb * n + i];
+    if (bb >= 1) {
+      const int k = bb - 1;
+      for (int q = 0; q < w.na[k]; q++) y[r++] = C[(size_t)k * pmax + w.act[k * pmax + q]];
+    }
+    for (int i = 0; i < r; i++) viol = tog_jlmax(viol, fabs(y[i]));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) viol = tog_jlmax(viol, __shfl_xor(viol, off, WAVE));
+  pn_sync();
+  return viol;
+}
+
+// rows of block bb on its own variables z_j = (x_j, u_j), j = bb-1, dense into LDS Yz (SM x (n+m))
+template <class M>
+__device__ void pn_block_rows(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, int bb,
+                              const double* X, double* Yz, int lane) {
+  constexpr int n = M::n, m = M::m, L = n + m;
+  const int N = P->N, pmax = P->pmax, SM = w.SM, j = bb - 1;
+  for (int e = lane; e < SM * L; e += WAVE) Yz[e] = 0.0;
+  pn_sync();
+  const int rb = (bb < N) ? n : 0;
+  if (bb < N) {
+    const double* AB = Bf.AB + ((size_t)b * (N - 1) + j) * n * L;
+    for (int e = lane; e < n * L; e += WAVE) Yz[(e % n) + SM * (e / n)] = AB[e];
+  }
+  if (lane < w.na[j]) {
+    const ConRow r = P->rows[P->knot_off[j] + w.act[j * pmax + lane]];
+    int idx[3];
+    double v[3];
+    const int nz = row_grad(r, X + (size_t)j * n, n, idx, v);
+    for (int z = 0; z < nz; z++) Yz[(rb + lane) + SM * idx[z]] = v[z];
+  }
+  pn_sync();
+}
+
+// S = Y H⁻¹ Yᵀ by blocks (projected_newton.jl:233-234; structure of _buildShurCompliment!, :728-757)
+template <class M>
+__device__ void pn_build_S(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
+                           double* Yz, int nb, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, SM = w.SM;
+  {
+    double* S0 = w.M(w.Sd, 0);
+    for (int e = lane; e < SM * SM; e += WAVE) S0[e] = ((e % SM) == (e / SM) && (e % SM) < n) ? pn_wx(P, 0, e % SM) : 0.0;
+  }
+  for (int bb = 1; bb < nb; bb++) {
+    const int j = bb - 1, sb = w.sz[bb], sp = w.sz[bb - 1], nv = (bb < N) ? n + m : n;
+    pn_block_rows<M>(P, Bf, b, w, bb, X, Yz, lane);
+    double* Sd = w.M(w.Sd, bb);
+    for (int e = lane; e < sb * sb; e += WAVE) {
+      const int i = e % sb, l = e / sb;
+      double acc = 0.0;
+      for (int v = 0; v < nv; v++) {
+        const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, v - n);
+        acc = fma(Yz[i + SM * v], wv * Yz[l + SM * v], acc);
+      }
+      if (bb < N && i < n && i == l) acc = acc + pn_wx(P, j + 1, i);
+      Sd[i + SM * l] = acc;
+    }
+    const double sg = (bb - 1 == 0) ? 1.0 : -1.0;
+    double* So = w.M(w.So, bb);
+    for (int e = lane; e < sb * sp; e += WAVE) {
+      const int i = e % sb, c = e / sb;
+      So[i + SM * c] = (c < n) ? Yz[i + SM * c] * (sg * pn_wx(P, j, c)) : 0.0;
+    }
+    pn_sync();
+  }
+}
+
+// block Cholesky of S + ρI; Lp/Lc: LDS (SM x SM each), LoL: LDS (SM x SM). Returns 0 or a failure.
+__device__ int pn_factor(const PNView& w, int nb, double rho, double* Lp, double* Lc, double* LoL, int lane) {
+  const int SM = w.SM;
+  for (int bb = 0; bb < nb; bb++) {
+    const int sb = w.sz[bb];
+    const int sp = bb >= 1 ? w.sz[bb - 1] : 0;
+    if (bb >= 1 && lane < sb) {  // Lo_b = So_b Lp^{-T}: lane i solves Lp y = So_b[i, :]ᵀ
+      const double* So = w.M(w.So, bb);
+      for (int l = 0; l < sp; l++) {
+        double t = So[lane + SM * l];
+        for (int q = 0; q < l; q++) t = fma(-Lp[l + SM * q], LoL[lane + SM * q], t);
+        LoL[lane + SM * l] = t / Lp[l + SM * l];
+      }
+    }
+    pn_sync();
+    const double* Sd = w.M(w.Sd, bb);
+    for (int e = lane; e < sb * sb; e += WAVE) {
+      const int i = e % sb, l = e / sb;
+      if (i < l) continue;
+      double t = Sd[i + SM * l];
+      if (i == l) t = t + rho;
+      for (int q = 0; q < sp; q++) t = fma(-LoL[i + SM * q], LoL[l + SM * q], t);
+      Lc[i + SM * l] = t;
+    }
+    pn_sync();
+    for (int j = 0; j < sb; j++) {  // right-looking Cholesky (oracle pn_chol)
+      const double a = Lc[j + SM * j];
+      if (!(a > 0.0)) return bb + 1;
+      const double d = sqrt(a);
+      pn_sync();
+      if (lane == j) Lc[j + SM * j] = d;
+      if (lane > j && lane < sb) Lc[lane + SM * j] = Lc[lane + SM * j] / d;
+      pn_sync();
+      const int t = sb - j - 1;
+      for (int e = lane; e < t * t; e += WAVE) {
+        const int i = j + 1 + e % t, l = j + 1 + e / t;
+        if (i >= l) Lc[i + SM * l] = fma(-Lc[i + SM * j], Lc[l + SM * j], Lc[i + SM * l]);
+      }
+      pn_sync();
+    }
+    double* Ld = w.M(w.Ld, bb);
+    double* Lo = w.M(w.Lo, bb);
+    for (int e = lane; e < SM * SM; e += WAVE) {
+      Ld[e] = Lc[e];
+      Lp[e] = Lc[e];
+      if (bb >= 1) Lo[e] = LoL[e];
+    }
+    pn_sync();
+  }
+  return 0;
+}
+
+// x = (S + ρI)⁻¹ r through the block factor (a row per lane, pivots broadcast by __shfl).
+// T1, T2: LDS staging (SM x SM) of the blocks being used; xn: LDS (SM) previous block's solution.
+__device__ void pn_fsolve(const PNView& w, int nb, const double* r, double* x, double* T1, double* T2, double* xn,
+                          int lane) {
+  const int SM = w.SM;
+  for (int bb = 0; bb < nb; bb++) {  // forward
+    const int sb = w.sz[bb], sp = bb >= 1 ? w.sz[bb - 1] : 0;
+    const double* Ld = w.M(w.Ld, bb);
+    const double* Lo = w.M(w.Lo, bb);
+    for (int e = lane; e < SM * SM; e += WAVE) {
+      T1[e] = Ld[e];
+      if (bb >= 1) T2[e] = Lo[e];
+    }
+    pn_sync();
+    double t = 0.0;
+    if (lane < sb) {
+      t = w.V(const_cast<double*>(r), bb)[lane];
+      for (int q = 0; q < sp; q++) t = fma(-T2[lane + SM * q], xn[q], t);
+    }
+    double* wb = w.V(w.wv, bb);
+    const double dl = (lane < sb) ? T1[lane + SM * lane] : 1.0;  // this lane's pivot L[i,i]
+    for (int l = 0; l < sb; l++) {
+      const double wl = __shfl(t / dl, l, WAVE);
+      if (lane == l) wb[l] = wl;
+      if (lane > l && lane < sb) t = fma(-T1[lane + SM * l], wl, t);
+    }
+    pn_sync();
+    if (lane < sb) xn[lane] = wb[lane];
+    pn_sync();
+  }
+  for (int bb = nb - 1; bb >= 0; bb--) {  // backward
+    const int sb = w.sz[bb], sn = bb + 1 < nb ? w.sz[bb + 1] : 0;
+    const double* Ld = w.M(w.Ld, bb);
+    for (int e = lane; e < SM * SM; e += WAVE) {
+      T1[e] = Ld[e];
+      if (bb + 1 < nb) T2[e] = w.M(w.Lo, bb + 1)[e];
+    }
+    pn_sync();
+    double t = 0.0;
+    if (lane < sb) {
+      t = w.V(w.wv, bb)[lane];
+      for (int q = 0; q < sn; q++) t = fma(-T2[q + SM * lane], xn[q], t);
+    }
+    double* xb = w.V(x, bb);
+    const double dl = (lane < sb) ? T1[lane + SM * lane] : 1.0;
+    for (int l = sb - 1; l >= 0; l--) {
+      const double xl = __shfl(t / dl, l, WAVE);
+      if (lane == l) xb[l] = xl;
+      if (lane < l) t = fma(-T1[l + SM * lane], xl, t);
+    }
+    pn_sync();
+    if (lane < sb) xn[lane] = xb[lane];
+    pn_sync();
+  }
+}
+
+// r = y - S x (a row per lane); |r|₂ with the oracle's sequential sum (lane 0), returned to all lanes
+__device__ double pn_residual(const PNView& w, int nb, const double* y, const double* x, double* r, double* rl,
+                              int lane) {
+  const int SM = w.SM;
+  double ss = 0.0;
+  for (int bb = 0; bb < nb; bb++) {
+    const int sb = w.sz[bb];
+    if (lane < sb) {
+      const int i = lane;
+      const double* Sd = w.M(w.Sd, bb);
+      const double* xb = w.V(const_cast<double*>(x), bb);
+      double t = 0.0;
+      for (int q = 0; q < sb; q++) t = fma(Sd[i + SM * q], xb[q], t);
+      if (bb >= 1) {
+        const double* So = w.M(w.So, bb);
+        const double* xp = w.V(const_cast<double*>(x), bb - 1);
+        for (int q = 0; q < w.sz[bb - 1]; q++) t = fma(So[i + SM * q], xp[q], t);
+      }
+      if (bb + 1 < nb) {
+        const double* So1 = w.M(w.So, bb + 1);
+        const double* xq = w.V(const_cast<double*>(x), bb + 1);
+        for (int q = 0; q < w.sz[bb + 1]; q++) t = fma(So1[q + SM * i], xq[q], t);
+      }
+      const double ri = w.V(const_cast<double*>(y), bb)[i] - t;
+      w.V(r, bb)[i] = ri;
+      rl[i] = ri;
+    }
+    pn_sync();
+    if (lane == 0)
+      for (int i = 0; i < sb; i++) ss = fma(rl[i], rl[i], ss);
+    pn_sync();
+  }
+  return sqrt(__shfl(ss, 0, WAVE));
+}
+
+struct PNLds {  // LDS of k_pn_project (SM <= PN_SM_MAX)
+  double A[PN_SM_MAX * PN_SM_MAX], Bm[PN_SM_MAX * PN_SM_MAX], Cm[PN_SM_MAX * PN_SM_MAX];
+  double Yz[PN_SM_MAX * 24];
+  double vec[PN_SM_MAX], vec2[PN_SM_MAX];
+};
+
+// reg_solve(S, y, Sreg, 1e-8, 25) into xv (projected_newton.jl:286-303)
+__device__ void pn_reg_solve(const PNView& w, int nb, PNLds& sh, PNState& s, int lane) {
+  pn_fsolve(w, nb, w.yv, w.xv, sh.A, sh.Bm, sh.vec, lane);
+  for (int cnt = 0; cnt < 25; cnt++) {
+    const double nr = pn_residual(w, nb, w.yv, w.xv, w.rv, sh.vec2, lane);
+    if (nr < 1e-8) break;
+    pn_fsolve(w, nb, w.rv, w.dv, sh.A, sh.Bm, sh.vec, lane);
+    for (int bb = 0; bb < nb; bb++)
+      if (lane < w.sz[bb]) w.V(w.xv, bb)[lane] = w.V(w.xv, bb)[lane] + w.V(w.dv, bb)[lane];
+    pn_sync();
+    s.refinements++;
+  }
+}
+
+// trial point Z_ = Z + α δZ, δZ = -H⁻¹ Yᵀ δλ, into X̄, Ū (a variable per lane)
+template <class M>
+__device__ void pn_trial(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, double* Yz,
+                         double alpha, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, SM = w.SM;
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  double* Xt = Bf.Xb + (size_t)b * N * n;
+  double* Ut = Bf.Ub + (size_t)b * (N - 1) * m;
+  for (int j = 0; j < N; j++) {
+    const int bb = j + 1, nv = (j < N - 1) ? n + m : n;
+    pn_block_rows<M>(P, Bf, b, w, bb, w.Xs, Yz, lane);  // H⁻¹Yᵀ of _projection_solve!: Jacobians at its start
+    if (lane < nv) {
+      const int v = lane;
+      double t = 0.0;
+      if (v < n) t = (j == 0) ? w.V(w.xv, 0)[v] : -w.V(w.xv, j)[v];
+      const double* lb = w.V(w.xv, bb);
+      for (int i = 0; i < w.sz[bb]; i++) t = fma(Yz[i + SM * v], lb[i], t);
+      const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, v - n);
+      const double dz = -(wv * t);
+      if (v < n)
+        Xt[(size_t)j * n + v] = X[(size_t)j * n + v] + alpha * dz;
+      else
+        Ut[(size_t)j * m + (v - n)] = U[(size_t)j * m + (v - n)] + alpha * dz;
+    }
+    pn_sync();
+  }
+}
+
+// newton_step! prologue (update!: active set at V) and projection_solve!'s first viol
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_begin(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  PNState& s = W.st[b];
+  if (s.finished) return;
+  const PNView w = pn_view(W, P, b);
+  const int N = P->N;
+  pn_eval<M, INTEG>(P, Bf, b, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
+  pn_active_set(P, Bf, b, w, W.atol, W.nb, lane);
+  const double viol = pn_gather_y(P, Bf, b, w, W.nb, lane);
+  if (lane == 0) {
+    s.viol = viol;
+    s.count = 0;
+  }
+}
+
+// one pass of projection_solve!'s loop: _projection_solve! (Jacobians from k_jacobian at X, U)
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_project(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ PNLds sh;
+  PNState s = W.st[b];
+  if (s.finished || s.error || s.count >= 10 || !(s.viol > W.eps)) return;  // while count < 10 && viol > eps
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, nb = W.nb;
+  const PNView w = pn_view(W, P, b);
+  double* X = Bf.X + (size_t)b * N * n;
+  double* U = Bf.U + (size_t)b * (N - 1) * m;
+  s.count++;
+  s.projections++;
+  for (int e = lane; e < N * n; e += WAVE) w.Xs[e] = X[e];
+  pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
+  pn_active_set(P, Bf, b, w, W.atol, nb, lane);
+  const double viol0 = pn_gather_y(P, Bf, b, w, nb, lane);
+  pn_build_S<M>(P, Bf, b, w, X, sh.Yz, nb, lane);
+  double viol = viol0;
+  if (pn_factor(w, nb, 1e-2, sh.A, sh.Bm, sh.Cm, lane)) {
+    s.error = 1;  // PosDefException in cholesky
+  } else {
+    double viol_prev = viol0;
+    for (int count = 0; count < 10; count++) {
+      // _projection_linesearch!: y at the current point (last evaluation), δλ, trial, y at the trial
+      const double vls0 = pn_gather_y(P, Bf, b, w, nb, lane);
+      s.linesearches++;
+      pn_reg_solve(w, nb, sh, s, lane);
+      pn_trial<M>(P, Bf, b, w, sh.Yz, 1.0, lane);
+      double* Xt = Bf.Xb + (size_t)b * N * n;
+      double* Ut = Bf.Ub + (size_t)b * (N - 1) * m;
+      pn_eval<M, INTEG>(P, Bf, b, w, Xt, Ut, lane);
+      viol = pn_gather_y(P, Bf, b, w, nb, lane);
+      if (!(viol < vls0)) {  // `count += a` (MethodError) in the reference
+        s.error = 1;
+        break;
+      }
+      for (int e = lane; e < N * n; e += WAVE) X[e] = Xt[e];
+      for (int e = lane; e < (N - 1) * m; e += WAVE) U[e] = Ut[e];
+      pn_sync();
+      const double rate = log10(viol) / log10(viol_prev);
+      viol_prev = viol;
+      if (rate < 1.1 || viol < W.eps) break;
+    }
+    if (!s.error) viol = viol_prev;
+  }
+  s.viol = viol;
+  if (lane == 0) W.st[b] = s;
+}
+
+// record_iteration!: J = cost(prob), c_max = max_violation(prob) at X, U; the solve! loop's break
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_finish(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  PNState s = W.st[b];
+  if (s.finished) return;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  double* C = Bf.C + (size_t)b * N * pmax;
+  for (int k = lane; k < N; k += WAVE) {
+    const int cnt = P->knot_cnt[k];
+    const ConRow* rows = P->rows + P->knot_off[k];
+    for (int r = 0; r < cnt; r++)
+      C[(size_t)k * pmax + r] = row_value(rows[r], X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
+  }
+  pn_sync();
+  if (lane != 0) return;
+  s.steps++;
+  s.c_max = traj_max_violation(P, Bf, b);
+  s.J = traj_cost<M>(P, Bf, b, X, U, false, nullptr);
+  if (s.error || s.c_max <= W.eps) s.finished = 1;
+  if (s.error) Bf.st[b].flags |= TOG_TRAJ_PN_ERROR;
+  W.st[b] = s;
+}
+
+}  // namespace tog

@@ -76,6 +76,9 @@ struct tog_handle {
   // second stream + fork/join events: the forward pass overlaps the decided trajectories' commit
   // with the second speculative round (tog_kernels.hpp forward_i)
   StreamPair sp = {nullptr, nullptr, nullptr};
+  // projected Newton workspace, allocated by the first tog_solve_pn (tog_pn.hpp)
+  PNBuffers pn = {};
+  bool pn_alloc = false;
 };
 
 static hipEvent_t next_event(tog_handle* h) {
@@ -1067,6 +1070,77 @@ int32_t tog_profile_read(tog_handle* h, double* total_ms, int64_t* launches) {
     HIPCHECK(hipEventElapsedTime(&ms, h->ev_pool[2 * p], h->ev_pool[2 * p + 1]));
     total_ms[h->ev_kind[p]] += ms;
     launches[h->ev_kind[p]] += 1;
+  }
+  return TOG_OK;
+}
+
+void tog_default_pn_options(tog_pn_options* o) {
+  o->n_steps = 1;
+  o->solve_type = 0;
+  o->active_set_tolerance = 1e-3;
+  o->feasibility_tolerance = 1e-6;
+}
+
+// solve!(prob, ProjectedNewtonSolver) (projected_newton.jl:6-20): per newton step, k_pn_begin
+// (update! + the first viol), then projection_solve!'s loop of at most 10 _projection_solve!s (each
+// after k_jacobian at the current X, U), then k_pn_finish (record_iteration!). Trajectories that
+// are done return at once from every launch.
+int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
+  if (!h || !opts) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h))
+    return each_part(h, [&](tog_handle* p, size_t o) {
+      return tog_solve_pn(p, opts, out ? out + o * TOG_PN_NSTATS : nullptr);
+    });
+  if (opts->solve_type != 0) return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal is not built");
+  if (opts->n_steps < 0) return fail(TOG_ERR_ARG, "n_steps must be >= 0");
+  if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton on an infeasible (slack) problem is not built");
+  const int SM = h->n + h->pmax;
+  if (SM > PN_SM_MAX || h->n + h->m > 24)
+    return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than 32 rows (n + pmax) are not built");
+  HIPCHECK(hipSetDevice(h->device));
+  PNBuffers& W = h->pn;
+  const long long B = h->B;
+  if (!h->pn_alloc) {
+    W.SM = SM;
+    W.nb = h->N + 1;
+    const size_t blk = (size_t)B * W.nb * SM * SM, vec = (size_t)B * W.nb * SM;
+    int rc;
+    if ((rc = dalloc(h, &W.Sd, blk)) || (rc = dalloc(h, &W.So, blk)) || (rc = dalloc(h, &W.Ld, blk)) ||
+        (rc = dalloc(h, &W.Lo, blk)) || (rc = dalloc(h, &W.yv, vec)) || (rc = dalloc(h, &W.xv, vec)) ||
+        (rc = dalloc(h, &W.rv, vec)) || (rc = dalloc(h, &W.wv, vec)) || (rc = dalloc(h, &W.dv, vec)) ||
+        (rc = dalloc(h, &W.yd, (size_t)B * h->N * h->n)) || (rc = dalloc(h, &W.Xs, (size_t)B * h->N * h->n)) ||
+        (rc = dalloc(h, &W.act, (size_t)B * h->N * (h->pmax > 0 ? h->pmax : 1))) ||
+        (rc = dalloc(h, &W.na, (size_t)B * h->N)) || (rc = dalloc(h, &W.sz, (size_t)B * W.nb)) ||
+        (rc = dalloc(h, &W.st, (size_t)B)))
+      return rc;
+    h->pn_alloc = true;
+  }
+  W.atol = opts->active_set_tolerance;
+  W.eps = opts->feasibility_tolerance;
+  HIPCHECK(hipMemsetAsync(W.st, 0, sizeof(PNState) * B, h->stream));
+  for (int step = 0; step < opts->n_steps; step++) {
+    h->ops->pn(h->dP, h->buf, W, B, h->integ, 0, h->stream);
+    for (int it = 0; it < 10; it++) {
+      h->ops->jacobian(h->dP, h->buf, B, h->N, h->integ, h->stream);
+      h->ops->pn(h->dP, h->buf, W, B, h->integ, 1, h->stream);
+    }
+    h->ops->pn(h->dP, h->buf, W, B, h->integ, 2, h->stream);
+    HIPCHECK(hipGetLastError());
+  }
+  if (out) {
+    std::vector<PNState> st(B);
+    HIPCHECK(hipMemcpyAsync(st.data(), W.st, sizeof(PNState) * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    for (long long b = 0; b < B; b++) {
+      double* o = out + b * TOG_PN_NSTATS;
+      o[TOG_PN_VIOL] = st[b].viol;
+      o[TOG_PN_C_MAX] = st[b].c_max;
+      o[TOG_PN_J] = st[b].J;
+      o[TOG_PN_PROJECTIONS] = st[b].projections;
+      o[TOG_PN_LINESEARCHES] = st[b].linesearches;
+      o[TOG_PN_REFINEMENTS] = st[b].refinements;
+      o[TOG_PN_STEPS] = st[b].steps;
+    }
   }
   return TOG_OK;
 }

@@ -143,6 +143,12 @@ class BatchHandle:
     def solve(self, mode, max_steps=10000):
         abi.check(self.lib, self.lib.tog_solve(self.h, int(mode), int(max_steps)))
 
+    def solve_pn(self, pn_opts: abi.tog_pn_options):
+        """tog_solve_pn: returns the (B, PN_NSTATS) statistics rows."""
+        out = np.zeros((self.B, abi.PN_NSTATS))
+        abi.check(self.lib, self.lib.tog_solve_pn(self.h, C.byref(pn_opts), abi.as_dp(out)))
+        return out
+
     def batch_stats(self):
         out = np.empty(3)
         abi.check(self.lib, self.lib.tog_batch_stats(self.h, abi.as_dp(out)))

@@ -191,6 +191,37 @@ def car_parallel_park(U0=None):
     return Problem(model_d, obj, U0, x0=x0, xf=xf, N=N, dt=dt)
 
 
+def car_obstacles(U0=None, u_max=1.5, B=1):
+    """test/projected_newton_test.jl:1-27 (the projected Newton tests' problem; test/altro_tests.jl:1-21
+    is the same with ``Dynamics.car_costfun``, which this snapshot does not define): car, rk4, N=51,
+    tf=3, Q=R=Qf=1e-2 I, xf=[0,1,0]; knot 1: u_min; knots 2..N-1: x in [-0.5,0.5]x[-0.01,1.01],
+    u in [0.1,-2]..u_max, two planar obstacles; knot N: goal; U = ones."""
+    model_d = rk4(Dynamics.car)
+    n, m, N = 3, 2, 51
+    dt = 3.0 / (N - 1)
+    Q, R, Qf = 0.01 * np.eye(n), 0.01 * np.eye(m), 0.01 * np.eye(n)
+    xf = np.array([0.0, 1.0, 0.0])
+    obj = LQRObjective(Q, R, Qf, xf, N)
+    bnd = BoundConstraint(n, m, x_min=[-0.5, -0.01, -math.inf], x_max=[0.5, 1.01, math.inf], u_min=[0.1, -2.0],
+                          u_max=u_max)
+    bnd1 = BoundConstraint(n, m, u_min=[0.1, -2.0])
+    obs1 = CircleConstraints(n, m, [[0.2, 0.6, 0.25]], label="obstacle1")
+    obs2 = CircleConstraints(n, m, [[-0.5, 0.5, 0.4]], label="obstacle2")
+    cons = Constraints(N)
+    cons[0] += bnd1
+    for k in range(1, N - 1):
+        cons[k] += bnd
+        cons[k] += obs1
+        cons[k] += obs2
+    cons[N - 1] += goal_constraint(xf)
+    if U0 is None:
+        U0 = np.ones((N - 1, m))
+    U0 = np.asarray(U0, dtype=np.float64)
+    if B > 1 and U0.ndim == 2:
+        U0 = np.broadcast_to(U0, (B,) + U0.shape).copy()
+    return Problem(model_d, obj, U0, constraints=cons, x0=np.zeros(n), xf=xf, N=N, dt=dt)
+
+
 # ---------------------------------------------------------------------------- BASELINE configs
 
 def dynamics_bias(model, x):

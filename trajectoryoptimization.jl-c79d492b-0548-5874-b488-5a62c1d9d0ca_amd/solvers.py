@@ -85,10 +85,39 @@ class AugmentedLagrangianSolverOptions:
 
 
 @dataclass
+class ProjectedNewtonSolverOptions:
+    """``ProjectedNewtonSolverOptions`` (src/solvers/direct/direct_solvers.jl:14-30). Only
+    ``solve_type = "feasible"`` (the default) is built."""
+
+    verbose: bool = True
+    n_steps: int = 1
+    solve_type: str = "feasible"
+    active_set_tolerance: float = 1.0e-3
+    feasibility_tolerance: float = 1.0e-6
+
+    def copy(self):
+        return _copy.deepcopy(self)
+
+
+def to_tog_pn_options(opts: ProjectedNewtonSolverOptions) -> abi.tog_pn_options:
+    if opts.solve_type not in ("feasible", "optimal"):
+        raise ValueError("solve_type must be :feasible or :optimal")
+    if opts.solve_type == "optimal":
+        raise NotImplementedError("projected Newton solve_type :optimal is not built")
+    o = abi.tog_pn_options()
+    o.n_steps = int(opts.n_steps)
+    o.solve_type = 0
+    o.active_set_tolerance = float(opts.active_set_tolerance)
+    o.feasibility_tolerance = float(opts.feasibility_tolerance)
+    return o
+
+
+@dataclass
 class ALTROSolverOptions:
     """src/solvers/altro/altro_solver.jl:6-65. With a NaN initial state trajectory ALTRO is the AL
     solve; with a given X it is the infeasible-start solve (altro_methods.jl:98-124, infeasible.jl).
-    The minimum-time and projected-Newton phases are SURVEY.md §8(f) "next" (not built)."""
+    ``projected_newton`` adds phase 2, the projected Newton feasible projection
+    (altro_methods.jl:5-39). Minimum time is SURVEY.md §8(f) "next" (not built)."""
 
     verbose: bool = False
     opts_al: AugmentedLagrangianSolverOptions = field(default_factory=AugmentedLagrangianSolverOptions)
@@ -106,6 +135,7 @@ class ALTROSolverOptions:
     penalty_scaling_minimum_time_inequality: float = 1.0
     penalty_scaling_minimum_time_equality: float = 1.0
     projected_newton: bool = False
+    opts_pn: ProjectedNewtonSolverOptions = field(default_factory=ProjectedNewtonSolverOptions)
     projected_newton_tolerance: float = 1.0e-3
 
     def copy(self):
@@ -264,7 +294,47 @@ class AugmentedLagrangianSolver(AbstractSolver):
 
 
 class ALTROSolver(AugmentedLagrangianSolver):
-    """``ALTROSolver`` (altro_solver.jl:70-94): AL phase only (projected_newton=false)."""
+    """``ALTROSolver`` (altro_solver.jl:70-94): the AL phase, and with ``projected_newton`` the
+    projected Newton phase on the same device buffers (``solver_pn``)."""
+
+
+class ProjectedNewtonSolver(AbstractSolver):
+    """``ProjectedNewtonSolver`` (direct_solvers.jl:43-113): the feasible projection of ALTRO's
+    phase 2 on the device (tog_solve_pn). ``V`` starts from the problem's X, U
+    (``PrimalDual(prob)``, primals.jl:158-193). ``stats`` holds per-trajectory ``c_max``, ``cost``,
+    ``iterations`` (newton steps), the final projection ``viol`` and work counters."""
+
+    mode = abi.MODE_AL
+
+    def __init__(self, prob, opts: ProjectedNewtonSolverOptions | None = None, **kw):
+        opts = ProjectedNewtonSolverOptions() if opts is None else opts
+        super().__init__(prob, iLQRSolverOptions(), **kw)
+        self.opts = opts
+        self.handle.upload_state(prob)
+
+
+def _pn_stats(out, flags):
+    return {"c_max": out[:, abi.PN_C_MAX].copy(), "cost": out[:, abi.PN_J].copy(),
+            "viol": out[:, abi.PN_VIOL].copy(), "iterations": out[:, abi.PN_STEPS].astype(int),
+            "projections": out[:, abi.PN_PROJECTIONS].astype(int),
+            "linesearches": out[:, abi.PN_LINESEARCHES].astype(int),
+            "refinements": out[:, abi.PN_REFINEMENTS].astype(int), "flags": flags}
+
+
+def _solve_pn(prob, solver: ProjectedNewtonSolver):
+    """``solve!(prob, ::ProjectedNewtonSolver)`` (projected_newton.jl:6-20). The reference raises
+    (a MethodError in ``_projection_linesearch!``, projected_newton.jl:273-277) when a line search's
+    first trial does not reduce the violation; that trajectory is flagged TRAJ_PN_ERROR and a
+    ``RuntimeError`` is raised after the batch."""
+    h = solver.handle
+    out = h.solve_pn(to_tog_pn_options(solver.opts))
+    h.download_state(prob)
+    flags = h.status()
+    solver.stats = _pn_stats(out, flags)
+    if np.any(flags & abi.TRAJ_PN_ERROR):
+        raise RuntimeError("projected Newton: line search did not reduce the violation "
+                           "(the reference's _projection_linesearch! raises here)")
+    return solver
 
 
 def AbstractSolverFor(prob, opts, **kw):
@@ -273,15 +343,30 @@ def AbstractSolverFor(prob, opts, **kw):
         return iLQRSolver(prob, opts, **kw)
     if isinstance(opts, ALTROSolverOptions):
         _altro_check(prob, opts)
+        _altro_pn_tolerances(opts)
         return ALTROSolver(prob, opts, **kw)
+    if isinstance(opts, ProjectedNewtonSolverOptions):
+        return ProjectedNewtonSolver(prob, opts, **kw)
     if isinstance(opts, AugmentedLagrangianSolverOptions):
         return AugmentedLagrangianSolver(prob, opts, **kw)
     raise ValueError("Can't create an Abstract Solver without knowing the type of the Solver Options")
 
 
 def _altro_check(prob, opts):
+    if opts.projected_newton and _altro_infeasible(prob):
+        raise NotImplementedError("projected Newton on the infeasible-start problem (slack controls) is not built")
+
+
+def _altro_pn_tolerances(opts):
+    """altro_methods.jl:5-13: with projected Newton the AL phase stops at projected_newton_tolerance
+    (or runs to kickout at max penalty when that is negative). Mutates opts.opts_al, as the
+    reference does."""
     if opts.projected_newton:
-        raise NotImplementedError("ALTRO projected-Newton phase is SURVEY.md §8(f) 'next' (not built)")
+        if opts.projected_newton_tolerance >= 0:
+            opts.opts_al.constraint_tolerance = opts.projected_newton_tolerance
+        else:
+            opts.opts_al.constraint_tolerance = 0.0
+            opts.opts_al.kickout_max_penalty = True
 
 
 def _altro_infeasible(prob) -> bool:
@@ -334,15 +419,21 @@ def _solve_altro_infeasible(prob, opts, max_steps, device):
 def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int = 0):
     """``solve!(prob, opts)`` / ``solve!(prob, solver)`` (src/solvers.jl:91-94). Mutates
     ``prob.X``/``prob.U`` in place and returns the solver."""
+    if isinstance(solver_or_opts, ProjectedNewtonSolver):
+        solver_or_opts.handle.upload_state(prob)
+        return _solve_pn(prob, solver_or_opts)
     if isinstance(solver_or_opts, AbstractSolver):
         solver = solver_or_opts
         solver.handle.upload_state(prob)
     else:
         opts = solver_or_opts
+        if isinstance(opts, ProjectedNewtonSolverOptions):
+            return _solve_pn(prob, ProjectedNewtonSolver(prob, opts, device=device))
         if isinstance(opts, ALTROSolverOptions):
             _altro_check(prob, opts)
             if _altro_infeasible(prob):
                 return _solve_altro_infeasible(prob, opts, max_steps, device)
+            _altro_pn_tolerances(opts)
         if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
             # solve!(prob, ::AugmentedLagrangianSolverOptions) on an unconstrained problem
             # falls back to the unconstrained solver (augmented_lagrangian_methods.jl:33-36)
@@ -356,6 +447,16 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
     flags = solver.stats["flags"]
     if np.any(flags & abi.TRAJ_COST_INCREASED):
         raise RuntimeError("Error: Cost increased during Forward Pass")
+    if isinstance(solver_or_opts, ALTROSolverOptions) and solver_or_opts.projected_newton:
+        # phase 2 (altro_methods.jl:31-39): solver_pn.V = PrimalDual(prob_altro); solve! on the same
+        # device buffers (X, U of the AL solve are already resident)
+        pn = h.solve_pn(to_tog_pn_options(solver_or_opts.opts_pn))
+        h.download_state(prob)
+        flags = h.status()
+        solver.stats_pn = _pn_stats(pn, flags)
+        if np.any(flags & abi.TRAJ_PN_ERROR):
+            raise RuntimeError("projected Newton: line search did not reduce the violation "
+                               "(the reference's _projection_linesearch! raises here)")
     return solver
 
 
