@@ -120,6 +120,14 @@ def test_oracle_projection_noop_when_feasible(tog, oracle):
     assert np.array_equal(o.get("X"), X) and np.array_equal(o.get("U"), U)
 
 
+def test_car_batch_problem(tog, oracle):
+    """The batched car problem the GPU tests use: B trajectories, the AL iterates are finite."""
+    prob = car_batch(tog, 2)
+    assert prob.B == 2 and prob._U.shape == (2, 50, 2)
+    st = oracle_al_state(tog, oracle, prob, car_al_opts(tog))
+    assert np.isfinite(st._X).all() and np.isfinite(st._U).all()
+
+
 # ----------------------------------------------------------------------------- GPU: device vs oracle
 
 
@@ -163,6 +171,9 @@ def test_gpu_altro_projected_newton(tog, oracle, gpu):
     opts = tog.ALTROSolverOptions(opts_al=al, projected_newton=True, projected_newton_tolerance=1e-2)
     opts.opts_pn.feasibility_tolerance = 1e-10
     opts.opts_pn.active_set_tolerance = 1e-4
+    # one newton step (the default) leaves rows that were outside the 1e-4 active set violated by
+    # up to ~1e-2 (the step moves them); later steps re-evaluate the active set and finish the polish
+    opts.opts_pn.n_steps = 6
     gp = prob.copy()
     solver = tog.solve_b(gp, opts)
     assert opts.opts_al.constraint_tolerance == 1e-2
@@ -170,8 +181,9 @@ def test_gpu_altro_projected_newton(tog, oracle, gpu):
         o = oracle.OracleSolver(prob, opts.opts_al, b=b)
         o.solve()
         out = o.solve_pn(opts.opts_pn)
-        assert rel(gp._X[b], o.get("X")) < 1e-6 and rel(gp._U[b], o.get("U")) < 1e-6, b
+        assert rel(gp._X[b], o.get("X")) < TOL_STEP and rel(gp._U[b], o.get("U")) < TOL_STEP, b
         assert solver.stats_pn["iterations"][b] == out[tog.abi.PN_STEPS]
+        assert abs(solver.stats_pn["c_max"][b] - out[tog.abi.PN_C_MAX]) <= 1e-13
         if not solver.stats_pn["flags"][b] & tog.abi.TRAJ_PN_ERROR:
             assert solver.stats_pn["c_max"][b] < 1e-10
 

@@ -25,7 +25,8 @@ struct PNState {
   int count;     // _projection_solve! calls of the current projection_solve!
   int finished;  // no further newton step (c_max <= tol after a step, or an error)
   int error;     // TOG_TRAJ_PN_ERROR path
-  int steps, projections, linesearches, refinements, pad;
+  int steps, projections, linesearches, refinements;
+  int active0;   // the solver's own active flag, restored by k_pn_finish (k_jacobian gates on it)
 };
 
 struct PNBuffers {
@@ -408,6 +409,9 @@ __global__ void __launch_bounds__(64) k_pn_begin(const DevProblem* __restrict__ 
   if (lane == 0) {
     s.viol = viol;
     s.count = 0;
+    // k_jacobian runs only for active trajectories: a converged AL solve left them inactive
+    s.active0 = Bf.st[b].active;
+    Bf.st[b].active = (viol > W.eps) ? 1 : 0;
   }
 }
 
@@ -460,7 +464,10 @@ __global__ void __launch_bounds__(64) k_pn_project(const DevProblem* __restrict_
     if (!s.error) viol = viol_prev;
   }
   s.viol = viol;
-  if (lane == 0) W.st[b] = s;
+  if (lane == 0) {
+    W.st[b] = s;
+    if (s.error || s.count >= 10 || !(s.viol > W.eps)) Bf.st[b].active = 0;  // no further Jacobians
+  }
 }
 
 // record_iteration!: J = cost(prob), c_max = max_violation(prob) at X, U; the solve! loop's break
@@ -483,6 +490,7 @@ __global__ void __launch_bounds__(64) k_pn_finish(const DevProblem* __restrict__
   }
   pn_sync();
   if (lane != 0) return;
+  Bf.st[b].active = s.active0;
   s.steps++;
   s.c_max = traj_max_violation(P, Bf, b);
   s.J = traj_cost<M>(P, Bf, b, X, U, false, nullptr);

@@ -219,7 +219,9 @@ def car_obstacles(U0=None, u_max=1.5, B=1):
     U0 = np.asarray(U0, dtype=np.float64)
     if B > 1 and U0.ndim == 2:
         U0 = np.broadcast_to(U0, (B,) + U0.shape).copy()
-    return Problem(model_d, obj, U0, constraints=cons, x0=np.zeros(n), xf=xf, N=N, dt=dt)
+    B = U0.shape[0] if U0.ndim == 3 else B
+    x0 = np.zeros((B, n)) if B > 1 else np.zeros(n)
+    return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
 
 
 # ---------------------------------------------------------------------------- BASELINE configs
