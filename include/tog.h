@@ -76,7 +76,12 @@ enum tog_model_id {
 enum tog_integrator {
   TOG_RK3 = 0, /* src/integration.jl:149-158 */
   TOG_RK4 = 1, /* src/integration.jl:115-125 */
-  TOG_MIDPOINT = 2 /* explicit midpoint, src/integration.jl:26-33 (discretize_model(model, :midpoint)) */
+  TOG_MIDPOINT = 2, /* explicit midpoint, src/integration.jl:26-33 (discretize_model(model, :midpoint)) */
+  /* implicit schemes: a Newton solve per step to ||g||_2 <= 1e-12 (src/integration.jl:44-73 and
+     :171-205); built for models with n <= 4 (double integrator, pendulum, car, cartpole), else
+     tog_create returns TOG_ERR_UNSUPPORTED */
+  TOG_RK3_IMPLICIT = 3,
+  TOG_MIDPOINT_IMPLICIT = 4
 };
 
 /* ---------------------------------------------------------------- constraints */

@@ -559,9 +559,163 @@ static void model_f(int model, dual* xd, const dual* x, const dual* u) {
   }
 }
 
+/* ---------------------------------------------------------------------------------------------
+ * Implicit integrators (src/integration.jl:44-73 midpoint_implicit, :171-205 rk3_implicit).
+ * The reference differentiates fd! with ForwardDiff straight through the Newton loop, so its
+ * iterate y and residual g carry partials, and ∇g = I - ½dt·∇f(Xm) is itself a nested-dual matrix.
+ * This restatement runs the same loop on duals with ∇g taken at the values only: the dropped term
+ * is (∇g⁻¹)' g, which vanishes with g, so the Jacobian agrees with the reference's to the loop's
+ * own tolerance (‖g‖ <= 1e-12), and the values are the reference's loop exactly.
+ * Parity trap (reproduced): rk3_implicit writes `fc1 = fc2 = fc3 = zero(x)`, one array under three
+ * names, so after f(fc1,x,u); f(fc3,y,u) the midpoint term dt/8*(fc1 - fc3) is F - F, and
+ * g = y - x - dt/6*F - 4/6*dt*F - dt/6*F with F = f(Xm) for all three.
+ * --------------------------------------------------------------------------------------------- */
+static void model_f(int model, dual* xd, const dual* x, const dual* u);
+
+/* ∂f/∂x at the values of (x, u): ForwardDiff.jacobian(f_aug, zero(x), [x;u])[:, 1:n], one partial
+   per column (each partial of a dual evaluation is independent of the others) */
+static void jac_x_val(int model, int n, int m, double* A, const dual* x, const dual* u) {
+  int save = g_nd;
+  g_nd = 1;
+  for (int j = 0; j < n; j++) {
+    dual X[16], U[OM], F[16];
+    for (int i = 0; i < n; i++) {
+      X[i].v = x[i].v;
+      X[i].p[0] = (i == j) ? 1.0 : 0.0;
+    }
+    for (int i = 0; i < m; i++) {
+      U[i].v = u[i].v;
+      U[i].p[0] = 0.0;
+    }
+    model_f(model, F, X, U);
+    for (int i = 0; i < n; i++) A[i + n * j] = F[i].p[0];
+  }
+  g_nd = save;
+}
+
+/* LinearAlgebra.generic_norm2 (Julia 1.1): unscaled sum of squares when n·max² is finite and
+   nonzero, else scaled by max|g| (NaN propagates) */
+static double jl_norm2(const double* g, int n) {
+  double mx = 0.0;
+  for (int i = 0; i < n; i++) mx = tog_jlmax(mx, fabs(g[i]));
+  if (mx != mx || mx == 0.0 || isinf(mx)) return mx;
+  if (isfinite((double)n * mx * mx) && mx * mx != 0.0) {
+    double s = g[0] * g[0];
+    for (int i = 1; i < n; i++) s = s + g[i] * g[i];
+    return sqrt(s);
+  }
+  double t = fabs(g[0]) / mx, s = t * t;
+  for (int i = 1; i < n; i++) {
+    t = fabs(g[i]) / mx;
+    s = s + t * t;
+  }
+  return mx * sqrt(s);
+}
+
+/* δ = (-G) \ b (the reference's `-∇g\g` parses as (-∇g)\g): generic_lufact! with partial pivoting
+   (first max |a_ik|, reciprocal scaling, column-by-column rank-1 updates), row swaps applied to b in
+   order, unit-lower forward and upper backward substitution (naivesub!, column oriented). b is
+   dual; the factor is real. */
+static void lu_neg_solve(int n, const double* G, dual* b) {
+  double a[16 * 16];
+  for (int e = 0; e < n * n; e++) a[e] = -G[e];
+  int piv[16];
+  for (int k = 0; k < n; k++) {
+    int kp = k;
+    double amax = 0.0;
+    for (int i = k; i < n; i++) {
+      double ai = fabs(a[i + n * k]);
+      if (ai > amax) {
+        kp = i;
+        amax = ai;
+      }
+    }
+    piv[k] = kp;
+    if (a[kp + n * k] != 0.0) {
+      if (kp != k)
+        for (int j = 0; j < n; j++) {
+          double t = a[k + n * j];
+          a[k + n * j] = a[kp + n * j];
+          a[kp + n * j] = t;
+        }
+      double inv = 1.0 / a[k + n * k];
+      for (int i = k + 1; i < n; i++) a[i + n * k] = a[i + n * k] * inv;
+    }
+    for (int j = k + 1; j < n; j++)
+      for (int i = k + 1; i < n; i++) a[i + n * j] = a[i + n * j] - a[i + n * k] * a[k + n * j];
+  }
+  for (int k = 0; k < n; k++)
+    if (piv[k] != k) {
+      dual t = b[k];
+      b[k] = b[piv[k]];
+      b[piv[k]] = t;
+    }
+  for (int j = 0; j < n; j++)
+    for (int i = j + 1; i < n; i++) b[i] = dsub(b[i], dscale(b[j], a[i + n * j]));
+  for (int j = n - 1; j >= 0; j--) {
+    b[j] = ddivc(b[j], a[j + n * j]);
+    for (int i = j - 1; i >= 0; i--) b[i] = dsub(b[i], dscale(b[j], a[i + n * j]));
+  }
+}
+
+static void implicit_step_dual(int model, int integ, int n, int m, dual* y, const dual* x, const dual* u, dual dt) {
+  for (int i = 0; i < n; i++) y[i] = x[i];
+  double gn = INFINITY;
+  int cnt = 0;
+  while (gn > 1e-12) {
+    if (++cnt > 1000) { /* error("Integration convergence fail"): the state becomes NaN here */
+      for (int i = 0; i < n; i++) y[i] = dc(NAN);
+      return;
+    }
+    dual g[16], xm[16], F[16];
+    double G[16 * 16], A[16 * 16];
+    if (integ == TOG_MIDPOINT_IMPLICIT) {
+      for (int i = 0; i < n; i++) xm[i] = dscale(dadd(x[i], y[i]), 0.5); /* Xm = 0.5*(x + y) */
+      model_f(model, F, xm, u);                                            /* f(fc, Xm, u) */
+      for (int i = 0; i < n; i++) g[i] = dsub(dsub(y[i], x[i]), dmul(dt, F[i])); /* y - x - dt*fc */
+      jac_x_val(model, n, m, A, xm, u);
+      double h = 0.5 * dt.v; /* ∇g = I - 0.5*dt*A */
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < n; i++) G[i + n * j] = (i == j ? 1.0 : 0.0) - h * A[i + n * j];
+    } else {
+      dual d[16];
+      model_f(model, F, y, u); /* f(fc1,x,u) then f(fc3,y,u) into the same array: F = f(y) */
+      for (int i = 0; i < n; i++) d[i] = dsub(F[i], F[i]);
+      dual dt8 = ddivc(dt, 8.0);
+      for (int i = 0; i < n; i++) xm[i] = dadd(dscale(dadd(x[i], y[i]), 0.5), dmul(dt8, d[i]));
+      model_f(model, F, xm, u); /* f(fc2, Xm, u): fc1 = fc2 = fc3 = f(Xm) */
+      dual dt6 = ddivc(dt, 6.0), dt46 = dscale(dt, 4.0 / 6.0);
+      for (int i = 0; i < n; i++)
+        g[i] = dsub(dsub(dsub(dsub(y[i], x[i]), dmul(dt6, F[i])), dmul(dt46, F[i])), dmul(dt6, F[i]));
+      double A2[16 * 16], M2[16 * 16];
+      jac_x_val(model, n, m, A, xm, u); /* A1 */
+      jac_x_val(model, n, m, A2, y, u);
+      double c8 = dt.v / 8.0, c46 = (4.0 / 6.0) * dt.v, c6 = dt.v / 6.0;
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < n; i++) M2[i + n * j] = (i == j ? 0.5 : 0.0) - c8 * A2[i + n * j];
+      /* ∇g = I - (4/6*dt*A1)*(0.5I - dt/8*A2) - dt/6*A2, the product summed over k in order */
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < n; i++) {
+          double p = (c46 * A[i]) * M2[n * j];
+          for (int k = 1; k < n; k++) p = p + (c46 * A[i + n * k]) * M2[k + n * j];
+          G[i + n * j] = ((i == j ? 1.0 : 0.0) - p) - c6 * A2[i + n * j];
+        }
+    }
+    double gv[16];
+    for (int i = 0; i < n; i++) gv[i] = g[i].v;
+    gn = jl_norm2(gv, n);
+    lu_neg_solve(n, G, g); /* δy = -∇g\g */
+    for (int i = 0; i < n; i++) y[i] = dadd(y[i], g[i]); /* y .+= δy */
+  }
+}
+
 /* rk4: src/integration.jl:115-125 ; rk3: src/integration.jl:149-158 (dt is a Dual input) */
 static void discrete_f_dual(int model, int integ, int n, dual* xn, const dual* x, const dual* u, dual dt) {
   dual k1[16], k2[16], k3[16], k4[16], t[16];
+  if (integ == TOG_MIDPOINT_IMPLICIT || integ == TOG_RK3_IMPLICIT) {
+    implicit_step_dual(model, integ, n, model_m[model], xn, x, u, dt);
+    return;
+  }
   if (integ == TOG_MIDPOINT) { /* src/integration.jl:26-33 */
     model_f(model, k1, x, u);
     dual h = ddivc(dt, 2.0); /* xdot .*= dt/2. */

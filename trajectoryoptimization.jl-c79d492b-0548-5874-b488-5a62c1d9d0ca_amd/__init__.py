@@ -14,7 +14,7 @@ from . import abi
 from .problem import (BoundConstraint, CircleConstraints, Constraints, ConstraintSet, Dynamics, GoalConstraint,
                       LQRCost, LQRCostTerminal, LQRObjective, Model, Objective, Problem, QuadraticCost,
                       SphereConstraints, circle_constraint, discretize_model, goal_constraint, initial_controls_b,
-                      initial_states_b, max_violation, midpoint, rk3, rk4, set_x0_b, sphere_constraint, add_slack_controls,
+                      initial_states_b, max_violation, midpoint, midpoint_implicit, rk3, rk3_implicit, rk4, set_x0_b, sphere_constraint, add_slack_controls,
                       InfeasibleConstraint, infeasible_constraints, infeasible_problem, line_trajectory)
 from .solvers import (Expansion, AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
                       AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, ProjectedNewtonSolver,
@@ -27,7 +27,7 @@ __all__ = [
     "abi", "BoundConstraint", "CircleConstraints", "Constraints", "ConstraintSet", "Dynamics", "GoalConstraint",
     "LQRCost", "LQRCostTerminal", "LQRObjective", "Model", "Objective", "Problem", "QuadraticCost",
     "SphereConstraints", "circle_constraint", "discretize_model", "goal_constraint", "initial_controls_b",
-    "initial_states_b", "max_violation", "midpoint", "rk3", "rk4", "set_x0_b", "sphere_constraint", "AbstractSolver",
+    "initial_states_b", "max_violation", "midpoint", "midpoint_implicit", "rk3", "rk3_implicit", "rk4", "set_x0_b", "sphere_constraint", "AbstractSolver",
     "AbstractSolverFor", "ALTROSolver", "ALTROSolverOptions", "AugmentedLagrangianSolver",
     "AugmentedLagrangianSolverOptions", "iLQRSolver", "iLQRSolverOptions", "solve", "solve_b", "solver_name",
     "to_tog_options", "Expansion", "backwardpass_b", "cost", "cost_expansion_b", "update_constraints_b", "forwardpass_b", "jacobian_b", "rollout_b",

@@ -24,7 +24,7 @@ MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1), 5: (14, 7)}
 # status codes (include/tog.h tog_status_code)
 OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 
-RK3, RK4, MIDPOINT = 0, 1, 2
+RK3, RK4, MIDPOINT, RK3_IMPLICIT, MIDPOINT_IMPLICIT = 0, 1, 2, 3, 4
 CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE = range(5)
 PROB_INFEASIBLE = 1  # tog_problem_flag
 MODE_ILQR, MODE_AL = 0, 1

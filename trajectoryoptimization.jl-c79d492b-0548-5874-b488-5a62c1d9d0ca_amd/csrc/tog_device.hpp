@@ -705,12 +705,197 @@ template <class M>
 struct ModelTraits {
   using Base = M;
   static constexpr int slack = 0;
+  static constexpr bool implicit_ok = M::n <= 4;  // implicit integrators instantiated
 };
 template <class Mb>
 struct ModelTraits<Infeasible<Mb>> {
   using Base = Mb;
   static constexpr int slack = Mb::n;
+  static constexpr bool implicit_ok = false;
 };
+
+// ---------------------------------------------------------------------------------------------
+// Implicit integrators (src/integration.jl:44-73 midpoint_implicit, :171-205 rk3_implicit): a
+// Newton solve for x+ per step, run while ||g||_2 > 1e-12. Same operations, in the same order, as
+// the oracle's implicit_step_dual (oracle/tog_oracle.c): the iterate carries the Jacobian's partials
+// when T is a Dual, ∇g is formed at the values (∂f/∂x one Dual<1> column at a time), and
+// δy = (-∇g)\g by partial-pivoting LU. rk3_implicit reproduces the reference's aliasing of
+// fc1 = fc2 = fc3 (one array), so its residual is y - x - dt/6 F - 4/6 dt F - dt/6 F, F = f(Xm).
+// Built for models with n <= 4 (ModelTraits::implicit_ok); the reference's 1000-iteration error
+// becomes a NaN state (the rollout then fails as diverged).
+template <int n>
+__host__ __device__ __forceinline__ double jl_norm2(const double* g) {
+  double mx = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; i++) mx = tog_jlmax(mx, fabs(g[i]));
+  if (mx != mx || mx == 0.0 || isinf(mx)) return mx;
+  if (isfinite((double)n * mx * mx) && mx * mx != 0.0) {
+    double s = g[0] * g[0];
+#pragma unroll
+    for (int i = 1; i < n; i++) s = s + g[i] * g[i];
+    return sqrt(s);
+  }
+  double t = fabs(g[0]) / mx, s = t * t;
+#pragma unroll
+  for (int i = 1; i < n; i++) {
+    t = fabs(g[i]) / mx;
+    s = s + t * t;
+  }
+  return mx * sqrt(s);
+}
+
+template <class M, class T>
+__host__ __device__ __forceinline__ void jac_x_val(double* A, const T* x, const T* u) {
+  constexpr int n = M::n, m = M::m;
+#pragma unroll
+  for (int j = 0; j < n; j++) {
+    Dual<1> X[n], U[m], F[n];
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      X[i].v = val_(x[i]);
+      X[i].g[0] = (i == j) ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      U[i].v = val_(u[i]);
+      U[i].g[0] = 0.0;
+    }
+    M::f(F, X, U);
+#pragma unroll
+    for (int i = 0; i < n; i++) A[i + n * j] = F[i].g[0];
+  }
+}
+
+// b <- (-G) \ b (generic_lufact! + naivesub!, see the oracle's lu_neg_solve)
+template <int n, class T>
+__host__ __device__ __forceinline__ void lu_neg_solve(const double* G, T* b) {
+  double a[n * n];
+#pragma unroll
+  for (int e = 0; e < n * n; e++) a[e] = -G[e];
+  int piv[n];
+#pragma unroll
+  for (int k = 0; k < n; k++) {
+    int kp = k;
+    double amax = 0.0;
+#pragma unroll
+    for (int i = k; i < n; i++) {
+      const double ai = fabs(a[i + n * k]);
+      if (ai > amax) {
+        kp = i;
+        amax = ai;
+      }
+    }
+    piv[k] = kp;
+    if (a[kp + n * k] != 0.0) {
+      if (kp != k) {
+#pragma unroll
+        for (int j = 0; j < n; j++) {
+          // select-based swap keeps the matrix in registers (no dynamic indexing)
+#pragma unroll
+          for (int i = k + 1; i < n; i++)
+            if (i == kp) {
+              const double t = a[k + n * j];
+              a[k + n * j] = a[i + n * j];
+              a[i + n * j] = t;
+            }
+        }
+      }
+      const double inv = 1.0 / a[k + n * k];
+#pragma unroll
+      for (int i = k + 1; i < n; i++) a[i + n * k] = a[i + n * k] * inv;
+    }
+#pragma unroll
+    for (int j = k + 1; j < n; j++)
+#pragma unroll
+      for (int i = k + 1; i < n; i++) a[i + n * j] = a[i + n * j] - a[i + n * k] * a[k + n * j];
+  }
+#pragma unroll
+  for (int k = 0; k < n; k++) {
+#pragma unroll
+    for (int i = k + 1; i < n; i++)
+      if (piv[k] == i) {
+        const T t = b[k];
+        b[k] = b[i];
+        b[i] = t;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < n; j++)
+#pragma unroll
+    for (int i = j + 1; i < n; i++) b[i] = b[i] - a[i + n * j] * b[j];
+#pragma unroll
+  for (int j = n - 1; j >= 0; j--) {
+    b[j] = b[j] / a[j + n * j];
+#pragma unroll
+    for (int i = j - 1; i >= 0; i--) b[i] = b[i] - a[i + n * j] * b[j];
+  }
+}
+
+template <class M, int INTEG, class T>
+__host__ __device__ __forceinline__ void implicit_step(T* y, const T* x, const T* u, double dt) {
+  constexpr int n = M::n;
+#pragma unroll
+  for (int i = 0; i < n; i++) y[i] = x[i];
+  double gn = INFINITY;
+  int cnt = 0;
+  while (gn > 1e-12) {
+    if (++cnt > 1000) {  // error("Integration convergence fail")
+#pragma unroll
+      for (int i = 0; i < n; i++) y[i] = cst_(NAN, x[i]);
+      return;
+    }
+    T g[n], xm[n], F[n];
+    double G[n * n], A[n * n];
+    if constexpr (INTEG == TOG_MIDPOINT_IMPLICIT) {
+#pragma unroll
+      for (int i = 0; i < n; i++) xm[i] = 0.5 * (x[i] + y[i]);
+      M::f(F, xm, u);
+#pragma unroll
+      for (int i = 0; i < n; i++) g[i] = (y[i] - x[i]) - dt * F[i];
+      jac_x_val<M>(A, xm, u);
+      const double h = 0.5 * dt;
+#pragma unroll
+      for (int j = 0; j < n; j++)
+#pragma unroll
+        for (int i = 0; i < n; i++) G[i + n * j] = (i == j ? 1.0 : 0.0) - h * A[i + n * j];
+    } else {
+      T d[n];
+      M::f(F, y, u);  // f(fc1, x, u); f(fc3, y, u) -- one array: F = f(y)
+#pragma unroll
+      for (int i = 0; i < n; i++) d[i] = F[i] - F[i];
+      const double dt8 = dt / 8.0;
+#pragma unroll
+      for (int i = 0; i < n; i++) xm[i] = 0.5 * (x[i] + y[i]) + dt8 * d[i];
+      M::f(F, xm, u);  // f(fc2, Xm, u): fc1 = fc2 = fc3 = f(Xm)
+      const double dt6 = dt / 6.0, dt46 = (4.0 / 6.0) * dt;
+#pragma unroll
+      for (int i = 0; i < n; i++) g[i] = (((y[i] - x[i]) - dt6 * F[i]) - dt46 * F[i]) - dt6 * F[i];
+      double A2[n * n], M2[n * n];
+      jac_x_val<M>(A, xm, u);
+      jac_x_val<M>(A2, y, u);
+#pragma unroll
+      for (int j = 0; j < n; j++)
+#pragma unroll
+        for (int i = 0; i < n; i++) M2[i + n * j] = (i == j ? 0.5 : 0.0) - dt8 * A2[i + n * j];
+#pragma unroll
+      for (int j = 0; j < n; j++)
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          double p = (dt46 * A[i]) * M2[n * j];
+#pragma unroll
+          for (int k = 1; k < n; k++) p = p + (dt46 * A[i + n * k]) * M2[k + n * j];
+          G[i + n * j] = ((i == j ? 1.0 : 0.0) - p) - dt6 * A2[i + n * j];
+        }
+    }
+    double gv[n];
+#pragma unroll
+    for (int i = 0; i < n; i++) gv[i] = val_(g[i]);
+    gn = jl_norm2<n>(gv);
+    lu_neg_solve<n>(G, g);
+#pragma unroll
+    for (int i = 0; i < n; i++) y[i] = y[i] + g[i];
+  }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Explicit Runge-Kutta discretisation with runtime dt (src/integration.jl:115-158). Running-sum
@@ -725,7 +910,10 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
     for (int i = 0; i < Mb::n; i++) xn[i] = xn[i] + u[Mb::m + i];  // x+ .+= u[idx.inf]
   } else {
   constexpr int n = M::n;
-  if constexpr (INTEG == TOG_MIDPOINT) {
+  if constexpr (INTEG == TOG_MIDPOINT_IMPLICIT || INTEG == TOG_RK3_IMPLICIT) {
+    implicit_step<M, INTEG, T>(xn, x, u, dt);
+    return;
+  } else if constexpr (INTEG == TOG_MIDPOINT) {
     // midpoint (src/integration.jl:26-33): ẋ = f(x,u); ẋ .*= dt/2; ẋ = f(x + ẋ, u); x+ = x + ẋ*dt
     T k[n], t[n];
     M::f(k, x, u);

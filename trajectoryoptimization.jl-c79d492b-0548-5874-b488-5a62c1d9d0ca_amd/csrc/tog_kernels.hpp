@@ -1887,6 +1887,7 @@ struct ModelOps {
   // projected Newton (tog_pn.hpp): phase 0 = k_pn_begin, 1 = k_pn_project, 2 = k_pn_finish; null for
   // the infeasible (slack) models
   void (*pn)(const DevProblem*, const DevBuffers&, const PNBuffers&, long long B, int integ, int phase, hipStream_t);
+  bool implicit;                   // TOG_RK3_IMPLICIT / TOG_MIDPOINT_IMPLICIT instantiated
   int bwd_lds_bytes;
   int team_tpw;                    // trajectories per wave of k_bwd_team
   int (*team_stride)(int pmax, int sqrt);  // per-team LDS stride of k_bwd_team (doubles)
@@ -1904,31 +1905,44 @@ struct ModelLaunch {
   using Mb = typename ModelTraits<M>::Base;  // the differentiated model (infeasible: without slacks)
   static constexpr int JW = (Mb::n + Mb::m) <= 6 ? (Mb::n + Mb::m) : (Mb::id == TOG_MODEL_KUKA ? 1 : TOG_JW);
   static unsigned grid(long long total, int blk) { return (unsigned)((total + blk - 1) / blk); }
+  // runtime integrator -> compile-time INTEG (the implicit schemes only where instantiated; tog_create
+  // rejects them elsewhere)
+  template <class F>
+  static void with_integ(int integ, F&& f) {
+    if (integ == TOG_RK4) {
+      f(std::integral_constant<int, TOG_RK4>{});
+    } else if (integ == TOG_MIDPOINT) {
+      f(std::integral_constant<int, TOG_MIDPOINT>{});
+    } else if (integ == TOG_RK3_IMPLICIT || integ == TOG_MIDPOINT_IMPLICIT) {
+      if constexpr (ModelTraits<M>::implicit_ok) {
+        if (integ == TOG_RK3_IMPLICIT)
+          f(std::integral_constant<int, TOG_RK3_IMPLICIT>{});
+        else
+          f(std::integral_constant<int, TOG_MIDPOINT_IMPLICIT>{});
+      }
+    } else {
+      f(std::integral_constant<int, TOG_RK3>{});
+    }
+  }
   static void init(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, hipStream_t st) {
-    if (integ == TOG_RK4)
-      hipLaunchKernelGGL((k_init<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
-    else if (integ == TOG_MIDPOINT)
-      hipLaunchKernelGGL((k_init<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
-    else
-      hipLaunchKernelGGL((k_init<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
+    with_integ(integ, [&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      hipLaunchKernelGGL((k_init<M, I>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode);
+    });
   }
   static void rollout_open(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, hipStream_t st) {
-    if (integ == TOG_RK4)
-      hipLaunchKernelGGL((k_rollout_open<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
-    else if (integ == TOG_MIDPOINT)
-      hipLaunchKernelGGL((k_rollout_open<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
-    else
-      hipLaunchKernelGGL((k_rollout_open<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+    with_integ(integ, [&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      hipLaunchKernelGGL((k_rollout_open<M, I>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+    });
   }
   static void jacobian(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int integ, hipStream_t st) {
     constexpr int NCH = (Mb::n + Mb::m + JW - 1) / JW;
     const long long total = B * (long long)(N - 1) * NCH;
-    if (integ == TOG_RK4)
-      hipLaunchKernelGGL((k_jacobian<M, TOG_RK4, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
-    else if (integ == TOG_MIDPOINT)
-      hipLaunchKernelGGL((k_jacobian<M, TOG_MIDPOINT, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
-    else
-      hipLaunchKernelGGL((k_jacobian<M, TOG_RK3, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+    with_integ(integ, [&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      hipLaunchKernelGGL((k_jacobian<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+    });
   }
   static void backward(const DevProblem* P, const DevBuffers& Bf, long long B, int sq, int al, int flags, int team,
                        hipStream_t st) {
@@ -2019,9 +2033,7 @@ struct ModelLaunch {
   }
   static void forward(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, int mode, int bk,
                       const double* Jp, double* Jo, hipStream_t st, const StreamPair* sp) {
-    if (integ == TOG_RK4) forward_i<TOG_RK4>(P, Bf, B, mode, bk, Jp, Jo, st, sp);
-    else if (integ == TOG_MIDPOINT) forward_i<TOG_MIDPOINT>(P, Bf, B, mode, bk, Jp, Jo, st, sp);
-    else forward_i<TOG_RK3>(P, Bf, B, mode, bk, Jp, Jo, st, sp);
+    with_integ(integ, [&](auto ic) { forward_i<decltype(ic)::value>(P, Bf, B, mode, bk, Jp, Jo, st, sp); });
   }
   static void cost(const DevProblem* P, const DevBuffers& Bf, long long B, int al, int bar, double* J,
                    hipStream_t st) {
@@ -2029,21 +2041,17 @@ struct ModelLaunch {
   }
   static void rollout(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, double alpha, int* ok,
                       hipStream_t st) {
-    if (integ == TOG_RK4)
-      hipLaunchKernelGGL((k_rollout<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
-    else if (integ == TOG_MIDPOINT)
-      hipLaunchKernelGGL((k_rollout<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
-    else
-      hipLaunchKernelGGL((k_rollout<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
+    with_integ(integ, [&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      hipLaunchKernelGGL((k_rollout<M, I>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, alpha, ok);
+    });
   }
   static void slack_controls(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, hipStream_t st) {
     if constexpr (ModelTraits<M>::slack > 0) {
-      if (integ == TOG_RK4)
-        hipLaunchKernelGGL((k_slack_controls<M, TOG_RK4>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
-      else if (integ == TOG_MIDPOINT)
-        hipLaunchKernelGGL((k_slack_controls<M, TOG_MIDPOINT>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
-      else
-        hipLaunchKernelGGL((k_slack_controls<M, TOG_RK3>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+      with_integ(integ, [&](auto ic) {
+        constexpr int I = decltype(ic)::value;
+        hipLaunchKernelGGL((k_slack_controls<M, I>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);
+      });
     }
   }
   static void cost_expansion(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int sq, int al,
@@ -2066,12 +2074,7 @@ struct ModelLaunch {
   }
   static void pn(const DevProblem* P, const DevBuffers& Bf, const PNBuffers& W, long long B, int integ, int phase,
                  hipStream_t st) {
-    if (integ == TOG_RK4)
-      pn_phase<TOG_RK4>(P, Bf, W, B, phase, st);
-    else if (integ == TOG_MIDPOINT)
-      pn_phase<TOG_MIDPOINT>(P, Bf, W, B, phase, st);
-    else
-      pn_phase<TOG_RK3>(P, Bf, W, B, phase, st);
+    with_integ(integ, [&](auto ic) { pn_phase<decltype(ic)::value>(P, Bf, W, B, phase, st); });
   }
   static ModelOps ops() {
     ModelOps o;
@@ -2079,6 +2082,7 @@ struct ModelLaunch {
     o.m = M::m;
     o.slack = ModelTraits<M>::slack;
     o.pcap = pcap_of<M>();
+    o.implicit = ModelTraits<M>::implicit_ok;
     o.slack_controls = slack_controls;
     o.cost_expansion = cost_expansion;
     o.init = init;

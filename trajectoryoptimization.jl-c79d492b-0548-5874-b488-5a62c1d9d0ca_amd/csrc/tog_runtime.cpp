@@ -545,8 +545,11 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
   if (d->batch < 1) return fail(TOG_ERR_ARG, "batch must be >= 1");
   if (!(d->dt > 0)) return fail(TOG_ERR_ARG, "dt must be strictly positive");  // src/problem.jl:66-68
-  if (d->integrator != TOG_RK3 && d->integrator != TOG_RK4 && d->integrator != TOG_MIDPOINT)
+  if (d->integrator != TOG_RK3 && d->integrator != TOG_RK4 && d->integrator != TOG_MIDPOINT &&
+      d->integrator != TOG_RK3_IMPLICIT && d->integrator != TOG_MIDPOINT_IMPLICIT)
     return fail(TOG_ERR_UNSUPPORTED, "integrator");
+  if ((d->integrator == TOG_RK3_IMPLICIT || d->integrator == TOG_MIDPOINT_IMPLICIT) && !ops->implicit)
+    return fail(TOG_ERR_UNSUPPORTED, "implicit integrators are built for models with n <= 4 (no slack controls)");
   int ndev = tog_device_count();
   if (device < 0 || device >= ndev) return fail(TOG_ERR_DEVICE, "no such HIP device");
   tog_handle* h = new tog_handle();

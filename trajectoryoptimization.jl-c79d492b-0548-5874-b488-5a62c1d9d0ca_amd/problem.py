@@ -52,17 +52,31 @@ def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) ->
     if model.discrete:
         raise ValueError("model is already discrete")
     key = discretizer.lstrip(":")
-    if key in ("rk3_implicit", "midpoint_implicit"):
-        raise NotImplementedError(f"implicit integration {discretizer!r} is not built (SURVEY.md §8(f))")
-    if key not in ("rk3", "rk4", "midpoint"):
+    integs = {"rk3": abi.RK3, "rk4": abi.RK4, "midpoint": abi.MIDPOINT, "rk3_implicit": abi.RK3_IMPLICIT,
+              "midpoint_implicit": abi.MIDPOINT_IMPLICIT}
+    if key not in integs:
         raise ValueError(f"Integration not defined: {discretizer!r}")  # src/model.jl:659
-    integ = {"rk3": abi.RK3, "rk4": abi.RK4, "midpoint": abi.MIDPOINT}[key]
-    return Model(model.model_id, model.n, model.m, model.name, integ)
+    if integs[key] in (abi.RK3_IMPLICIT, abi.MIDPOINT_IMPLICIT) and model.n > 4:
+        # the device instantiates the implicit Newton step for n <= 4 (csrc/tog_device.hpp)
+        raise NotImplementedError(f"implicit integration {discretizer!r} is built for models with n <= 4")
+    return Model(model.model_id, model.n, model.m, model.name, integs[key])
 
 
 def midpoint(model: Model, dt: float = 1.0) -> Model:
     """``midpoint(model)`` (src/model.jl:642, src/integration.jl:26-33)."""
     return discretize_model(model, "midpoint", dt)
+
+
+def midpoint_implicit(model: Model, dt: float = 1.0) -> Model:
+    """``midpoint_implicit(model)`` (src/model.jl:647, src/integration.jl:44-73): x+ solves
+    g = x+ - x - dt f((x + x+)/2) = 0 by Newton iterations to ||g|| <= 1e-12."""
+    return discretize_model(model, "midpoint_implicit", dt)
+
+
+def rk3_implicit(model: Model, dt: float = 1.0) -> Model:
+    """``rk3_implicit(model)`` (src/model.jl:646, src/integration.jl:171-205), including the
+    reference's aliasing of its three stage buffers (see csrc/tog_device.hpp implicit_step)."""
+    return discretize_model(model, "rk3_implicit", dt)
 
 
 def add_slack_controls(model: Model) -> Model:
