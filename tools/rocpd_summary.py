@@ -52,7 +52,7 @@ def main(d):
     return traffic(d)
 
 
-GROUPS = {"backward": ("k_bwd_team", "k_backward"), "forward": ("k_ls_spec", "k_ls_compact", "k_ls_commit"),
+GROUPS = {"backward": ("k_bwd_team", "k_backward"), "forward": ("k_ls_spec", "k_ls_compact", "k_ls_commit", "k_ls_decide", "k_ls_apply", "k_ls_book"),
           "jacobian": ("k_jacobian",)}
 
 

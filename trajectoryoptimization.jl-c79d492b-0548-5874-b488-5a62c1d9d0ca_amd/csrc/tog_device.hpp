@@ -105,7 +105,12 @@ struct DevBuffers {
   int bwd_stride2[2]; // [std, sqrt] strides
   int bwd_shmem2[2];  // [std, sqrt] LDS bytes
   int rows_shmem;     // LDS bytes of a block's copy of the row tables (rollout kernels)
-  int pad2_;
+  int ls_first;       // width of the first speculative round (>= nc: one round)
+  int nknots;         // N (host-side launch geometry)
+  double* cand;       // (n+m, N, NC, B) every trial's rollout (candidate-copy line search), or null
+  int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
+  double* ls_Jw;      // (B) its cost
+  double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū
   TrajState* st;
 };
 

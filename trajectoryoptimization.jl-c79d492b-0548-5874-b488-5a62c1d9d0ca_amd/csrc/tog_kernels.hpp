@@ -30,6 +30,12 @@ constexpr int WAVE = 64;
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroups: s_barrier is ~free
 
+// candidate slot layout of the line search (k_ls_spec<CAND>): per knot [ū_k (m) | x̄_k (n)], padded to an
+// even width so that every knot starts 16-byte aligned (wide stores)
+template <class M>
+__host__ __device__ constexpr int cand_w() {
+  return (M::n + M::m + 1) & ~1;
+}
 template <class M>
 __host__ __device__ constexpr int nq_of() {
   return M::n + M::m + M::n * M::n + M::m * M::m + M::m * M::n;
@@ -1224,7 +1230,8 @@ __device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS tra
 // trajectory (objective.jl:40-48 / AL cost augmented_lagrangian_methods.jl:298-313), summed in the
 // oracle's order. WMODE 0: cost only. WMODE 1: also write X̄, Ū. WMODE 2: write the new trajectory in
 // place into X, U (the accepted step; old X[k] is read before it is overwritten) and return the
-// todorov gradient of the new U (ilqr_methods.jl:122-129).
+// todorov gradient of the new U (ilqr_methods.jl:122-129). WMODE 3: write the rolled-out trajectory
+// into the candidate slot `cw` (knot-major, n+m doubles per knot: x̄_k then ū_k), for k_ls_apply.
 // Constraint-row tables for the rollouts: the global ones, or a block's LDS copy (block_row_tables).
 struct RowTables {
   const ConRow* rows;
@@ -1253,7 +1260,8 @@ __device__ __forceinline__ RowTables block_row_tables(const DevProblem* P, void*
 
 template <class M, int INTEG, int WMODE>
 __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha,
-                             bool al, double& Jout, double* grad_out, const RowTables& RT) {
+                             bool al, double& Jout, double* grad_out, const RowTables& RT,
+                             double* __restrict__ cw = nullptr) {
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
   double* X = Bf.X + (size_t)b * N * n;
@@ -1325,6 +1333,10 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
 #pragma unroll
       for (int i = 0; i < m; i++) Ub[(size_t)(k - 1) * m + i] = ub[i];
     }
+    if (WMODE == 3) {
+#pragma unroll
+      for (int i = 0; i < m; i++) cw[(size_t)(k - 1) * cand_w<M>() + i] = ub[i];
+    }
     if (WMODE == 2) {
       double mx = -INFINITY;
 #pragma unroll
@@ -1379,6 +1391,10 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
 #pragma unroll
       for (int i = 0; i < n; i++) Xb[(size_t)k * n + i] = xn[i];
     }
+    if (WMODE == 3) {
+#pragma unroll
+      for (int i = 0; i < n; i++) cw[(size_t)k * cand_w<M>() + m + i] = xn[i];
+    }
     if (!ok) return false;
   }
   J += terminal_cost<n>(P, xb);
@@ -1400,11 +1416,9 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
 
 // solve! bookkeeping after an accepted forward pass (ilqr_methods.jl:21-42) and the AL outer update
 // when the inner solve finished (augmented_lagrangian_methods.jl:53-126). One lane per trajectory.
-template <class M>
-__device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, TrajState& s,
-                                 double J, bool copied, double grad, int mode) {
-  constexpr int n = M::n, m = M::m;
-  const int N = P->N, pmax = P->pmax;
+// Inner part: returns true when the AL outer update is due (inner solve finished in AL mode).
+__device__ inline bool inner_bookkeeping(const DevProblem* __restrict__ P, TrajState& s, double J, double grad,
+                                         int mode) {
   const tog_options& o = P->o;
   const bool al = (mode == TOG_MODE_AL);
   s.total_steps++;
@@ -1413,7 +1427,6 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
     s.flags |= TOG_TRAJ_COST_BLOWUP;
     inner_done = true;
   } else {
-    (void)copied;
     s.dJ = fabs(J - s.J);
     s.J = J;
     s.iters++;
@@ -1426,12 +1439,50 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
       if (s.iters >= o.iterations) s.flags |= TOG_TRAJ_MAX_ITERS;
     }
   }
-  if (!inner_done) return;
+  if (!inner_done) return false;
   if (!al) {
     s.flags |= TOG_TRAJ_CONVERGED;
     s.active = 0;
-    return;
+    return false;
   }
+  return true;
+}
+
+// AL outer update after the inner solve (augmented_lagrangian_methods.jl:53-126): cost(prob) to refresh
+// C, dual_update!, penalty_update!, max_violation, convergence, and the next outer iteration's reset.
+__device__ inline void al_outer_finish(const DevProblem* __restrict__ P, TrajState& s, double mumax, double c_max,
+                                       double Jnext, int mode) {
+  const tog_options& o = P->o;
+  s.mu_max = mumax;
+  s.c_max = c_max;
+  const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (s.c_max < o.constraint_tolerance);
+  if (conv) {
+    s.flags |= TOG_TRAJ_AL_CONVERGED;
+    s.active = 0;
+  } else if (s.al_iter >= o.al_iterations) {
+    s.flags |= TOG_TRAJ_AL_MAX_ITERS;
+    s.active = 0;
+  } else {
+    // next outer iteration: reset!(solver_uncon), set_tolerances!, solve! init (rollout is a no-op)
+    s.al_iter++;
+    set_tolerances(P, s, mode);
+    s.rho = 0.0;
+    s.drho = 0.0;
+    s.J = Jnext;
+    s.iters = 1;
+    s.dJ = INFINITY;
+    s.zero_cnt = 0;
+  }
+}
+
+template <class M>
+__device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, TrajState& s,
+                                 double J, bool copied, double grad, int mode) {
+  (void)copied;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  const tog_options& o = P->o;
+  if (!inner_bookkeeping(P, s, J, grad, mode)) return;
   const double* X = Bf.X + (size_t)b * N * n;
   const double* U = Bf.U + (size_t)b * (N - 1) * m;
   double* C = Bf.C + (size_t)b * N * pmax;
@@ -1452,26 +1503,10 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
       mumax = fmax(mumax, mu[q]);
     }
   }
-  s.mu_max = mumax;
-  s.c_max = traj_max_violation(P, Bf, b);
-  const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (s.c_max < o.constraint_tolerance);
-  if (conv) {
-    s.flags |= TOG_TRAJ_AL_CONVERGED;
-    s.active = 0;
-  } else if (s.al_iter >= o.al_iterations) {
-    s.flags |= TOG_TRAJ_AL_MAX_ITERS;
-    s.active = 0;
-  } else {
-    // next outer iteration: reset!(solver_uncon), set_tolerances!, solve! init (rollout is a no-op)
-    s.al_iter++;
-    set_tolerances(P, s, mode);
-    s.rho = 0.0;
-    s.drho = 0.0;
-    s.J = traj_cost<M>(P, Bf, b, X, U, true, C);
-    s.iters = 1;
-    s.dJ = INFINITY;
-    s.zero_cnt = 0;
-  }
+  const double c_max = traj_max_violation(P, Bf, b);
+  const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (c_max < o.constraint_tolerance);
+  const double Jnext = (conv || s.al_iter >= o.al_iterations) ? 0.0 : traj_cost<M>(P, Bf, b, X, U, true, C);
+  al_outer_finish(P, s, mumax, c_max, Jnext, mode);
 }
 
 // Does the sequential acceptance logic of forwardpass! (forward_pass.jl:19-65) settle within the
@@ -1496,7 +1531,7 @@ __device__ __forceinline__ bool ls_decided_within(const tog_options& o, const De
 // k_ls_compact (list != nullptr, length *count) — the earlier trials did not settle them. Lanes past
 // the list's end exit at once, so whole waves retire (the step-level path passes its J_prev through
 // Jprev_in).
-template <class M, int INTEG>
+template <class M, int INTEG, bool CAND>
 __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
                                                  int cnt, const int* __restrict__ list, const int* __restrict__ count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1513,7 +1548,14 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
   const TrajState& st = Bf.st[b];
   if (!st.active) return;
   double Jj = INFINITY;
-  const bool ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
+  bool ok;
+  if constexpr (CAND) {  // every trial keeps its rollout: the accepted one is copied, not replayed
+    double* cw = static_cast<double*>(
+        __builtin_assume_aligned(Bf.cand + ((size_t)b * NC + j) * (size_t)P->N * cand_w<M>(), 16));
+    ok = rollout_cost<M, INTEG, 3>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw);
+  } else {
+    ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
+  }
   Bf.lsJ[b * NC + j] = Jj;
   Bf.lsok[b * NC + j] = ok ? 1 : 0;
 }
@@ -1644,6 +1686,274 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
       step_bookkeeping<M>(P, Bf, b, s, J, copied, grad, mode);
     }
   }
+  Bf.st[b] = s;
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Candidate-copy line search (DevBuffers::cand != nullptr). The speculative trials keep their
+// rollouts (k_ls_spec<CAND>), so the accepted trajectory is copied instead of replayed:
+//   k_ls_decide  forwardpass!'s sequential acceptance loop over the stored trials (forward_pass.jl:
+//                19-65), one lane per trajectory; the ones trials [0, hi) do not settle are listed
+//                for the next round;
+//   k_ls_apply   winner's X̄, Ū -> X, U (or X̄, Ū at step level), one lane per element, plus the
+//                per-knot todorov gradient terms (ilqr_methods.jl:122-129);
+//   k_ls_book    J, flags, gradient sum and solve! / AL bookkeeping (ilqr_methods.jl:21-42,
+//                augmented_lagrangian_methods.jl:53-126), one lane per trajectory.
+// Decisions, trajectories and sums are those of k_ls_commit bit for bit: the copy holds exactly the
+// values its replay recomputes, and the gradient terms are summed in the replay's knot order.
+// ls_win: accepted trial j >= 0; -2: max line-search iterations (X̄ = X fallback); -3: accepted with
+// no evaluated trial (J_prev NaN), replayed at α = 0 by k_ls_book.
+template <class M>
+__global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict__ P, DevBuffers Bf, int hi,
+                                                   int bookkeeping, const double* __restrict__ Jprev_in,
+                                                   const int* __restrict__ in_list, const int* __restrict__ in_count,
+                                                   int* __restrict__ out_list, int* __restrict__ out_count) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nb = in_list ? (long long)*in_count : P->B;
+  bool und = false;
+  long long b = 0;
+  if (t < nb) {
+    b = in_list ? (long long)in_list[t] : t;
+    TrajState* st = Bf.st + b;
+    if (st->active) {
+      const tog_options& o = P->o;
+      const int NC = Bf.nc;
+      const double J_prev = bookkeeping ? st->J : Jprev_in[b];
+      const double dV0 = st->dV0, dV1 = st->dV1;
+      double J = INFINITY, z = -1.0, expected = 0.0, alpha_last = 0.0;
+      int trials = 0, state = 0, win = -1;
+      for (int jj = 0;; jj++) {
+        if (!((z <= o.line_search_lower_bound || z > o.line_search_upper_bound) && J >= J_prev)) {
+          state = 1;
+          break;
+        }
+        if (jj > o.iterations_linesearch) {
+          state = 2;
+          break;
+        }
+        if (jj >= hi) break;  // not settled by the trials evaluated so far
+        trials++;
+        if (!Bf.lsok[b * NC + jj]) continue;
+        const double aj = ldexp(1.0, -jj);
+        J = Bf.lsJ[b * NC + jj];
+        expected = -aj * (dV0 + aj * dV1);
+        z = (expected > 0.0) ? (J_prev - J) / expected : -1.0;
+        alpha_last = aj;
+        win = jj;
+      }
+      if (state == 0) {
+        und = true;
+      } else {
+        if (state == 2) {  // forward_pass.jl:22-37: z = expected = α = 0, J from cost(X) in k_ls_book
+          win = -2;
+          z = 0.0;
+          expected = 0.0;
+          alpha_last = 0.0;
+        } else if (win < 0) {
+          win = -3;
+        }
+        st->alpha = alpha_last;
+        st->z = z;
+        st->expected = expected;
+        st->ls_trials = trials;
+        Bf.ls_win[b] = win;
+        Bf.ls_Jw[b] = J;
+      }
+    }
+  }
+  if (!out_list) return;
+  const unsigned long long mask = __ballot(und);
+  if (mask == 0) return;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int leader = __ffsll((long long)mask) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(out_count, __popcll(mask));
+  base = __shfl(base, leader);
+  if (und) out_list[base + __popcll(mask & ((1ull << lane) - 1))] = (int)b;
+}
+
+template <class M>
+__global__ void __launch_bounds__(256) k_ls_apply(const DevProblem* __restrict__ P, DevBuffers Bf, int bookkeeping) {
+  constexpr int n = M::n, m = M::m, CW = cand_w<M>();
+  const int N = P->N;
+  const long long per = (long long)N * CW;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P->B * per) return;
+  const long long b = t / per;
+  const int e = (int)(t - b * per);
+  if (!Bf.st[b].active) return;
+  const int w = Bf.ls_win[b];
+  if (w < 0) return;
+  if (bookkeeping && Bf.ls_Jw[b] > P->o.max_cost_value) return;  // ilqr_methods.jl:25-28: X̄ not copied
+  const int k = e / CW, c = e - k * CW;
+  const double* src = Bf.cand + ((size_t)b * Bf.nc + w) * (size_t)per;
+  if (c >= m && c < m + n) {
+    double* Xd = (bookkeeping ? Bf.X : Bf.Xb) + ((size_t)b * N + k) * n;
+    Xd[c - m] = (k == 0) ? Bf.x0[(size_t)b * n + c - m] : src[e];
+  } else if (c < m && k < N - 1) {
+    double* Ud = (bookkeeping ? Bf.U : Bf.Ub) + ((size_t)b * (N - 1) + k) * m;
+    Ud[c] = src[e];
+    if (bookkeeping && c == 0) {  // max_i |d_i| / (|ū_i| + 1) of knot k (rollout_cost WMODE 2)
+      const double* dk = Bf.d + ((size_t)b * (N - 1) + k) * m;
+      double mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        const double v = fabs(dk[i]) / (fabs(src[(size_t)k * CW + i]) + 1.0);
+        if (v > mx || isnan(v)) mx = v;
+      }
+      Bf.gk[(size_t)b * N + k] = mx;
+    }
+  }
+}
+
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+                                                int bookkeeping, const double* Jprev_in, double* Jout) {
+  extern __shared__ double book_lds[];
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const RowTables RT =
+      (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, book_lds) : global_row_tables(P);
+  if (t >= P->B) return;
+  const long long b = t;
+  if (!Bf.st[b].active) return;
+  constexpr int n = M::n, m = M::m;
+  const tog_options& o = P->o;
+  const bool al = (mode == TOG_MODE_AL);
+  const int N = P->N;
+  TrajState s = Bf.st[b];
+  const int win = Bf.ls_win[b];
+  double J = Bf.ls_Jw[b];
+  const double J_prev = bookkeeping ? s.J : Jprev_in[b];
+  double grad = 0.0;
+  bool copied = false;
+  if (win == -2) {  // max line-search iterations (forward_pass.jl:22-37), as k_ls_commit
+    const double* X = Bf.X + (size_t)b * N * n;
+    const double* U = Bf.U + (size_t)b * (N - 1) * m;
+    if (!bookkeeping) {
+      double* Xb = Bf.Xb + (size_t)b * N * n;
+      double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
+      for (int i = 0; i < N * n; i++) Xb[i] = X[i];
+      for (int i = 0; i < (N - 1) * m; i++) Ub[i] = U[i];
+    }
+    J = traj_cost<M>(P, Bf, b, X, U, al, al ? Bf.C + (size_t)b * N * P->pmax : nullptr);
+    reg_increase(P, s);
+    s.rho += o.bp_reg_fp;
+    grad = traj_gradient<M>(P, Bf, b);
+    copied = true;
+  } else if (win == -3) {
+    double Jw;
+    if (!bookkeeping) {
+      rollout_cost<M, INTEG, 1>(P, Bf, b, s.alpha, al, Jw, nullptr, RT);
+    } else if (!(J > o.max_cost_value)) {
+      rollout_cost<M, INTEG, 2>(P, Bf, b, s.alpha, al, Jw, &grad, RT);
+      copied = true;
+    }
+  } else if (bookkeeping && !(J > o.max_cost_value)) {
+    const double* g = Bf.gk + (size_t)b * N;
+    double gsum = 0.0;
+    for (int k = 0; k < N - 1; k++) gsum += g[k];
+    grad = gsum / N;
+    copied = true;
+  }
+  if (J > J_prev) s.flags |= TOG_TRAJ_COST_INCREASED;
+  if (Jout) Jout[b] = J;
+  (void)copied;
+  if (bookkeeping) {
+    if (s.flags & TOG_TRAJ_COST_INCREASED) {
+      s.active = 0;  // reference: error("Cost increased during Forward Pass")
+    } else if (inner_bookkeeping(P, s, J, grad, mode)) {
+      // the AL outer update runs wave-parallel over the knots in k_al_outer
+      Bf.ls_list[P->B + atomicAdd(Bf.ls_count + 1, 1)] = (int)b;
+    }
+  }
+  Bf.st[b] = s;
+}
+
+// AL outer update (augmented_lagrangian_methods.jl:53-126) of the trajectories k_ls_book listed, one
+// wave per trajectory, lanes over knots. Per knot: C (update_constraints!, the side effect of
+// cost(prob)), dual_update! and penalty_update! of its rows, the max_violation and μ_max partials,
+// and the knot's stage cost and AL terms at the updated multipliers (the next outer iteration's J).
+// The knot terms are summed by lane 0 in traj_cost's order, so J is bit-identical to the serial
+// update's; the maxima are order-independent (NaN-propagating max).
+template <class M>
+__global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+                                                 const int* __restrict__ list, const int* __restrict__ count) {
+  if ((int)blockIdx.x >= *count) return;
+  extern __shared__ double alo_lds[];
+  constexpr int n = M::n, m = M::m;
+  constexpr bool SL = ModelTraits<M>::slack > 0;
+  const int N = P->N, pmax = P->pmax;
+  const tog_options& o = P->o;
+  const long long b = list[blockIdx.x];
+  const int lane = threadIdx.x;
+  double* sk = alo_lds;       // [N] stage / terminal cost of knot k
+  double* ak = alo_lds + N;   // [N] λ'c + ½c'Iμc of knot k (NaN-free flag in hk)
+  int* hk = reinterpret_cast<int*>(alo_lds + 2 * N);  // [N] knot has rows
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  double* C = Bf.C + (size_t)b * N * pmax;
+  double* lam = Bf.lam + (size_t)b * N * pmax;
+  double* mu = Bf.mu + (size_t)b * N * pmax;
+  double mumax = 0.0, cmax = 0.0;
+  for (int k = lane; k < N; k += WAVE) {
+    const double* x = X + (size_t)k * n;
+    const double* u = (k < N - 1) ? U + (size_t)k * m : nullptr;
+    sk[k] = (k < N - 1) ? stage_cost<n, m>(P, x, u) : terminal_cost<n>(P, x);
+    const int cnt = P->knot_cnt[k];
+    const ConRow* rows = P->rows + P->knot_off[k];
+    double lc = 0.0, cIc = 0.0, e = 0.0, im = -INFINITY;
+    int ni = 0;
+    for (int i = 0; i < cnt; i++) {
+      const size_t q = (size_t)k * pmax + i;
+      const ConRow r = rows[i];
+      const double c = row_value<SL>(r, x, u);
+      C[q] = c;
+      const bool ineq = row_inequality<SL>(r);
+      double l = lam[q] + mu[q] * c;  // dual_update! (:107-118)
+      l = tog_jlmax(o.dual_min, tog_jlmin(o.dual_max, l));
+      if (ineq) l = tog_jlmax(0.0, l);
+      const double mn = fmax(0.0, fmin(o.penalty_max, o.penalty_scaling * mu[q]));  // penalty_update! (:121-126)
+      lam[q] = l;
+      mu[q] = mn;
+      mumax = fmax(mumax, mn);
+      if (ineq) {  // max_violation (:171-184)
+        ni++;
+        im = tog_jlmax(im, c);
+      } else {
+        e = tog_jlmax(e, fabs(c));
+      }
+      const bool a = ineq ? ((c >= 0.0) || (l > 0.0)) : true;  // active set at the new multipliers
+      const double w = a ? mn : 0.0;
+      lc = fma(l, c, lc);
+      cIc = fma(c * w, c, cIc);
+    }
+    if (cnt) {
+      cmax = tog_jlmax(e, cmax);
+      if (ni > 0) cmax = tog_jlmax(tog_jlmax(0.0, im), cmax);
+    }
+    ak[k] = lc + 0.5 * cIc;
+    hk[k] = cnt;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    mumax = fmax(mumax, __shfl_xor(mumax, off));
+    cmax = tog_jlmax(cmax, __shfl_xor(cmax, off));
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  TrajState s = Bf.st[b];
+  const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (cmax < o.constraint_tolerance);
+  double Jnext = 0.0;
+  if (!conv && s.al_iter < o.al_iterations) {  // traj_cost's order: stage terms, terminal, then AL terms
+    double J = 0.0, Jc = 0.0;
+    for (int k = 0; k < N - 1; k++) J += sk[k];
+    J += sk[N - 1];
+    for (int k = 0; k < N; k++)
+      if (hk[k]) Jc += ak[k];
+    Jnext = J + Jc;
+  }
+  al_outer_finish(P, s, mumax, cmax, Jnext, mode);
   Bf.st[b] = s;
 }
 
@@ -1977,8 +2287,41 @@ struct ModelLaunch {
   static void spec(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int lo, int cnt, const int* list,
                    const int* count, hipStream_t st) {
     const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
-    hipLaunchKernelGGL((k_ls_spec<M, INTEG>), dim3(gs), dim3(256), (unsigned)Bf.rows_shmem, st, P, Bf, mode, lo, cnt,
-                       list, count);
+    if (Bf.cand)
+      hipLaunchKernelGGL((k_ls_spec<M, INTEG, true>), dim3(gs), dim3(256), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
+                         lo, cnt, list, count);
+    else
+      hipLaunchKernelGGL((k_ls_spec<M, INTEG, false>), dim3(gs), dim3(256), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
+                         lo, cnt, list, count);
+  }
+  // candidate-copy line search: one or two speculative rounds, each followed by its decisions, then the
+  // copy of the accepted rollouts and the bookkeeping (no replay rollout on the critical path)
+  template <int INTEG>
+  static void forward_cand(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
+                           double* Jo, hipStream_t st) {
+    const int F = Bf.ls_first;
+    (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_MAX_ROUNDS, st);
+    if (F >= Bf.nc) {
+      spec<INTEG>(P, Bf, B, mode, 0, Bf.nc, nullptr, nullptr, st);
+      hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, Bf.nc, bk, Jp, nullptr,
+                         nullptr, nullptr, nullptr);
+    } else {
+      spec<INTEG>(P, Bf, B, mode, 0, F, nullptr, nullptr, st);
+      hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, F, bk, Jp, nullptr, nullptr,
+                         Bf.ls_list, Bf.ls_count);
+      spec<INTEG>(P, Bf, B, mode, F, Bf.nc - F, Bf.ls_list, Bf.ls_count, st);
+      hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, Bf.nc, bk, Jp, Bf.ls_list,
+                         Bf.ls_count, nullptr, nullptr);
+    }
+    const long long tot = B * (long long)Bf.nknots * cand_w<M>();
+    hipLaunchKernelGGL((k_ls_apply<M>), dim3(grid(tot, 256)), dim3(256), 0, st, P, Bf, bk);
+    hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
+                       bk, Jp, Jo);
+    if (bk && mode == TOG_MODE_AL) {
+      const unsigned sm = (unsigned)(Bf.nknots * (2 * sizeof(double) + sizeof(int)));
+      hipLaunchKernelGGL((k_al_outer<M>), dim3((unsigned)B), dim3(64), sm, st, P, Bf, mode, Bf.ls_list + B,
+                         Bf.ls_count + 1);
+    }
   }
   template <int INTEG>
   static void commit(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
@@ -1989,6 +2332,10 @@ struct ModelLaunch {
   template <int INTEG>
   static void forward_i(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
                         double* Jo, hipStream_t st, const StreamPair* sp) {
+    if (Bf.cand) {
+      forward_cand<INTEG>(P, Bf, B, mode, bk, Jp, Jo, st);
+      return;
+    }
     // speculative line search in two rounds: trials [0, 8) for every trajectory (settles ~98% of them
     // on configs 2, 3 and 5), then [8, nc) only for the trajectories the first round left undecided
     // (k_ls_compact lists them, so the second round's waves are dense). Narrower first rounds were

@@ -49,6 +49,7 @@ struct tog_handle {
   bool own_stream = false;
   int model = 0, integ = 0, n = 0, m = 0, N = 0, pmax = 0, nrows = 0, nq = 0;
   long long B = 0;
+  double last_active = -1.0;  // n_active of the last host stats readback (-1: none yet)
   int mode = TOG_MODE_ILQR;
   tog_options opts;
   DevProblem hostP;
@@ -516,6 +517,20 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   b.sdbg = nullptr;
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
   if (b.nc < 1) b.nc = 1;
+  b.nknots = N;
+  b.ls_first = LS_FIRST;
+  b.cand = nullptr;
+  // candidate-copy line search when every trial fits the speculative window (TOG_LS=replay: the
+  // replaying k_ls_commit path, for A/B checks)
+  {
+    const char* ev = getenv("TOG_LS");
+    const bool replay = ev && strcmp(ev, "replay") == 0;
+    if (!replay && opts->iterations_linesearch + 1 <= 64) {
+      if ((rc = dalloc(h, &b.cand, B * (size_t)b.nc * N * ((n + m + 1) & ~1))) || (rc = dalloc(h, &b.ls_win, B)) ||
+          (rc = dalloc(h, &b.ls_Jw, B)) || (rc = dalloc(h, &b.gk, B * N)))
+        return rc;
+    }
+  }
   // reference constructor state: X = NaN, U = 0, K = d = 0, λ = 0, μ = opts.penalty_initial,
   // ρ = dρ = 0 (ilqr_solver.jl:118-144, augmented_lagrangian_solver.jl:143-169)
   fill(h, b.x0, B * n, 0.0);
@@ -937,6 +952,7 @@ int32_t tog_solve_init(tog_handle* h, int32_t mode) {
   if (mode != TOG_MODE_ILQR && mode != TOG_MODE_AL) return fail(TOG_ERR_ARG, "mode");
   HIPCHECK(hipSetDevice(h->device));
   h->mode = mode;
+  h->last_active = -1.0;
   h->ops->init(h->dP, h->buf, h->B, h->integ, mode, h->stream);
   HIPCHECK(hipGetLastError());
   return TOG_OK;
@@ -947,6 +963,9 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t) { return tog_solve_step(p, nsteps); });
   HIPCHECK(hipSetDevice(h->device));
   const int al = (h->mode == TOG_MODE_AL);
+  // few active trajectories (the convergence tail): every trial in one speculative round, so the
+  // forward pass is a single rollout chain
+  h->buf.ls_first = (h->last_active >= 0.0 && h->last_active * h->buf.nc <= 65536.0) ? h->buf.nc : LS_FIRST;
   for (int i = 0; i < nsteps; i++) {
     timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
     timed(h, TOG_KERNEL_BACKWARD,
@@ -984,6 +1003,7 @@ int32_t tog_batch_stats(tog_handle* h, double* out3) {
       HIPCHECK(hipSetDevice(p->device));
       HIPCHECK(hipMemcpyAsync(v, p->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, p->stream));
       HIPCHECK(hipStreamSynchronize(p->stream));
+      p->last_active = v[0];
       out3[0] += v[0];
       out3[1] += v[1];
       out3[2] = tog_jlmax(out3[2], v[2]);
@@ -994,6 +1014,7 @@ int32_t tog_batch_stats(tog_handle* h, double* out3) {
   if (rc) return rc;
   HIPCHECK(hipMemcpyAsync(out3, h->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, h->stream));
   HIPCHECK(hipStreamSynchronize(h->stream));
+  h->last_active = out3[0];
   return TOG_OK;
 }
 
