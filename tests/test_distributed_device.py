@@ -60,10 +60,13 @@ def _rccl_world1(port, q):
         red_host = red.cpu().numpy().copy()  # waits on the stream
         out.append((red_host.tolist(), h.batch_stats().tolist()))
     steps = h.total_steps()
-    # the same steps without the collective, on the handle's own stream
+    # the same steps without the collective, on the handle's own stream (with the same host stats
+    # readbacks: the line-search round schedule follows the last n_active read on the host)
     s2 = tog.AbstractSolverFor(prob, opts, device=0)
     s2.handle.solve_init(tog.abi.MODE_AL)
-    s2.handle.solve_step(6)
+    for _ in range(6):
+        s2.handle.solve_step(1)
+        s2.handle.batch_stats()
     q.put((out, steps, s2.handle.total_steps(), s2.handle.batch_stats().tolist()))
     dist.destroy_process_group()
 

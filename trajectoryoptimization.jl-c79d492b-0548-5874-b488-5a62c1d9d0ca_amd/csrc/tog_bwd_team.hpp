@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     }
     __syncthreads();
   }
-  const bool live = (b < P->B) && Bf.st[b].active;
+  const bool live = (b < P->B) && Bf.st[b].active && !Bf.st[b].ls_pend;
   const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
   const bool state_reg = (P->o.bp_reg_type == 1);
   const double dt = P->dt;

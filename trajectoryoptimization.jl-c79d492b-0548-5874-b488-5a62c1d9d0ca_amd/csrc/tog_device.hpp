@@ -72,6 +72,9 @@ struct TrajState {
   double c_max, mu_max;
   double cost_tol, grad_tol; // current inner tolerances (set_tolerances!, :39-50)
   int iters, zero_cnt, al_iter, total_steps, ls_trials, bp_restarts, flags, active;
+  // line search carried over to the next batch step (k_ls_decide, pending mode): the trials [0, ls_pend)
+  // are evaluated and stored; the trajectory skips that step's Jacobians and backward pass
+  int ls_pend, pad_;
 };
 
 // the regularisation scalars the backward pass mutates (kept in registers)
@@ -107,6 +110,7 @@ struct DevBuffers {
   int rows_shmem;     // LDS bytes of a block's copy of the row tables (rollout kernels)
   int ls_first;       // width of the first speculative round (>= nc: one round)
   int nknots;         // N (host-side launch geometry)
+  int ls_pend_ok;     // solve steps may carry an undecided line search over to the next step
   double* cand;       // (n+m, N, NC, B) every trial's rollout (candidate-copy line search), or null
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost

@@ -345,7 +345,7 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   const long long bk = t / NCH;
   const int k = (int)(bk % (N - 1));
   const long long b = bk / (N - 1);
-  if (!Bf.st[b].active) return;
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
   Dual<W> xd[n], ud[mb], xn[n];
@@ -762,7 +762,7 @@ __global__ void __launch_bounds__(64) k_backward(const DevProblem* __restrict__ 
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
   const int N = P->N;
-  if (!Bf.st[b].active) return;
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
   RegState s;
   s.rho = Bf.st[b].rho;
   s.drho = Bf.st[b].drho;
@@ -1544,9 +1544,9 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
   if (t >= nb * cnt) return;
   const long long i = t / cnt;
   const long long b = list ? (long long)list[i] : i;
-  const int j = lo + (int)(t % cnt);
   const TrajState& st = Bf.st[b];
-  if (!st.active) return;
+  const int j = lo + st.ls_pend + (int)(t % cnt);  // a pending line search continues after its stored trials
+  if (!st.active || j >= NC) return;
   double Jj = INFINITY;
   bool ok;
   if constexpr (CAND) {  // every trial keeps its rollout: the accepted one is copied, not replayed
@@ -1708,7 +1708,7 @@ template <class M>
 __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict__ P, DevBuffers Bf, int hi,
                                                    int bookkeeping, const double* __restrict__ Jprev_in,
                                                    const int* __restrict__ in_list, const int* __restrict__ in_count,
-                                                   int* __restrict__ out_list, int* __restrict__ out_count) {
+                                                   int* __restrict__ out_list, int* __restrict__ out_count, int pend) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nb = in_list ? (long long)*in_count : P->B;
   bool und = false;
@@ -1721,6 +1721,7 @@ __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict_
       const int NC = Bf.nc;
       const double J_prev = bookkeeping ? st->J : Jprev_in[b];
       const double dV0 = st->dV0, dV1 = st->dV1;
+      if (pend) hi = (st->ls_pend + hi < NC) ? st->ls_pend + hi : NC;  // trials stored so far
       double J = INFINITY, z = -1.0, expected = 0.0, alpha_last = 0.0;
       int trials = 0, state = 0, win = -1;
       for (int jj = 0;; jj++) {
@@ -1744,7 +1745,12 @@ __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict_
       }
       if (state == 0) {
         und = true;
+        if (pend) {  // continue in the next batch step (no Jacobians / backward pass for it meanwhile)
+          st->ls_pend = hi;
+          Bf.ls_win[b] = -9;
+        }
       } else {
+        st->ls_pend = 0;
         if (state == 2) {  // forward_pass.jl:22-37: z = expected = α = 0, J from cost(X) in k_ls_book
           win = -2;
           z = 0.0;
@@ -1762,7 +1768,7 @@ __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict_
       }
     }
   }
-  if (!out_list) return;
+  if (!out_list || pend) return;
   const unsigned long long mask = __ballot(und);
   if (mask == 0) return;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1821,8 +1827,9 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
   const tog_options& o = P->o;
   const bool al = (mode == TOG_MODE_AL);
   const int N = P->N;
-  TrajState s = Bf.st[b];
   const int win = Bf.ls_win[b];
+  if (win == -9) return;  // line search still pending
+  TrajState s = Bf.st[b];
   double J = Bf.ls_Jw[b];
   const double J_prev = bookkeeping ? s.J : Jprev_in[b];
   double grad = 0.0;
@@ -2304,14 +2311,20 @@ struct ModelLaunch {
     if (F >= Bf.nc) {
       spec<INTEG>(P, Bf, B, mode, 0, Bf.nc, nullptr, nullptr, st);
       hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, Bf.nc, bk, Jp, nullptr,
-                         nullptr, nullptr, nullptr);
+                         nullptr, nullptr, nullptr, 0);
+    } else if (bk && Bf.ls_pend_ok) {
+      // pending mode: one round per batch step; a trajectory the round leaves undecided continues its
+      // line search in the next step's round, so no step waits on a second serial rollout chain
+      spec<INTEG>(P, Bf, B, mode, 0, F, nullptr, nullptr, st);
+      hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, F, bk, Jp, nullptr, nullptr,
+                         nullptr, nullptr, 1);
     } else {
       spec<INTEG>(P, Bf, B, mode, 0, F, nullptr, nullptr, st);
       hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, F, bk, Jp, nullptr, nullptr,
-                         Bf.ls_list, Bf.ls_count);
+                         Bf.ls_list, Bf.ls_count, 0);
       spec<INTEG>(P, Bf, B, mode, F, Bf.nc - F, Bf.ls_list, Bf.ls_count, st);
       hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, Bf.nc, bk, Jp, Bf.ls_list,
-                         Bf.ls_count, nullptr, nullptr);
+                         Bf.ls_count, nullptr, nullptr, 0);
     }
     const long long tot = B * (long long)Bf.nknots * cand_w<M>();
     hipLaunchKernelGGL((k_ls_apply<M>), dim3(grid(tot, 256)), dim3(256), 0, st, P, Bf, bk);

@@ -518,6 +518,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
   if (b.nc < 1) b.nc = 1;
   b.nknots = N;
+  b.ls_pend_ok = getenv("TOG_LS_NOPEND") ? 0 : 1;
   b.ls_first = LS_FIRST;
   b.cand = nullptr;
   // candidate-copy line search when every trial fits the speculative window (TOG_LS=replay: the
@@ -963,9 +964,12 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t) { return tog_solve_step(p, nsteps); });
   HIPCHECK(hipSetDevice(h->device));
   const int al = (h->mode == TOG_MODE_AL);
-  // few active trajectories (the convergence tail): every trial in one speculative round, so the
-  // forward pass is a single rollout chain
-  h->buf.ls_first = (h->last_active >= 0.0 && h->last_active * h->buf.nc <= 65536.0) ? h->buf.nc : LS_FIRST;
+  // few trajectories (a small batch, or the convergence tail as of the last host readback of n_active):
+  // every trial in one speculative round, so the forward pass is one rollout chain and every step
+  // completes an iteration of every active trajectory. Otherwise rounds of LS_FIRST trials, an
+  // undecided line search continuing in the next step (pending mode).
+  const double few = 65536.0 / h->buf.nc;
+  h->buf.ls_first = ((double)h->B <= few || (h->last_active >= 0.0 && h->last_active <= few)) ? h->buf.nc : LS_FIRST;
   for (int i = 0; i < nsteps; i++) {
     timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
     timed(h, TOG_KERNEL_BACKWARD,
