@@ -111,7 +111,9 @@ struct DevBuffers {
   int ls_first;       // width of the first speculative round (>= nc: one round)
   int nknots;         // N (host-side launch geometry)
   int ls_pend_ok;     // solve steps may carry an undecided line search over to the next step
-  double* cand;       // (n+m, N, NC, B) every trial's rollout (candidate-copy line search), or null
+  double* cand;       // (NCP, n+m, N, B) every trial's rollout (candidate-copy line search), or null
+  int ncp;            // candidate slots per element (nc rounded up to 8)
+  int pad3_;
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū

@@ -30,11 +30,21 @@ constexpr int WAVE = 64;
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroups: s_barrier is ~free
 
-// candidate slot layout of the line search (k_ls_spec<CAND>): per knot [ū_k (m) | x̄_k (n)], padded to an
-// even width so that every knot starts 16-byte aligned (wide stores)
+// candidate layout of the line search (k_ls_spec<CAND>): per knot the elements c of [ū_k (m) | x̄_k (n)]
+// in quads q = c / 4; element (k, c) of trial j of trajectory b at
+//   (((b N + k) Q + q) NCP + j) 4 + c % 4,      Q = ceil((n + m) / 4), NCP = nc rounded up to 8.
+// A round's lanes for one trajectory's trials are adjacent: each trial stores 32-byte quads and the 8
+// trials of a round fill 256 contiguous bytes, while k_ls_apply reads the winner's quads 32 bytes at a time.
 template <class M>
 __host__ __device__ constexpr int cand_w() {
-  return (M::n + M::m + 1) & ~1;
+  return M::n + M::m;
+}
+template <class M>
+__host__ __device__ constexpr int cand_q() {
+  return (M::n + M::m + 3) / 4;
+}
+__device__ __forceinline__ size_t cand_at(int k, int c, int Q, int ncp) {
+  return ((size_t)(k * Q + (c >> 2)) * ncp) * 4 + (c & 3);
 }
 template <class M>
 __host__ __device__ constexpr int nq_of() {
@@ -1261,7 +1271,7 @@ __device__ __forceinline__ RowTables block_row_tables(const DevProblem* P, void*
 template <class M, int INTEG, int WMODE>
 __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha,
                              bool al, double& Jout, double* grad_out, const RowTables& RT,
-                             double* __restrict__ cw = nullptr) {
+                             double* __restrict__ cw = nullptr, int ncp = 0) {
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
   double* X = Bf.X + (size_t)b * N * n;
@@ -1335,7 +1345,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (WMODE == 3) {
 #pragma unroll
-      for (int i = 0; i < m; i++) cw[(size_t)(k - 1) * cand_w<M>() + i] = ub[i];
+      for (int i = 0; i < m; i++) cw[cand_at(k - 1, i, cand_q<M>(), ncp)] = ub[i];
     }
     if (WMODE == 2) {
       double mx = -INFINITY;
@@ -1393,7 +1403,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (WMODE == 3) {
 #pragma unroll
-      for (int i = 0; i < n; i++) cw[(size_t)k * cand_w<M>() + m + i] = xn[i];
+      for (int i = 0; i < n; i++) cw[cand_at(k, m + i, cand_q<M>(), ncp)] = xn[i];
     }
     if (!ok) return false;
   }
@@ -1551,8 +1561,8 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
   bool ok;
   if constexpr (CAND) {  // every trial keeps its rollout: the accepted one is copied, not replayed
     double* cw = static_cast<double*>(
-        __builtin_assume_aligned(Bf.cand + ((size_t)b * NC + j) * (size_t)P->N * cand_w<M>(), 16));
-    ok = rollout_cost<M, INTEG, 3>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw);
+        __builtin_assume_aligned(Bf.cand + ((size_t)b * P->N * cand_q<M>() * Bf.ncp + j) * 4, 32));
+    ok = rollout_cost<M, INTEG, 3>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw, Bf.ncp);
   } else {
     ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
   }
@@ -1781,35 +1791,46 @@ __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict_
 
 template <class M>
 __global__ void __launch_bounds__(256) k_ls_apply(const DevProblem* __restrict__ P, DevBuffers Bf, int bookkeeping) {
-  constexpr int n = M::n, m = M::m, CW = cand_w<M>();
+  // one lane per (trajectory, knot, quad): reads the winner's 32-byte quad, writes its X / U elements
+  constexpr int n = M::n, m = M::m, Q = cand_q<M>();
   const int N = P->N;
-  const long long per = (long long)N * CW;
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= P->B * per) return;
-  const long long b = t / per;
-  const int e = (int)(t - b * per);
+  const unsigned per = (unsigned)N * Q;
+  const unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (unsigned long long)P->B * per) return;
+  const long long b = (long long)(t / per);
+  const unsigned r = (unsigned)(t - (unsigned long long)b * per);
+  const int k = (int)(r / Q), q = (int)(r - (unsigned)k * Q);
   if (!Bf.st[b].active) return;
   const int w = Bf.ls_win[b];
   if (w < 0) return;
   if (bookkeeping && Bf.ls_Jw[b] > P->o.max_cost_value) return;  // ilqr_methods.jl:25-28: X̄ not copied
-  const int k = e / CW, c = e - k * CW;
-  const double* src = Bf.cand + ((size_t)b * Bf.nc + w) * (size_t)per;
-  if (c >= m && c < m + n) {
-    double* Xd = (bookkeeping ? Bf.X : Bf.Xb) + ((size_t)b * N + k) * n;
-    Xd[c - m] = (k == 0) ? Bf.x0[(size_t)b * n + c - m] : src[e];
-  } else if (c < m && k < N - 1) {
-    double* Ud = (bookkeeping ? Bf.U : Bf.Ub) + ((size_t)b * (N - 1) + k) * m;
-    Ud[c] = src[e];
-    if (bookkeeping && c == 0) {  // max_i |d_i| / (|ū_i| + 1) of knot k (rollout_cost WMODE 2)
-      const double* dk = Bf.d + ((size_t)b * (N - 1) + k) * m;
-      double mx = -INFINITY;
+  const int ncp = Bf.ncp;
+  const double* tb = Bf.cand + (size_t)b * per * ncp * 4;  // trajectory b's candidates
+  const double* src = tb + ((size_t)r * ncp + w) * 4;      // quad q of knot k of trial w
+  double v[4];
 #pragma unroll
-      for (int i = 0; i < m; i++) {
-        const double v = fabs(dk[i]) / (fabs(src[(size_t)k * CW + i]) + 1.0);
-        if (v > mx || isnan(v)) mx = v;
-      }
-      Bf.gk[(size_t)b * N + k] = mx;
+  for (int e = 0; e < 4; e++) v[e] = src[e];
+  double* Xd = (bookkeeping ? Bf.X : Bf.Xb) + ((size_t)b * N + k) * n;
+  double* Ud = (bookkeeping ? Bf.U : Bf.Ub) + ((size_t)b * (N - 1) + k) * m;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int c = 4 * q + e;
+    if (c < m) {
+      if (k < N - 1) Ud[c] = v[e];
+    } else if (c < m + n) {
+      Xd[c - m] = (k == 0) ? Bf.x0[(size_t)b * n + c - m] : v[e];
     }
+  }
+  if (bookkeeping && q == 0 && k < N - 1) {  // max_i |d_i| / (|ū_i| + 1) of knot k (rollout_cost WMODE 2)
+    const double* dk = Bf.d + ((size_t)b * (N - 1) + k) * m;
+    double mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      const double ui = (i < 4) ? v[i] : tb[cand_at(k, i, Q, ncp) + (size_t)w * 4];
+      const double vv = fabs(dk[i]) / (fabs(ui) + 1.0);
+      if (vv > mx || isnan(vv)) mx = vv;
+    }
+    Bf.gk[(size_t)b * N + k] = mx;
   }
 }
 
@@ -2326,7 +2347,7 @@ struct ModelLaunch {
       hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, Bf.nc, bk, Jp, Bf.ls_list,
                          Bf.ls_count, nullptr, nullptr, 0);
     }
-    const long long tot = B * (long long)Bf.nknots * cand_w<M>();
+    const long long tot = B * (long long)Bf.nknots * cand_q<M>();
     hipLaunchKernelGGL((k_ls_apply<M>), dim3(grid(tot, 256)), dim3(256), 0, st, P, Bf, bk);
     hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
                        bk, Jp, Jo);

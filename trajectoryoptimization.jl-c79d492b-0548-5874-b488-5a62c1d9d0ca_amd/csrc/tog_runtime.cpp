@@ -518,6 +518,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
   if (b.nc < 1) b.nc = 1;
   b.nknots = N;
+  b.ncp = (b.nc + 7) & ~7;
   b.ls_pend_ok = getenv("TOG_LS_NOPEND") ? 0 : 1;
   b.ls_first = LS_FIRST;
   b.cand = nullptr;
@@ -527,7 +528,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     const char* ev = getenv("TOG_LS");
     const bool replay = ev && strcmp(ev, "replay") == 0;
     if (!replay && opts->iterations_linesearch + 1 <= 64) {
-      if ((rc = dalloc(h, &b.cand, B * (size_t)b.nc * N * ((n + m + 1) & ~1))) || (rc = dalloc(h, &b.ls_win, B)) ||
+      if ((rc = dalloc(h, &b.cand, B * (size_t)b.ncp * N * 4 * ((n + m + 3) / 4))) || (rc = dalloc(h, &b.ls_win, B)) ||
           (rc = dalloc(h, &b.ls_Jw, B)) || (rc = dalloc(h, &b.gk, B * N)))
         return rc;
     }
