@@ -1345,7 +1345,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (WMODE == 3) {
 #pragma unroll
-      for (int i = 0; i < m; i++) cw[cand_at(k - 1, i, cand_q<M>(), ncp)] = ub[i];
+      for (int i = 0; i < m; i++) __builtin_nontemporal_store(ub[i], cw + cand_at(k - 1, i, cand_q<M>(), ncp));
     }
     if (WMODE == 2) {
       double mx = -INFINITY;
@@ -1403,7 +1403,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (WMODE == 3) {
 #pragma unroll
-      for (int i = 0; i < n; i++) cw[cand_at(k, m + i, cand_q<M>(), ncp)] = xn[i];
+      for (int i = 0; i < n; i++) __builtin_nontemporal_store(xn[i], cw + cand_at(k, m + i, cand_q<M>(), ncp));
     }
     if (!ok) return false;
   }
