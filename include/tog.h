@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TOG_ABI_VERSION 1
+#define TOG_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status */
 enum tog_status_code {
@@ -70,7 +70,10 @@ enum tog_model_id {
   TOG_MODEL_CAR = 3,               /* dynamics/car.jl:3-8                 n=3  m=2 */
   TOG_MODEL_PENDULUM = 4,          /* dynamics/pendulum.jl:3-12           n=2  m=1 */
   TOG_MODEL_KUKA = 5,              /* src/model.jl:394-431 RBD Model(urdf) n=14 m=7 (include/tog_kuka.h) */
-  TOG_MODEL_COUNT = 6
+  TOG_MODEL_COUNT = 6,
+  /* Model(f!, n, m) (src/model.jl:103-131) with user dynamics: a plugin loaded by tog_model_load,
+     passed in tog_problem_desc.user_model */
+  TOG_MODEL_USER = 100
 };
 
 enum tog_integrator {
@@ -154,6 +157,8 @@ typedef struct tog_problem_desc {
   int32_t reserved1;
   const tog_constraint_set* sets;
   const int32_t* knot_set;
+  /* model == TOG_MODEL_USER: the loaded user model (tog_model_load), else ignored */
+  const struct tog_model* user_model;
 } tog_problem_desc;
 
 /* ---------------------------------------------------------------- options */
@@ -252,6 +257,19 @@ typedef struct tog_handle tog_handle;
 
 /* ---------------------------------------------------------------- API */
 int32_t tog_version(void);
+
+/* ---------------------------------------------------------------- user models (plugins)
+   Replaces Model(f!, n, m) (src/model.jl:103-131, continuous dynamics from a user function, its
+   Jacobian by ForwardDiff src/model.jl:491-522). The user's f!(ẋ, x, u), written once as a C++
+   template over the scalar type (double and the dual numbers of the Jacobian kernel), is compiled
+   with hipcc for gfx950 against csrc/tog_plugin.hpp into a shared object that instantiates every
+   kernel of the path for it (and for its infeasible-start variant, add_slack_controls
+   src/model.jl:761-779). tog_model_load dlopens it and checks its layout fingerprint against
+   this library's. */
+typedef struct tog_model tog_model;
+int32_t tog_model_load(const char* path, tog_model** out);
+int32_t tog_model_dims(const tog_model* model, int32_t* n, int32_t* m);
+int32_t tog_model_free(tog_model* model); /* after every handle built on it is destroyed */
 /* dynamics_bias(state) at x = [q; v] for RBD models (TOG_MODEL_KUKA): c(q, v) into tau[m].
    Replaces RigidBodyDynamics.dynamics_bias as used by hold_trajectory (dynamics/kuka.jl:117-132).
    Host evaluation; TOG_ERR_UNSUPPORTED for analytical models. */

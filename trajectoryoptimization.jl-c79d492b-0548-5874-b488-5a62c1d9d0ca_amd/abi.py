@@ -16,11 +16,12 @@ import numpy as np
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "csrc" / "libtog.so"
 
-TOG_ABI_VERSION = 1
+TOG_ABI_VERSION = 2
 
 # models (include/tog.h tog_model_id)
 MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM, MODEL_KUKA = range(6)
 MODEL_NM = {0: (2, 1), 1: (4, 1), 2: (13, 4), 3: (3, 2), 4: (2, 1), 5: (14, 7)}
+MODEL_USER = 100  # Model(f!, n, m) from a plugin (tog_model_load)
 # status codes (include/tog.h tog_status_code)
 OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 
@@ -76,6 +77,7 @@ class tog_problem_desc(C.Structure):
         ("Qf", _dp), ("qf", _dp), ("cf", C.c_double),
         ("n_sets", C.c_int32), ("reserved1", C.c_int32),
         ("sets", C.POINTER(tog_constraint_set)), ("knot_set", _ip),
+        ("user_model", C.c_void_p),
     ]
 
 
@@ -152,7 +154,7 @@ class DescBuilder:
     """
 
     def __init__(self, model, integrator, n, m, N, dt, Q, R, H, q, r, c, Qf, qf, cf, sets, knot_set,
-                 batch=1, flags=0):
+                 batch=1, flags=0, user_model=None):
         self._keep = []
 
         def arr(x, shape):
@@ -193,6 +195,7 @@ class DescBuilder:
         assert ks.shape == (N,)
         self._keep.append(ks)
         d.knot_set = ks.ctypes.data_as(_ip)
+        d.user_model = user_model
         self.desc = d
 
 
@@ -249,13 +252,17 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_solve_al.argtypes = [vp]
     lib.tog_default_pn_options.argtypes = [C.POINTER(tog_pn_options)]
     lib.tog_solve_pn.argtypes = [vp, C.POINTER(tog_pn_options), _dp]
+    lib.tog_model_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+    lib.tog_model_dims.argtypes = [vp, _ip, _ip]
+    lib.tog_model_free.argtypes = [vp]
     for name in ("tog_create", "tog_create_multi", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
                  "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
                  "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
-                 "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn"):
+                 "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn", "tog_model_load", "tog_model_dims",
+                 "tog_model_free"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")

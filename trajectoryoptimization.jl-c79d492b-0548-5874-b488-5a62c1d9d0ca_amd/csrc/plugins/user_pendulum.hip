@@ -1,0 +1,17 @@
+// A user model written against the plugin API (tog_plugin.hpp): the reference's pendulum
+// (dynamics/pendulum.jl:3-12) as a user would define it with Model(pendulum_dynamics!, 2, 1). The
+// operation sequence is the built-in Pendulum's, so tests can hold the plugin path bit for bit against
+// the built-in model and the CPU oracle.
+#include "../tog_plugin.hpp"
+
+struct UserPendulum {
+  static constexpr int n = 2, m = 1, id = TOG_MODEL_USER;
+  template <class T>
+  __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    const double mm = 1.0, b = 0.1, lc = 0.5, I = 0.25, g = 9.81;
+    xd[0] = x[1];
+    xd[1] = ((u[0] - (mm * g * lc) * tog::sin_(x[0])) - b * x[1]) / I;
+  }
+};
+
+TOG_PLUGIN(UserPendulum)

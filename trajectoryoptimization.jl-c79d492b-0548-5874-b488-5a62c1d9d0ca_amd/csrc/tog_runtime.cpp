@@ -11,7 +11,9 @@
 #include <string>
 #include <vector>
 
-#include "tog_kernels.hpp"
+#include <dlfcn.h>
+
+#include "tog_plugin.hpp"
 
 using namespace tog;
 
@@ -105,7 +107,15 @@ static void timed(tog_handle* h, int kind, F&& fn) {
   h->ev_kind.push_back(kind);
 }
 
-static const ModelOps* ops_for(int model, bool infeasible) {
+// a loaded user model plugin (tog_model_load)
+struct tog_model {
+  void* so;
+  const tog::ModelOps* ops;
+  const tog::ModelOps* ops_inf;
+};
+
+static const ModelOps* ops_for(int model, bool infeasible, const tog_model* user) {
+  if (model == TOG_MODEL_USER) return user ? (infeasible ? user->ops_inf : user->ops) : nullptr;
   if (infeasible) {
     switch (model) {
       case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_inf_double_integrator();
@@ -279,6 +289,41 @@ __global__ void k_reset_state(TrajState* st, long long B, double mu0) {
 extern "C" {
 
 int32_t tog_version(void) { return TOG_ABI_VERSION; }
+
+int32_t tog_model_load(const char* path, tog_model** out) {
+  if (!path || !out) return fail(TOG_ERR_ARG, "null argument");
+  *out = nullptr;
+  void* so = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!so) return fail(TOG_ERR_ARG, std::string("cannot load model plugin: ") + dlerror());
+  auto fp = reinterpret_cast<long long (*)()>(dlsym(so, "tog_plugin_fingerprint"));
+  auto ops = reinterpret_cast<const ModelOps* (*)()>(dlsym(so, "tog_plugin_ops"));
+  auto opi = reinterpret_cast<const ModelOps* (*)()>(dlsym(so, "tog_plugin_ops_infeasible"));
+  if (!fp || !ops || !opi) {
+    dlclose(so);
+    return fail(TOG_ERR_ARG, "not a libtog model plugin (TOG_PLUGIN symbols missing)");
+  }
+  if (fp() != plugin_fingerprint()) {
+    dlclose(so);
+    return fail(TOG_ERR_ARG, "model plugin was built against different libtog headers");
+  }
+  tog_model* m = new tog_model{so, ops(), opi()};
+  *out = m;
+  return TOG_OK;
+}
+
+int32_t tog_model_dims(const tog_model* model, int32_t* n, int32_t* m) {
+  if (!model || !n || !m) return fail(TOG_ERR_ARG, "null argument");
+  *n = model->ops->n;
+  *m = model->ops->m;
+  return TOG_OK;
+}
+
+int32_t tog_model_free(tog_model* model) {
+  if (!model) return fail(TOG_ERR_ARG, "null model");
+  dlclose(model->so);
+  delete model;
+  return TOG_OK;
+}
 
 // dynamics_bias(state) of an RBD model at x = [q; v] (RigidBodyDynamics, used by
 // hold_trajectory dynamics/kuka.jl:117-132): host evaluation of the same model code the kernels run.
@@ -556,7 +601,7 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
   *out = nullptr;
   if (d->flags & ~(int32_t)TOG_PROB_INFEASIBLE) return fail(TOG_ERR_ARG, "unknown problem flags");
-  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0);
+  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0, d->user_model);
   if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
   if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
   if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");

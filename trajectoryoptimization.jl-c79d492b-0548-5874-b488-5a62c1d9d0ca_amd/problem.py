@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import copy as _copy
 import math
+import pathlib
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -31,8 +32,10 @@ from . import abi
 class Model:
     """``AnalyticalModel{Nominal, Continuous|Discrete}`` (src/model.jl:36-74).
 
-    Only the canned dynamics built into the HIP kernels exist (``Dynamics.*``); a
-    discrete model carries its integrator (``rk3``/``rk4``, src/model.jl:642-644).
+    Either one of the canned dynamics built into libtog (``Dynamics.*``) or a user model
+    ``Model(f!, n, m)`` (src/model.jl:103-131) compiled into a plugin (``user_model`` /
+    ``Model.from_plugin``, csrc/tog_plugin.hpp). A discrete model carries its integrator
+    (``rk3``/``rk4``, src/model.jl:642-644).
     """
 
     model_id: int
@@ -41,6 +44,13 @@ class Model:
     name: str
     integration: int | None = None  # None = Continuous; abi.RK3 / abi.RK4 = Discrete
     slack: int = 0  # add_slack_controls: the last `slack` (= n) controls are infeasible slacks
+    plugin: "UserModelPlugin | None" = None  # model_id == abi.MODEL_USER
+
+    @staticmethod
+    def from_plugin(path, name: str | None = None) -> "Model":
+        """A user model from a compiled plugin (``tog_model_load``); n, m come from the plugin."""
+        plug = UserModelPlugin.load(path)
+        return Model(abi.MODEL_USER, plug.n, plug.m, name or pathlib.Path(path).stem, plugin=plug)
 
     @property
     def discrete(self) -> bool:
@@ -59,7 +69,7 @@ def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) ->
     if integs[key] in (abi.RK3_IMPLICIT, abi.MIDPOINT_IMPLICIT) and model.n > 4:
         # the device instantiates the implicit Newton step for n <= 4 (csrc/tog_device.hpp)
         raise NotImplementedError(f"implicit integration {discretizer!r} is built for models with n <= 4")
-    return Model(model.model_id, model.n, model.m, model.name, integs[key])
+    return Model(model.model_id, model.n, model.m, model.name, integs[key], plugin=model.plugin)
 
 
 def midpoint(model: Model, dt: float = 1.0) -> Model:
@@ -87,7 +97,8 @@ def add_slack_controls(model: Model) -> Model:
         raise ValueError("add_slack_controls needs a discrete model")
     if model.slack:
         raise ValueError("model already has slack controls")
-    return Model(model.model_id, model.n, model.m + model.n, model.name + "_inf", model.integration, model.n)
+    return Model(model.model_id, model.n, model.m + model.n, model.name + "_inf", model.integration, model.n,
+                 plugin=model.plugin)
 
 
 def rk3(model: Model, dt: float = 1.0) -> Model:
@@ -96,6 +107,78 @@ def rk3(model: Model, dt: float = 1.0) -> Model:
 
 def rk4(model: Model, dt: float = 1.0) -> Model:
     return discretize_model(model, "rk4", dt)
+
+
+class UserModelPlugin:
+    """A loaded user-model plugin (``tog_model_load``, include/tog.h). Kept alive by every
+    ``Model`` built on it; freed (``tog_model_free``) when the last reference goes."""
+
+    _cache: dict = {}
+
+    def __init__(self, path, ptr, n, m):
+        self.path, self.ptr, self.n, self.m = str(path), ptr, n, m
+
+    @classmethod
+    def load(cls, path):
+        path = str(pathlib.Path(path).resolve())
+        if path in cls._cache:
+            return cls._cache[path]
+        import ctypes as C
+
+        lib = abi.load_library()
+        h = C.c_void_p()
+        abi.check(lib, lib.tog_model_load(path.encode(), C.byref(h)))
+        n, m = C.c_int32(), C.c_int32()
+        abi.check(lib, lib.tog_model_dims(h, C.byref(n), C.byref(m)))
+        plug = cls(path, h.value, n.value, m.value)
+        cls._cache[path] = plug  # a plugin stays loaded for the life of the process (kernels registered)
+        return plug
+
+
+_PLUGIN_TEMPLATE = """// generated by user_model() (problem.py): Model(f!, n, m) as a libtog plugin
+#include "{hdr}"
+
+struct {name} {{
+  static constexpr int n = {n}, m = {m}, id = TOG_MODEL_USER;
+  template <class T>
+  __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {{
+    using namespace tog;
+{body}
+  }}
+}};
+
+TOG_PLUGIN({name})
+"""
+
+
+def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=None) -> Model:
+    """``Model(f!, n, m)`` (src/model.jl:103-131) for user dynamics: ``f_body`` is the body of
+    ``f(T* xd, const T* x, const T* u)`` in C++ over the scalar type ``T`` (double in rollouts,
+    dual numbers in the Jacobian kernel, as ForwardDiff differentiates the Julia f!). Use
+    ``sin_``, ``cos_``, ``sqrt_``, ``inv_``. The plugin is compiled once with hipcc for gfx950
+    (cached by the hash of its source under ``csrc/plugins/``) and loaded with ``tog_model_load``."""
+    import hashlib
+    import subprocess
+
+    csrc = pathlib.Path(__file__).resolve().parent / "csrc"
+    out_dir = pathlib.Path(build_dir) if build_dir else csrc / "plugins"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    body = "\n".join("    " + ln for ln in f_body.strip().splitlines())
+    src = _PLUGIN_TEMPLATE.format(hdr=str(csrc / "tog_plugin.hpp"), name=name, n=int(n), m=int(m), body=body)
+    key = hashlib.sha1(src.encode()).hexdigest()[:12]
+    so = out_dir / f"gen_{name}_{key}.so"
+    if not so.exists():
+        hip = out_dir / f"gen_{name}_{key}.hip"
+        hip.write_text(src)
+        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-fPIC",
+               "-shared", "-o", str(so), str(hip)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise ValueError(f"user model {name!r} does not compile:\n{r.stderr[-4000:]}")
+    model = Model.from_plugin(so, name)
+    if (model.n, model.m) != (int(n), int(m)):
+        raise ValueError("plugin dimensions do not match")
+    return model
 
 
 class Dynamics:
@@ -574,7 +657,8 @@ class Problem:
         R = stage.R if stage.R.size else np.zeros((m, m))
         return abi.DescBuilder(self.model.model_id, self.model.integration, n, m, N, self.dt, stage.Q, R, stage.H,
                                stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B,
-                               flags=abi.PROB_INFEASIBLE if self.model.slack else 0)
+                               flags=abi.PROB_INFEASIBLE if self.model.slack else 0,
+                               user_model=self.model.plugin.ptr if self.model.plugin else None)
 
 
 def _validate_time(N, tf, dt):

@@ -158,10 +158,11 @@ def car_sqrt_bp(constrained=False):
     return Problem(model_d, obj, np.ones((N - 1, m)), constraints=cons, x0=x0, N=N, dt=dt)
 
 
-def pendulum(integration="rk3", U0=None):
+def pendulum(integration="rk3", U0=None, model=None):
     """problems/pendulum.jl:1-35: rk3, N=31, dt=0.15, Q=R=Qf=1e-3 I, xf=[π,0], |u|<=3 at
-    k<N, goal at N, U=ones."""
-    model_d = discretize_model(Dynamics.pendulum, integration)
+    k<N, goal at N, U=ones. ``model``: another continuous model with the pendulum's n, m (e.g. a
+    user plugin of the same dynamics)."""
+    model_d = discretize_model(model or Dynamics.pendulum, integration)
     n, m = 2, 1
     Q, R = 1e-3 * np.eye(n), 1e-3 * np.eye(m)
     x0, xf = np.zeros(n), np.array([math.pi, 0.0])
@@ -460,3 +461,41 @@ def config_quadrotor_maze_infeasible(B=1024, offset=0):
     p0b.X = Xs.reshape(B, N, 13)
     opts = maze_altro_options()
     return infeasible_problem(p0b, opts.R_inf), opts
+
+
+# --------------------------------------------------------------------- user models (plugins)
+# Model(f!, n, m) (src/model.jl:103-131) with user dynamics compiled into a libtog plugin
+# (csrc/tog_plugin.hpp). The unicycle below is not among the built-in dynamics.
+UNICYCLE_F = """
+const double cv = 0.1, cw = 0.2;
+xd[0] = x[3] * cos_(x[2]);
+xd[1] = x[3] * sin_(x[2]);
+xd[2] = x[4];
+xd[3] = u[0] - cv * x[3];
+xd[4] = u[1] - cw * x[4];
+"""
+
+
+def unicycle_model():
+    """The unicycle with first-order actuators as a user model: x = [px, py, θ, v, ω], u = [a, α]."""
+    from .problem import user_model
+
+    return user_model(UNICYCLE_F, 5, 2, name="Unicycle")
+
+
+def unicycle(model=None, B=1, offset=0, N=51, dt=0.1):
+    """Drive the unicycle from rest at the origin to xf = (2, 1, 0, 0, 0): rk3, LQR objective
+    (Q = 1e-2 I, R = 1e-1 I, Qf = 100 I), |u| <= 2 at every stage knot, goal at N. U0 = 0.1 N(0,1)
+    (seed 6000+b)."""
+    model_d = rk3(model or unicycle_model())
+    n, m = 5, 2
+    xf = np.array([2.0, 1.0, 0.0, 0.0, 0.0])
+    U0 = _per_traj_rng(6000 + offset, B, lambda r: 0.1 * r.standard_normal((N - 1, m)))
+    cons = Constraints(N)
+    bnd = BoundConstraint(n, m, u_min=-2.0, u_max=2.0)
+    for k in range(N - 1):
+        cons[k] += bnd
+    cons[N - 1] += goal_constraint(xf)
+    obj = LQRObjective(1e-2 * np.eye(n), 1e-1 * np.eye(m), 100.0 * np.eye(n), xf, N)
+    return Problem(model_d, obj, U0 if B > 1 else U0[0], constraints=cons, x0=np.zeros((B, n)) if B > 1 else np.zeros(n),
+                   xf=xf, N=N, dt=dt)
