@@ -103,7 +103,11 @@ enum tog_constraint_type {
   /* infeasible_constraints(n, m), src/constraints.jl:306-314: the n slack controls of an
      infeasible-start problem must vanish, c = u[m_model + i] (stage equality, n rows, no data).
      Only valid in a TOG_PROB_INFEASIBLE problem. */
-  TOG_CON_INFEASIBLE = 4
+  TOG_CON_INFEASIBLE = 4,
+  /* Constraint{Inequality|Equality}(c!, n, m, p) with a user function (src/constraints.jl:85-89):
+     count = p rows, data = [fid, equality (0/1), where (0 stage knots, 1 terminal knot, 2 both)];
+     evaluated by the user model plugin's con(fid, c, x, u), Jacobian by dual numbers */
+  TOG_CON_USER = 5
 };
 
 /* problem flags (tog_problem_desc.flags) */

@@ -122,3 +122,52 @@ def test_user_unicycle_jacobian_and_solve(tog, gpu):
     flags = s.stats["flags"]
     assert np.all(flags & tog.abi.TRAJ_AL_CONVERGED)
     assert np.all(np.abs(prob._X[:, -1] - np.array([2.0, 1.0, 0, 0, 0])) < 1e-2)
+
+
+def test_user_constraint_rows_cpu(tog):
+    """UserConstraint marshals as TOG_CON_USER; a model without con() is refused at tog_create."""
+    uc = tog.UserConstraint(2, 1, 1, fid=0, label="obstacle")
+    t, cnt, data = uc.to_abi()
+    assert (t, cnt, list(data)) == (tog.abi.CON_USER, 1, [0.0, 0.0, 0.0])
+    assert uc.length("stage") == 1 and uc.length("terminal") == 0
+    assert np.isnan(uc.evaluate(np.zeros(2), np.zeros(1))).all()
+    prob = tog.Problems.pendulum(stage_constraints=(uc,))  # built-in pendulum: no con()
+    lib = tog.abi.load_library()
+    b = prob.build_desc()
+    o = tog.to_tog_options(tog.AugmentedLagrangianSolverOptions())
+    h = C.c_void_p()
+    rc = lib.tog_create(C.byref(b.desc), C.byref(o), 0, C.byref(h))
+    assert rc in (tog.abi.ERR_ARG, tog.abi.ERR_DEVICE) and not h.value
+
+
+@pytest.mark.gpu
+def test_user_circle_constraint_equals_builtin_and_oracle(tog, oracle, gpu):
+    """A circle obstacle as a user constraint function (plugin con, fid 0; dense dual Jacobian, LDS
+    backward kernel) against the built-in circle rows (team backward kernel) and the oracle."""
+    user = tog.Model.from_plugin(PLUG / "user_pendulum.so")
+    opts = tog.AugmentedLagrangianSolverOptions()
+    circ = tog.CircleConstraints(2, 1, [[1.2, 2.5, 0.6]])
+    p_user = tog.Problems.pendulum(model=user, stage_constraints=(tog.UserConstraint(2, 1, 1, fid=0),))
+    p_builtin = tog.Problems.pendulum(stage_constraints=(circ,))
+    s_user = tog.solve_b(p_user, opts)
+    s_builtin = tog.solve_b(p_builtin, opts)
+    assert np.array_equal(p_user._X, p_builtin._X) and np.array_equal(p_user._U, p_builtin._U)
+    assert np.array_equal(s_user.stats["iterations_total"], s_builtin.stats["iterations_total"])
+    ref = oracle.OracleSolver(tog.Problems.pendulum(stage_constraints=(circ,)), opts, b=0)
+    ref.solve()
+    X, U = ref.get("X"), ref.get("U")
+    assert np.max(np.abs(p_user._X[0] - X)) <= 1e-6 * max(1.0, np.max(np.abs(X)))
+    assert np.max(np.abs(p_user._U[0] - U)) <= 1e-6 * max(1.0, np.max(np.abs(U)))
+
+
+@pytest.mark.gpu
+def test_user_constraints_unicycle_solve(tog, gpu):
+    """State (obstacle) and control-dependent (traction a·v <= 1) user rows on a user model."""
+    model = tog.Problems.unicycle_model()
+    prob = tog.Problems.unicycle(model, B=8, user_constraints=True)
+    opts = tog.AugmentedLagrangianSolverOptions()
+    s = tog.solve_b(prob, opts)
+    assert np.all(s.stats["flags"] & tog.abi.TRAJ_AL_CONVERGED)
+    cmax = tog.max_violation(prob)
+    assert np.all(cmax < opts.constraint_tolerance)
+    assert np.all(np.abs(prob._X[:, -1] - np.array([2.0, 1.0, 0, 0, 0])) < 1e-2)

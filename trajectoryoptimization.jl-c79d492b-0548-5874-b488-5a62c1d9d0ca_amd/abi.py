@@ -26,7 +26,7 @@ MODEL_USER = 100  # Model(f!, n, m) from a plugin (tog_model_load)
 OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 
 RK3, RK4, MIDPOINT, RK3_IMPLICIT, MIDPOINT_IMPLICIT = 0, 1, 2, 3, 4
-CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE = range(5)
+CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE, CON_USER = range(6)
 PROB_INFEASIBLE = 1  # tog_problem_flag
 MODE_ILQR, MODE_AL = 0, 1
 

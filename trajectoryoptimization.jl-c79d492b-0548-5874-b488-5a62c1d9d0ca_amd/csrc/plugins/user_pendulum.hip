@@ -12,6 +12,19 @@ struct UserPendulum {
     xd[0] = x[1];
     xd[1] = ((u[0] - (mm * g * lc) * tog::sin_(x[0])) - b * x[1]) / I;
   }
+  // user constraint functions (Constraint{Inequality}(c!, n, m, p), src/constraints.jl:85-89):
+  // fid 0 is circle_constraint(x, 1.2, 2.5, 0.6) (src/utils.jl:140-144), an obstacle in the (θ, ω)
+  // plane, written as the built-in circle rows evaluate it.
+  static constexpr bool has_con = true;
+  template <class T>
+  __host__ __device__ __forceinline__ static void con(int fid, T* c, const T* x, const T* u) {
+    (void)u;
+    if (fid == 0) {
+      const double a = 1.2, bb = 2.5, r = 0.6;
+      const T dx = x[0] - a, dy = x[1] - bb;
+      c[0] = -((dx * dx + dy * dy) - r * r);
+    }
+  }
 };
 
 TOG_PLUGIN(UserPendulum)

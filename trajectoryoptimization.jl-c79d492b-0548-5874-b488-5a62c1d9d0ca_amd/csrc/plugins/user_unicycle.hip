@@ -14,6 +14,17 @@ struct UserUnicycle {
     xd[3] = u[0] - cv * x[3];
     xd[4] = u[1] - cw * x[4];
   }
+  // fid 0: a disc obstacle at (1, 0.5), radius 0.3 (stage); fid 1: traction limit a·v <= 1 (depends on u)
+  static constexpr bool has_con = true;
+  template <class T>
+  __host__ __device__ __forceinline__ static void con(int fid, T* c, const T* x, const T* u) {
+    if (fid == 0) {
+      const T dx = x[0] - 1.0, dy = x[1] - 0.5;
+      c[0] = -((dx * dx + dy * dy) - 0.09);
+    } else {
+      c[0] = u[0] * x[3] - 1.0;
+    }
+  }
 };
 
 TOG_PLUGIN(UserUnicycle)

@@ -98,6 +98,7 @@ inline bool team_rows_fit(const int* knot_off, const int* knot_cnt, const ConRow
     if (knot_cnt[k] > PCAP) return false;
     for (int r = 0; r < knot_cnt[k]; r++) {
       const int t = rows[knot_off[k] + r].type;
+      if (t == ROW_USER_INEQ || t == ROW_USER_EQ) return false;  // dense user rows: LDS kernel
       if (t == ROW_UMAX || t == ROW_UMIN) nu++;
       else nx++;
     }

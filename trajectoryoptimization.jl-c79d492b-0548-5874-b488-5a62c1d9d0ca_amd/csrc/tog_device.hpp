@@ -10,6 +10,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/tog.h"
 #include "../../include/tog_math.h"
 #include "../../include/tog_kuka.h"
@@ -31,8 +33,13 @@ enum RowType : int {
   ROW_GOAL = 4,  // c = x[i] - a            (equality, goal_constraint src/constraints.jl:299-304)
   ROW_CIRCLE = 5,  // c = -((x1-a)^2 + (x2-b)^2 - r^2)            src/utils.jl:140-144
   ROW_SPHERE = 6,  // c = -((x1-a)^2 + (x2-b)^2 + (x3-c)^2 - r^2)  src/utils.jl:150-156
-  ROW_USLACK = 7   // c = u[i]  (equality; infeasible_constraints, src/constraints.jl:306-314)
+  ROW_USLACK = 7,  // c = u[i]  (equality; infeasible_constraints, src/constraints.jl:306-314)
+  // Constraint{S}(c!, n, m, p) with a user function (src/constraints.jl:85-89, Jacobian by ForwardDiff):
+  // row idx of the plugin model's con(fid = a, c, x, u) (p = b outputs)
+  ROW_USER_INEQ = 8,
+  ROW_USER_EQ = 9
 };
+constexpr int PUSER = 16;  // max outputs of one user constraint function
 
 struct ConRow {
   int type;
@@ -705,11 +712,23 @@ struct Kuka {
 // [u (Mb::m); s (Mb::n)], x+ = f_d(x, u) + s. Kernels see it as a model with m = Mb::m + Mb::n;
 // discrete_step adds the slacks after the base model's RK step, k_jacobian writes the identity
 // slack block directly (the reference's ∇f! copies Diagonal(1.0I, n), it is never differentiated).
+// models that define user constraint functions (plugins: static constexpr bool has_con = true and
+// template <class T> static void con(int fid, T* c, const T* x, const T* u))
+template <class M, class = void>
+struct HasCon : std::false_type {};
+template <class M>
+struct HasCon<M, std::void_t<decltype(M::has_con)>> : std::integral_constant<bool, M::has_con> {};
+
 template <class Mb>
 struct Infeasible {
   using Base = Mb;
   static constexpr int n = Mb::n, m = Mb::m + Mb::n, id = Mb::id;
   static constexpr int slack = Mb::n;
+  static constexpr bool has_con = HasCon<Mb>::value;  // constraints see the base controls u[1:m]
+  template <class T>
+  __host__ __device__ __forceinline__ static void con(int fid, T* c, const T* x, const T* u) {
+    if constexpr (HasCon<Mb>::value) Mb::con(fid, c, x, u);
+  }
 };
 
 template <class M>
@@ -1068,7 +1087,7 @@ __device__ __forceinline__ double row_value(const ConRow& r, const double* x, co
 }
 template <bool SLACK = true>
 __device__ __forceinline__ bool row_inequality(const ConRow& r) {
-  return r.type != ROW_GOAL && (!SLACK || r.type != ROW_USLACK);
+  return r.type != ROW_GOAL && r.type != ROW_USER_EQ && (!SLACK || r.type != ROW_USLACK);
 }
 
 // The same row seen by every lane of a wave (lanes iterate knots and rows in lockstep over the
@@ -1105,6 +1124,58 @@ __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n,
       idx[2] = 2; v[2] = -(2.0 * (x[2] - r.c));
       return 3;
   }
+}
+
+// Rows of a model: the built-in row types, plus the user constraint rows of a plugin model. A user
+// row evaluates the model's con(fid, c, x, u) (u = zeros at the terminal knot) and takes output idx;
+// its gradient over [x; u_base] comes from dual numbers with n + m_base partials (ForwardDiff).
+template <class M>
+__device__ __forceinline__ double row_value_m(const ConRow& r, const double* x, const double* u) {
+  if constexpr (HasCon<M>::value) {
+    if (r.type == ROW_USER_INEQ || r.type == ROW_USER_EQ) {
+      using Mb = typename ModelTraits<M>::Base;
+      double u0[Mb::m], c[PUSER];
+#pragma unroll
+      for (int i = 0; i < Mb::m; i++) u0[i] = u ? u[i] : 0.0;
+      M::con((int)r.a, c, x, u0);
+      return c[r.idx];
+    }
+  }
+  return row_value<(ModelTraits<M>::slack > 0)>(r, x, u);
+}
+template <class M>
+__host__ __device__ constexpr int row_grad_cap() {
+  return HasCon<M>::value ? M::n + ModelTraits<M>::Base::m : 3;
+}
+template <class M>
+__device__ __forceinline__ int row_grad_m(const ConRow& r, const double* x, const double* u, int* idx, double* v) {
+  if constexpr (HasCon<M>::value) {
+    if (r.type == ROW_USER_INEQ || r.type == ROW_USER_EQ) {
+      using Mb = typename ModelTraits<M>::Base;
+      constexpr int n = M::n, mb = Mb::m, W = n + mb;
+      Dual<W> xd[n], ud[mb], c[PUSER];
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        xd[i].v = x[i];
+#pragma unroll
+        for (int w = 0; w < W; w++) xd[i].g[w] = (w == i) ? 1.0 : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < mb; i++) {
+        ud[i].v = u ? u[i] : 0.0;
+#pragma unroll
+        for (int w = 0; w < W; w++) ud[i].g[w] = (w == n + i) ? 1.0 : 0.0;
+      }
+      M::con((int)r.a, c, xd, ud);
+      const int nz = u ? W : n;  // terminal rows: state gradient only
+      for (int w = 0; w < nz; w++) {
+        idx[w] = w;
+        v[w] = c[r.idx].g[w];
+      }
+      return nz;
+    }
+  }
+  return row_grad(r, x, M::n, idx, v);
 }
 
 // regularization_update! (ilqr_methods.jl:164-176)

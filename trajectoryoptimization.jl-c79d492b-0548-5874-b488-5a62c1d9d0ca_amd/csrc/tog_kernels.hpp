@@ -58,7 +58,7 @@ __host__ __device__ constexpr int nq_of() {
 // AL terms λ'c + ½ c'Iμ c of one knot (augmented_lagrangian_methods.jl:298-313), rows in order. The
 // multipliers are loaded four rows at a time so their global loads overlap instead of serialising
 // one round trip per row. Ck (constraint values out) may be null.
-template <bool SLACK>
+template <class M>
 __device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const double* lamk, const double* muk,
                                               const double* x, const double* u, double& lc, double& cIc,
                                               double* Ck) {
@@ -73,9 +73,9 @@ __device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const
     for (int q = 0; q < 4; q++) {
       if (base + q < cnt) {
         const ConRow r = uniform_row(rows[base + q]);
-        const double c = row_value<SLACK>(r, x, u);
+        const double c = row_value_m<M>(r, x, u);
         const double l = lv[q];
-        const bool a = row_inequality<SLACK>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
+        const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
         const double w = a ? mv[q] : 0.0;
         lc = fma(l, c, lc);
         cIc = fma(c * w, c, cIc);
@@ -105,7 +105,7 @@ __device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& 
     const double* x = Xs + (size_t)k * n;
     const double* u = (k < N - 1) ? Us + (size_t)k * m : nullptr;
     double lc = 0.0, cIc = 0.0;
-    al_knot_terms<(ModelTraits<M>::slack > 0)>(rows, cnt, lam + (size_t)k * pmax, mu + (size_t)k * pmax, x, u, lc, cIc,
+    al_knot_terms<M>(rows, cnt, lam + (size_t)k * pmax, mu + (size_t)k * pmax, x, u, lc, cIc,
                   Cout ? Cout + (size_t)k * pmax : nullptr);
     Jc += lc + 0.5 * cIc;
   }
@@ -321,7 +321,7 @@ __global__ void __launch_bounds__(64) k_update_constraints(const DevProblem* __r
     const ConRow* rows = P->rows + P->knot_off[k];
     for (int i = 0; i < cnt; i++)
       Bf.C[((size_t)b * N + k) * pmax + i] =
-          row_value(uniform_row(rows[i]), X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
+          row_value_m<M>(uniform_row(rows[i]), X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
   }
 }
 
@@ -544,7 +544,7 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
   for (int e = lane; e < p * m; e += WAVE) sh.cu[e] = 0.0;
   wsync();
   for (int r = lane; r < p; r += WAVE) {  // p may exceed the wave (PCAP > 64)
-    const double c = row_value(rows[r], sh.xk, term ? nullptr : sh.uk);
+    const double c = row_value_m<M>(rows[r], sh.xk, term ? nullptr : sh.uk);
     const double l = lam[r];
     const bool a = row_inequality(rows[r]) ? ((c >= 0.0) || (l > 0.0)) : true;
     const double w = a ? mu[r] : 0.0;
@@ -552,9 +552,9 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
     sh.wv[r] = w;
     sh.wsv[r] = a ? sqrt(mu[r]) : 0.0;
     sh.gv[r] = w * c + l;
-    int idx[3];
-    double v[3];
-    const int nz = row_grad(rows[r], sh.xk, n, idx, v);
+    int idx[row_grad_cap<M>()];
+    double v[row_grad_cap<M>()];
+    const int nz = row_grad_m<M>(rows[r], sh.xk, term ? nullptr : sh.uk, idx, v);
     for (int z = 0; z < nz; z++) {
       if (idx[z] < n)
         sh.cx[r + p * idx[z]] = v[z];
@@ -1368,7 +1368,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
         for (int q = 0; q < RB; q++) {
           if (q < cnt) {
             const ConRow r = uniform_row(rows[q]);
-            const double c = row_value<(ModelTraits<M>::slack > 0)>(r, xb, ub);
+            const double c = row_value_m<M>(r, xb, ub);
             const double l = lk[q];
             const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
             const double w = a ? mk[q] : 0.0;
@@ -1377,7 +1377,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
           }
         }
         if (cnt > RB)
-          al_knot_terms<(ModelTraits<M>::slack > 0)>(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB, mu + (size_t)(k - 1) * pmax + RB, xb,
+          al_knot_terms<M>(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB, mu + (size_t)(k - 1) * pmax + RB, xb,
                         ub, lc, cIc, nullptr);
         Jc += lc + 0.5 * cIc;
       }
@@ -1413,7 +1413,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     if (cnt) {
       const ConRow* rows = RT.rows + RT.koff[N - 1];
       double lc = 0.0, cIc = 0.0;
-      al_knot_terms<(ModelTraits<M>::slack > 0)>(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax, xb, nullptr, lc, cIc,
+      al_knot_terms<M>(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax, xb, nullptr, lc, cIc,
                     nullptr);
       Jc += lc + 0.5 * cIc;
     }
@@ -1935,7 +1935,7 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
     for (int i = 0; i < cnt; i++) {
       const size_t q = (size_t)k * pmax + i;
       const ConRow r = rows[i];
-      const double c = row_value<SL>(r, x, u);
+      const double c = row_value_m<M>(r, x, u);
       C[q] = c;
       const bool ineq = row_inequality<SL>(r);
       double l = lam[q] + mu[q] * c;  // dual_update! (:107-118)
@@ -2134,9 +2134,9 @@ __global__ void __launch_bounds__(64) k_cost_expansion(const DevProblem* __restr
   for (int i = 0; i < p * m; i++) cu[i] = 0.0;
   for (int r = 0; r < p; r++) {
     const ConRow row = rows[r];
-    int idx[3];
-    double v[3];
-    const int nz = row_grad(row, x, n, idx, v);
+    int idx[row_grad_cap<M>()];
+    double v[row_grad_cap<M>()];
+    const int nz = row_grad_m<M>(row, x, u, idx, v);
     for (int z = 0; z < nz; z++) {
       if (idx[z] < n) cx[r + p * idx[z]] = v[z];
       else if (!term) cu[r + p * (idx[z] - n)] = v[z];
@@ -2209,6 +2209,7 @@ struct ModelOps {
   int n, m;
   int slack;  // n for an infeasible model (add_slack_controls), else 0
   int pcap;   // max constraint rows per knot of the backward kernels' LDS layout
+  int has_con;  // the model defines user constraint functions (ROW_USER_*)
   void (*slack_controls)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*cost_expansion)(const DevProblem*, const DevBuffers&, long long B, int N, int sqrt, int al, int* fail,
                          hipStream_t);
@@ -2463,6 +2464,7 @@ struct ModelLaunch {
     o.m = M::m;
     o.slack = ModelTraits<M>::slack;
     o.pcap = pcap_of<M>();
+    o.has_con = HasCon<M>::value ? 1 : 0;
     o.implicit = ModelTraits<M>::implicit_ok;
     o.slack_controls = slack_controls;
     o.cost_expansion = cost_expansion;

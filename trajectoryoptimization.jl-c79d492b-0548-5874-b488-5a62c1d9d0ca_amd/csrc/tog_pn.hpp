@@ -99,7 +99,7 @@ __device__ void pn_eval(const DevProblem* P, const DevBuffers& Bf, long long b, 
     }
     const int cnt = P->knot_cnt[k];
     const ConRow* rows = P->rows + P->knot_off[k];
-    for (int r = 0; r < cnt; r++) C[(size_t)k * pmax + r] = row_value(rows[r], xk, k < N - 1 ? U + (size_t)k * m : nullptr);
+    for (int r = 0; r < cnt; r++) C[(size_t)k * pmax + r] = row_value_m<M>(rows[r], xk, k < N - 1 ? U + (size_t)k * m : nullptr);
   }
   pn_sync();
 }
@@ -159,9 +159,9 @@ __device__ void pn_block_rows(const DevProblem* P, const DevBuffers& Bf, long lo
   }
   if (lane < w.na[j]) {
     const ConRow r = P->rows[P->knot_off[j] + w.act[j * pmax + lane]];
-    int idx[3];
-    double v[3];
-    const int nz = row_grad(r, X + (size_t)j * n, n, idx, v);
+    int idx[row_grad_cap<M>()];
+    double v[row_grad_cap<M>()];
+    const int nz = row_grad_m<M>(r, X + (size_t)j * n, j < N - 1 ? Bf.U + ((size_t)b * (N - 1) + j) * m : nullptr, idx, v);
     for (int z = 0; z < nz; z++) Yz[(rb + lane) + SM * idx[z]] = v[z];
   }
   pn_sync();
@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(64) k_pn_finish(const DevProblem* __restrict__
     const int cnt = P->knot_cnt[k];
     const ConRow* rows = P->rows + P->knot_off[k];
     for (int r = 0; r < cnt; r++)
-      C[(size_t)k * pmax + r] = row_value(rows[r], X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
+      C[(size_t)k * pmax + r] = row_value_m<M>(rows[r], X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
   }
   pn_sync();
   if (lane != 0) return;

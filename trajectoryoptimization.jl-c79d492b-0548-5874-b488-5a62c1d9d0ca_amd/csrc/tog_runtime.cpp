@@ -156,7 +156,7 @@ static bool host_chol_upper(const double* A, int n, double* U) {
 }
 
 // Flatten the ordered constraint sets into per-knot rows (src/constraint_sets.jl:64-131).
-static int build_rows(const tog_problem_desc* d, int slack, int pcap, std::vector<ConRow>& rows,
+static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_con, std::vector<ConRow>& rows,
                       std::vector<int>& off, std::vector<int>& cnt) {
   const int n = d->n, m = d->m, N = d->N;
   off.assign(N, 0);
@@ -206,6 +206,15 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, std::vecto
           if (!term)
             for (int i = 0; i < slack; i++) rows.push_back({ROW_USLACK, m - slack + i, 0.0, 0.0, 0.0, 0.0});
           break;
+        case TOG_CON_USER: {
+          if (!has_con) return fail(TOG_ERR_ARG, "TOG_CON_USER needs a user model plugin that defines con()");
+          const int where = (int)D[2];
+          if (con.count < 1 || con.count > PUSER) return fail(TOG_ERR_ARG, "user constraint: 1 <= p <= 16");
+          if ((term && where != 0) || (!term && where != 1))
+            for (int i = 0; i < con.count; i++)
+              rows.push_back({D[1] != 0.0 ? ROW_USER_EQ : ROW_USER_INEQ, i, D[0], (double)con.count, 0.0, 0.0});
+          break;
+        }
         default:
           return fail(TOG_ERR_ARG, "unknown constraint type");
       }
@@ -460,7 +469,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
 
   std::vector<ConRow> rows;
   std::vector<int> off, cnt;
-  int rc = build_rows(d, ops->slack, ops->pcap, rows, off, cnt);
+  int rc = build_rows(d, ops->slack, ops->pcap, ops->has_con, rows, off, cnt);
   if (rc) return rc;
   h->nrows = (int)rows.size();
   h->pmax = 0;

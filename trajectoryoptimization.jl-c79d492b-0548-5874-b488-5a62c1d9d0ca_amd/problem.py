@@ -144,18 +144,29 @@ struct {name} {{
   __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {{
     using namespace tog;
 {body}
-  }}
+  }}{con}
 }};
 
 TOG_PLUGIN({name})
 """
 
+_CON_TEMPLATE = """
+  static constexpr bool has_con = true;
+  template <class T>
+  __host__ __device__ __forceinline__ static void con(int fid, T* c, const T* x, const T* u) {{
+    using namespace tog;
+{body}
+  }}
+"""
 
-def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=None) -> Model:
+
+def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=None, con_body: str | None = None) -> Model:
     """``Model(f!, n, m)`` (src/model.jl:103-131) for user dynamics: ``f_body`` is the body of
     ``f(T* xd, const T* x, const T* u)`` in C++ over the scalar type ``T`` (double in rollouts,
     dual numbers in the Jacobian kernel, as ForwardDiff differentiates the Julia f!). Use
-    ``sin_``, ``cos_``, ``sqrt_``, ``inv_``. The plugin is compiled once with hipcc for gfx950
+    ``sin_``, ``cos_``, ``sqrt_``, ``inv_``. ``con_body`` (optional) is the body of the user
+    constraint functions ``con(int fid, T* c, const T* x, const T* u)`` that ``UserConstraint``
+    rows evaluate. The plugin is compiled once with hipcc for gfx950
     (cached by the hash of its source under ``csrc/plugins/``) and loaded with ``tog_model_load``."""
     import hashlib
     import subprocess
@@ -164,7 +175,11 @@ def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=N
     out_dir = pathlib.Path(build_dir) if build_dir else csrc / "plugins"
     out_dir.mkdir(parents=True, exist_ok=True)
     body = "\n".join("    " + ln for ln in f_body.strip().splitlines())
-    src = _PLUGIN_TEMPLATE.format(hdr=str(csrc / "tog_plugin.hpp"), name=name, n=int(n), m=int(m), body=body)
+    con = ""
+    if con_body:
+        con = _CON_TEMPLATE.format(body="\n".join("    " + ln for ln in con_body.strip().splitlines()))
+    src = _PLUGIN_TEMPLATE.format(hdr=str(csrc / "tog_plugin.hpp"), name=name, n=int(n), m=int(m), body=body,
+                                  con=con)
     key = hashlib.sha1(src.encode()).hexdigest()[:12]
     so = out_dir / f"gen_{name}_{key}.so"
     if not so.exists():
@@ -442,6 +457,44 @@ class GoalConstraint(_Constraint):
 
 def goal_constraint(xf):
     return GoalConstraint(xf)
+
+
+class UserConstraint(_Constraint):
+    """``Constraint{Inequality|Equality}(c!, n, m, p, label)`` with a user function
+    (src/constraints.jl:85-89; Jacobian by ForwardDiff, src/model.jl:460-489). The function is
+    the user model plugin's ``con(fid, c, x, u)`` (csrc/tog_plugin.hpp): it runs on the device,
+    its Jacobian over [x; u] by dual numbers. ``where``: "stage" (knots 1..N-1), "terminal" (knot
+    N, u = 0) or "both". ``host`` (optional): a numpy restatement ``f(x, u) -> c`` used only by
+    the host-side ``max_violation(prob)``."""
+
+    _WHERE = {"stage": 0, "terminal": 1, "both": 2}
+
+    def __init__(self, n, m, p, fid=0, equality=False, where="stage", label="user", host=None):
+        if not 1 <= p <= 16:
+            raise ValueError("user constraint: 1 <= p <= 16 outputs")
+        if where not in self._WHERE:
+            raise ValueError(f"where must be one of {sorted(self._WHERE)}")
+        self.n, self.m, self.p, self.fid = n, m, int(p), int(fid)
+        self.inequality = not equality
+        self.where, self.label, self.host = where, label, host
+
+    def length(self, kind="stage"):
+        if kind == "stage":
+            return self.p if self.where in ("stage", "both") else 0
+        return self.p if self.where in ("terminal", "both") else 0
+
+    def evaluate(self, x, u=None):
+        kind = "stage" if u is not None else "terminal"
+        if self.length(kind) == 0:
+            return np.zeros(0)
+        if self.host is None:
+            return np.full(self.p, np.nan)
+        return np.asarray(self.host(np.asarray(x), np.zeros(self.m) if u is None else np.asarray(u)),
+                          dtype=np.float64)
+
+    def to_abi(self):
+        return (abi.CON_USER, self.p, np.array([self.fid, 0.0 if self.inequality else 1.0,
+                                                 self._WHERE[self.where]], dtype=np.float64))
 
 
 def circle_constraint(x, x0, y0=None, r=None):

@@ -158,7 +158,7 @@ def car_sqrt_bp(constrained=False):
     return Problem(model_d, obj, np.ones((N - 1, m)), constraints=cons, x0=x0, N=N, dt=dt)
 
 
-def pendulum(integration="rk3", U0=None, model=None):
+def pendulum(integration="rk3", U0=None, model=None, stage_constraints=()):
     """problems/pendulum.jl:1-35: rk3, N=31, dt=0.15, Q=R=Qf=1e-3 I, xf=[π,0], |u|<=3 at
     k<N, goal at N, U=ones. ``model``: another continuous model with the pendulum's n, m (e.g. a
     user plugin of the same dynamics)."""
@@ -173,6 +173,8 @@ def pendulum(integration="rk3", U0=None, model=None):
     bnd = BoundConstraint(n, m, u_min=-3.0, u_max=3.0)
     for k in range(N - 1):
         cons[k] += bnd
+        for c in stage_constraints:
+            cons[k] += c
     cons[N - 1] += goal_constraint(xf)
     obj = LQRObjective(Q, R, Q, xf, N)
     return Problem(model_d, obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=dt)
@@ -476,14 +478,38 @@ xd[4] = u[1] - cw * x[4];
 """
 
 
+# user constraint functions of the unicycle: fid 0 a disc obstacle at (1, 0.5), r = 0.3; fid 1 the
+# traction limit a v <= 1 (a control-dependent row)
+UNICYCLE_CON = """
+if (fid == 0) {
+  const T dx = x[0] - 1.0, dy = x[1] - 0.5;
+  c[0] = -((dx * dx + dy * dy) - 0.09);
+} else {
+  c[0] = u[0] * x[3] - 1.0;
+}
+"""
+
+
 def unicycle_model():
-    """The unicycle with first-order actuators as a user model: x = [px, py, θ, v, ω], u = [a, α]."""
+    """The unicycle with first-order actuators as a user model: x = [px, py, θ, v, ω], u = [a, α],
+    with the user constraint functions UNICYCLE_CON."""
     from .problem import user_model
 
-    return user_model(UNICYCLE_F, 5, 2, name="Unicycle")
+    return user_model(UNICYCLE_F, 5, 2, name="Unicycle", con_body=UNICYCLE_CON)
 
 
-def unicycle(model=None, B=1, offset=0, N=51, dt=0.1):
+def unicycle_constraints(n=5, m=2):
+    """UserConstraint rows of the unicycle's con(): the obstacle (fid 0) and the traction limit (fid 1),
+    with host restatements for max_violation(prob)."""
+    from .problem import UserConstraint
+
+    obs = UserConstraint(n, m, 1, fid=0, label="obstacle",
+                         host=lambda x, u: np.array([-((x[0] - 1.0) ** 2 + (x[1] - 0.5) ** 2 - 0.09)]))
+    trac = UserConstraint(n, m, 1, fid=1, label="traction", host=lambda x, u: np.array([u[0] * x[3] - 1.0]))
+    return obs, trac
+
+
+def unicycle(model=None, B=1, offset=0, N=51, dt=0.1, user_constraints=False):
     """Drive the unicycle from rest at the origin to xf = (2, 1, 0, 0, 0): rk3, LQR objective
     (Q = 1e-2 I, R = 1e-1 I, Qf = 100 I), |u| <= 2 at every stage knot, goal at N. U0 = 0.1 N(0,1)
     (seed 6000+b)."""
@@ -493,8 +519,11 @@ def unicycle(model=None, B=1, offset=0, N=51, dt=0.1):
     U0 = _per_traj_rng(6000 + offset, B, lambda r: 0.1 * r.standard_normal((N - 1, m)))
     cons = Constraints(N)
     bnd = BoundConstraint(n, m, u_min=-2.0, u_max=2.0)
+    extra = unicycle_constraints(n, m) if user_constraints else ()
     for k in range(N - 1):
         cons[k] += bnd
+        for c in extra:
+            cons[k] += c
     cons[N - 1] += goal_constraint(xf)
     obj = LQRObjective(1e-2 * np.eye(n), 1e-1 * np.eye(m), 100.0 * np.eye(n), xf, N)
     return Problem(model_d, obj, U0 if B > 1 else U0[0], constraints=cons, x0=np.zeros((B, n)) if B > 1 else np.zeros(n),
