@@ -336,8 +336,8 @@ def test_gpu_quadrotor_maze_step_level(tog, oracle, gpu, sqrt):
 
 @pytest.mark.gpu
 def test_gpu_infeasible_error_paths(tog, gpu):
-    """slack_controls on a plain handle, a slack constraint in a plain problem and the unbuilt Kuka
-    slack variant fail loudly through the ABI (no silent fallback)."""
+    """slack_controls on a plain handle and a slack constraint in a plain problem fail loudly through
+    the ABI (no silent fallback)."""
     prob, opts = tog.Problems.config_quadrotor(B=2)
     h = tog.AugmentedLagrangianSolver(prob, opts).handle
     with pytest.raises(RuntimeError, match="TOG_PROB_INFEASIBLE"):
@@ -346,7 +346,22 @@ def test_gpu_infeasible_error_paths(tog, gpu):
     bad.constraints[0] = bad.constraints[0] + tog.infeasible_constraints(13, 4)
     with pytest.raises(RuntimeError, match="TOG_CON_INFEASIBLE"):
         tog.AugmentedLagrangianSolver(bad, opts)
-    pk, ok = tog.Problems.config_kuka(B=1)
-    pk.X = np.zeros((pk.N, 14))
-    with pytest.raises(RuntimeError, match="model not built"):
-        tog.ALTROSolver(tog.infeasible_problem(pk, 1.0), tog.ALTROSolverOptions(opts_al=ok))
+
+
+@pytest.mark.gpu
+def test_gpu_infeasible_kuka(tog, oracle, gpu):
+    """add_slack_controls on the Kuka RBD model (src/model.jl:761-779 over src/model.jl:394-447): m = 7 +
+    14 slack controls (LDS backward kernel). Infeasible-start AL solves from a straight-line joint
+    guess x0 -> xf, against the oracle per trajectory (final X, U within 1e-6, equal iteration counts)."""
+    pk, ok = tog.Problems.config_kuka(B=2)
+    N = pk.N
+    t = np.linspace(0.0, 1.0, N)[None, :, None]
+    pk.X = pk.x0[:, None, :] + (pk.xf - pk.x0)[:, None, :] * t
+    opts = tog.ALTROSolverOptions(opts_al=ok, resolve_feasible_problem=False)
+    ref = pk.copy()
+    solver = tog.solve_b(pk, opts)
+    for b in range(pk.B):
+        Xo, Uo, si, _ = oracle.solve_altro_infeasible(ref, opts, b)
+        assert rel(pk._X[b], Xo) < TOL_SOLVE, b
+        assert rel(pk._U[b], Uo) < TOL_SOLVE, b
+        assert int(solver.stats["iterations_total"][b]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS]), b

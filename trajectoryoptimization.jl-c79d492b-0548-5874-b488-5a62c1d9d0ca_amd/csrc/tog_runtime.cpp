@@ -30,6 +30,7 @@ const ModelOps* ops_inf_cartpole();
 const ModelOps* ops_inf_quadrotor();
 const ModelOps* ops_inf_car();
 const ModelOps* ops_inf_pendulum();
+const ModelOps* ops_inf_kuka();
 }  // namespace tog
 
 static thread_local std::string g_err;
@@ -123,8 +124,9 @@ static const ModelOps* ops_for(int model, bool infeasible, const tog_model* user
       case TOG_MODEL_QUADROTOR: return ops_inf_quadrotor();
       case TOG_MODEL_CAR: return ops_inf_car();
       case TOG_MODEL_PENDULUM: return ops_inf_pendulum();
+      case TOG_MODEL_KUKA: return ops_inf_kuka();
     }
-    return nullptr;  // the Kuka infeasible variant is not built
+    return nullptr;
   }
   switch (model) {
     case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_double_integrator();
