@@ -92,7 +92,8 @@ enum tog_constraint_type {
   /* BoundConstraint(n,m; x_min,x_max,u_min,u_max, trim=true), src/constraints.jl:155-188.
      data = [x_max(n), x_min(n), u_max(m), u_min(m)]; ±INFINITY entries are trimmed. */
   TOG_CON_BOUND = 0,
-  /* goal_constraint(xf), src/constraints.jl:299-304. Terminal equality. data = xf(n) */
+  /* goal_constraint(xf), src/constraints.jl:299-304. Terminal equality. data = xf(count): rows
+     x[1:count] - xf (the goal's inds; count 0 = n, count < n for a minimum-time state [x; τ]) */
   TOG_CON_GOAL = 1,
   /* `count` circle_constraint rows (src/utils.jl:140-144) on x[1],x[2]:
      c = -((x1-x0)^2 + (x2-y0)^2 - r^2). data = [x0,y0,r]*count. Stage inequality. */
@@ -107,7 +108,10 @@ enum tog_constraint_type {
   /* Constraint{Inequality|Equality}(c!, n, m, p) with a user function (src/constraints.jl:85-89):
      count = p rows, data = [fid, equality (0/1), where (0 stage knots, 1 terminal knot, 2 both)];
      evaluated by the user model plugin's con(fid, c, x, u), Jacobian by dual numbers */
-  TOG_CON_USER = 5
+  TOG_CON_USER = 5,
+  /* mintime_equality(n, m) (src/solvers/altro/minimum_time.jl:106-124): h_k - τ_k = 0, stage knots;
+     count and data unused (TOG_PROB_MIN_TIME problems) */
+  TOG_CON_MIN_TIME_EQ = 6
 };
 
 /* problem flags (tog_problem_desc.flags) */
@@ -116,7 +120,13 @@ enum tog_problem_flag {
      add_slack_controls(model) (src/model.jl:761-779), x+ = f_d(x, u[1:m]) + u[m+1:m+n], so
      desc.m = m_model + n and R, H, r, the bound data are given for the augmented controls
      (R = blockdiag(R, R_inf I / dt), H and r zero-padded). */
-  TOG_PROB_INFEASIBLE = 1
+  TOG_PROB_INFEASIBLE = 1,
+  /* minimum_time_problem(prob, R_min_time, dt_max, dt_min) (src/solvers/altro/minimum_time.jl:2-34):
+     model add_min_time_controls(model) (n = n_base + 1 states [x; τ], m = m_base + 1 controls [u; h],
+     dt_k = h_k²), objective MinTimeCost with weight R_min_time (Q, R, H, q, r, Qf, qf the base cost's,
+     zero-padded to n, m), constraints from mintime_constraints (h bounds in the BoundConstraint,
+     TOG_CON_MIN_TIME_EQ rows). Std backward pass only (there is no sqrt MinTimeCost expansion). */
+  TOG_PROB_MIN_TIME = 2
 };
 
 typedef struct tog_constraint {
@@ -163,6 +173,8 @@ typedef struct tog_problem_desc {
   const int32_t* knot_set;
   /* model == TOG_MODEL_USER: the loaded user model (tog_model_load), else ignored */
   const struct tog_model* user_model;
+  /* TOG_PROB_MIN_TIME: MinTimeCost's R_min_time (ALTROSolverOptions.R_minimum_time) */
+  double R_min_time;
 } tog_problem_desc;
 
 /* ---------------------------------------------------------------- options */

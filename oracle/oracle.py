@@ -248,3 +248,15 @@ def solve_altro_infeasible(prob, opts, b=0):
         sf.solve()
         X, U = sf.get("X"), sf.get("U")
     return X, U, si, sf
+
+
+def solve_altro_min_time(prob, opts, b=0):
+    """Oracle restatement of ``solve!(prob, ::ALTROSolverOptions)`` for tf = 0 (altro_methods.jl:98-124,
+    minimum_time.jl:2-34) for trajectory ``b``: returns (X[1:n], U[1:m], h, solver). Mirrors
+    ``solvers._solve_altro_min_time``."""
+    n, m = prob.model.n, prob.model.m
+    pmt = _pkg.minimum_time_problem(prob, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    s = OracleSolver(pmt, opts.opts_al, b)
+    s.solve()
+    X, U = s.get("X"), s.get("U")
+    return X[:, :n].copy(), U[:, :m].copy(), U[:, m].copy(), s

@@ -1115,6 +1115,8 @@ typedef struct {
 typedef struct oc_solver {
   int model, integ, n, m, N;
   int slack, mb; /* infeasible problem: slack = n slack controls after the mb model controls */
+  int mt;        /* minimum-time problem (add_min_time_controls): x = [x_b; τ], u = [u_b; h], dt_k = h_k² */
+  double R_mt;   /* MinTimeCost R_min_time */
   double dt;
   double *Q, *R, *H, *q, *r, c, *Qf, *qf, cf;
   int nsets;
@@ -1170,12 +1172,14 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
       oc->p_term = cx + cxn; /* length(bnd, :terminal) constraints.jl:244-252 */
       break;
     }
-    case TOG_CON_GOAL:
-      for (int i = 0; i < n; i++) oc->xf[i] = tc->data[i];
+    case TOG_CON_GOAL: { /* count: rows x[1:count] - xf (inds, constraints.jl:303); 0 = n */
+      const int ng = tc->count > 0 ? tc->count : n;
+      for (int i = 0; i < ng; i++) oc->xf[i] = tc->data[i];
       oc->inequality = 0;
       oc->p_stage = 0; /* terminal-only (term=:terminal) */
-      oc->p_term = n;
+      oc->p_term = ng;
       break;
+    }
     case TOG_CON_CIRCLES:
       oc->count = tc->count;
       memcpy(oc->obs, tc->data, sizeof(double) * 3 * tc->count);
@@ -1194,6 +1198,11 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
       oc->inequality = 0;
       oc->p_stage = n;
       oc->p_term = 0; /* :stage only */
+      break;
+    case TOG_CON_MIN_TIME_EQ: /* mintime_equality(n, m) minimum_time.jl:106-124, :stage */
+      oc->inequality = 0;
+      oc->p_stage = 1;
+      oc->p_term = 0;
       break;
   }
 }
@@ -1249,7 +1258,7 @@ static int con_eval(const oc_con* oc, int n, int m, const double* x, const doubl
       break;
     case TOG_CON_GOAL:
       if (term) {
-        for (int i = 0; i < n; i++) {
+        for (int i = 0; i < oc->p_term; i++) {
           v[r] = x[i] - oc->xf[i];
           if (Jx) Jx[r + ldj * i] = 1.0;
           r++;
@@ -1279,6 +1288,14 @@ static int con_eval(const oc_con* oc, int n, int m, const double* x, const doubl
           if (Ju) Ju[r + ldj * (mb + i)] = 1.0;
           r++;
         }
+      }
+      break;
+    case TOG_CON_MIN_TIME_EQ: /* con_eq(v, x, u): v[1] = u[end] - x[end]; ∇ = [0 .. -1 | 0 .. 1] */
+      if (!term) {
+        v[r] = u[m - 1] - x[n - 1];
+        if (Jx) Jx[r + ldj * (n - 1)] = -1.0;
+        if (Ju) Ju[r + ldj * (m - 1)] = 1.0;
+        r++;
       }
       break;
     case TOG_CON_SPHERES:
@@ -1333,6 +1350,8 @@ static void desc_load(oc_solver* s, const tog_problem_desc* d) {
   s->dt = d->dt;
   s->slack = (d->flags & TOG_PROB_INFEASIBLE) ? d->n : 0;
   s->mb = d->m - s->slack;
+  s->mt = (d->flags & TOG_PROB_MIN_TIME) ? 1 : 0;
+  s->R_mt = s->mt ? d->R_min_time : 0.0;
   int n = s->n, m = s->m, N = s->N;
   s->Q = malloc(sizeof(double) * n * n);
   memcpy(s->Q, d->Q, sizeof(double) * n * n);
@@ -1473,7 +1492,15 @@ static double terminal_cost(const oc_solver* s, const double* x) {
 static double obj_cost(const oc_solver* s, const double* X, const double* U) {
   int n = s->n, m = s->m, N = s->N;
   double J = 0.0;
-  for (int k = 0; k < N - 1; k++) J += stage_cost(s, X + (size_t)k * n, U + (size_t)k * m, s->dt);
+  for (int k = 0; k < N - 1; k++) {
+    const double* u = U + (size_t)k * m;
+    if (s->mt) { /* MinTimeCost (minimum_time.jl:148): stage_cost(cost, x, u, h) + R_min_time u[end]^2, h = get_dt */
+      const double h = u[m - 1];
+      J += stage_cost(s, X + (size_t)k * n, u, h * h) + s->R_mt * (h * h);
+    } else {
+      J += stage_cost(s, X + (size_t)k * n, u, s->dt);
+    }
+  }
   J += terminal_cost(s, X + (size_t)(N - 1) * n);
   return J;
 }
@@ -1532,6 +1559,12 @@ OC_EXPORT double oc_cost_bar(oc_solver* s, int al) { return cost(s, al, s->Xb, s
 /* evaluate!(x+, model, x, u, dt) of the solver's model. For an infeasible problem this is
    add_slack_controls (src/model.jl:761-779): f!(x+, x, u[1:m], dt) then x+ .+= u[m+1:m+n]. */
 static void traj_f(const oc_solver* s, double* xn, const double* x, const double* u) {
+  if (s->mt) { /* add_min_time_controls f!: h = u[end]; model.f(x+, x, u, h^2); x+[n̄] = h (minimum_time.jl:91-95) */
+    const double h = u[s->m - 1];
+    oc_discrete_f(s->model, s->integ, xn, x, u, h * h);
+    xn[s->n - 1] = h;
+    return;
+  }
   oc_discrete_f(s->model, s->integ, xn, x, u, s->dt);
   for (int i = 0; i < s->slack; i++) xn[i] += u[s->mb + i];
 }
@@ -1540,6 +1573,22 @@ static void traj_f(const oc_solver* s, double* xn, const double* x, const double
    columns [x; u[1:m]] and dt, and Diagonal(1.0I, n) in the slack columns (src/model.jl:771-774). */
 static void traj_jacobian(const oc_solver* s, double* F, const double* x, const double* u) {
   int n = s->n, mb = s->mb, m = s->m;
+  if (s->mt) {
+    /* ∇f! of add_min_time_controls (minimum_time.jl:97-101): model.∇f(view(Z, idx.x, idx2), x, u, h^2) with
+       idx2 = [x columns; u columns + n̄; last], Z[idx.x, end] .*= 2h, Z[n̄, end] = 1 */
+    const int nb = n - 1, mbb = m - 1;
+    const double h = u[m - 1];
+    double Z[16 * (16 + OM + 1)];
+    oc_discrete_jacobian(s->model, s->integ, Z, x, u, h * h); /* nb x (nb + mbb + 1) */
+    memset(F, 0, sizeof(double) * n * (n + m + 1));
+    for (int j = 0; j < nb; j++)
+      for (int i = 0; i < nb; i++) F[i + n * j] = Z[i + nb * j];
+    for (int j = 0; j < mbb; j++)
+      for (int i = 0; i < nb; i++) F[i + n * (n + j)] = Z[i + nb * (nb + j)];
+    for (int i = 0; i < nb; i++) F[i + n * (n + mbb)] = Z[i + nb * (nb + mbb)] * (2.0 * h);
+    F[nb + n * (n + mbb)] = 1.0;
+    return;
+  }
   if (!s->slack) {
     oc_discrete_jacobian(s->model, s->integ, F, x, u, s->dt);
     return;
@@ -1635,25 +1684,48 @@ static void expansion_stage(oc_solver* s, int k) {
   int n = s->n, m = s->m;
   const double* x = Xk(s, k);
   const double* u = Uk(s, k);
-  double dt = s->dt;
+  /* minimum time: τ = u[end], dt = τ^2 (MinTimeCost cost_expansion!, minimum_time.jl:155-188) */
+  double dt = s->mt ? u[m - 1] * u[m - 1] : s->dt;
   double* Qx = s->Qx + (size_t)k * n;
   double* Qu = s->Qu + (size_t)k * m;
+  double gx[16], gu[OM]; /* unscaled Qx, Qu (MinTimeCost's tmp and Q.ux rows) */
   /* Q.x .= cost.Q*x + cost.q + cost.H'*u ; Q.u .= cost.R*u + cost.r + cost.H*x ; then Q*dt */
   for (int i = 0; i < n; i++) {
     double a = 0, b = 0;
     for (int j = 0; j < n; j++) a = fma(s->Q[IDX(i, j, n)], x[j], a);
     for (int j = 0; j < m; j++) b = fma(s->H[IDX(j, i, m)], u[j], b);
-    Qx[i] = ((a + s->q[i]) + b) * dt;
+    gx[i] = (a + s->q[i]) + b;
+    Qx[i] = gx[i] * dt;
   }
   for (int i = 0; i < m; i++) {
     double a = 0, b = 0;
     for (int j = 0; j < m; j++) a = fma(s->R[IDX(i, j, m)], u[j], a);
     for (int j = 0; j < n; j++) b = fma(s->H[IDX(i, j, m)], x[j], b);
-    Qu[i] = ((a + s->r[i]) + b) * dt;
+    gu[i] = (a + s->r[i]) + b;
+    Qu[i] = gu[i] * dt;
   }
   for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = s->Q[i] * dt;
   for (int i = 0; i < m * m; i++) s->Quu[(size_t)k * m * m + i] = s->R[i] * dt;
   for (int i = 0; i < m * n; i++) s->Qux[(size_t)k * m * n + i] = s->H[i] * dt;
+  if (s->mt) {
+    /* ℓ1 = stage_cost(cost.cost, x, u); tmp = 2τ Qu; Q.u[end] = τ(2ℓ1 + R); Q.uu[u, end] = tmp;
+       Q.uu[end, end] = 2ℓ1 + R; Q.ux[end, x] = 2τ Qx'; Q.x[end] = R x[end]; Q.xx[end, end] = R */
+    const double R = s->R_mt, tau = u[m - 1];
+    const double l1 = stage_cost(s, x, u, 1.0);
+    const double w = 2.0 * l1 + R, t2 = 2.0 * tau;
+    double* Quu = s->Quu + (size_t)k * m * m;
+    double* Qux = s->Qux + (size_t)k * m * n;
+    for (int i = 0; i < m - 1; i++) {
+      const double tmp = t2 * gu[i];
+      Quu[IDX(i, m - 1, m)] = tmp;
+      Quu[IDX(m - 1, i, m)] = tmp;
+    }
+    Qu[m - 1] = tau * w;
+    Quu[IDX(m - 1, m - 1, m)] = w;
+    for (int j = 0; j < n - 1; j++) Qux[IDX(m - 1, j, m)] = t2 * gx[j];
+    Qx[n - 1] = R * x[n - 1];
+    s->Qxx[(size_t)k * n * n + IDX(n - 1, n - 1, n)] = R;
+  }
 }
 static void expansion_terminal(oc_solver* s) {
   int n = s->n, k = s->N - 1;
@@ -1663,6 +1735,10 @@ static void expansion_terminal(oc_solver* s) {
     double a = 0;
     for (int j = 0; j < n; j++) a = fma(s->Qf[IDX(i, j, n)], x[j], a);
     s->Qx[(size_t)k * n + i] = a + s->qf[i];
+  }
+  if (s->mt) { /* MinTimeCost terminal: S.xx[end,end] = R_min_time, S.x[end] = R_min_time xN[end] */
+    s->Qxx[(size_t)k * n * n + IDX(n - 1, n - 1, n)] = s->R_mt;
+    s->Qx[(size_t)k * n + n - 1] = s->R_mt * x[n - 1];
   }
 }
 

@@ -1,0 +1,130 @@
+"""Minimum time: ``minimum_time_problem`` (src/solvers/altro/minimum_time.jl:2-34)
+solved by ALTRO's AL phase, on the CPU oracle and on the device.
+
+The augmented model carries the time step as a control: x = [x; τ], u = [u; h], dt_k = h_k²
+(add_min_time_controls, :83-104), the objective is MinTimeCost (:142-200) and the constraints gain the h
+bounds and h_k = τ_k (mintime_constraints, :125-141). The reference's own thresholds come from
+test/minimum_time_tests.jl (pendulum and the box parallel park): the minimum-time solve must at least halve
+(pendulum) / cut by a quarter (car) the fixed-time duration, reach the goal to 1e-3 and satisfy the
+constraints. The device is held to the oracle: X, U and h within 1e-6 and equal iteration counts.
+"""
+import math
+
+import numpy as np
+import pytest
+
+
+def pendulum_case(tog):
+    """test/minimum_time_tests.jl:1-63."""
+    model_d = tog.rk3(tog.Dynamics.pendulum)
+    n, m, N = 2, 1, 31
+    Q, R = 1e-3 * np.eye(n), 1e-3 * np.eye(m)
+    xf, x0 = np.array([math.pi, 0.0]), np.zeros(n)
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(), iterations=50, penalty_scaling=10.0)
+    opts = tog.ALTROSolverOptions(opts_al=al, R_minimum_time=15.0, dt_max=0.15, dt_min=1.0e-3)
+
+    def make(U, dt, tf=None):
+        cons = tog.Constraints(N)
+        bnd = tog.BoundConstraint(n, m, u_min=-5.0, u_max=5.0)
+        for k in range(N - 1):
+            cons[k] += bnd
+        cons[N - 1] += tog.goal_constraint(xf)
+        return tog.Problem(model_d, tog.LQRObjective(Q, R, Q, xf, N), U, constraints=cons, dt=dt, x0=x0, N=N, tf=tf)
+
+    return make, opts, xf, np.ones((N - 1, m)), 0.15, 0.15 / 2.0, (0.5, 1.0)
+
+
+def car_case(tog):
+    """test/minimum_time_tests.jl:65-121 (box parallel park)."""
+    model_d = tog.discretize_model(tog.Dynamics.car, "rk4")
+    n, m, N = 3, 2, 51
+    x0, xf = np.zeros(3), np.array([0.0, 1.0, 0.0])
+    Qf, Q, R = 100.0 * np.eye(n), 1e-2 * np.eye(n), 1e-2 * np.eye(m)
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(), iterations=30, penalty_scaling=10.0)
+    opts = tog.ALTROSolverOptions(opts_al=al, R_minimum_time=40.0, dt_max=0.2, dt_min=1.0e-3)
+    bnd1 = tog.BoundConstraint(n, m, u_min=-2.0, u_max=2.0)
+    bnd2 = tog.BoundConstraint(n, m, x_min=[-0.25, -0.001, -math.inf], x_max=[0.25, 1.001, math.inf],
+                               u_min=-2.0, u_max=2.0)
+
+    def make(U, dt, tf=None):
+        cons = tog.Constraints(N)
+        cons[0] += bnd1
+        for k in range(1, N - 1):
+            cons[k] += bnd2
+        cons[N - 1] += tog.goal_constraint(xf)
+        return tog.Problem(model_d, tog.LQRObjective(Q, R, Qf, xf, N), U, constraints=cons, dt=dt, x0=x0, N=N, tf=tf)
+
+    return make, opts, xf, np.ones((N - 1, m)), 0.06, 0.06, (0.75, 2.1)
+
+
+CASES = {"pendulum": pendulum_case, "car": car_case}
+
+
+def test_mintime_constraint_sets(tog):
+    """test/minimum_time_tests.jl:39-47: lengths of mintime_constraints' sets."""
+    make, *_ = pendulum_case(tog)
+    prob = make(np.ones((30, 1)), 0.15)
+    pc = tog.mintime_constraints(prob)
+    assert (len(pc[0]), len(pc[1]), len(pc[prob.N - 1])) == (1, 2, 2)
+    pmt = tog.minimum_time_problem(prob, 15.0, 0.15, 1e-3)
+    assert (pmt.model.n, pmt.model.m, pmt.tf) == (3, 2, 0.0) and pmt.model.min_time
+    assert np.all(pmt._U[0, :, 1] == math.sqrt(0.15)) and np.all(pmt._X[0, :, 2] == math.sqrt(0.15))
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_oracle_min_time_reference_thresholds(tog, oracle, case):
+    """The oracle's minimum-time solve meets test/minimum_time_tests.jl's assertions."""
+    make, opts, xf, U0, dt, dt_mt, (frac, tmax) = CASES[case](tog)
+    p = make(U0, dt)
+    s = oracle.OracleSolver(p, opts.opts_al, 0)
+    s.solve()
+    tt = dt * (p.N - 1)
+    pm = make(s.get("U"), dt_mt, tf="min")
+    X, U, h, _ = oracle.solve_altro_min_time(pm, opts, 0)
+    tt_mt = float(np.sum(h ** 2))
+    assert tt_mt < frac * tt and tt_mt < tmax
+    assert np.max(np.abs(X[-1] - xf)) < 1e-3
+    pm._X[0], pm._U[0] = X, U
+    assert tog.max_violation(pm) < opts.opts_al.constraint_tolerance
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_gpu_min_time_equals_oracle(tog, oracle, gpu, case):
+    """solve_b(prob, ALTROSolverOptions) with tf = :min on the device vs the oracle: X, U, h within
+    1e-6, equal iteration counts, and the reference's thresholds."""
+    make, opts, xf, U0, dt, dt_mt, (frac, tmax) = CASES[case](tog)
+    p = make(U0, dt)
+    s = oracle.OracleSolver(p, opts.opts_al, 0)
+    s.solve()
+    pm = make(s.get("U"), dt_mt, tf="min")
+    ref = pm.copy()
+    solver = tog.solve_b(pm, opts)
+    Xo, Uo, ho, so = oracle.solve_altro_min_time(ref, opts, 0)
+    scale = lambda a: max(1.0, float(np.max(np.abs(a))))  # noqa: E731
+    assert np.max(np.abs(pm._X[0] - Xo)) <= 1e-6 * scale(Xo)
+    assert np.max(np.abs(pm._U[0] - Uo)) <= 1e-6 * scale(Uo)
+    assert np.max(np.abs(pm.h[0] - ho)) <= 1e-6
+    assert int(solver.stats["iterations_total"][0]) == int(so.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+    tt_mt = tog.total_time(pm)
+    assert tt_mt < frac * dt * (p.N - 1) and tt_mt < tmax
+
+
+@pytest.mark.gpu
+def test_gpu_min_time_jacobian(tog, oracle, gpu):
+    """∇f! of add_min_time_controls on the device (k_jacobian_mt) vs the oracle's, per knot."""
+    make, opts, *_ = car_case(tog)
+    p = make(np.ones((50, 2)) * 0.3, 0.06)
+    pmt = tog.minimum_time_problem(p, 40.0, 0.2, 1e-3)
+    h = tog.ALTROSolver(pmt, opts).handle
+    h.upload_state(pmt)
+    tog.abi.check(h.lib, h.lib.tog_rollout_open_loop(h.h))
+    tog.abi.check(h.lib, h.lib.tog_jacobians(h.h))
+    A, B = h.get(tog.abi.FIELD_A)[0], h.get(tog.abi.FIELD_B)[0]
+    o = oracle.OracleSolver(pmt, opts.opts_al, 0)
+    o.rollout_open_loop()
+    o.jacobians()
+    Ao, Bo = o.get("A"), o.get("B")
+    assert np.allclose(A, Ao, rtol=1e-13, atol=1e-15)
+    assert np.allclose(B, Bo, rtol=1e-13, atol=1e-15)
+    assert np.all(B[:, 3, 2] == 1.0) and np.all(A[:, 3, :] == 0.0)  # τ+ = h

@@ -16,7 +16,8 @@ from .problem import (BoundConstraint, CircleConstraints, Constraints, Constrain
                       SphereConstraints, circle_constraint, discretize_model, goal_constraint, initial_controls_b,
                       initial_states_b, max_violation, midpoint, midpoint_implicit, rk3, rk3_implicit, rk4, set_x0_b, sphere_constraint, add_slack_controls,
                       InfeasibleConstraint, infeasible_constraints, infeasible_problem, line_trajectory, user_model,
-                      UserModelPlugin, UserConstraint)
+                      UserModelPlugin, UserConstraint, add_min_time_controls,
+                      minimum_time_problem, mintime_constraints, total_time, MinTimeEquality)
 from .solvers import (Expansion, AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
                       AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, ProjectedNewtonSolver,
                       ProjectedNewtonSolverOptions, solve, solve_b, solver_name, to_tog_options, to_tog_pn_options)

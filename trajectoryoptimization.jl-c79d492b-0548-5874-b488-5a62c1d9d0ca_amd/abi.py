@@ -26,8 +26,9 @@ MODEL_USER = 100  # Model(f!, n, m) from a plugin (tog_model_load)
 OK, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 
 RK3, RK4, MIDPOINT, RK3_IMPLICIT, MIDPOINT_IMPLICIT = 0, 1, 2, 3, 4
-CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE, CON_USER = range(6)
+CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE, CON_USER, CON_MIN_TIME_EQ = range(7)
 PROB_INFEASIBLE = 1  # tog_problem_flag
+PROB_MIN_TIME = 2
 MODE_ILQR, MODE_AL = 0, 1
 
 (FIELD_X, FIELD_U, FIELD_XBAR, FIELD_UBAR, FIELD_K, FIELD_D, FIELD_A, FIELD_B, FIELD_S, FIELD_SX,
@@ -77,7 +78,7 @@ class tog_problem_desc(C.Structure):
         ("Qf", _dp), ("qf", _dp), ("cf", C.c_double),
         ("n_sets", C.c_int32), ("reserved1", C.c_int32),
         ("sets", C.POINTER(tog_constraint_set)), ("knot_set", _ip),
-        ("user_model", C.c_void_p),
+        ("user_model", C.c_void_p), ("R_min_time", C.c_double),
     ]
 
 
@@ -154,7 +155,7 @@ class DescBuilder:
     """
 
     def __init__(self, model, integrator, n, m, N, dt, Q, R, H, q, r, c, Qf, qf, cf, sets, knot_set,
-                 batch=1, flags=0, user_model=None):
+                 batch=1, flags=0, user_model=None, R_min_time=0.0):
         self._keep = []
 
         def arr(x, shape):
@@ -196,6 +197,7 @@ class DescBuilder:
         self._keep.append(ks)
         d.knot_set = ks.ctypes.data_as(_ip)
         d.user_model = user_model
+        d.R_min_time = float(R_min_time)
         self.desc = d
 
 

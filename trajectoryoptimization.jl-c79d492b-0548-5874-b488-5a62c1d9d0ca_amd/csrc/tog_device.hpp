@@ -37,7 +37,8 @@ enum RowType : int {
   // Constraint{S}(c!, n, m, p) with a user function (src/constraints.jl:85-89, Jacobian by ForwardDiff):
   // row idx of the plugin model's con(fid = a, c, x, u) (p = b outputs)
   ROW_USER_INEQ = 8,
-  ROW_USER_EQ = 9
+  ROW_USER_EQ = 9,
+  ROW_MT_EQ = 10  // c = u[a] - x[idx] (equality; mintime_equality, src/solvers/altro/minimum_time.jl:106-124)
 };
 constexpr int PUSER = 16;  // max outputs of one user constraint function
 
@@ -63,6 +64,8 @@ struct DevProblem {
   // zeros off the diagonal, so the diagonal fast paths are bit-identical to them.
   int diag_cost;  // 0 dense; 1 diagonal Q/R/Qf, H = 0; 2 = 1 with +0.0 off-diagonals (literal zeros)
   int pad1;
+  double R_min_time;  // MinTimeCost weight (minimum-time problems; Q, R, H, q, r, Qf, qf are the base
+                      // cost's, zero-padded to the augmented sizes)
   const int* knot_off;  // [N] first row of knot k
   const int* knot_cnt;  // [N] rows at knot k (p_k)
   const ConRow* rows;
@@ -731,17 +734,36 @@ struct Infeasible {
   }
 };
 
+// add_min_time_controls(model) (src/solvers/altro/minimum_time.jl:83-104): state [x; τ], control
+// [u; h], x+ = f_d(x, u, h²), τ+ = h. The time step of every knot is a control (dt_k = h_k², get_dt
+// src/problem.jl:300-314); the objective is MinTimeCost (:142-200) and the problem gets the h bounds and
+// the h_k = τ_k equalities (mintime_constraints, :125-141).
+template <class Mb>
+struct MinTime {
+  using Base = Mb;
+  static constexpr int n = Mb::n + 1, m = Mb::m + 1, id = Mb::id;
+};
+
 template <class M>
 struct ModelTraits {
   using Base = M;
   static constexpr int slack = 0;
   static constexpr bool implicit_ok = M::n <= 4;  // implicit integrators instantiated
+  static constexpr bool min_time = false;
+};
+template <class Mb>
+struct ModelTraits<MinTime<Mb>> {
+  using Base = Mb;
+  static constexpr int slack = 0;
+  static constexpr bool implicit_ok = false;
+  static constexpr bool min_time = true;
 };
 template <class Mb>
 struct ModelTraits<Infeasible<Mb>> {
   using Base = Mb;
   static constexpr int slack = Mb::n;
   static constexpr bool implicit_ok = false;
+  static constexpr bool min_time = false;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -931,11 +953,17 @@ __host__ __device__ __forceinline__ void implicit_step(T* y, const T* x, const T
 // Explicit Runge-Kutta discretisation with runtime dt (src/integration.jl:115-158). Running-sum
 // form keeps the reference's left-to-right association: RK4 ((k1 + 2k2) + 2k3) + k4,
 // RK3 (k1 + 4k2) + k3, with RK3's third stage at (x - k1) + 2k2.
-template <class M, int INTEG, class T>
-__host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, double dt) {
-  if constexpr (ModelTraits<M>::slack > 0) {
+template <class M, int INTEG, class T, class TD = double>
+__host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const T* u, TD dt) {
+  if constexpr (ModelTraits<M>::min_time) {
+    using Mb = typename ModelTraits<M>::Base;  // f!(x+, x, u, dt): h = u[end]; model.f(x+, x, u, h^2); x+[n̄] = h
+    const T h = u[Mb::m];
+    discrete_step<Mb, INTEG, T, T>(xn, x, u, h * h);
+    xn[Mb::n] = h;
+    (void)dt;
+  } else if constexpr (ModelTraits<M>::slack > 0) {
     using Mb = typename ModelTraits<M>::Base;
-    discrete_step<Mb, INTEG, T>(xn, x, u, dt);  // model.f(x+, x, u[idx.u], dt)
+    discrete_step<Mb, INTEG, T, TD>(xn, x, u, dt);  // model.f(x+, x, u[idx.u], dt)
 #pragma unroll
     for (int i = 0; i < Mb::n; i++) xn[i] = xn[i] + u[Mb::m + i];  // x+ .+= u[idx.inf]
   } else {
@@ -947,7 +975,7 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
     // midpoint (src/integration.jl:26-33): ẋ = f(x,u); ẋ .*= dt/2; ẋ = f(x + ẋ, u); x+ = x + ẋ*dt
     T k[n], t[n];
     M::f(k, x, u);
-    const double h = dt / 2.0;
+    const TD h = dt / 2.0;
 #pragma unroll
     for (int i = 0; i < n; i++) t[i] = x[i] + k[i] * h;
     M::f(k, t, u);
@@ -1010,7 +1038,7 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
 // Costs (src/cost.jl:171-181), same association as the oracle. The outer loops are kept rolled:
 // fully unrolled, the compiler hoists all of Q into registers across the knot loop and spills.
 template <int n, int m>
-__device__ __forceinline__ double stage_cost(const DevProblem* P, const double* x, const double* u) {
+__device__ __forceinline__ double stage_cost_dt(const DevProblem* P, const double* x, const double* u, double dt) {
   double xQx = 0.0, uRu = 0.0, qx = 0.0, ru = 0.0, uHx = 0.0;
   if (P->diag_cost) {
 #pragma unroll
@@ -1041,7 +1069,11 @@ __device__ __forceinline__ double stage_cost(const DevProblem* P, const double* 
   for (int i = 0; i < n; i++) qx = fma(P->q[i], x[i], qx);
 #pragma unroll
   for (int i = 0; i < m; i++) ru = fma(P->r[i], u[i], ru);
-  return ((((xQx + uRu) + qx) + ru) + P->c + uHx) * P->dt;
+  return ((((xQx + uRu) + qx) + ru) + P->c + uHx) * dt;
+}
+template <int n, int m>
+__device__ __forceinline__ double stage_cost(const DevProblem* P, const double* x, const double* u) {
+  return stage_cost_dt<n, m>(P, x, u, P->dt);
 }
 
 template <int n>
@@ -1063,12 +1095,30 @@ __device__ __forceinline__ double terminal_cost(const DevProblem* P, const doubl
   return (xQx + qx) + P->cf;
 }
 
+// stage / terminal cost of model M: MinTimeCost for a minimum-time model (minimum_time.jl:148-149:
+// stage_cost(cost, x[1:n], u[1:m], h) + R_min_time u[end]^2 with dt = h = u[end]^2, terminal unchanged;
+// the zero-padded base matrices give the base cost of the leading parts bit for bit)
+template <class M>
+__device__ __forceinline__ double stage_cost_m(const DevProblem* P, const double* x, const double* u) {
+  if constexpr (ModelTraits<M>::min_time) {
+    const double h = u[M::m - 1];
+    return stage_cost_dt<M::n, M::m>(P, x, u, h * h) + P->R_min_time * (h * h);
+  } else {
+    return stage_cost<M::n, M::m>(P, x, u);
+  }
+}
+template <class M>
+__device__ __forceinline__ double terminal_cost_m(const DevProblem* P, const double* x) {
+  return terminal_cost<M::n>(P, x);
+}
+
 // constraint row value (u == nullptr at the terminal knot: only x rows exist there)
 // SLACK = false compiles the infeasible-start slack row out (plain models never have it; the extra
 // case costs the team backward kernel registers)
 template <bool SLACK = true>
 __device__ __forceinline__ double row_value(const ConRow& r, const double* x, const double* u) {
   if (SLACK && r.type == ROW_USLACK) return u[r.idx];
+  if (r.type == ROW_MT_EQ) return u[(int)r.a] - x[r.idx];
   switch (r.type) {
     case ROW_XMAX: return x[r.idx] - r.a;
     case ROW_UMAX: return u[r.idx] - r.a;
@@ -1087,7 +1137,7 @@ __device__ __forceinline__ double row_value(const ConRow& r, const double* x, co
 }
 template <bool SLACK = true>
 __device__ __forceinline__ bool row_inequality(const ConRow& r) {
-  return r.type != ROW_GOAL && r.type != ROW_USER_EQ && (!SLACK || r.type != ROW_USLACK);
+  return r.type != ROW_GOAL && r.type != ROW_USER_EQ && r.type != ROW_MT_EQ && (!SLACK || r.type != ROW_USLACK);
 }
 
 // The same row seen by every lane of a wave (lanes iterate knots and rows in lockstep over the
@@ -1107,6 +1157,13 @@ __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n,
     idx[0] = n + r.idx;
     v[0] = 1.0;
     return 1;
+  }
+  if (r.type == ROW_MT_EQ) {
+    idx[0] = r.idx;
+    v[0] = -1.0;
+    idx[1] = n + (int)r.a;
+    v[1] = 1.0;
+    return 2;
   }
   switch (r.type) {
     case ROW_XMAX: idx[0] = r.idx; v[0] = 1.0; return 1;

@@ -93,8 +93,8 @@ __device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& 
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
   double J = 0.0, Jc = 0.0;
-  for (int k = 0; k < N - 1; k++) J += stage_cost<n, m>(P, Xs + (size_t)k * n, Us + (size_t)k * m);
-  J += terminal_cost<n>(P, Xs + (size_t)(N - 1) * n);
+  for (int k = 0; k < N - 1; k++) J += stage_cost_m<M>(P, Xs + (size_t)k * n, Us + (size_t)k * m);
+  J += terminal_cost_m<M>(P, Xs + (size_t)(N - 1) * n);
   if (!al) return J;
   const double* lam = Bf.lam + (size_t)b * N * pmax;
   const double* mu = Bf.mu + (size_t)b * N * pmax;
@@ -388,12 +388,104 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   }
 }
 
+// Minimum-time model (add_min_time_controls, src/solvers/altro/minimum_time.jl:91-96): the base
+// model's ForwardDiff Jacobian over [x; u; dt] at dt = h² (partial c of the chunk, dt the last one),
+// placed at the augmented columns; the dt column times 2h becomes the h column, and row τ+ = h has a 1
+// there. The τ column and the other entries of row τ are zero.
+template <class M, int INTEG, int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TOG_JAC_WAVES)))
+k_jacobian_mt(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
+  using Mb = typename ModelTraits<M>::Base;
+  constexpr int n = M::n, m = M::m, L = n + m, nb = Mb::n, mb = Mb::m, Lz = nb + mb + 1, NCH = (Lz + W - 1) / W;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int N = P->N;
+  const int c = (int)(t % NCH);
+  const long long bk = t / NCH;
+  const int k = (int)(bk % (N - 1));
+  const long long b = bk / (N - 1);
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  const double* x = Bf.X + ((size_t)b * N + k) * n;
+  const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
+  const double h = u[mb];
+  Dual<W> xd[nb], ud[mb], xn[nb + 1], dtd;
+#pragma unroll
+  for (int i = 0; i < nb; i++) {
+    xd[i].v = x[i];
+#pragma unroll
+    for (int w = 0; w < W; w++) xd[i].g[w] = (i == c * W + w) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < mb; i++) {
+    ud[i].v = u[i];
+#pragma unroll
+    for (int w = 0; w < W; w++) ud[i].g[w] = (nb + i == c * W + w) ? 1.0 : 0.0;
+  }
+  dtd.v = h * h;
+#pragma unroll
+  for (int w = 0; w < W; w++) dtd.g[w] = (nb + mb == c * W + w) ? 1.0 : 0.0;
+  discrete_step<Mb, INTEG, Dual<W>, Dual<W>>(xn, xd, ud, dtd);
+  double* out = Bf.AB + ((size_t)b * (N - 1) + k) * n * L;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int col = c * W + w;
+    if (col < nb) {  // x column
+#pragma unroll
+      for (int i = 0; i < nb; i++) out[i + n * col] = xn[i].g[w];
+      out[nb + n * col] = 0.0;
+    } else if (col < nb + mb) {  // u column
+#pragma unroll
+      for (int i = 0; i < nb; i++) out[i + n * (n + col - nb)] = xn[i].g[w];
+      out[nb + n * (n + col - nb)] = 0.0;
+    } else if (col == nb + mb) {  // h column: (∂f/∂dt) .* (2h); τ+ = h
+#pragma unroll
+      for (int i = 0; i < nb; i++) out[i + n * (n + mb)] = xn[i].g[w] * (2.0 * h);
+      out[nb + n * (n + mb)] = 1.0;
+    }
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int i = 0; i < n; i++) out[i + n * nb] = 0.0;  // τ column
+  }
+}
+
 // =============================================================================================
 // Wave-level small dense linear algebra on LDS (column-major). All 64 lanes cooperate; sizes are
 // compile-time so every loop unrolls. Callers synchronise (wsync) between dependent steps.
 // =============================================================================================
 
 // C (R x Cc) [+]= op(A) * op(B);  op(A) is R x Kd, op(B) is Kd x Cc
+#ifdef TOG_MFMA
+// A/B variant (DESIGN.md §5 "MFMA"): the product on the fp64 matrix cores, v_mfma_f64_16x16x4_f64, in
+// 16 x 16 output tiles, 4-deep k steps, operands straight from LDS (A[i][k]: lane i + 16 k, B[k][j]:
+// lane j + 16 k; D: col = lane & 15, row = (lane >> 4) + 4 reg). The matrix core's accumulation order
+// is not the oracle's fma chain, so this build is not bit-identical to the oracle.
+typedef double tog_d4 __attribute__((ext_vector_type(4)));
+template <int R, int Kd, int Cc, bool TA, bool TB, bool ACC>
+__device__ __forceinline__ void wmm(double* C, const double* A, int lda, const double* B, int ldb) {
+  const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int ti = 0; ti < (R + 15) / 16; ti++) {
+#pragma unroll
+    for (int tj = 0; tj < (Cc + 15) / 16; tj++) {
+      tog_d4 acc = {0.0, 0.0, 0.0, 0.0};
+      const int i = 16 * ti + lr, j = 16 * tj + lr;
+#pragma unroll
+      for (int k0 = 0; k0 < Kd; k0 += 4) {
+        const int l = k0 + lk;
+        const double a = (i < R && l < Kd) ? (TA ? A[l + lda * i] : A[i + lda * l]) : 0.0;
+        const double bb = (j < Cc && l < Kd) ? (TB ? B[j + ldb * l] : B[l + ldb * j]) : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 16 * ti + lk + 4 * r, col = 16 * tj + lr;
+        if (row < R && col < Cc) C[row + R * col] = ACC ? C[row + R * col] + acc[r] : acc[r];
+      }
+    }
+  }
+}
+#else
 template <int R, int Kd, int Cc, bool TA, bool TB, bool ACC>
 __device__ __forceinline__ void wmm(double* C, const double* A, int lda, const double* B, int ldb) {
   for (int e = threadIdx.x; e < R * Cc; e += WAVE) {
@@ -408,6 +500,7 @@ __device__ __forceinline__ void wmm(double* C, const double* A, int lda, const d
     C[i + R * j] = ACC ? C[i + R * j] + s : s;
   }
 }
+#endif
 
 // Householder QR of the rows x cols matrix A (ld = rows) in place; R ends up in the upper
 // triangle of the top cols rows (LAPACK dgeqr2/dlarfg; Julia qr(P).R, backward_pass.jl:172-183).
@@ -488,6 +581,7 @@ struct BwdLds {
   double Ri[m * m];
   double Aj[m * m];
   double vv[m];
+  double mtx[n], mtu[m];  // unscaled Qx, Qu of a minimum-time model's MinTimeCost expansion
   int piv[m];
   int flag;
   int pad;
@@ -502,7 +596,9 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
   const int lane = threadIdx.x;
   const int N = P->N;
   const bool term = (k == N - 1);
-  const double dt = P->dt;
+  constexpr bool MT = ModelTraits<M>::min_time;
+  // minimum time: dt = τ² with τ = u[end] (MinTimeCost cost_expansion!, minimum_time.jl:155-188)
+  const double dt = (MT && !term) ? sh.uk[m - 1] * sh.uk[m - 1] : P->dt;
   if (!term) {
     if (lane < n) {
       const int i = lane;
@@ -511,7 +607,9 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
       for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], sh.xk[j], a);
 #pragma unroll
       for (int j = 0; j < m; j++) bb = fma(P->H[j + m * i], sh.uk[j], bb);
-      sh.Qx[i] = ((a + P->q[i]) + bb) * dt;
+      const double g = (a + P->q[i]) + bb;
+      sh.Qx[i] = g * dt;
+      if (MT) sh.mtx[i] = g;
     } else if (lane < n + m) {
       const int i = lane - n;
       double a = 0.0, bb = 0.0;
@@ -519,11 +617,34 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
       for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], sh.uk[j], a);
 #pragma unroll
       for (int j = 0; j < n; j++) bb = fma(P->H[i + m * j], sh.xk[j], bb);
-      sh.Qu[i] = ((a + P->r[i]) + bb) * dt;
+      const double g = (a + P->r[i]) + bb;
+      sh.Qu[i] = g * dt;
+      if (MT) sh.mtu[i] = g;
     }
     for (int e = lane; e < n * n; e += WAVE) sh.Qxx[e] = SQRT ? P->cQ[e] : P->Q[e] * dt;
     for (int e = lane; e < m * m; e += WAVE) sh.Quu[e] = SQRT ? P->cR[e] : P->R[e] * dt;
     for (int e = lane; e < m * n; e += WAVE) sh.Qux[e] = P->H[e] * dt;
+    if constexpr (MT) {
+      // the τ / h entries: ℓ1 = stage_cost(cost, x, u) (no dt), tmp = 2τ Qu
+      wsync();
+      const double R = P->R_min_time, tau = sh.uk[m - 1];
+      const double l1 = stage_cost_dt<n, m>(P, sh.xk, sh.uk, 1.0);
+      const double w = 2.0 * l1 + R, t2 = 2.0 * tau;
+      if (lane < m - 1) {
+        const double tmp = t2 * sh.mtu[lane];
+        sh.Quu[lane + m * (m - 1)] = tmp;
+        sh.Quu[(m - 1) + m * lane] = tmp;
+      } else if (lane == m - 1) {
+        sh.Qu[m - 1] = tau * w;
+        sh.Quu[(m - 1) + m * (m - 1)] = w;
+        sh.Qx[n - 1] = R * sh.xk[n - 1];
+        sh.Qxx[(n - 1) + n * (n - 1)] = R;
+      }
+      if (lane >= WAVE - (n - 1)) {
+        const int j = lane - (WAVE - (n - 1));
+        sh.Qux[(m - 1) + m * j] = t2 * sh.mtx[j];
+      }
+    }
   } else {
     for (int e = lane; e < n * n; e += WAVE) sh.Qxx[e] = SQRT ? P->cQf[e] : P->Qf[e];
     if (lane < n) {
@@ -531,6 +652,13 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
 #pragma unroll
       for (int j = 0; j < n; j++) a = fma(P->Qf[lane + n * j], sh.xk[j], a);
       sh.Qx[lane] = a + P->qf[lane];
+    }
+    if constexpr (MT) {  // S.xx[end,end] = R_min_time, S.x[end] = R_min_time xN[end]
+      wsync();
+      if (lane == 0) {
+        sh.Qxx[(n - 1) + n * (n - 1)] = P->R_min_time;
+        sh.Qx[n - 1] = P->R_min_time * sh.xk[n - 1];
+      }
     }
   }
   if (!AL) return;
@@ -1358,7 +1486,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       gsum += mx;
     }
     // stage cost and AL terms of knot k-1 (x̄_{k-1}, ū_{k-1})
-    J += stage_cost<n, m>(P, xb, ub);
+    J += stage_cost_m<M>(P, xb, ub);
     if (al) {
       const int cnt = RT.kcnt[k - 1];
       if (cnt) {
@@ -1407,7 +1535,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (!ok) return false;
   }
-  J += terminal_cost<n>(P, xb);
+  J += terminal_cost_m<M>(P, xb);
   if (al) {
     const int cnt = RT.kcnt[N - 1];
     if (cnt) {
@@ -1927,7 +2055,7 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
   for (int k = lane; k < N; k += WAVE) {
     const double* x = X + (size_t)k * n;
     const double* u = (k < N - 1) ? U + (size_t)k * m : nullptr;
-    sk[k] = (k < N - 1) ? stage_cost<n, m>(P, x, u) : terminal_cost<n>(P, x);
+    sk[k] = (k < N - 1) ? stage_cost_m<M>(P, x, u) : terminal_cost_m<M>(P, x);
     const int cnt = P->knot_cnt[k];
     const ConRow* rows = P->rows + P->knot_off[k];
     double lc = 0.0, cIc = 0.0, e = 0.0, im = -INFINITY;
@@ -2210,6 +2338,7 @@ struct ModelOps {
   int slack;  // n for an infeasible model (add_slack_controls), else 0
   int pcap;   // max constraint rows per knot of the backward kernels' LDS layout
   int has_con;  // the model defines user constraint functions (ROW_USER_*)
+  int min_time; // minimum-time model (MinTime<M>): std backward pass on the LDS kernel only
   void (*slack_controls)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*cost_expansion)(const DevProblem*, const DevBuffers&, long long B, int N, int sqrt, int al, int* fail,
                          hipStream_t);
@@ -2242,7 +2371,8 @@ struct ModelLaunch {
   // (the Kuka RBD step keeps per-joint force and mass-matrix arrays live: one partial per thread
   // holds its scratch to ~4 KB/lane against ~12 KB with 4)
   using Mb = typename ModelTraits<M>::Base;  // the differentiated model (infeasible: without slacks)
-  static constexpr int JW = (Mb::n + Mb::m) <= 6 ? (Mb::n + Mb::m) : (Mb::id == TOG_MODEL_KUKA ? 1 : TOG_JW);
+  static constexpr int JW = (Mb::n + Mb::m) <= 6 ? (Mb::n + Mb::m + (ModelTraits<M>::min_time ? 1 : 0))
+                                                 : (Mb::id == TOG_MODEL_KUKA ? 1 : TOG_JW);
   static unsigned grid(long long total, int blk) { return (unsigned)((total + blk - 1) / blk); }
   // runtime integrator -> compile-time INTEG (the implicit schemes only where instantiated; tog_create
   // rejects them elsewhere)
@@ -2276,16 +2406,25 @@ struct ModelLaunch {
     });
   }
   static void jacobian(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int integ, hipStream_t st) {
-    constexpr int NCH = (Mb::n + Mb::m + JW - 1) / JW;
-    const long long total = B * (long long)(N - 1) * NCH;
-    with_integ(integ, [&](auto ic) {
-      constexpr int I = decltype(ic)::value;
-      hipLaunchKernelGGL((k_jacobian<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
-    });
+    if constexpr (ModelTraits<M>::min_time) {
+      constexpr int NCHT = (Mb::n + Mb::m + 1 + JW - 1) / JW;
+      const long long total = B * (long long)(N - 1) * NCHT;
+      with_integ(integ, [&](auto ic) {
+        constexpr int I = decltype(ic)::value;
+        hipLaunchKernelGGL((k_jacobian_mt<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+      });
+    } else {
+      constexpr int NCH = (Mb::n + Mb::m + JW - 1) / JW;
+      const long long total = B * (long long)(N - 1) * NCH;
+      with_integ(integ, [&](auto ic) {
+        constexpr int I = decltype(ic)::value;
+        hipLaunchKernelGGL((k_jacobian<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
+      });
+    }
   }
   static void backward(const DevProblem* P, const DevBuffers& Bf, long long B, int sq, int al, int flags, int team,
                        hipStream_t st) {
-    if constexpr (M::m <= M::n && M::n + 1 <= 16) {
+    if constexpr (M::m <= M::n && M::n + 1 <= 16 && !ModelTraits<M>::min_time) {
     if (team) {  // column-per-lane teams, TPW trajectories per wave (tog_bwd_team.hpp)
       constexpr int TPW = TeamCfg<M>::TPW;
       const dim3 g((unsigned)((B + TPW - 1) / TPW)), blk(64);
@@ -2465,6 +2604,7 @@ struct ModelLaunch {
     o.slack = ModelTraits<M>::slack;
     o.pcap = pcap_of<M>();
     o.has_con = HasCon<M>::value ? 1 : 0;
+    o.min_time = ModelTraits<M>::min_time ? 1 : 0;
     o.implicit = ModelTraits<M>::implicit_ok;
     o.slack_controls = slack_controls;
     o.cost_expansion = cost_expansion;
@@ -2476,7 +2616,7 @@ struct ModelLaunch {
     o.cost = cost;
     o.rollout = rollout;
     o.update_constraints = update_constraints;
-    if constexpr (ModelTraits<M>::slack == 0)
+    if constexpr (ModelTraits<M>::slack == 0 && !ModelTraits<M>::min_time)
       o.pn = pn;
     else
       o.pn = nullptr;

@@ -31,6 +31,10 @@ const ModelOps* ops_inf_quadrotor();
 const ModelOps* ops_inf_car();
 const ModelOps* ops_inf_pendulum();
 const ModelOps* ops_inf_kuka();
+// add_min_time_controls(model) variants (minimum time, src/solvers/altro/minimum_time.jl:83-104)
+const ModelOps* ops_mt_pendulum();
+const ModelOps* ops_mt_car();
+const ModelOps* ops_mt_double_integrator();
 }  // namespace tog
 
 static thread_local std::string g_err;
@@ -115,7 +119,16 @@ struct tog_model {
   const tog::ModelOps* ops_inf;
 };
 
-static const ModelOps* ops_for(int model, bool infeasible, const tog_model* user) {
+static const ModelOps* ops_for(int model, bool infeasible, bool min_time, const tog_model* user) {
+  if (min_time) {
+    if (infeasible) return nullptr;
+    switch (model) {
+      case TOG_MODEL_PENDULUM: return ops_mt_pendulum();
+      case TOG_MODEL_CAR: return ops_mt_car();
+      case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_mt_double_integrator();
+    }
+    return nullptr;
+  }
   if (model == TOG_MODEL_USER) return user ? (infeasible ? user->ops_inf : user->ops) : nullptr;
   if (infeasible) {
     switch (model) {
@@ -188,10 +201,13 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
               if (isfinite(D[2 * n + m + i])) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
           break;
         }
-        case TOG_CON_GOAL:
+        case TOG_CON_GOAL: {  // count: rows x[1:count] - xf (the goal's inds); 0 = n
+          const int ng = con.count > 0 ? con.count : n;
+          if (ng > n) return fail(TOG_ERR_ARG, "goal constraint longer than the state");
           if (term)
-            for (int i = 0; i < n; i++) rows.push_back({ROW_GOAL, i, D[i], 0, 0, 0});
+            for (int i = 0; i < ng; i++) rows.push_back({ROW_GOAL, i, D[i], 0, 0, 0});
           break;
+        }
         case TOG_CON_CIRCLES:
           if (!term)
             for (int o = 0; o < con.count; o++)
@@ -207,6 +223,10 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
           if (!slack) return fail(TOG_ERR_ARG, "TOG_CON_INFEASIBLE needs a TOG_PROB_INFEASIBLE problem");
           if (!term)
             for (int i = 0; i < slack; i++) rows.push_back({ROW_USLACK, m - slack + i, 0.0, 0.0, 0.0, 0.0});
+          break;
+        case TOG_CON_MIN_TIME_EQ:
+          if (!(d->flags & TOG_PROB_MIN_TIME)) return fail(TOG_ERR_ARG, "TOG_CON_MIN_TIME_EQ needs a TOG_PROB_MIN_TIME problem");
+          if (!term) rows.push_back({ROW_MT_EQ, n - 1, (double)(m - 1), 0.0, 0.0, 0.0});
           break;
         case TOG_CON_USER: {
           if (!has_con) return fail(TOG_ERR_ARG, "TOG_CON_USER needs a user model plugin that defines con()");
@@ -531,6 +551,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     }
   }
   P.o = *opts;
+  P.R_min_time = (d->flags & TOG_PROB_MIN_TIME) ? d->R_min_time : 0.0;
   const size_t B = (size_t)h->B, P1 = (size_t)(h->pmax > 0 ? h->pmax : 1);
   if ((rc = dalloc(h, &h->d_knot_off, N)) || (rc = dalloc(h, &h->d_knot_cnt, N)) ||
       (rc = dalloc(h, &h->d_rows, rows.size() + 1)) || (rc = dalloc(h, &h->dP, 1)))
@@ -542,7 +563,8 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     // TOG_BWD=lds forces the one-wave-per-trajectory LDS backward kernel (A/B checks)
     const char* ev = getenv("TOG_BWD");
     const bool force_lds = ev && strcmp(ev, "lds") == 0;
-    h->bwd_team = (!force_lds && team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
+    h->bwd_team = (!force_lds && !ops->min_time &&
+                   team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
                       ? 1 : 0;
     h->buf.rows_shmem = (int)(sizeof(ConRow) * rows.size() + sizeof(int) * 2 * (size_t)N);
     if (h->buf.rows_shmem > 32 * 1024) h->buf.rows_shmem = 0;  // rollouts then read the global tables
@@ -611,8 +633,11 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
 int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t device, tog_handle** out) {
   if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
   *out = nullptr;
-  if (d->flags & ~(int32_t)TOG_PROB_INFEASIBLE) return fail(TOG_ERR_ARG, "unknown problem flags");
-  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0, d->user_model);
+  if (d->flags & ~(int32_t)(TOG_PROB_INFEASIBLE | TOG_PROB_MIN_TIME)) return fail(TOG_ERR_ARG, "unknown problem flags");
+  if ((d->flags & TOG_PROB_MIN_TIME) && opts->square_root)
+    return fail(TOG_ERR_UNSUPPORTED, "minimum time: MinTimeCost has no square-root expansion (std backward pass)");
+  const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0, (d->flags & TOG_PROB_MIN_TIME) != 0,
+                                d->user_model);
   if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
   if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
   if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
@@ -928,6 +953,7 @@ int32_t tog_cost_expansion(tog_handle* h, int32_t sq, int32_t al) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
   if (is_multi(h)) return each_part(h, [&](tog_handle* p, size_t) { return tog_cost_expansion(p, sq, al); });
   HIPCHECK(hipSetDevice(h->device));
+  if (h->ops->min_time) return fail(TOG_ERR_UNSUPPORTED, "tog_cost_expansion: minimum-time problems (fused in the backward pass)");
   HIPCHECK(hipMemsetAsync(h->d_iscratch, 0, sizeof(int) * h->B, h->stream));
   h->ops->cost_expansion(h->dP, h->buf, h->B, h->N, sq, al, h->d_iscratch, h->stream);
   HIPCHECK(hipGetLastError());

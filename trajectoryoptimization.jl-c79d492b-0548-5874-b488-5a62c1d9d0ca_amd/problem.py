@@ -45,6 +45,7 @@ class Model:
     integration: int | None = None  # None = Continuous; abi.RK3 / abi.RK4 = Discrete
     slack: int = 0  # add_slack_controls: the last `slack` (= n) controls are infeasible slacks
     plugin: "UserModelPlugin | None" = None  # model_id == abi.MODEL_USER
+    min_time: bool = False  # add_min_time_controls: x = [x; τ], u = [u; h], dt_k = h_k² (last state / control)
 
     @staticmethod
     def from_plugin(path, name: str | None = None) -> "Model":
@@ -235,7 +236,7 @@ class QuadraticCost:
         self.q = np.zeros(n) if q is None else np.asarray(q, dtype=np.float64).reshape(n).copy()
         self.r = np.zeros(m) if r is None else np.asarray(r, dtype=np.float64).reshape(m).copy()
         self.c = float(c)
-        if m and not _isposdef(self.R):
+        if m and not _isposdef(self.R) and not getattr(self, "_padded", False):
             import warnings
 
             warnings.warn("R is not positive definite")
@@ -452,7 +453,7 @@ class GoalConstraint(_Constraint):
         return np.asarray(x, dtype=np.float64) - self.xf if u is None else np.zeros(0)
 
     def to_abi(self):
-        return (abi.CON_GOAL, 0, self.xf)
+        return (abi.CON_GOAL, len(self.xf), self.xf)  # count: the goal rows x[1:count] - xf (inds, constraints.jl:303)
 
 
 def goal_constraint(xf):
@@ -708,18 +709,25 @@ class Problem:
                              for c in cs])
             knot_set.append(keys[key])
         R = stage.R if stage.R.size else np.zeros((m, m))
+        flags = (abi.PROB_INFEASIBLE if self.model.slack else 0) | (abi.PROB_MIN_TIME if self.model.min_time else 0)
         return abi.DescBuilder(self.model.model_id, self.model.integration, n, m, N, self.dt, stage.Q, R, stage.H,
                                stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B,
-                               flags=abi.PROB_INFEASIBLE if self.model.slack else 0,
-                               user_model=self.model.plugin.ptr if self.model.plugin else None)
+                               flags=flags, user_model=self.model.plugin.ptr if self.model.plugin else None,
+                               R_min_time=getattr(self, "R_min_time", 0.0))
 
 
 def _validate_time(N, tf, dt):
     """``_validate_time`` (src/problem.jl:169-220) for the fixed-time case."""
     if N is None and dt is None and tf is None:
         raise ValueError("Must specify at least 2: N, dt, or tf")
-    if tf == 0:
-        raise NotImplementedError("minimum-time problems are out of scope (SURVEY.md §8f)")
+    if isinstance(tf, str) and tf.lstrip(":") == "min":
+        tf = 0.0
+    if tf == 0:  # minimum time (src/problem.jl:174-178): dt is the initial time step guess
+        if dt is None or not dt > 0:
+            raise ValueError("a minimum-time problem needs the initial dt")
+        if N is None:
+            raise ValueError("a minimum-time problem needs N")
+        return N, 0.0, dt
     if tf is not None:
         if dt is None and N is not None:
             dt = tf / (N - 1)
@@ -834,6 +842,101 @@ def infeasible_problem(prob: Problem, R_inf: float = 1.0) -> Problem:
     p._U[:, :, m:] = 0.0
     p._X[...] = prob._X
     return p
+
+
+# ----------------------------------------------------------------------------- minimum time
+
+
+def add_min_time_controls(model: Model) -> Model:
+    """``add_min_time_controls(model)`` (src/solvers/altro/minimum_time.jl:83-104): state [x; τ],
+    control [u; h], x+ = f_d(x, u, h²), τ+ = h (the device's MinTime<M>)."""
+    if not model.discrete:
+        raise ValueError("add_min_time_controls needs a discrete model")
+    if model.slack or model.min_time or model.plugin:
+        raise NotImplementedError("minimum time is built for the plain built-in models")
+    return Model(model.model_id, model.n + 1, model.m + 1, model.name + "_mt", model.integration, min_time=True)
+
+
+class MinTimeEquality(_Constraint):
+    """``mintime_equality(n, m)`` (minimum_time.jl:106-124): h_k - τ_k = 0 (τ_k is h_{k-1})."""
+
+    inequality = False
+    label = "min_time_eq"
+
+    def length(self, kind="stage"):
+        return 1 if kind == "stage" else 0
+
+    def evaluate(self, x, u=None):
+        return np.zeros(0) if u is None else np.array([u[-1] - x[-1]])
+
+    def to_abi(self):
+        return (abi.CON_MIN_TIME_EQ, 1, np.zeros(1))
+
+
+def mintime_constraints(prob: Problem, dt_max: float = 1.0, dt_min: float = 1.0e-3) -> Constraints:
+    """``mintime_constraints(prob, dt_max, dt_min)`` (minimum_time.jl:125-141): at every knot the
+    bounds are removed, combined with √dt_min <= h <= √dt_max (``combine``, constraints.jl:195-203; τ
+    unbounded) and appended after the other constraints (``update_constraint_set_jacobians``), then
+    h_k = τ_k at the knots 1 < k < N."""
+    n, m, N = prob.model.n, prob.model.m, prob.N
+    cons = Constraints(N)
+    eq = MinTimeEquality()
+    memo = {}
+    for k in range(N):
+        cs = prob.constraints[k]
+        key = (tuple(id(c) for c in cs), k == 0, k == N - 1)
+        if key not in memo:
+            others = [c for c in cs if not isinstance(c, BoundConstraint)]
+            bnds = [c for c in cs if isinstance(c, BoundConstraint)]
+            b = bnds[0] if bnds else BoundConstraint(n, m)
+            bnd2 = BoundConstraint(n + 1, m + 1, x_min=np.append(b.x_min, -math.inf), x_max=np.append(b.x_max, math.inf),
+                                   u_min=np.append(b.u_min, math.sqrt(dt_min)), u_max=np.append(b.u_max, math.sqrt(dt_max)))
+            memo[key] = ConstraintSet(others + [bnd2] + ([eq] if 0 < k < N - 1 else []))
+        cons.C[k] = memo[key]
+    return cons
+
+
+def minimum_time_problem(prob: Problem, R_min_time: float = 1.0, dt_max: float = 1.0, dt_min: float = 1.0e-3) -> Problem:
+    """``minimum_time_problem(prob, R_min_time, dt_max, dt_min)`` (minimum_time.jl:2-34): the model
+    ``add_min_time_controls``, the objective MinTimeCost (the quadratic costs zero-padded to the
+    augmented sizes plus R_min_time h², on the device), ``mintime_constraints``,
+    U = [U; √dt], X = [X; √dt], x0 = [x0; 0]."""
+    n, m, N = prob.model.n, prob.model.m, prob.N
+    stage, term = prob.obj.stage, prob.obj.terminal
+
+    def pad(A, r, c):
+        out = np.zeros((r, c))
+        A = np.asarray(A, dtype=np.float64)
+        if A.size:
+            out[:A.shape[0], :A.shape[1]] = A
+        return out
+
+    R = stage.R if stage.R.size else np.zeros((m, m))
+    st = QuadraticCost.__new__(QuadraticCost)
+    st._padded = True  # MinTimeCost's base cost on [x; τ], [u; h]: R is singular by construction
+    st.__init__(pad(stage.Q, n + 1, n + 1), pad(R, m + 1, m + 1), pad(stage.H, m + 1, n + 1),
+                np.append(stage.q, 0.0), np.append(stage.r if stage.r.size else np.zeros(m), 0.0), stage.c)
+    tm = QuadraticCost(pad(term.Q, n + 1, n + 1), None, None, np.append(term.q, 0.0), None, term.c)
+    obj = Objective(st, tm, N=N)
+    x0 = np.hstack([prob.x0, np.zeros((prob.B, 1))])
+    p = Problem(add_min_time_controls(prob.model), obj, constraints=mintime_constraints(prob, dt_max, dt_min),
+                x0=x0 if prob.batched else x0[0], xf=np.append(prob.xf, 0.0), N=N, dt=prob.dt)
+    p.tf = 0.0
+    p.R_min_time = float(R_min_time)
+    p._U[:, :, :m] = prob._U
+    p._U[:, :, m] = math.sqrt(prob.dt)
+    p._X[:, :, :n] = prob._X
+    p._X[:, :, n] = math.sqrt(prob.dt)
+    return p
+
+
+def total_time(prob: Problem):
+    """``total_time(prob)`` (minimum_time.jl:64-73): Σ h_k² for a minimum-time problem (its h comes
+    back from the solve in ``prob.h``), else dt (N - 1)."""
+    if prob.tf == 0.0:
+        tt = np.sum(np.asarray(prob.h) ** 2, axis=-1)
+        return tt if prob.batched else float(tt[0])
+    return prob.dt * (prob.N - 1)
 
 
 def line_trajectory(x0, xf, N):

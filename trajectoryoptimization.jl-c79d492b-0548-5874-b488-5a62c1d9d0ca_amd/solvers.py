@@ -117,7 +117,8 @@ class ALTROSolverOptions:
     """src/solvers/altro/altro_solver.jl:6-65. With a NaN initial state trajectory ALTRO is the AL
     solve; with a given X it is the infeasible-start solve (altro_methods.jl:98-124, infeasible.jl).
     ``projected_newton`` adds phase 2, the projected Newton feasible projection
-    (altro_methods.jl:5-39). Minimum time is SURVEY.md §8(f) "next" (not built)."""
+    (altro_methods.jl:5-39). A problem with tf = 0 is solved as minimum_time_problem
+    (src/solvers/altro/minimum_time.jl, R_minimum_time / dt_max / dt_min)."""
 
     verbose: bool = False
     opts_al: AugmentedLagrangianSolverOptions = field(default_factory=AugmentedLagrangianSolverOptions)
@@ -416,6 +417,32 @@ def _solve_altro_infeasible(prob, opts, max_steps, device):
     return solver
 
 
+def _solve_altro_min_time(prob, opts, max_steps, device):
+    """``solve!(prob, ::ALTROSolverOptions)`` for tf = 0 (altro_methods.jl:98-124, 55-95):
+    ``minimum_time_problem(prob, R_minimum_time, dt_max, dt_min)``, its AL solve (std backward pass:
+    MinTimeCost has no square-root expansion), then ``process_results!``: X[1:n] and U[1:m] go back to
+    ``prob``. The reference stores [u; u; h] in prob.U (its U[k][end] is h); here the time steps go to
+    ``prob.h`` and ``total_time(prob)`` reads them."""
+    from .problem import minimum_time_problem
+
+    n, m = prob.model.n, prob.model.m
+    pmt = minimum_time_problem(prob, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    solver = ALTROSolver(pmt, opts, device=device)
+    h = solver.handle
+    o = to_tog_options(opts)
+    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None
+            else int(o.iterations) * int(o.al_iterations) + 1)
+    h.download_state(pmt)
+    solver.stats = h.stats_dict()
+    solver.prob_min_time = pmt
+    if np.any(solver.stats["flags"] & abi.TRAJ_COST_INCREASED):
+        raise RuntimeError("Error: Cost increased during Forward Pass")
+    prob._X[...] = pmt._X[:, :, :n]
+    prob._U[...] = pmt._U[:, :, :m]
+    prob.h = pmt._U[:, :, m].copy()
+    return solver
+
+
 def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int = 0):
     """``solve!(prob, opts)`` / ``solve!(prob, solver)`` (src/solvers.jl:91-94). Mutates
     ``prob.X``/``prob.U`` in place and returns the solver."""
@@ -431,6 +458,10 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
             return _solve_pn(prob, ProjectedNewtonSolver(prob, opts, device=device))
         if isinstance(opts, ALTROSolverOptions):
             _altro_check(prob, opts)
+            if prob.tf == 0.0:
+                if _altro_infeasible(prob):
+                    raise NotImplementedError("infeasible start + minimum time is not built")
+                return _solve_altro_min_time(prob, opts, max_steps, device)
             if _altro_infeasible(prob):
                 return _solve_altro_infeasible(prob, opts, max_steps, device)
             _altro_pn_tolerances(opts)
