@@ -294,8 +294,10 @@ def test_undefined_integration_raises(tog):
     prob = tog.Problems.pendulum()
     with pytest.raises(ValueError):
         tog.Problem(tog.Dynamics.pendulum, prob.obj, integration="bogus", N=prob.N, dt=prob.dt)
+    # the implicit Newton step is instantiated for models with n <= 4 (csrc/tog_device.hpp implicit_step)
+    assert tog.discretize_model(tog.Dynamics.pendulum, "midpoint_implicit").integration == tog.abi.MIDPOINT_IMPLICIT
     with pytest.raises(NotImplementedError):
-        tog.discretize_model(tog.Dynamics.pendulum, "midpoint_implicit")
+        tog.discretize_model(tog.Dynamics.quadrotor, "midpoint_implicit")
 
 
 def test_midpoint_jacobian_matches_central_differences(tog, oracle):
