@@ -129,8 +129,12 @@ def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
     config-3 trajectories, OpenMP over trajectories (threads pinned, OMP_PROC_BIND=close). Every
     CPU this process may use takes part: the affinity set, capped by the cgroup quota when one
     is set (a GPU box's share of a larger host: oversubscribing the quota only adds contention).
-    Bounded sample (~`seconds` of work per run); runs repeat until two consecutive runs agree within
-    10 % (at most 4) and the last pair's mean is reported."""
+    Bounded sample (~`seconds` of work per run): one warm-up run is discarded (page faults, frequency
+    ramp: the first run on a fresh box measured 2-3x slow), then runs repeat until two consecutive runs
+    agree within 10 % (at most 5) and the median is reported with its spread. The rate of a run is its
+    sustained all-thread throughput, steps ÷ (Σ per-trajectory solve seconds ÷ threads): iteration counts
+    are heavy-tailed (a few trajectories run thousands of iterations), so the wall time of a bounded
+    sample measures its slowest trajectory rather than the cores (`wall_rates` are reported too)."""
     info = host_cpu_info()
     avail = info["affinity"]
     if info["cgroup_quota_cpus"]:
@@ -144,17 +148,21 @@ def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
     B = int(min(16384, 2 * threads * max(1.0, seconds / dt)))
     B = max(threads, B - B % threads)
     runs = []
-    for r in range(4):
+    prob, opts = pkg.Problems.config_quadrotor(B=B, offset=150000)
+    t = time.perf_counter()
+    warm = (orc.solve_batch(prob, opts, nthreads=threads), None)
+    warm = (warm[0], time.perf_counter() - t)
+    for r in range(5):
         prob, opts = pkg.Problems.config_quadrotor(B=B, offset=200000 + r * B)
         t = time.perf_counter()
-        steps = orc.solve_batch(prob, opts, nthreads=threads)
-        runs.append((steps, time.perf_counter() - t))
+        steps, busy = orc.solve_batch(prob, opts, nthreads=threads, busy=True)
+        runs.append((steps, time.perf_counter() - t, busy))
         if len(runs) >= 2:
-            a, b = (x[0] / x[1] for x in runs[-2:])
+            a, b = (x[0] / (x[2] / threads) for x in runs[-2:])
             if abs(a - b) <= 0.1 * max(a, b):
                 break
-    rates = [x[0] / x[1] for x in runs]
-    value = 0.5 * (rates[-1] + rates[-2]) if len(rates) >= 2 else rates[-1]
+    rates = [x[0] / (x[2] / threads) for x in runs]
+    value = float(np.median(rates))
     # single-thread rate next to the reference's published per-core figures
     p1, o1 = pkg.Problems.config_quadrotor(B=1, offset=300000)
     t1 = time.perf_counter()
@@ -162,9 +170,11 @@ def cpu_baseline(pkg, orc, seconds=10.0, threads=None):
     d1 = time.perf_counter() - t1
     return {"value": value, "unit": "iLQR iterations/s", "cores": threads, "kind": "port",
             "sample": f"{B} config-3 trajectories per run solved to AL convergence by oracle/tog_oracle.c, "
-                      f"OpenMP over trajectories; runs (steps, s): "
-                      + ", ".join(f"({x[0]}, {x[1]:.1f})" for x in runs),
+                      f"OpenMP over trajectories; warm-up run ({warm[0]}, {warm[1]:.1f}) discarded; runs (steps, s): "
+                      + ", ".join(f"({x[0]}, {x[1]:.1f})" for x in runs) + "; value = median",
             "run_rates": [round(x, 1) for x in rates],
+            "wall_rates": [round(x[0] / x[1], 1) for x in runs],
+            "spread": round((max(rates) - min(rates)) / value, 3),
             "nproc": info["nproc"], "affinity_cpus": info["affinity"],
             "cgroup_quota_cpus": info["cgroup_quota_cpus"], "cpu_model": info["cpu_model"],
             "single_thread": {"value": s1 / d1, "sample": f"1 trajectory, {s1} iLQR steps, {d1:.1f} s"}}

@@ -73,6 +73,9 @@ def lib():
         L.oc_solve_batch.restype = C.c_int64
         L.oc_solve_batch.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp, dp,
                                      C.c_int64, C.c_int]
+        L.oc_solve_batch_timed.restype = C.c_int64
+        L.oc_solve_batch_timed.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp,
+                                           dp, C.c_int64, C.c_int, C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -215,17 +218,20 @@ class OracleSolver:
         return out[:n]
 
 
-def solve_batch(prob, opts, nthreads=1, B=None):
+def solve_batch(prob, opts, nthreads=1, B=None, busy=False):
     """CPU baseline: solve ``B`` trajectories of ``prob`` with ``nthreads`` OpenMP threads.
-    Returns the total number of iLQR step!s."""
+    Returns the total number of iLQR step!s (and, with ``busy``, the summed per-trajectory solve
+    seconds)."""
     desc = prob.build_desc()
     o = _pkg.to_tog_options(opts)
     al = isinstance(opts, (_pkg.AugmentedLagrangianSolverOptions, _pkg.ALTROSolverOptions)) and prob.is_constrained()
     B = prob.B if B is None else B
     x0 = np.ascontiguousarray(prob.x0[:B])
     U0 = np.ascontiguousarray(prob._U[:B])
-    return int(lib().oc_solve_batch(C.byref(desc.desc), C.byref(o), abi.MODE_AL if al else abi.MODE_ILQR,
-                                    _dp(x0), _dp(U0), B, nthreads))
+    bt = C.c_double(0.0)
+    steps = int(lib().oc_solve_batch_timed(C.byref(desc.desc), C.byref(o), abi.MODE_AL if al else abi.MODE_ILQR,
+                                           _dp(x0), _dp(U0), B, nthreads, C.byref(bt)))
+    return (steps, bt.value) if busy else steps
 
 
 def solve_altro_infeasible(prob, opts, b=0):

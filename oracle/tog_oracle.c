@@ -23,6 +23,7 @@
  * cond via singular values).
  */
 #include <math.h>
+#include <time.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -2421,21 +2422,34 @@ OC_EXPORT double oc_max_violation(oc_solver* s) { return max_violation(s); }
  * Batched CPU baseline: B independent solves over `nthreads` OpenMP threads.
  * Returns Σ iLQR step!s. (bench.py cpu_baseline leg)
  * ===================================================================== */
-OC_EXPORT int64_t oc_solve_batch(const tog_problem_desc* d, const tog_options* o, int mode, const double* x0,
-                                 const double* U0, int64_t B, int nthreads) {
+/* busy (optional): Σ over trajectories of the seconds each one's solve took (the CPU baseline's
+   sustained rate is steps / (busy / nthreads): the heavy tail of iteration counts makes the wall time of a
+   bounded sample a measure of its slowest trajectory, not of the cores' throughput) */
+OC_EXPORT int64_t oc_solve_batch_timed(const tog_problem_desc* d, const tog_options* o, int mode, const double* x0,
+                                       const double* U0, int64_t B, int nthreads, double* busy) {
   int n = d->n, m = d->m, N = d->N;
   int64_t total = 0;
+  double bt = 0.0;
 #ifdef _OPENMP
-#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : total)
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : total, bt)
 #endif
   for (int64_t b = 0; b < B; b++) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     oc_solver* s = oc_create(d, o);
     oc_set_state(s, x0 + (size_t)b * n, U0 + (size_t)b * m * (N - 1), NULL);
     total += mode == TOG_MODE_AL ? oc_solve_al(s) : oc_solve_ilqr(s);
     oc_destroy(s);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    bt += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
   }
+  if (busy) *busy = bt;
   (void)nthreads;
   return total;
+}
+OC_EXPORT int64_t oc_solve_batch(const tog_problem_desc* d, const tog_options* o, int mode, const double* x0,
+                                 const double* U0, int64_t B, int nthreads) {
+  return oc_solve_batch_timed(d, o, mode, x0, U0, B, nthreads, NULL);
 }
 
 /* ALTRO phase 2: projected Newton feasible projection (oracle/tog_oracle_pn.c) */
