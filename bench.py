@@ -365,7 +365,8 @@ def time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_ra
         h.solve_step(chunk)
         done += chunk
         red = allreduce_stats()
-        n_active = float(red[0].item()) if red is not None else float(h.batch_stats()[0])
+        n_local = float(h.batch_stats()[0])  # host readback: also sets the handle's tail-mode hint
+        n_active = float(red[0].item()) if red is not None else n_local
         if n_active == 0.0:
             break
     barrier_sync()
