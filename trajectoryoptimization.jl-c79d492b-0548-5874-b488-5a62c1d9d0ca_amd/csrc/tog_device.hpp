@@ -127,6 +127,7 @@ struct DevBuffers {
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū
+  double* jws;        // staged RK3 Jacobian (Kuka): (2n duals, lanes) stage state between the kernels, or null
   TrajState* st;
 };
 

@@ -388,6 +388,81 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   }
 }
 
+// Staged RK3 Jacobian for the RBD model (config 5). One dual partial per lane through the RK3 step keeps
+// the stage state (x, s, t: 3n duals) live across three RNEA + CRBA + Cholesky evaluations; with it the
+// lane needs ~750 doubles and spills 4 KB (68 GB of scratch traffic per launch). Here each
+// RK3 stage is its own launch: the stage's f runs with only its inputs live, and the running sum s and
+// the next stage input t (2n duals per lane, element-major so lanes coalesce) go through HBM in between.
+// The operations and their order are discrete_step's RK3 (src/integration.jl:149-158), so the Jacobian
+// is bit-identical to k_jacobian's.
+template <class M, int STAGE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TOG_JAC_WAVES)))
+k_jacobian_rk3_stage(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
+  using Mb = typename ModelTraits<M>::Base;
+  constexpr int n = M::n, m = M::m, L = n + m, mb = Mb::m, Lb = n + mb;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int N = P->N;
+  const int c = (int)(t % Lb);
+  const long long bk = t / Lb;
+  const int k = (int)(bk % (N - 1));
+  const long long b = bk / (N - 1);
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  const double* x = Bf.X + ((size_t)b * N + k) * n;
+  const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
+  const double dt = P->dt;
+  Dual<1> xd[n], ud[mb], kk[n], sv[n], tv[n];
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    xd[i].v = x[i];
+    xd[i].g[0] = (i == c) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < mb; i++) {
+    ud[i].v = u[i];
+    ud[i].g[0] = (n + i == c) ? 1.0 : 0.0;
+  }
+  Dual<1>* ws = reinterpret_cast<Dual<1>*>(Bf.jws);  // element e of lane t at ws[e * total + t]
+  if constexpr (STAGE == 0) {
+    Mb::f(kk, xd, ud);
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      kk[i] = kk[i] * dt;
+      ws[(size_t)i * total + t] = kk[i];                  // s = k1
+      ws[(size_t)(n + i) * total + t] = xd[i] + kk[i] / 2.0;  // t = x + k1/2
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < n; i++) tv[i] = ws[(size_t)(n + i) * total + t];
+    Mb::f(kk, tv, ud);
+    // the running sum is read after f, so it is not live (and spilled) across it
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < n; i++) sv[i] = ws[(size_t)i * total + t];
+    if constexpr (STAGE == 1) {
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        kk[i] = kk[i] * dt;
+        ws[(size_t)(n + i) * total + t] = (xd[i] - sv[i]) + 2.0 * kk[i];  // t = (x - k1) + 2k2
+        ws[(size_t)i * total + t] = sv[i] + 4.0 * kk[i];                  // s = k1 + 4k2
+      }
+    } else {
+      double* out = Bf.AB + ((size_t)b * (N - 1) + k) * n * L;
+#pragma unroll
+      for (int i = 0; i < n; i++) {
+        kk[i] = kk[i] * dt;
+        const Dual<1> s3 = sv[i] + kk[i];
+        out[i + n * c] = (xd[i] + s3 / 6.0).g[0];
+      }
+      if constexpr (ModelTraits<M>::slack > 0) {
+        for (int j = c; j < n; j += Lb)
+#pragma unroll
+          for (int i = 0; i < n; i++) out[i + n * (Lb + j)] = (i == j) ? 1.0 : 0.0;
+      }
+    }
+  }
+}
+
 // Minimum-time model (add_min_time_controls, src/solvers/altro/minimum_time.jl:91-96): the base
 // model's ForwardDiff Jacobian over [x; u; dt] at dt = h² (partial c of the chunk, dt the last one),
 // placed at the augmented columns; the dt column times 2h becomes the h column, and row τ+ = h has a 1
@@ -2339,6 +2414,7 @@ struct ModelOps {
   int pcap;   // max constraint rows per knot of the backward kernels' LDS layout
   int has_con;  // the model defines user constraint functions (ROW_USER_*)
   int min_time; // minimum-time model (MinTime<M>): std backward pass on the LDS kernel only
+  long long jws_per_lane;  // doubles of staged-Jacobian state per (knot, partial) lane (0: not staged)
   void (*slack_controls)(const DevProblem*, const DevBuffers&, long long B, int integ, hipStream_t);
   void (*cost_expansion)(const DevProblem*, const DevBuffers&, long long B, int N, int sqrt, int al, int* fail,
                          hipStream_t);
@@ -2413,6 +2489,14 @@ struct ModelLaunch {
         constexpr int I = decltype(ic)::value;
         hipLaunchKernelGGL((k_jacobian_mt<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
       });
+    } else if (Mb::id == TOG_MODEL_KUKA && integ == TOG_RK3 && Bf.jws) {
+      if constexpr (Mb::id == TOG_MODEL_KUKA) {
+        const long long total = B * (long long)(N - 1) * (Mb::n + Mb::m);
+        const dim3 g(grid(total, 256)), blk(256);
+        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 0>), g, blk, 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 1>), g, blk, 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 2>), g, blk, 0, st, P, Bf, total);
+      }
     } else {
       constexpr int NCH = (Mb::n + Mb::m + JW - 1) / JW;
       const long long total = B * (long long)(N - 1) * NCH;
@@ -2605,6 +2689,7 @@ struct ModelLaunch {
     o.pcap = pcap_of<M>();
     o.has_con = HasCon<M>::value ? 1 : 0;
     o.min_time = ModelTraits<M>::min_time ? 1 : 0;
+    o.jws_per_lane = (Mb::id == TOG_MODEL_KUKA && !ModelTraits<M>::min_time) ? 2LL * M::n * 2 : 0;
     o.implicit = ModelTraits<M>::implicit_ok;
     o.slack_controls = slack_controls;
     o.cost_expansion = cost_expansion;

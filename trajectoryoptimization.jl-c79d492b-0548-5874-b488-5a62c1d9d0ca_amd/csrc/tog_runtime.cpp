@@ -596,6 +596,12 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
   if (b.nc < 1) b.nc = 1;
   b.nknots = N;
+  b.jws = nullptr;
+  // staged RK3 Jacobian (the RBD model): the stage state of every (knot, partial) lane
+  if (ops->jws_per_lane > 0 && d->integrator == TOG_RK3 && !getenv("TOG_JAC_UNSTAGED")) {
+    const size_t lanes = B * (size_t)(N - 1) * (size_t)(ops->n + ops->m - ops->slack);
+    if ((rc = dalloc(h, &b.jws, lanes * (size_t)ops->jws_per_lane))) return rc;
+  }
   b.ncp = (b.nc + 7) & ~7;
   b.ls_pend_ok = getenv("TOG_LS_NOPEND") ? 0 : 1;
   b.ls_first = LS_FIRST;
