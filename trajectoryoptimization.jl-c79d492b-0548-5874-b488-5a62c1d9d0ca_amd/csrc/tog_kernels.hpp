@@ -1497,7 +1497,9 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
   }
   // Software pipeline: the inputs of the next knot (K, U, d, X and the first RB multipliers) are
   // loaded while the current knot computes, so every knot does not wait for its own HBM round trip.
+  // Not for large gain blocks (the Kuka's 7 x 14 K): held across the knot's RBD evaluations they spill.
   constexpr int RB = 8;
+  constexpr bool PREF = m * n <= 64;
   double Kp[m * n], up[m], dp[m], xp[n], lp[RB], mp[RB];
   auto prefetch = [&](int k) {  // inputs of the update that produces knot k+1
     const double* Kk = K + (size_t)k * m * n;
@@ -1517,8 +1519,9 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       }
     }
   };
-  prefetch(0);
+  if (PREF) prefetch(0);
   for (int k = 1; k < N; k++) {
+    if (!PREF) prefetch(k - 1);
     double Kk[m * n], uk[m], dk[m], lk[RB], mk[RB];
 #pragma unroll
     for (int e = 0; e < m * n; e++) Kk[e] = Kp[e];
@@ -1532,7 +1535,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       lk[q] = lp[q];
       mk[q] = mp[q];
     }
-    if (k < N - 1) prefetch(k);
+    if (PREF && k < N - 1) prefetch(k);
 #pragma unroll
     for (int i = 0; i < n; i++) xp[i] = X[(size_t)k * n + i];  // x_k of the current iterate (next x_old)
 #pragma unroll
