@@ -395,34 +395,39 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
 // the next stage input t (2n duals per lane, element-major so lanes coalesce) go through HBM in between.
 // The operations and their order are discrete_step's RK3 (src/integration.jl:149-158), so the Jacobian
 // is bit-identical to k_jacobian's.
-template <class M, int STAGE>
+#ifndef TOG_JAC_STAGE_W
+#define TOG_JAC_STAGE_W 1
+#endif
+template <class M, int STAGE, int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TOG_JAC_WAVES)))
 k_jacobian_rk3_stage(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   using Mb = typename ModelTraits<M>::Base;
-  constexpr int n = M::n, m = M::m, L = n + m, mb = Mb::m, Lb = n + mb;
+  constexpr int n = M::n, m = M::m, L = n + m, mb = Mb::m, Lb = n + mb, NCH = (Lb + W - 1) / W;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int N = P->N;
-  const int c = (int)(t % Lb);
-  const long long bk = t / Lb;
+  const int c = (int)(t % NCH);
+  const long long bk = t / NCH;
   const int k = (int)(bk % (N - 1));
   const long long b = bk / (N - 1);
   if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
   const double dt = P->dt;
-  Dual<1> xd[n], ud[mb], kk[n], sv[n], tv[n];
+  Dual<W> xd[n], ud[mb], kk[n], sv[n], tv[n];
 #pragma unroll
   for (int i = 0; i < n; i++) {
     xd[i].v = x[i];
-    xd[i].g[0] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int w = 0; w < W; w++) xd[i].g[w] = (i == c * W + w) ? 1.0 : 0.0;
   }
 #pragma unroll
   for (int i = 0; i < mb; i++) {
     ud[i].v = u[i];
-    ud[i].g[0] = (n + i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int w = 0; w < W; w++) ud[i].g[w] = (n + i == c * W + w) ? 1.0 : 0.0;
   }
-  Dual<1>* ws = reinterpret_cast<Dual<1>*>(Bf.jws);  // element e of lane t at ws[e * total + t]
+  Dual<W>* ws = reinterpret_cast<Dual<W>*>(Bf.jws);  // element e of lane t at ws[e * total + t]
   if constexpr (STAGE == 0) {
     Mb::f(kk, xd, ud);
 #pragma unroll
@@ -451,11 +456,13 @@ k_jacobian_rk3_stage(const DevProblem* __restrict__ P, DevBuffers Bf, long long 
 #pragma unroll
       for (int i = 0; i < n; i++) {
         kk[i] = kk[i] * dt;
-        const Dual<1> s3 = sv[i] + kk[i];
-        out[i + n * c] = (xd[i] + s3 / 6.0).g[0];
+        const Dual<W> xn = xd[i] + (sv[i] + kk[i]) / 6.0;
+#pragma unroll
+        for (int w = 0; w < W; w++)
+          if (c * W + w < Lb) out[i + n * (c * W + w)] = xn.g[w];
       }
       if constexpr (ModelTraits<M>::slack > 0) {
-        for (int j = c; j < n; j += Lb)
+        for (int j = c; j < n; j += NCH)
 #pragma unroll
           for (int i = 0; i < n; i++) out[i + n * (Lb + j)] = (i == j) ? 1.0 : 0.0;
       }
@@ -2494,11 +2501,12 @@ struct ModelLaunch {
       });
     } else if (Mb::id == TOG_MODEL_KUKA && integ == TOG_RK3 && Bf.jws) {
       if constexpr (Mb::id == TOG_MODEL_KUKA) {
-        const long long total = B * (long long)(N - 1) * (Mb::n + Mb::m);
+        constexpr int SW = TOG_JAC_STAGE_W, NCHS = (Mb::n + Mb::m + SW - 1) / SW;
+        const long long total = B * (long long)(N - 1) * NCHS;
         const dim3 g(grid(total, 256)), blk(256);
-        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 0>), g, blk, 0, st, P, Bf, total);
-        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 1>), g, blk, 0, st, P, Bf, total);
-        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 2>), g, blk, 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 0, SW>), g, blk, 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 1, SW>), g, blk, 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_jacobian_rk3_stage<M, 2, SW>), g, blk, 0, st, P, Bf, total);
       }
     } else {
       constexpr int NCH = (Mb::n + Mb::m + JW - 1) / JW;
