@@ -93,7 +93,10 @@ def measured_traffic(kernel):
     this same bench command, FETCH_SIZE x2 per the gfx950 correction). None if absent."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    # the headline workload's summaries are <round>_traffic.json; <round>_<workload>_traffic.json
+    # (e.g. r2e_kuka_traffic.json) belong to the other configs
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))
+                   if os.path.basename(f).count("_") == 1)
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -187,6 +190,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU (default: the config's)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="quadrotor")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="single process: split the GPU's batch into this many slices, each on its own stream "
+                         "(tog_create_multi over the same device), so one slice's latency-bound line search "
+                         "overlaps another's Jacobians")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-solve-leg", action="store_true", help="skip the full-solve timing leg")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -223,7 +230,10 @@ def main():
         tstream = torch.cuda.Stream(device=local_rank)
         torch.cuda.set_stream(tstream)
         stream = tstream.cuda_stream
-    solver = pkg.AbstractSolverFor(prob, opts, device=local_rank, stream=stream)
+    if args.parts > 1 and dist is not None:
+        raise SystemExit("--parts is for single-process runs (the multi-rank path sets one shared stream)")
+    devices = [local_rank] * args.parts if args.parts > 1 else None
+    solver = pkg.AbstractSolverFor(prob, opts, device=local_rank, stream=stream, devices=devices)
     h = solver.handle
     n, m, N = prob.model.n, prob.model.m, prob.N
 
@@ -335,6 +345,7 @@ def main():
             "data": wl_data,
             "config": {"workload": wl_desc, "n": n, "m": m, "N": N,
                        "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"batch-shard x{world}",
+                       "streams_per_gpu": args.parts,
                        "mean_line_search_trials": round(trials, 3),
                        "timed_window": {"solve_steps": [args.warmup + 1, args.warmup + args.steps],
                                         "active_at_start": active0, "active_at_end": active1,

@@ -286,6 +286,27 @@ typedef struct tog_model tog_model;
 int32_t tog_model_load(const char* path, tog_model** out);
 int32_t tog_model_dims(const tog_model* model, int32_t* n, int32_t* m);
 int32_t tog_model_free(tog_model* model); /* after every handle built on it is destroyed */
+/* ---------------------------------------------------------------- generic costs (plugins)
+   Replaces GenericCost(ℓ, ℓf, n, m) / GenericCost(ℓ, ℓf, grad, hess, n, m) (src/cost.jl:239-287),
+   its stage_cost (src/cost.jl:324-325) and cost_expansion! (src/cost.jl:327-345; ForwardDiff gradient
+   and Hessian of auto_expansion_function src/cost.jl:289-322). The user's ℓ(x, u) and ℓf(xN), written
+   once as C++ templates over the scalar type, are compiled with hipcc for gfx950 against
+   csrc/tog_cost_plugin.hpp (TOG_COST_PLUGIN); tog_generic_cost_load dlopens the plugin and checks its
+   fingerprint. tog_generic_cost_expand evaluates `count` points at once: X (n, count), U (m, count)
+   column-major (U unused when terminal); out J (count) = ℓ, Ex (n, count) = E.x, Eu (m, count) = E.u,
+   Exx (n, n, count) = E.xx, Euu (m, m, count) = E.uu, Eux (m, n, count) = E.ux (terminal: J, Ex, Exx;
+   the others may be NULL). Host pointers, synchronous on `device`; the _device variant takes device
+   pointers and enqueues on `hip_stream` (NULL = the default stream). The reference's solvers never
+   call a GenericCost (its stage_cost has no dt method), so it is not a solver cost here either. */
+typedef struct tog_generic_cost tog_generic_cost;
+int32_t tog_generic_cost_load(const char* path, tog_generic_cost** out);
+int32_t tog_generic_cost_dims(const tog_generic_cost* cost, int32_t* n, int32_t* m);
+int32_t tog_generic_cost_expand(const tog_generic_cost* cost, int32_t device, int32_t terminal, const double* X, const double* U,
+                        int64_t count, double* J, double* Ex, double* Eu, double* Exx, double* Euu, double* Eux);
+int32_t tog_generic_cost_expand_device(const tog_generic_cost* cost, int32_t terminal, const double* X, const double* U,
+                               int64_t count, double* J, double* Ex, double* Eu, double* Exx, double* Euu,
+                               double* Eux, void* hip_stream);
+int32_t tog_generic_cost_free(tog_generic_cost* cost);
 /* dynamics_bias(state) at x = [q; v] for RBD models (TOG_MODEL_KUKA): c(q, v) into tau[m].
    Replaces RigidBodyDynamics.dynamics_bias as used by hold_trajectory (dynamics/kuka.jl:117-132).
    Host evaluation; TOG_ERR_UNSUPPORTED for analytical models. */

@@ -266,3 +266,33 @@ def solve_altro_min_time(prob, opts, b=0):
     s.solve()
     X, U = s.get("X"), s.get("U")
     return X[:, :n].copy(), U[:, :m].copy(), U[:, m].copy(), s
+
+
+COST_MYCOST, COST_SOFT_OBSTACLE = 0, 1  # tog_oracle_cost.c example costs
+
+
+def generic_cost_expand(cost_id, X, U=None, analytic=False):
+    """oc_generic_cost_expand (tog_oracle_cost.c): GenericCost ℓ / ℓf and the expansion for count points;
+    returns (J, Ex, Eu, Exx, Euu, Eux) with matrices column-major per point (the ABI's layout)."""
+    import numpy as np
+
+    L = lib()
+    dp = C.POINTER(C.c_double)
+    L.oc_generic_cost_expand.argtypes = [C.c_int, C.c_int, C.c_int, dp, dp, C.c_longlong] + [dp] * 6
+    n, m = (2, 1) if cost_id == COST_MYCOST else (4, 2)
+    X = np.ascontiguousarray(np.atleast_2d(np.asarray(X, dtype=np.float64)))
+    cnt = X.shape[0]
+    term = U is None
+    mm = 0 if term else m
+    U = np.zeros((cnt, 1)) if term else np.ascontiguousarray(np.atleast_2d(np.asarray(U, dtype=np.float64)))
+    out = [np.zeros(cnt), np.zeros((cnt, n)), np.zeros((cnt, max(mm, 1))), np.zeros((cnt, n * n)),
+           np.zeros((cnt, max(mm * mm, 1))), np.zeros((cnt, max(mm * n, 1)))]
+    p = lambda a: a.ctypes.data_as(dp)
+    rc = L.oc_generic_cost_expand(cost_id, int(analytic), int(term), p(X), p(U), cnt, *[p(a) for a in out])
+    if rc != 0:
+        raise ValueError("oc_generic_cost_expand failed")
+    J, Ex, Eu, Exx, Euu, Eux = out
+    Exx = Exx.reshape(cnt, n, n).swapaxes(1, 2)
+    if term:
+        return J, Ex, np.zeros((cnt, 0)), Exx, np.zeros((cnt, 0, 0)), np.zeros((cnt, 0, n))
+    return J, Ex, Eu, Exx, Euu.reshape(cnt, m, m).swapaxes(1, 2), Eux.reshape(cnt, n, m).swapaxes(1, 2)

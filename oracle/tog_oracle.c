@@ -2454,3 +2454,4 @@ OC_EXPORT int64_t oc_solve_batch(const tog_problem_desc* d, const tog_options* o
 
 /* ALTRO phase 2: projected Newton feasible projection (oracle/tog_oracle_pn.c) */
 #include "tog_oracle_pn.c"
+#include "tog_oracle_cost.c"

@@ -17,7 +17,7 @@ from .problem import (BoundConstraint, CircleConstraints, Constraints, Constrain
                       initial_states_b, max_violation, midpoint, midpoint_implicit, rk3, rk3_implicit, rk4, set_x0_b, sphere_constraint, add_slack_controls,
                       InfeasibleConstraint, infeasible_constraints, infeasible_problem, line_trajectory, user_model,
                       UserModelPlugin, UserConstraint, add_min_time_controls,
-                      minimum_time_problem, mintime_constraints, total_time, MinTimeEquality)
+                      minimum_time_problem, mintime_constraints, total_time, MinTimeEquality, GenericCost, generic_cost)
 from .solvers import (Expansion, AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
                       AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, ProjectedNewtonSolver,
                       ProjectedNewtonSolverOptions, solve, solve_b, solver_name, to_tog_options, to_tog_pn_options)
@@ -35,4 +35,5 @@ __all__ = [
     "to_tog_options", "Expansion", "backwardpass_b", "cost", "cost_expansion_b", "update_constraints_b", "forwardpass_b", "jacobian_b", "rollout_b",
     "Problems", "add_slack_controls", "InfeasibleConstraint", "infeasible_constraints", "infeasible_problem",
     "line_trajectory", "ProjectedNewtonSolver", "ProjectedNewtonSolverOptions", "to_tog_pn_options",
+    "GenericCost", "generic_cost",
 ]

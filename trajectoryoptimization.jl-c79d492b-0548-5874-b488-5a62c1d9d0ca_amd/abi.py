@@ -257,6 +257,11 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_model_load.argtypes = [C.c_char_p, C.POINTER(vp)]
     lib.tog_model_dims.argtypes = [vp, _ip, _ip]
     lib.tog_model_free.argtypes = [vp]
+    lib.tog_generic_cost_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+    lib.tog_generic_cost_dims.argtypes = [vp, _ip, _ip]
+    lib.tog_generic_cost_expand.argtypes = [vp, C.c_int32, C.c_int32, _dp, _dp, C.c_int64] + [_dp] * 6
+    lib.tog_generic_cost_expand_device.argtypes = [vp, C.c_int32, vp, vp, C.c_int64] + [vp] * 6 + [vp]
+    lib.tog_generic_cost_free.argtypes = [vp]
     for name in ("tog_create", "tog_create_multi", "tog_destroy", "tog_set_stream", "tog_synchronize", "tog_set_state",
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
@@ -264,7 +269,8 @@ def load_library(path: os.PathLike | None = None):
                  "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
                  "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
                  "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn", "tog_model_load", "tog_model_dims",
-                 "tog_model_free"):
+                 "tog_model_free", "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device",
+                 "tog_generic_cost_free"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -282,6 +288,7 @@ EXPORTED_SYMBOLS = (
     "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
     "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
     "tog_solve_al", "tog_default_pn_options", "tog_solve_pn", "tog_model_load", "tog_model_dims", "tog_model_free",
+    "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device", "tog_generic_cost_free",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
 NKERNELS = 3

@@ -14,6 +14,7 @@
 #include <dlfcn.h>
 
 #include "tog_plugin.hpp"
+#include "tog_cost_plugin.hpp"
 
 using namespace tog;
 
@@ -111,6 +112,15 @@ static void timed(tog_handle* h, int kind, F&& fn) {
   (void)hipEventRecord(b, h->stream);
   h->ev_kind.push_back(kind);
 }
+
+// a loaded GenericCost plugin (tog_generic_cost_load)
+struct tog_generic_cost {
+  using expand_fn = int (*)(int, const double*, const double*, long long, double*, double*, double*, double*,
+                            double*, double*, void*);
+  void* so;
+  int n, m;
+  expand_fn ex;
+};
 
 // a loaded user model plugin (tog_model_load)
 struct tog_model {
@@ -353,6 +363,94 @@ int32_t tog_model_free(tog_model* model) {
   if (!model) return fail(TOG_ERR_ARG, "null model");
   dlclose(model->so);
   delete model;
+  return TOG_OK;
+}
+
+// GenericCost plugins (tog_cost_plugin.hpp): the plugin's kernels evaluate ℓ / ℓf with their
+// ForwardDiff-style gradient and Hessian; libtog stages host buffers and checks the results' launch
+int32_t tog_generic_cost_load(const char* path, tog_generic_cost** out) {
+  if (!path || !out) return fail(TOG_ERR_ARG, "null argument");
+  *out = nullptr;
+  void* so = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!so) return fail(TOG_ERR_ARG, std::string("cannot load cost plugin: ") + dlerror());
+  auto fp = reinterpret_cast<long long (*)()>(dlsym(so, "tog_cost_plugin_fingerprint"));
+  auto dims = reinterpret_cast<int (*)(int*, int*)>(dlsym(so, "tog_cost_plugin_dims"));
+  auto ex = reinterpret_cast<tog_generic_cost::expand_fn>(dlsym(so, "tog_cost_plugin_expand"));
+  if (!fp || !dims || !ex) {
+    dlclose(so);
+    return fail(TOG_ERR_ARG, "not a libtog cost plugin (TOG_COST_PLUGIN symbols missing)");
+  }
+  if (fp() != cost_plugin_fingerprint()) {
+    dlclose(so);
+    return fail(TOG_ERR_ARG, "cost plugin was built against different libtog headers");
+  }
+  tog_generic_cost* c = new tog_generic_cost{so, 0, 0, ex};
+  dims(&c->n, &c->m);
+  *out = c;
+  return TOG_OK;
+}
+
+int32_t tog_generic_cost_dims(const tog_generic_cost* cost, int32_t* n, int32_t* m) {
+  if (!cost || !n || !m) return fail(TOG_ERR_ARG, "null argument");
+  *n = cost->n;
+  *m = cost->m;
+  return TOG_OK;
+}
+
+int32_t tog_generic_cost_expand_device(const tog_generic_cost* cost, int32_t terminal, const double* X, const double* U,
+                               int64_t count, double* J, double* Ex, double* Eu, double* Exx, double* Euu,
+                               double* Eux, void* hip_stream) {
+  if (!cost) return fail(TOG_ERR_ARG, "null cost");
+  if (count < 0) return fail(TOG_ERR_ARG, "count < 0");
+  if (count == 0) return TOG_OK;
+  if (!X || !J || !Ex || !Exx || (!terminal && (!U || !Eu || !Euu || !Eux)))
+    return fail(TOG_ERR_ARG, "null buffer");
+  if (cost->ex(terminal ? 1 : 0, X, U, count, J, Ex, Eu, Exx, Euu, Eux, hip_stream) != 0)
+    return fail(TOG_ERR_DEVICE, "cost plugin launch failed");
+  return TOG_OK;
+}
+
+int32_t tog_generic_cost_expand(const tog_generic_cost* cost, int32_t device, int32_t terminal, const double* X, const double* U,
+                        int64_t count, double* J, double* Ex, double* Eu, double* Exx, double* Euu, double* Eux) {
+  if (!cost) return fail(TOG_ERR_ARG, "null cost");
+  if (count < 0) return fail(TOG_ERR_ARG, "count < 0");
+  if (count == 0) return TOG_OK;
+  if (!X || !J || !Ex || !Exx || (!terminal && (!U || !Eu || !Euu || !Eux)))
+    return fail(TOG_ERR_ARG, "null buffer");
+  const size_t n = cost->n, m = terminal ? 0 : cost->m, c = (size_t)count;
+  // one device block: X | U | J | Ex | Eu | Exx | Euu | Eux
+  const size_t sz[8] = {n * c, m * c, c, n * c, m * c, n * n * c, m * m * c, m * n * c};
+  size_t tot = 0;
+  for (size_t v : sz) tot += v;
+  HIPCHECK(hipSetDevice(device));
+  double* d = nullptr;
+  HIPCHECK(hipMalloc(&d, tot * sizeof(double)));
+  double* p[8];
+  size_t o = 0;
+  for (int i = 0; i < 8; i++) {
+    p[i] = d + o;
+    o += sz[i];
+  }
+  hipError_t e = hipMemcpy(p[0], X, sz[0] * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess && m) e = hipMemcpy(p[1], U, sz[1] * sizeof(double), hipMemcpyHostToDevice);
+  int rc = TOG_OK;
+  if (e == hipSuccess) {
+    rc = cost->ex(terminal ? 1 : 0, p[0], p[1], count, p[2], p[3], p[4], p[5], p[6], p[7], nullptr);
+    if (rc != 0) rc = fail(TOG_ERR_DEVICE, "cost plugin launch failed");
+  }
+  if (e == hipSuccess && rc == TOG_OK) e = hipDeviceSynchronize();
+  double* outs[6] = {J, Ex, Eu, Exx, Euu, Eux};
+  for (int i = 0; i < 6 && e == hipSuccess && rc == TOG_OK; i++)
+    if (sz[i + 2]) e = hipMemcpy(outs[i], p[i + 2], sz[i + 2] * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(TOG_ERR_DEVICE, std::string("tog_cost_expand: ") + hipGetErrorString(e));
+  return rc;
+}
+
+int32_t tog_generic_cost_free(tog_generic_cost* cost) {
+  if (!cost) return fail(TOG_ERR_ARG, "null cost");
+  dlclose(cost->so);
+  delete cost;
   return TOG_OK;
 }
 

@@ -286,6 +286,139 @@ def LQRCostTerminal(Qf, xf) -> QuadraticCost:
     return QuadraticCost(Qf, None, None, -Qf @ xf, None, 0.5 * xf @ Qf @ xf)
 
 
+class GenericCost:
+    """``GenericCost(ℓ, ℓf, n, m)`` / ``GenericCost(ℓ, ℓf, grad, hess, n, m)`` (src/cost.jl:239-287) from a
+    compiled cost plugin (``tog_generic_cost_load``, csrc/tog_cost_plugin.hpp). ``stage_cost`` and
+    ``cost_expansion`` (src/cost.jl:324-345) run on the device: the plugin's kernel evaluates ℓ with
+    ForwardDiff's gradient and Hessian (auto_expansion_function, src/cost.jl:289-322), or the user's
+    analytic expansion. Points are batched: x (n,) or (count, n), u (m,) or (count, m). As in the
+    reference, a GenericCost is not a solver cost (its stage_cost has no dt method, src/cost.jl:324)."""
+
+    _cache: dict = {}
+
+    def __init__(self, path, device: int = 0):
+        import ctypes as C
+
+        path = str(pathlib.Path(path).resolve())
+        lib = abi.load_library()
+        if path not in GenericCost._cache:  # a plugin stays loaded for the life of the process
+            h = C.c_void_p()
+            abi.check(lib, lib.tog_generic_cost_load(path.encode(), C.byref(h)))
+            n, m = C.c_int32(), C.c_int32()
+            abi.check(lib, lib.tog_generic_cost_dims(h, C.byref(n), C.byref(m)))
+            GenericCost._cache[path] = (h.value, n.value, m.value)
+        self.ptr, self.n, self.m = GenericCost._cache[path]
+        self.path, self.device = path, int(device)
+
+    def sizes(self):
+        return self.n, self.m
+
+    def expand(self, X, U=None):
+        """Batched ℓ and expansion: returns (J (count,), Expansion with leading dim count). With U None
+        the terminal cost ℓf and its (xx, x) expansion; u, uu, ux are then empty."""
+        import ctypes as C
+
+        from .solvers import Expansion
+
+        lib = abi.load_library()
+        n, m = self.n, self.m
+        X = np.ascontiguousarray(np.atleast_2d(np.asarray(X, dtype=np.float64)))
+        if X.shape[1] != n:
+            raise ValueError(f"x has {X.shape[1]} entries, the cost has n = {n}")
+        cnt = X.shape[0]
+        term = U is None
+        J = np.zeros(cnt)
+        Ex = np.zeros((cnt, n))
+        Exx = np.zeros((cnt, n, n))  # stored column-major per point: Exx[p].T is the matrix
+        if term:
+            Eu, Euu, Eux = np.zeros((cnt, 0)), np.zeros((cnt, 0, 0)), np.zeros((cnt, n, 0))
+            nul = C.cast(None, C.POINTER(C.c_double))
+            abi.check(lib, lib.tog_generic_cost_expand(self.ptr, self.device, 1, abi.as_dp(X), nul, cnt, abi.as_dp(J),
+                                                       abi.as_dp(Ex), nul, abi.as_dp(Exx), nul, nul))
+        else:
+            U = np.ascontiguousarray(np.atleast_2d(np.asarray(U, dtype=np.float64)))
+            if U.shape != (cnt, m):
+                raise ValueError(f"u must have shape ({cnt}, {m})")
+            Eu, Euu, Eux = np.zeros((cnt, m)), np.zeros((cnt, m, m)), np.zeros((cnt, n, m))
+            abi.check(lib, lib.tog_generic_cost_expand(self.ptr, self.device, 0, abi.as_dp(X), abi.as_dp(U), cnt,
+                                                       abi.as_dp(J), abi.as_dp(Ex), abi.as_dp(Eu), abi.as_dp(Exx),
+                                                       abi.as_dp(Euu), abi.as_dp(Eux)))
+        t = lambda a: np.ascontiguousarray(a.swapaxes(-1, -2))  # column-major per point -> row-major
+        return J, Expansion(Ex, Eu, t(Exx), t(Euu), t(Eux))
+
+    def stage_cost(self, x, u=None):
+        """``stage_cost(cost, x, u)`` / ``stage_cost(cost, xN)`` (src/cost.jl:324-325)."""
+        J, _ = self.expand(x, u)
+        return float(J[0]) if np.ndim(x) == 1 else J
+
+    def cost_expansion(self, E, x, u=None):
+        """``cost_expansion!(E, cost, x, u)`` / ``cost_expansion!(S, cost, xN)`` (src/cost.jl:327-345):
+        fills E.x, E.u, E.xx, E.uu, E.ux (E.xx, E.x for the terminal form) in place."""
+        _, e = self.expand(x, u)
+        single = np.ndim(x) == 1
+        fields = ("x", "xx") if u is None else ("x", "u", "xx", "uu", "ux")
+        for f in fields:
+            v = getattr(e, f)
+            getattr(E, f)[...] = v[0] if single else v
+        return None
+
+    def copy(self):
+        """``copy(cost::GenericCost)`` (src/cost.jl:347)."""
+        return GenericCost(self.path, self.device)
+
+
+_COST_TEMPLATE = """// generated by generic_cost() (problem.py): GenericCost(ℓ, ℓf, n, m) as a libtog cost plugin
+#include "{hdr}"
+
+struct {name} {{
+  static constexpr int n = {n}, m = {m};
+  template <class T>
+  __host__ __device__ __forceinline__ static T stage(const T* x, const T* u) {{
+    using namespace tog;
+{stage}
+  }}
+  template <class T>
+  __host__ __device__ __forceinline__ static T terminal(const T* x) {{
+    using namespace tog;
+{term}
+  }}
+}};
+
+TOG_COST_PLUGIN({name})
+"""
+
+
+def generic_cost(stage_body: str, terminal_body: str, n: int, m: int, name: str = "UserCost", build_dir=None,
+                 device: int = 0) -> GenericCost:
+    """``GenericCost(ℓ, ℓf, n, m)`` (src/cost.jl:279-287) from C++ source: ``stage_body`` is the body of
+    ``T stage(const T* x, const T* u)`` and ``terminal_body`` of ``T terminal(const T* x)`` over the scalar
+    type T (double, or the second-order dual numbers of the expansion kernel). Compiled once with hipcc
+    for gfx950 (cached by the hash of its source under ``csrc/plugins/``)."""
+    import hashlib
+    import subprocess
+
+    csrc = pathlib.Path(__file__).resolve().parent / "csrc"
+    out_dir = pathlib.Path(build_dir) if build_dir else csrc / "plugins"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    ind = lambda b: "\n".join("    " + ln for ln in b.strip().splitlines())
+    src = _COST_TEMPLATE.format(hdr=str(csrc / "tog_cost_plugin.hpp"), name=name, n=int(n), m=int(m),
+                                stage=ind(stage_body), term=ind(terminal_body))
+    key = hashlib.sha1(src.encode()).hexdigest()[:12]
+    so = out_dir / f"gen_{name}_{key}.so"
+    if not so.exists():
+        hip = out_dir / f"gen_{name}_{key}.hip"
+        hip.write_text(src)
+        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-fPIC",
+               "-shared", "-o", str(so), str(hip)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise ValueError(f"generic cost {name!r} does not compile:\n{r.stderr[-4000:]}")
+    cost = GenericCost(so, device)
+    if (cost.n, cost.m) != (int(n), int(m)):
+        raise ValueError("plugin dimensions do not match")
+    return cost
+
+
 class Objective:
     """``Objective(costs)`` (src/objective.jl:15-29). The HIP path requires one stage cost
     shared by knots 1..N-1 and one terminal cost (the form every config uses)."""
