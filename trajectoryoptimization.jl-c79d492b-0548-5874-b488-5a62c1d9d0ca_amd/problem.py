@@ -190,6 +190,7 @@ def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=N
                "-shared", "-o", str(so), str(hip)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
+            hip.unlink(missing_ok=True)  # no broken source left in the plugin directory
             raise ValueError(f"user model {name!r} does not compile:\n{r.stderr[-4000:]}")
     model = Model.from_plugin(so, name)
     if (model.n, model.m) != (int(n), int(m)):
@@ -412,6 +413,7 @@ def generic_cost(stage_body: str, terminal_body: str, n: int, m: int, name: str 
                "-shared", "-o", str(so), str(hip)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
+            hip.unlink(missing_ok=True)  # no broken source left in the plugin directory
             raise ValueError(f"generic cost {name!r} does not compile:\n{r.stderr[-4000:]}")
     cost = GenericCost(so, device)
     if (cost.n, cost.m) != (int(n), int(m)):
