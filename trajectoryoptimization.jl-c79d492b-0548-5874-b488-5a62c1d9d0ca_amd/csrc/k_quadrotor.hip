@@ -2,6 +2,11 @@
 #include "tog_kernels.hpp"
 
 namespace tog {
+// the Jacobian kernels are instantiated in k_quadrotor_jac.hip, built with another machine scheduler
+extern template __global__ void k_jacobian<Quadrotor, TOG_RK3, TOG_JW>(const DevProblem*, DevBuffers, long long);
+extern template __global__ void k_jacobian<Quadrotor, TOG_RK4, TOG_JW>(const DevProblem*, DevBuffers, long long);
+extern template __global__ void k_jacobian<Quadrotor, TOG_MIDPOINT, TOG_JW>(const DevProblem*, DevBuffers, long long);
+
 const ModelOps* ops_quadrotor() {
   static const ModelOps o = ModelLaunch<Quadrotor>::ops();
   return &o;
