@@ -4,8 +4,10 @@ One step = one batched AL-iLQR ``step!`` (jacobians -> cost expansion + square-r
 -> forward-pass line search -> bookkeeping / AL dual+penalty update) for every active trajectory of
 the per-GPU batch. Workload: BASELINE.json configs[2] (quadrotor n=13 m=4 N=101, AL-iLQR with
 u in [0,15] + goal, sqrt backward pass), 8192 trajectories per GPU, synthetic random starts
-(SURVEY.md §8(d)); inputs resident in HBM before timing. ``value`` = Σ trajectory-iterations
-completed on all GPUs / max-over-ranks wall time.
+(SURVEY.md §8(d)); inputs resident in HBM before timing. ``value`` = SURVEY.md §8(d)'s metric: Σ
+trajectory-iterations of the WHOLE solve (tog_solve_init until no trajectory is active, the stopping
+check included) on all GPUs / max-over-ranks wall time. The `--steps` window (every trajectory
+active) is reported beside it as ``window_rate``; ``steps``/``warmup``/``ms_per_step`` describe it.
 
 Multi-GPU: one process per GPU (torch.distributed.run); trajectories are independent so each rank
 solves its own shard (weak scaling). The only collective is one RCCL all-reduce per step of the
@@ -53,17 +55,19 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X public spec, fp64 vector (the local guide has 
 #                          256 CU x 4 SIMD x 16 lanes x 2 FLOP x 2.4 GHz
 
 
-def kernel_bytes(n, m, N, p_stage, p_term, trials):
+def kernel_bytes(n, m, N, p_stage, p_term, trials, dense_knots=1):
     """Algorithmic HBM bytes per trajectory-step for each kernel (SURVEY.md §8(d) staged design;
-    DESIGN.md §4 lists the terms)."""
+    DESIGN.md §4-5 list the terms). The expansion records (k_expand_team) hold Q.x, Q.u, Q.uu per
+    knot and Q.xx at the `dense_knots` knots whose AL terms change it (config 3: the terminal one)."""
     K = N - 1
+    rec = 8 * (N * (n + m + m * m) + dense_knots * n * n)       # one trajectory's expansion records
     jac = 8 * K * ((n + m) + n * (n + m))                       # read x,u ; write [A|B]
-    bwd = 8 * (K * (n * (n + m) + (n + m) + m * (n + 1))        # read [A|B], x,u ; write K,d
-               + n + 2 * (K * p_stage + p_term))                # x_N ; read λ, μ
+    exp_ = 8 * (N * n + K * m + 2 * (K * p_stage + p_term)) + rec  # read x,u,λ,μ ; write records
+    bwd = 8 * (K * (n * (n + m) + m * (n + 1))) + rec           # read [A|B], records ; write K,d
     fwd = 8 * (trials * K * (2 * (n + m) + m * (n + 1))         # per trial: read x,u,K,d ; write x̄,ū
                + 2 * K * (n + m)                                # accept: copy X̄,Ū -> X,U
                + trials * 3 * (K * p_stage + p_term))           # λ, μ read, C written per trial
-    return {"jacobian": jac, "backward": bwd, "forward": fwd}
+    return {"jacobian": jac, "backward": bwd, "forward": fwd, "expansion": exp_}
 
 
 def bwd_flops(n, m, N, p_x, p_u, sqrt=True):
@@ -284,16 +288,22 @@ def main():
         St[:, abi.STAT_LS_TRIALS] > 0) else 1.0
 
     if dist is not None:
-        value, steps_all, elapsed = pkg.distributed.job_rate(steps_done, elapsed, dist, device=f"cuda:{local_rank}")
+        window_rate, steps_all, elapsed = pkg.distributed.job_rate(steps_done, elapsed, dist,
+                                                                   device=f"cuda:{local_rank}")
     else:
         steps_all = float(steps_done)
-        value = steps_all / elapsed
+        window_rate = steps_all / elapsed
     # roofline for the dominant kernel (largest total device time over the timed region)
     cons = prob.constraints
     p_stage = cons[0].num_constraints("stage") if al_mode else 0
     p_term = cons[N - 1].num_constraints("terminal") if al_mode else 0
-    kb = kernel_bytes(n, m, N, p_stage, p_term, trials)
-    names = ["jacobian", "backward", "forward"]
+    # knots with a dense expansion record: the terminal one, plus every stage knot whose AL rows change
+    # Q.xx (sqrt: a row with a state gradient; std: any row)
+    sq = bool(pkg.solvers.to_tog_options(opts).square_root)
+    p_xrows = max(0, p_stage - 2 * m) if al_mode else 0
+    dense = 1 + ((N - 1) if (al_mode and ((p_xrows > 0) if sq else (p_stage > 0))) else 0)
+    kb = kernel_bytes(n, m, N, p_stage, p_term, trials, dense)
+    names = ["jacobian", "backward", "forward", "expansion"]
     dom = int(np.argmax(ms))
     avg_ms = ms[dom] / max(1, launches[dom])
     # algorithmic bytes per launch = per-trajectory bytes x trajectories processed per launch
@@ -331,6 +341,9 @@ def main():
     solve_leg = None
     if not args.no_solve_leg:
         solve_leg = time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_rank, pkg)
+    # value: SURVEY.md §8(d)'s metric, the whole solve (tog_solve_init until no trajectory is active);
+    # the full-batch step window is reported beside it as window_rate
+    value = solve_leg["value"] if solve_leg is not None else window_rate
 
     if rank == 0:
         cpu = None
@@ -349,8 +362,11 @@ def main():
                        "mean_line_search_trials": round(trials, 3),
                        "timed_window": {"solve_steps": [args.warmup + 1, args.warmup + args.steps],
                                         "active_at_start": active0, "active_at_end": active1,
-                                        "note": "value = trajectory-iterations in this window of the solve "
-                                                "/ its wall time; solve_rate below times the whole solve"}},
+                                        "rate": round(window_rate, 2),
+                                        "note": "steps / warmup / ms_per_step are this window's (batch "
+                                                "steps of the solve with every trajectory active); value "
+                                                "is solve_rate, the whole solve"}},
+            "window_rate": round(window_rate, 2),
             "solve_rate": solve_leg,
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -372,16 +388,23 @@ def time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_ra
     t0 = time.perf_counter()
     h.solve_init(mode)
     done = 0
+    B_job = float(prob.B) * (dist.get_world_size() if dist is not None else 1)
+    timeline = [(0.0, B_job)]  # (seconds since init, job-wide n_active) at every stopping check
     while done < max_steps:
         h.solve_step(chunk)
         done += chunk
         red = allreduce_stats()
         n_local = float(h.batch_stats()[0])  # host readback: also sets the handle's tail-mode hint
         n_active = float(red[0].item()) if red is not None else n_local
+        timeline.append((time.perf_counter() - t0, n_active))
         if n_active == 0.0:
             break
     barrier_sync()
     wall = time.perf_counter() - t0
+    # tail share: the fraction of the solve's wall time spent with fewer than 1 % of the job's
+    # trajectories active (each check interval counted by the n_active at its start)
+    tail = sum(t1 - t0_ for (t0_, a0), (t1, _) in zip(timeline, timeline[1:]) if a0 < 0.01 * B_job)
+    bulk_steps = next((i * chunk for i, (_, a) in enumerate(timeline) if a < 0.01 * B_job), done)
     steps = h.total_steps()  # k_init (tog_solve_init) zeroes the per-trajectory counters
     St = h.get(abi.FIELD_STATS)
     conv = int(np.count_nonzero(St[:, abi.STAT_FLAGS].astype(np.int64) &
@@ -393,6 +416,10 @@ def time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_ra
     it = St[:, abi.STAT_TOTAL_STEPS]
     return {"value": round(rate, 2), "unit": "iLQR iterations/s", "steps": int(steps_all),
             "wall_s": round(wall_all, 4), "batch_steps": done,
+            "ms_per_batch_step": round(1e3 * wall / max(1, done), 4),
+            "tail_share": round(tail / wall, 4),
+            "tail": {"threshold_active": 0.01 * B_job, "batch_steps_before": bulk_steps,
+                     "seconds": round(tail, 4)},
             "traj_iterations": {"min": int(it.min()), "mean": round(float(it.mean()), 2), "max": int(it.max())},
             "converged": conv, "batch": int(prob.B),
             "note": "tog_solve_init .. last trajectory finished, stopping check every 4 steps included"}

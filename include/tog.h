@@ -438,7 +438,8 @@ enum tog_kernel_id {
   TOG_KERNEL_JACOBIAN = 0,
   TOG_KERNEL_BACKWARD = 1,
   TOG_KERNEL_FORWARD = 2,
-  TOG_NKERNELS = 3
+  TOG_KERNEL_EXPANSION = 3, /* knot-parallel cost expansion ahead of the team backward pass */
+  TOG_NKERNELS = 4
 };
 int32_t tog_profile(tog_handle* h, int32_t enable);
 /* blocking: total milliseconds and launch counts per tog_kernel_id since tog_profile(h, 1) */

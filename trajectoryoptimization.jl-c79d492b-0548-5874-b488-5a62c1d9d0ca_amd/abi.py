@@ -201,6 +201,23 @@ class DescBuilder:
         self.desc = d
 
 
+def header_hash() -> str:
+    """sha1 of the text of libtog's headers (csrc/Makefile HDRS, same files, same order), first 15
+    hex digits: the TOG_HEADER_HASH libtog was built with. Plugins generated at run time are compiled
+    with it and cached under it, so a header change rebuilds them, and the fingerprint check in
+    tog_model_load / tog_generic_cost_load refuses a stale one."""
+    import hashlib
+    import re
+
+    csrc = PKG_DIR / "csrc"
+    mk = (csrc / "Makefile").read_text()
+    hdrs = re.search(r"^HDRS = (.*)$", mk, re.M).group(1).split()
+    h = hashlib.sha1()
+    for f in hdrs:
+        h.update((csrc / f).read_bytes())
+    return h.hexdigest()[:15]
+
+
 _LIB = None
 
 
@@ -290,8 +307,8 @@ EXPORTED_SYMBOLS = (
     "tog_solve_al", "tog_default_pn_options", "tog_solve_pn", "tog_model_load", "tog_model_dims", "tog_model_free",
     "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device", "tog_generic_cost_free",
 )
-KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD = 0, 1, 2
-NKERNELS = 3
+KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD, KERNEL_EXPANSION = 0, 1, 2, 3
+NKERNELS = 4
 
 
 def check(lib, rc):

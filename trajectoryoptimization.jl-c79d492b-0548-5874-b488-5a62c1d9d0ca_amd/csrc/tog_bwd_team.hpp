@@ -60,12 +60,11 @@ struct RowInfo {  // one constraint row of the current knot (AL terms), 64 B
   int idx[3];
   int nnz;
 };
+static_assert(sizeof(RowInfo) == 64, "RowInfo: 8 doubles of LDS (expand_team_stride)");
 
-// Dynamic LDS layout of k_bwd_team (sizes from the host, bwd_team_layout):
-//   per team (stride doubles): [region 1: n*L][region 2: max(R2, rows area)]
-//     rows area (inside region 2, used only during the expansion): RowInfo[pmax], int xr[pmax],
-//     int ur[pmax], x[n], u[m]
-//   per block: ConRow cache[nrows] (deduplicated row table), int knot_off[N], int knot_cnt[N]
+// Dynamic LDS layout of k_bwd_team (sizes from the host, bwd_team_stride / bwd_team_shmem):
+//   per team (stride doubles): [S-region][region 1: n*L][region 2: R2 | R2S]
+//   per block: int knot_cnt[N], int knot_nx[N] (dense-record test of the expansion records)
 // S-region (persistent across knots, before region 1): S column-major and s (n*n + n); sqrt
 // stores its upper factor dense, explicit zeros below the diagonal, so the rolled S [A B] product
 // reads the oracle's dense operand without per-entry selects.
@@ -74,17 +73,40 @@ __host__ __device__ constexpr int sreg_size(bool) {  // S, s, then the knot's Q.
   return M::n * M::n + M::n + M::m * M::m;
 }
 template <class M>
-__host__ __device__ inline int bwd_team_stride(int pmax, int sqrt) {
+__host__ __device__ inline int bwd_team_stride(int /*pmax*/, int sqrt) {
   using C = TeamCfg<M>;
-  const int rows_area = M::n * C::L + pmax * 8 + pmax + M::n + M::m;  // doubles (2 int lists = pmax doubles)
-  const int busp = sqrt ? C::BUSPS : C::BUSP;
-  int s = busp > rows_area ? busp : rows_area;
+  int s = sqrt ? C::BUSPS : C::BUSP;
   s += sreg_size<M>(sqrt != 0);
   s += (34 - s % 32) % 32;  // s = 2 mod 32: the TPW teams' broadcast reads land on distinct banks
   return s;
 }
-inline size_t bwd_team_shmem(int stride, int tpw, int nrows, int N) {
-  return sizeof(double) * (size_t)stride * tpw + sizeof(ConRow) * (size_t)nrows + sizeof(int) * 2 * (size_t)N;
+inline size_t bwd_team_shmem(int stride, int tpw, int /*nrows*/, int N) {
+  return sizeof(double) * (size_t)stride * tpw + sizeof(int) * 2 * (size_t)N;
+}
+
+// Expansion records (Bf.E, written by k_expand_team, read by k_bwd_team): per (trajectory, knot)
+// a record of NE = n + m + m² + n² doubles
+//   [0, n) Q.x | [n, n+m) Q.u | [n+m, n+m+m²) Q.uu | [n+m+m², NE) Q.xx   (column-major blocks;
+// sqrt: Q.uu, Q.xx are the upper factors). Q.xx is written only at "dense" knots — the terminal
+// knot and the knots whose AL terms change it (std: any row; sqrt: a row with a state gradient);
+// elsewhere it is the problem constant (Q dt, or cholesky(Q dt).U), which the backward pass reads
+// from DevProblem. Q.ux never depends on the trajectory for the team kernel's rows (bounds, goal,
+// circles and spheres each have either a state or a control gradient): H dt (+ 0.0 where the std
+// AL expansion adds its zero cu'Iμcx term, so the sign of a zero matches).
+template <class M>
+__host__ __device__ constexpr int ne_of() {
+  return M::n + M::m + M::m * M::m + M::n * M::n;
+}
+template <bool SQRT, bool AL>
+__device__ __forceinline__ bool knot_dense(int k, int N, int cnt, int nx) {
+  return k == N - 1 || (AL && (SQRT ? nx > 0 : cnt > 0));
+}
+// LDS per team of k_expand_team (doubles): bus for the 8-lane QR, then RowInfo[pmax], xr/ur lists
+// (pmax ints each), x[n], u[m]
+template <class M>
+__host__ __device__ inline int expand_team_stride(int pmax) {
+  int s = 48 + pmax * 8 + pmax + M::n + M::m;
+  return s + (s & 1);
 }
 
 // Host-side admissibility of the team kernel for a problem (otherwise the LDS kernel runs).
@@ -361,6 +383,243 @@ __device__ __forceinline__ bool cond_exceeds_team(const double (&R)[m][m], const
   return r;
 }
 
+// ============================================================================================
+// k_expand_team: cost_expansion! (ilqr_methods.jl:55-62 -> objective.jl:51-94, cost.jl:183-198;
+// AL terms augmented_lagrangian_methods.jl:186-276) for every (trajectory, knot) at once, into the
+// expansion records Bf.E. The reference expands every knot before the backward pass starts, and
+// nothing here depends on the cost-to-go, so this runs knot-parallel, off the Riccati recursion's
+// serial chain: a TEAM-lane team per (trajectory, knot), consecutive knots of one trajectory in
+// neighbouring teams (coalesced X, U, λ, μ reads and record writes). Lane c forms column c of Q.xx
+// and Q.uu exactly as the fused expansion of round 2 did (same operations, same order: DESIGN.md §3).
+// ============================================================================================
+template <class M, bool SQRT, bool AL, bool TERM>
+__device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffers& Bf, long long b, int k,
+                                            double* tlds, int tl, int team) {
+  using Cfg = TeamCfg<M>;
+  constexpr int n = M::n, m = M::m, TEAM = Cfg::TEAM, RQ = Cfg::RQ, PU = Cfg::PU, NE = ne_of<M>();
+  const int N = P->N, pmax = P->pmax;
+  const double dt = P->dt;
+  const bool colx = tl < n, colu = tl < m;
+  const int c = colx ? tl : 0, cu = colu ? tl : 0;
+  const double* xg = Bf.X + ((size_t)b * N + k) * n;
+  const double* ug = TERM ? nullptr : Bf.U + ((size_t)b * (N - 1) + k) * m;
+  double* bus = tlds;
+  double Qxc[n], Quuc[m], Qu[m], Qxs;
+  const double xc = xg[c];
+  const int diag_mode = P->diag_cost;
+  if (!TERM && diag_mode == 2) {
+    // diagonal cost with +0.0 off-diagonals (host-checked): the per-lane constants are one
+    // diagonal entry each, the rest literal zeros -- the same values the general path loads
+    const double Qcc = P->Q[c + n * c], qc = P->q[c];
+    const double qd = SQRT ? P->cQ[c + n * c] : Qcc * dt;
+    const double rd = SQRT ? P->cR[cu + m * cu] : P->R[cu + m * cu] * dt;
+    Qxs = ((fma(Qcc, xc, 0.0) + qc) + 0.0) * dt;
+#pragma unroll
+    for (int i = 0; i < m; i++) Qu[i] = ((fma(P->R[i + m * i], ug[i], 0.0) + P->r[i]) + 0.0) * dt;
+#pragma unroll
+    for (int i = 0; i < n; i++) Qxc[i] = (i == c) ? qd : 0.0;
+#pragma unroll
+    for (int i = 0; i < m; i++) Quuc[i] = (i == cu) ? rd : 0.0;
+  } else if (!TERM) {
+    double a = 0.0, bq = 0.0;
+    if (diag_mode) {
+      a = fma(P->Q[c + n * c], xc, 0.0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < n; j++) a = fma(P->Q[c + n * j], xg[j], a);
+#pragma unroll
+      for (int j = 0; j < m; j++) bq = fma(P->H[j + m * c], ug[j], bq);
+    }
+    Qxs = ((a + P->q[c]) + bq) * dt;
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      double a2 = 0.0, b2 = 0.0;
+      if (diag_mode) {
+        a2 = fma(P->R[i + m * i], ug[i], 0.0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
+#pragma unroll
+        for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
+      }
+      Qu[i] = ((a2 + P->r[i]) + b2) * dt;
+    }
+#pragma unroll
+    for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
+#pragma unroll
+    for (int i = 0; i < m; i++) Quuc[i] = SQRT ? P->cR[i + m * cu] : P->R[i + m * cu] * dt;
+  } else {
+    double a = 0.0;
+    if (diag_mode) {
+      a = fma(P->Qf[c + n * c], xc, 0.0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < n; j++) a = fma(P->Qf[c + n * j], xg[j], a);
+    }
+    Qxs = a + P->qf[c];
+#pragma unroll
+    for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQf[i + n * c] : P->Qf[i + n * c];
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      Qu[i] = 0.0;
+      Quuc[i] = 0.0;
+    }
+  }
+  const int p = AL ? P->knot_cnt[k] : 0;
+  if (AL && p > 0) {
+    // rows area after the 8-lane QR bus
+    RowInfo* rows = reinterpret_cast<RowInfo*>(tlds + 48);
+    int* xr = reinterpret_cast<int*>(rows + pmax);
+    int* ur = xr + pmax;
+    double* xs = reinterpret_cast<double*>(ur + pmax);  // (2 pmax ints: 8-byte aligned)
+    double* us = xs + n;
+    if (colx) xs[tl] = xc;
+    if (!TERM && colu) us[tl] = ug[tl];
+    team_sync();
+    int nx, nu;
+    team_rows<M>(Bf, b, k, N, pmax, p, P->rows + P->knot_off[k], xs, TERM ? nullptr : us, rows, xr, ur, nx, nu,
+                 team, tl, TEAM);
+    team_sync();
+    if (!SQRT) {
+      // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order; the
+      // team kernel's rows never couple x and u, so the Q.ux term is an exact zero: ne_of)
+      double tX[n], tUu[m];
+#pragma unroll
+      for (int i = 0; i < n; i++) tX[i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < m; i++) tUu[i] = 0.0;
+      for (int r = 0; r < p; r++) {
+        const RowInfo& ri = rows[r];
+        const double vxc = colx ? row_at(ri, c) : 0.0;
+        const double vuc = (colu && !TERM) ? row_at(ri, n + cu) : 0.0;
+        if (vxc == 0.0 && vuc == 0.0) continue;
+        for (int z = 0; z < ri.nnz; z++) {
+          const int id = ri.idx[z];
+          const double vw = ri.v[z] * ri.w;
+#pragma unroll
+          for (int i = 0; i < n; i++)
+            if (id == i && vxc != 0.0) tX[i] = fma(vw, vxc, tX[i]);
+#pragma unroll
+          for (int i = 0; i < m; i++)
+            if (id == n + i && vuc != 0.0) tUu[i] = fma(vw, vuc, tUu[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] += tX[i];
+      if (!TERM) {
+#pragma unroll
+        for (int i = 0; i < m; i++) Quuc[i] += tUu[i];
+      }
+    } else {
+      // chol_plus!(Q.xx, Iμ_sqrt cx): QR of [Q.xx; ws.*cx]; rows without a state gradient are
+      // zero rows of the stacked matrix and do not change R
+      if (nx > 0) {
+        double a[RQ];
+#pragma unroll
+        for (int i = 0; i < RQ; i++) {
+          if (i < n) {
+            a[i] = Qxc[i];
+          } else if (i - n < nx) {
+            const RowInfo& ri = rows[xr[i - n]];
+            a[i] = ri.ws * row_at(ri, c);
+          } else {
+            a[i] = 0.0;
+          }
+        }
+        team_qr<RQ, n, n, TEAM>(a, n + nx, tl, bus);
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
+      }
+      // chol_plus!(Q.uu, Iμ_sqrt cu)
+      if (!TERM && nu > 0) {
+        double a[m + PU];
+#pragma unroll
+        for (int i = 0; i < m + PU; i++) {
+          if (i < m) {
+            a[i] = Quuc[i];
+          } else if (i - m < nu) {
+            const RowInfo& ri = rows[ur[i - m]];
+            // (control-bound rows: one gradient entry, ±1 at n + control)
+            a[i] = ri.ws * ((ri.idx[0] == n + cu) ? ri.v[0] : 0.0);
+          } else {
+            a[i] = 0.0;
+          }
+        }
+        // (16-lane teams run every QR over the zero-padded compile-time rows; 8-lane teams
+        // specialise the common case, every control bounded on both sides)
+        if (TEAM == 16 || nu == PU)
+          team_qr<m + PU, m, m, TEAM, true>(a, m + PU, tl, bus);
+        else
+          team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
+#pragma unroll
+        for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+      }
+    }
+    // Q.x .+= cx'g ; Q.u .+= cu'g
+    {
+      double tx = 0.0;
+      for (int z = 0; z < nx; z++) {
+        const RowInfo& ri = rows[xr[z]];
+        const double v = colx ? row_at(ri, c) : 0.0;
+        if (v != 0.0) tx = fma(v, ri.g, tx);
+      }
+      Qxs += tx;
+      if (!TERM) {
+        double tu[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) tu[i] = 0.0;
+        for (int z = 0; z < nu; z++) {
+          const RowInfo& ri = rows[ur[z]];
+          const int id = ri.idx[0];
+#pragma unroll
+          for (int i = 0; i < m; i++)
+            if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) Qu[i] += tu[i];
+      }
+    }
+  }
+  // record (ne_of): Q.x, Q.u, Q.uu, and Q.xx at dense knots
+  double* e = Bf.E + ((size_t)b * N + k) * NE;
+  if (colx) e[tl] = Qxs;
+  if (!TERM) {
+    if (colu) {
+      double qu = Qu[0];
+#pragma unroll
+      for (int i = 1; i < m; i++)
+        if (tl == i) qu = Qu[i];
+      e[n + tl] = qu;
+#pragma unroll
+      for (int i = 0; i < m; i++) e[n + m + i + m * tl] = Quuc[i];
+    }
+  }
+  int nxk = 0;
+  if (AL && SQRT) nxk = P->knot_nx[k];
+  if (colx && knot_dense<SQRT, AL>(k, N, p, nxk)) {
+#pragma unroll
+    for (int i = 0; i < n; i++) e[n + m + m * m + i + n * tl] = Qxc[i];
+  }
+}
+
+template <class M, int SQRTI, int ALI>
+__global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuffers Bf) {
+  using Cfg = TeamCfg<M>;
+  extern __shared__ double expand_lds[];
+  const int team = threadIdx.x / Cfg::TEAM, tl = threadIdx.x % Cfg::TEAM;
+  const int N = P->N;
+  const long long idx = (long long)blockIdx.x * Cfg::TPW + team;
+  const long long b = idx / N;
+  const int k = (int)(idx - b * N);
+  if (b >= P->B) return;  // whole teams return together (DPP broadcasts stay within a team)
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  double* tlds = expand_lds + (size_t)team * expand_team_stride<M>(P->pmax);
+  if (k == N - 1)
+    team_expand<M, SQRTI != 0, ALI != 0, true>(P, Bf, b, k, tlds, tl, team);
+  else
+    team_expand<M, SQRTI != 0, ALI != 0, false>(P, Bf, b, k, tlds, tl, team);
+}
+
 #ifndef TOG_BWD_WAVES
 #define TOG_BWD_WAVES 2
 #endif
@@ -395,30 +654,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   // constants out of the knot loop and keep them in registers for the whole kernel)
   using Cfg = TeamCfg<M>;
   constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
-  constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, RQ = Cfg::RQ, PU = Cfg::PU, NQ = nq_of<M>();
+  constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, NQ = nq_of<M>(), NE = ne_of<M>();
   static_assert(m <= n && n + 1 <= TEAM, "team layout");
   extern __shared__ double team_lds[];
   const int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
   const long long b = (long long)blockIdx.x * Cfg::TPW + team;
-  const int N = P->N, pmax = P->pmax;
+  const int N = P->N;
   const int stride = Bf.bwd_stride;
   constexpr int SREG = sreg_size<M>(SQRT);
   constexpr int SOFF = n * n;                            // offset of s in the S-region
   double* Sreg = team_lds + (size_t)team * stride;      // S (persistent between knots)
   double* QU = Sreg + SOFF + n;                          // Q.uu of the current knot (column-major)
   double* bus = Sreg + SREG;                             // region 1 | region 2
-  // block-wide caches: deduplicated constraint rows and the per-knot tables (read every knot)
-  ConRow* row_cache = reinterpret_cast<ConRow*>(team_lds + (size_t)Cfg::TPW * stride);
-  int* koff = reinterpret_cast<int*>(row_cache + P->nrows);
-  int* kcnt = koff + N;
+  // block-wide per-knot tables (dense-record test, knot_dense)
+  int* kcnt = reinterpret_cast<int*>(team_lds + (size_t)Cfg::TPW * stride);
+  int* knx = kcnt + N;
   if (AL) {
-    const int nr = P->nrows;
-    const double* src = reinterpret_cast<const double*>(P->rows);
-    double* dst = reinterpret_cast<double*>(row_cache);
-    for (int e = threadIdx.x; e < nr * (int)(sizeof(ConRow) / 8); e += 64) dst[e] = src[e];
     for (int e = threadIdx.x; e < N; e += 64) {
-      koff[e] = P->knot_off[e];
       kcnt[e] = P->knot_cnt[e];
+      knx[e] = P->knot_nx[e];
     }
     __syncthreads();
   }
@@ -428,12 +682,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   const double dt = P->dt;
   const long long bb = live ? b : 0;  // safe base for idle teams (they never store)
   // per-trajectory bases, formed at each use from an opaque copy of bb (see opaque())
-#define Xg (Bf.X + (size_t)opaque(bb) * N * n)
-#define Ug (Bf.U + (size_t)opaque(bb) * (N - 1) * m)
 #define ABg (Bf.AB + (size_t)opaque(bb) * (N - 1) * n * L)
 #define Kg (Bf.K + (size_t)opaque(bb) * (N - 1) * m * n)
 #define dg (Bf.d + (size_t)opaque(bb) * (N - 1) * m)
 #define Qs (Bf.Qscr + (size_t)opaque(bb) * N * NQ)
+#define Eg (Bf.E + (size_t)opaque(bb) * N * NE)
   const bool colx = tl < n;  // this lane owns a state column
   const bool colu = tl < m;  // this lane owns a control column
   const int c = colx ? tl : 0;
@@ -450,74 +703,35 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
   bool done = !live;
   BPROF_DECL
 
-  // cost expansion of knot k (terminal when TERM) into this lane's Q blocks; the AL terms use the
-  // team's row table (objective.jl:51-94, augmented_lagrangian_methods.jl:186-276)
-  const int diag_mode = P->diag_cost;  // read once (P is not __restrict__)
+  // Q blocks of knot k (terminal when TERM) from its expansion record (k_expand_team, ne_of):
+  // this lane's columns of Q.xx, Q.uu, Q.ux, its Q.x entry and the whole Q.u
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
                     double(&Quxc)[m]) {
     constexpr bool term = decltype(term_c)::value;
-    const double* xg = Xg + (size_t)k * n;
-    const double* ug = term ? nullptr : Ug + (size_t)k * m;
-    const int tlk = opaque(tl);  // per-lane columns of the problem constants, formed per knot
+    const int tlk = opaque(tl);  // per-lane columns, formed per knot (not kept live across the loop)
     const int c = tlk < n ? tlk : 0, cu = tlk < m ? tlk : 0;
-    const double xc = xg[c];
-    if (!term && diag_mode == 2) {
-      // diagonal cost with +0.0 off-diagonals (host-checked): the per-lane constants are one
-      // diagonal entry each, the rest literal zeros -- the same values the general path loads
-      const double Qcc = P->Q[c + n * c], qc = P->q[c];
-      const double qd = SQRT ? P->cQ[c + n * c] : Qcc * dt;
-      const double rd = SQRT ? P->cR[cu + m * cu] : P->R[cu + m * cu] * dt;
-      Qxs = ((fma(Qcc, xc, 0.0) + qc) + 0.0) * dt;
+    const double* e = Eg + (size_t)k * NE;
+    const int cnt = AL ? kcnt[k] : 0;
+    Qxs = e[c];
+    if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
 #pragma unroll
-      for (int i = 0; i < m; i++) Qu[i] = ((fma(P->R[i + m * i], ug[i], 0.0) + P->r[i]) + 0.0) * dt;
-#pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = (i == c) ? qd : 0.0;
-#pragma unroll
-      for (int i = 0; i < m; i++) {
-        Quuc[i] = (i == cu) ? rd : 0.0;
-        Quxc[i] = 0.0;
-      }
-    } else if (!term) {
-      double a = 0.0, bq = 0.0;
-      if (diag_mode) {
-        a = fma(P->Q[c + n * c], xc, 0.0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < n; j++) a = fma(P->Q[c + n * j], xg[j], a);
-#pragma unroll
-        for (int j = 0; j < m; j++) bq = fma(P->H[j + m * c], ug[j], bq);
-      }
-      Qxs = ((a + P->q[c]) + bq) * dt;
-#pragma unroll
-      for (int i = 0; i < m; i++) {
-        double a2 = 0.0, b2 = 0.0;
-        if (diag_mode) {
-          a2 = fma(P->R[i + m * i], ug[i], 0.0);
-        } else {
-#pragma unroll
-          for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
-#pragma unroll
-          for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
-        }
-        Qu[i] = ((a2 + P->r[i]) + b2) * dt;
-      }
+      for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+    } else {
 #pragma unroll
       for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
+    }
+    if (!term) {
 #pragma unroll
-      for (int i = 0; i < m; i++) Quuc[i] = SQRT ? P->cR[i + m * cu] : P->R[i + m * cu] * dt;
+      for (int i = 0; i < m; i++) Qu[i] = e[n + i];
 #pragma unroll
-      for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;
-    } else {
-      double a = 0.0;
-      if (diag_mode) {
-        a = fma(P->Qf[c + n * c], xc, 0.0);
-      } else {
+      for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
+      const bool zterm = !SQRT && AL && cnt > 0;  // the std AL expansion's "+= cu'Iμcx" (an exact zero)
 #pragma unroll
-        for (int j = 0; j < n; j++) a = fma(P->Qf[c + n * j], xg[j], a);
+      for (int i = 0; i < m; i++) {
+        const double h = P->H[i + m * c] * dt;
+        Quxc[i] = zterm ? h + 0.0 : h;
       }
-      Qxs = a + P->qf[c];
-#pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQf[i + n * c] : P->Qf[i + n * c];
+    } else {
 #pragma unroll
       for (int i = 0; i < m; i++) {
         Qu[i] = 0.0;
@@ -525,137 +739,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
         Quxc[i] = 0.0;
       }
     }
-    if (!term) BPROF(12)  // expand: cost terms (x/u loads)
-    if (AL && kcnt[k] > 0) {
-      const int p = kcnt[k];
-      // rows area inside the second bus region (free during the expansion)
-      RowInfo* rows = reinterpret_cast<RowInfo*>(bus + n * L);
-      int* xr = reinterpret_cast<int*>(rows + pmax);
-      int* ur = xr + pmax;
-      double* xs = bus + n * L + pmax * 8 + pmax;
-      double* us = xs + n;
-      if (colx) xs[tl] = xc;
-      if (!term && colu) us[tl] = ug[tl];
-      team_sync();
-      int nx, nu;
-      team_rows<M>(Bf, b, k, N, pmax, p, row_cache + koff[k], xs, term ? nullptr : us, rows, xr, ur, nx, nu, team,
-                   tl, TEAM);
-      team_sync();
-      if (!term) BPROF(13)  // expand: team_rows (lam/mu loads, row eval)
-      if (!SQRT) {
-        // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order)
-        double tX[n], tUx[m], tUu[m];
-#pragma unroll
-        for (int i = 0; i < n; i++) tX[i] = 0.0;
-#pragma unroll
-        for (int i = 0; i < m; i++) {
-          tUx[i] = 0.0;
-          tUu[i] = 0.0;
-        }
-        for (int r = 0; r < p; r++) {
-          const RowInfo& ri = rows[r];
-          const double vxc = colx ? row_at(ri, c) : 0.0;
-          const double vuc = (colu && !term) ? row_at(ri, n + cu) : 0.0;
-          if (vxc == 0.0 && vuc == 0.0) continue;
-          for (int z = 0; z < ri.nnz; z++) {
-            const int id = ri.idx[z];
-            const double vw = ri.v[z] * ri.w;
-#pragma unroll
-            for (int i = 0; i < n; i++)
-              if (id == i && vxc != 0.0) tX[i] = fma(vw, vxc, tX[i]);
-#pragma unroll
-            for (int i = 0; i < m; i++)
-              if (id == n + i) {
-                if (vxc != 0.0) tUx[i] = fma(vw, vxc, tUx[i]);
-                if (vuc != 0.0) tUu[i] = fma(vw, vuc, tUu[i]);
-              }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] += tX[i];
-        if (!term) {
-#pragma unroll
-          for (int i = 0; i < m; i++) {
-            Quuc[i] += tUu[i];
-            Quxc[i] += tUx[i];
-          }
-        }
-      } else {
-        // chol_plus!(Q.xx, Iμ_sqrt cx): QR of [Q.xx; ws.*cx]; rows without a state gradient are
-        // zero rows of the stacked matrix and do not change R
-        if (nx > 0) {
-          double a[RQ];
-#pragma unroll
-          for (int i = 0; i < RQ; i++) {
-            if (i < n) {
-              a[i] = Qxc[i];
-            } else if (i - n < nx) {
-              const RowInfo& ri = rows[xr[i - n]];
-              a[i] = ri.ws * row_at(ri, c);
-            } else {
-              a[i] = 0.0;
-            }
-          }
-          team_qr<RQ, n, n, TEAM>(a, n + nx, tl, bus);
-#pragma unroll
-          for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
-        }
-        // chol_plus!(Q.uu, Iμ_sqrt cu)
-        if (!term && nu > 0) {
-          double a[m + PU];
-#pragma unroll
-          for (int i = 0; i < m + PU; i++) {
-            if (i < m) {
-              a[i] = Quuc[i];
-            } else if (i - m < nu) {
-              const RowInfo& ri = rows[ur[i - m]];
-              // (control-bound rows: one gradient entry, ±1 at n + control)
-              a[i] = ri.ws * ((ri.idx[0] == n + cu) ? ri.v[0] : 0.0);
-            } else {
-              a[i] = 0.0;
-            }
-          }
-          if (!term) BPROF(14)  // expand: chol_plus operand rows
-          // (16-lane teams run every QR over the zero-padded compile-time rows; 8-lane teams
-          // specialise the common case, every control bounded on both sides)
-          if (TEAM == 16 || nu == PU)
-            team_qr<m + PU, m, m, TEAM, true>(a, m + PU, tl, bus);
-          else
-            team_qr<m + PU, m, m, TEAM>(a, m + nu, tl, bus);
-#pragma unroll
-          for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
-          if (!term) BPROF(15)  // expand: chol_plus QR
-        }
-      }
-      // Q.x .+= cx'g ; Q.u .+= cu'g
-      {
-        double tx = 0.0;
-        for (int z = 0; z < nx; z++) {
-          const RowInfo& ri = rows[xr[z]];
-          const double v = colx ? row_at(ri, c) : 0.0;
-          if (v != 0.0) tx = fma(v, ri.g, tx);
-        }
-        Qxs += tx;
-        if (!term) BPROF(16)  // expand: Q.x += cx'g
-        if (!term) {
-          double tu[m];
-#pragma unroll
-          for (int i = 0; i < m; i++) tu[i] = 0.0;
-          for (int z = 0; z < nu; z++) {
-            const RowInfo& ri = rows[ur[z]];
-            const int id = ri.idx[0];
-#pragma unroll
-            for (int i = 0; i < m; i++)
-              if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
-          }
-#pragma unroll
-          for (int i = 0; i < m; i++) Qu[i] += tu[i];
-        }
-      }
-      team_sync();
-    }
   };
-
   while (!done) {  // one attempt of the backward pass; a regularisation restart begins a new one
     TEAM_FENCE();
     {
@@ -1456,8 +1540,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD
     if (aborted) g.active = 0;  // no forward pass, no bookkeeping: the trajectory is finished
   }
 }
-#undef Xg
-#undef Ug
+#undef Eg
 #undef ABg
 #undef Kg
 #undef dg

@@ -335,7 +335,10 @@ int generic_cost_launch(int terminal, const double* X, const double* U, long lon
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-constexpr long long cost_plugin_fingerprint() { return 0x7c057LL * 1000003LL + (long long)sizeof(HDual<3>); }
+// (TOG_HEADER_HASH: the build's hash of every libtog header's text, tog_plugin.hpp)
+constexpr long long cost_plugin_fingerprint() {
+  return (0x7c057LL * 1000003LL + (long long)sizeof(HDual<3>)) ^ (long long)TOG_HEADER_HASH;
+}
 
 }  // namespace tog
 

@@ -16,6 +16,14 @@
 #include "../../include/tog_math.h"
 #include "../../include/tog_kuka.h"
 
+// Hash of the text of every libtog header (the Makefile's HDRS, in order; abi.header_hash() computes
+// the same value for plugins generated at run time). libtog and every plugin are compiled with it and
+// the plugin fingerprints include it, so tog_model_load / tog_generic_cost_load refuse a plugin built
+// against other headers.
+#ifndef TOG_HEADER_HASH
+#define TOG_HEADER_HASH 0LL
+#endif
+
 namespace tog {
 
 constexpr int NMAX = 16;  // max states (Kuka n=14)
@@ -69,6 +77,7 @@ struct DevProblem {
   const int* knot_off;  // [N] first row of knot k
   const int* knot_cnt;  // [N] rows at knot k (p_k)
   const ConRow* rows;
+  const int* knot_nx;   // [N] rows with a state gradient at knot k (expansion records, ne_of)
   tog_options o;
 };
 
@@ -108,6 +117,7 @@ struct DevBuffers {
   double* Sdbg; // (n, n, N, B) or null
   double* sdbg; // (n, N, B) or null
   double* Qscr; // (nq, N, B) accumulated Q blocks for the restart replay path
+  double* E;    // (ne, N, B) expansion records of k_expand_team (tog_bwd_team.hpp ne_of), or null
   double* lsJ;  // (NC, B) speculative line-search trial costs
   int* lsok;    // (NC, B) speculative line-search trial rollout status
   int nc;       // candidates evaluated per trajectory per launch (<= 64)

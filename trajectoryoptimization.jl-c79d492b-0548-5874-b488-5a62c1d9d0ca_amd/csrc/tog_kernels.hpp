@@ -2433,6 +2433,8 @@ struct ModelOps {
   void (*jacobian)(const DevProblem*, const DevBuffers&, long long B, int N, int integ, hipStream_t);
   void (*backward)(const DevProblem*, const DevBuffers&, long long B, int sqrt, int al, int flags, int team,
                    hipStream_t);
+  // k_expand_team: the cost expansion records the team backward kernel reads (tog_bwd_team.hpp)
+  void (*expand)(const DevProblem*, const DevBuffers&, long long B, int N, int pmax, int sqrt, int al, hipStream_t);
   void (*forward)(const DevProblem*, const DevBuffers&, long long B, int integ, int mode, int bookkeeping,
                   const double* Jprev, double* Jout, hipStream_t, const StreamPair* sp);
   void (*cost)(const DevProblem*, const DevBuffers&, long long B, int al, int use_bar, double* J, hipStream_t);
@@ -2544,6 +2546,22 @@ struct ModelLaunch {
     } else {
       if (al) hipLaunchKernelGGL((k_backward<M, 0, 1>), g, blk, 0, st, P, Bf, flags);
       else hipLaunchKernelGGL((k_backward<M, 0, 0>), g, blk, 0, st, P, Bf, flags);
+    }
+  }
+  static void expand(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int pmax, int sq, int al,
+                     hipStream_t st) {
+    if constexpr (M::m <= M::n && M::n + 1 <= 16 && !ModelTraits<M>::min_time) {
+      constexpr int TPW = TeamCfg<M>::TPW;
+      const long long teams = B * (long long)N;
+      const dim3 g((unsigned)((teams + TPW - 1) / TPW)), blk(64);
+      const unsigned sm = (unsigned)(sizeof(double) * TPW * expand_team_stride<M>(pmax));
+      if (sq) {
+        if (al) hipLaunchKernelGGL((k_expand_team<M, 1, 1>), g, blk, sm, st, P, Bf);
+        else hipLaunchKernelGGL((k_expand_team<M, 1, 0>), g, blk, sm, st, P, Bf);
+      } else {
+        if (al) hipLaunchKernelGGL((k_expand_team<M, 0, 1>), g, blk, sm, st, P, Bf);
+        else hipLaunchKernelGGL((k_expand_team<M, 0, 0>), g, blk, sm, st, P, Bf);
+      }
     }
   }
   template <int INTEG>
@@ -2708,6 +2726,7 @@ struct ModelLaunch {
     o.rollout_open = rollout_open;
     o.jacobian = jacobian;
     o.backward = backward;
+    o.expand = expand;
     o.forward = forward;
     o.cost = cost;
     o.rollout = rollout;

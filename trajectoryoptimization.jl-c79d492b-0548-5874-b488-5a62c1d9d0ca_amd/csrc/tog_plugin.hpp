@@ -23,10 +23,13 @@
 #include "tog_kernels.hpp"
 
 namespace tog {
-// layout fingerprint of the structures shared across the plugin boundary
+// layout fingerprint of the structures shared across the plugin boundary, combined with the hash of
+// the text of every libtog header (TOG_HEADER_HASH, tog_device.hpp): a plugin built against other
+// kernel code -- same struct sizes, different numerics or protocol -- is refused as well
 constexpr long long plugin_fingerprint() {
-  return (long long)TOG_ABI_VERSION * 1000003LL + (long long)sizeof(DevProblem) * 7919LL +
-         (long long)sizeof(DevBuffers) * 131LL + (long long)sizeof(ModelOps) * 17LL + (long long)sizeof(TrajState);
+  return ((long long)TOG_ABI_VERSION * 1000003LL + (long long)sizeof(DevProblem) * 7919LL +
+          (long long)sizeof(DevBuffers) * 131LL + (long long)sizeof(ModelOps) * 17LL + (long long)sizeof(TrajState)) ^
+         (long long)TOG_HEADER_HASH;
 }
 }  // namespace tog
 

@@ -64,6 +64,7 @@ struct tog_handle {
   DevProblem* dP = nullptr;
   int* d_knot_off = nullptr;
   int* d_knot_cnt = nullptr;
+  int* d_knot_nx = nullptr;
   ConRow* d_rows = nullptr;
   DevBuffers buf = {};
   const ModelOps* ops = nullptr;
@@ -651,11 +652,21 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   P.o = *opts;
   P.R_min_time = (d->flags & TOG_PROB_MIN_TIME) ? d->R_min_time : 0.0;
   const size_t B = (size_t)h->B, P1 = (size_t)(h->pmax > 0 ? h->pmax : 1);
+  // rows with a state gradient per knot (every row type but the control bounds): the knots whose
+  // square-root expansion changes Q.xx (expansion records, tog_bwd_team.hpp ne_of)
+  std::vector<int> nxk(N, 0);
+  for (int k = 0; k < N; k++)
+    for (int r = 0; r < cnt[k]; r++) {
+      const int t = rows[off[k] + r].type;
+      if (t != ROW_UMAX && t != ROW_UMIN) nxk[k]++;
+    }
   if ((rc = dalloc(h, &h->d_knot_off, N)) || (rc = dalloc(h, &h->d_knot_cnt, N)) ||
-      (rc = dalloc(h, &h->d_rows, rows.size() + 1)) || (rc = dalloc(h, &h->dP, 1)))
+      (rc = dalloc(h, &h->d_knot_nx, N)) || (rc = dalloc(h, &h->d_rows, rows.size() + 1)) ||
+      (rc = dalloc(h, &h->dP, 1)))
     return rc;
   HIPCHECK(hipMemcpy(h->d_knot_off, off.data(), sizeof(int) * N, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(h->d_knot_cnt, cnt.data(), sizeof(int) * N, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(h->d_knot_nx, nxk.data(), sizeof(int) * N, hipMemcpyHostToDevice));
   if (!rows.empty()) HIPCHECK(hipMemcpy(h->d_rows, rows.data(), sizeof(ConRow) * rows.size(), hipMemcpyHostToDevice));
   {
     // TOG_BWD=lds forces the one-wave-per-trajectory LDS backward kernel (A/B checks)
@@ -674,6 +685,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   }
   P.knot_off = h->d_knot_off;
   P.knot_cnt = h->d_knot_cnt;
+  P.knot_nx = h->d_knot_nx;
   P.rows = h->d_rows;
   HIPCHECK(hipMemcpy(h->dP, &P, sizeof(P), hipMemcpyHostToDevice));
 
@@ -691,6 +703,11 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     return rc;
   b.Sdbg = nullptr;
   b.sdbg = nullptr;
+  b.E = nullptr;
+  if (h->bwd_team) {  // expansion records of the team backward pass (k_expand_team)
+    const size_t ne = (size_t)n + m + (size_t)m * m + (size_t)n * n;
+    if ((rc = dalloc(h, &b.E, B * N * ne))) return rc;
+  }
   b.nc = opts->iterations_linesearch + 1 < 64 ? opts->iterations_linesearch + 1 : 64;
   if (b.nc < 1) b.nc = 1;
   b.nknots = N;
@@ -1092,6 +1109,7 @@ int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, 
     const size_t B = h->B, n = h->n, N = h->N;
     if ((rc = dalloc(h, &h->buf.Sdbg, B * N * n * n)) || (rc = dalloc(h, &h->buf.sdbg, B * N * n))) return rc;
   }
+  if (h->bwd_team) h->ops->expand(h->dP, h->buf, h->B, h->N, h->pmax, sq, al, h->stream);
   h->ops->backward(h->dP, h->buf, h->B, sq, al, flags, h->bwd_team, h->stream);
   HIPCHECK(hipGetLastError());
   if (dV_out) return tog_get(h, TOG_FIELD_DV, dV_out);
@@ -1159,6 +1177,10 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   h->buf.ls_first = ((double)h->B <= few || (h->last_active >= 0.0 && h->last_active <= few)) ? h->buf.nc : LS_FIRST;
   for (int i = 0; i < nsteps; i++) {
     timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
+    if (h->bwd_team)
+      timed(h, TOG_KERNEL_EXPANSION, [&] {
+        h->ops->expand(h->dP, h->buf, h->B, h->N, h->pmax, h->opts.square_root, al, h->stream);
+      });
     timed(h, TOG_KERNEL_BACKWARD,
           [&] { h->ops->backward(h->dP, h->buf, h->B, h->opts.square_root, al, 0, h->bwd_team, h->stream); });
     timed(h, TOG_KERNEL_FORWARD,

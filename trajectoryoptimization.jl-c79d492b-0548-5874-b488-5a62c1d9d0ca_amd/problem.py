@@ -181,13 +181,14 @@ def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=N
         con = _CON_TEMPLATE.format(body="\n".join("    " + ln for ln in con_body.strip().splitlines()))
     src = _PLUGIN_TEMPLATE.format(hdr=str(csrc / "tog_plugin.hpp"), name=name, n=int(n), m=int(m), body=body,
                                   con=con)
-    key = hashlib.sha1(src.encode()).hexdigest()[:12]
+    hh = abi.header_hash()  # the plugin is compiled against (and cached under) libtog's header text
+    key = hashlib.sha1((src + hh).encode()).hexdigest()[:12]
     so = out_dir / f"gen_{name}_{key}.so"
     if not so.exists():
         hip = out_dir / f"gen_{name}_{key}.hip"
         hip.write_text(src)
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-fPIC",
-               "-shared", "-o", str(so), str(hip)]
+               f"-DTOG_HEADER_HASH=0x{hh}LL", "-shared", "-o", str(so), str(hip)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             hip.unlink(missing_ok=True)  # no broken source left in the plugin directory
@@ -404,13 +405,14 @@ def generic_cost(stage_body: str, terminal_body: str, n: int, m: int, name: str 
     ind = lambda b: "\n".join("    " + ln for ln in b.strip().splitlines())
     src = _COST_TEMPLATE.format(hdr=str(csrc / "tog_cost_plugin.hpp"), name=name, n=int(n), m=int(m),
                                 stage=ind(stage_body), term=ind(terminal_body))
-    key = hashlib.sha1(src.encode()).hexdigest()[:12]
+    hh = abi.header_hash()  # the plugin is compiled against (and cached under) libtog's header text
+    key = hashlib.sha1((src + hh).encode()).hexdigest()[:12]
     so = out_dir / f"gen_{name}_{key}.so"
     if not so.exists():
         hip = out_dir / f"gen_{name}_{key}.hip"
         hip.write_text(src)
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-fPIC",
-               "-shared", "-o", str(so), str(hip)]
+               f"-DTOG_HEADER_HASH=0x{hh}LL", "-shared", "-o", str(so), str(hip)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             hip.unlink(missing_ok=True)  # no broken source left in the plugin directory
