@@ -1,0 +1,47 @@
+"""A plain C caller of the ABI (tests/c/test_capi_config3.c): it fills tog_problem_desc for BASELINE
+config 3 exactly as integration/julia/libtog.jl's tog_desc marshals the reference Problem (the Julia
+binding itself cannot run here: no Julia in the image), solves through tog_create -> tog_set_state ->
+tog_solve -> tog_get, and must equal the Python (ctypes) path bit for bit: same descriptor, same
+device code, so X, U and every per-trajectory statistic agree exactly."""
+import pathlib
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+BIN = ROOT / "tests" / "c" / "test_capi_config3"
+
+
+def test_c_caller_links_the_library(tog):
+    """The C program links libtog.so and sees the same ABI version (no device needed)."""
+    assert BIN.exists(), "tests/c/test_capi_config3 not built: __graft_entry__.build() builds it"
+    r = subprocess.run([str(BIN), "--version"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert int(r.stdout.strip()) == tog.abi.TOG_ABI_VERSION
+
+
+@pytest.mark.gpu
+def test_c_caller_equals_python_path(tog, gpu, tmp_path):
+    B = 16
+    prob, opts = tog.Problems.config_quadrotor(B=B)
+    n, m, N = 13, 4, 101
+    # prob.x0 (B, n) and prob.U (B, N-1, m) row-major are the ABI's column-major (n, B), (m, N-1, B)
+    U0 = np.ascontiguousarray(prob.U)
+    with open(tmp_path / "in.bin", "wb") as f:
+        f.write(np.int64(B).tobytes())
+        f.write(np.ascontiguousarray(prob.x0).tobytes())
+        f.write(U0.tobytes())
+    r = subprocess.run([str(BIN), str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = np.fromfile(tmp_path / "out.bin", dtype=np.float64)
+    X_c = out[:B * N * n].reshape(B, N, n)
+    U_c = out[B * N * n:B * N * n + B * (N - 1) * m].reshape(B, N - 1, m)
+    St_c = out[B * N * n + B * (N - 1) * m:].reshape(B, tog.abi.NSTATS)
+    gpu = prob.copy()
+    solver = tog.solve_b(gpu, opts)
+    St_py = solver.handle.get(tog.abi.FIELD_STATS)
+    assert np.array_equal(X_c, gpu._X), np.max(np.abs(X_c - gpu._X))
+    assert np.array_equal(U_c, gpu._U), np.max(np.abs(U_c - gpu._U))
+    assert np.array_equal(St_c, St_py)

@@ -648,8 +648,11 @@ static __device__ unsigned long long tog_bwd_prof[BPROF_N];
 #define BPROF(id) {}
 #define BPROF_FLUSH
 #endif
-template <class M, int SQRTI, int ALI>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TOG_BWD_WAVES))) k_bwd_team(const DevProblem* P, DevBuffers Bf, int flags) {
+// WPE: waves per SIMD the register budget is sized for. The full batch runs WPE = TOG_BWD_WAVES (2:
+// 256 registers, latency hidden by the second wave); the convergence tail -- few trajectories, most
+// SIMDs idle -- runs WPE = 1 (512 registers, no spills on the serial chain; DevBuffers::tail).
+template <class M, int SQRTI, int ALI, int WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) k_bwd_team(const DevProblem* P, DevBuffers Bf, int flags) {
   // (P is deliberately not __restrict__: that would let LICM hoist ~100 loop-invariant problem
   // constants out of the knot loop and keep them in registers for the whole kernel)
   using Cfg = TeamCfg<M>;

@@ -133,7 +133,7 @@ struct DevBuffers {
   int ls_pend_ok;     // solve steps may carry an undecided line search over to the next step
   double* cand;       // (NCP, n+m, N, B) every trial's rollout (candidate-copy line search), or null
   int ncp;            // candidate slots per element (nc rounded up to 8)
-  int pad3_;
+  int tail;           // few trajectories active (last host readback): latency-sized backward kernels
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū

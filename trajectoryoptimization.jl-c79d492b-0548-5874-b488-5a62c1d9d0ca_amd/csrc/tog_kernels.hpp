@@ -2529,13 +2529,20 @@ struct ModelLaunch {
       Bl.bwd_stride = Bf.bwd_stride2[sq ? 1 : 0];
       Bl.bwd_shmem = Bf.bwd_shmem2[sq ? 1 : 0];
       const unsigned sm = (unsigned)Bl.bwd_shmem;
-      if (sq) {
-        if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1>), g, blk, sm, st, P, Bl, flags);
-        else hipLaunchKernelGGL((k_bwd_team<M, 1, 0>), g, blk, sm, st, P, Bl, flags);
-      } else {
-        if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1>), g, blk, sm, st, P, Bl, flags);
-        else hipLaunchKernelGGL((k_bwd_team<M, 0, 0>), g, blk, sm, st, P, Bl, flags);
-      }
+      auto launch = [&](auto wpe_c) {
+        constexpr int W = decltype(wpe_c)::value;
+        if (sq) {
+          if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1, W>), g, blk, sm, st, P, Bl, flags);
+          else hipLaunchKernelGGL((k_bwd_team<M, 1, 0, W>), g, blk, sm, st, P, Bl, flags);
+        } else {
+          if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1, W>), g, blk, sm, st, P, Bl, flags);
+          else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
+        }
+      };
+      if (Bf.tail)
+        launch(std::integral_constant<int, 1>{});
+      else
+        launch(std::integral_constant<int, TOG_BWD_WAVES>{});
       return;
     }
     }

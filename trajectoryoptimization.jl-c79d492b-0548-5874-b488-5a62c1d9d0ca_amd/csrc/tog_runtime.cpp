@@ -40,6 +40,10 @@ const ModelOps* ops_mt_double_integrator();
 
 static thread_local std::string g_err;
 
+// active trajectories at or below which tog_solve_step runs the latency-sized kernel variants
+// (DevBuffers::tail): 2048 trajectories = 512 team waves, at most one per SIMD
+static constexpr double TAIL_ACTIVE = 2048.0;
+
 static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -718,6 +722,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     if ((rc = dalloc(h, &b.jws, lanes * (size_t)ops->jws_per_lane))) return rc;
   }
   b.ncp = (b.nc + 7) & ~7;
+  b.tail = 0;
   b.ls_pend_ok = getenv("TOG_LS_NOPEND") ? 0 : 1;
   b.ls_first = LS_FIRST;
   b.cand = nullptr;
@@ -1175,6 +1180,8 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   // undecided line search continuing in the next step (pending mode).
   const double few = 65536.0 / h->buf.nc;
   h->buf.ls_first = ((double)h->B <= few || (h->last_active >= 0.0 && h->last_active <= few)) ? h->buf.nc : LS_FIRST;
+  // convergence tail (or a small batch): the latency-sized backward kernels (k_bwd_team WPE = 1)
+  h->buf.tail = ((double)h->B <= TAIL_ACTIVE || (h->last_active >= 0.0 && h->last_active <= TAIL_ACTIVE)) ? 1 : 0;
   for (int i = 0; i < nsteps; i++) {
     timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
     if (h->bwd_team)
