@@ -82,6 +82,27 @@ TOG_HD double tog_cos(double x) {
  * fmax/fmin, which drop it. The AL bookkeeping uses them where the reference calls max/min/maximum/
  * norm(., Inf) (augmented_lagrangian_methods.jl:107-118, 171-184), so a NaN constraint value is
  * reported as a NaN violation on both sides instead of reading as feasible. */
+/* 1/sqrt(y) of the rank-1 Cholesky downdates in the square-root backward pass (chol_minus,
+ * contract v4): a bit-pattern seed (relative error below 3.5e-2) and four Newton
+ * steps r += r (1/2 - (y/2) r^2) in fma form, so host and device produce the same bits; within 2 ulp
+ * of the correctly rounded value for every normal y > 0 (tests/test_reference_kats.py checks 2^20
+ * points). y == 0 gives +Inf, y < 0 or NaN gives NaN. One long dependent chain replaces the sqrt
+ * and the division of the reference's c = sqrt(1 - s^2), (.)/c. */
+TOG_HD double tog_rsqrt(double y) {
+  long long i;
+  double r;
+  __builtin_memcpy(&i, &y, sizeof(i));
+  i = 0x5FE6EB50C7B537A9LL - (i >> 1);
+  __builtin_memcpy(&r, &i, sizeof(r));
+  const double h = 0.5 * y;
+  for (int k = 0; k < 4; k++) {
+    const double hr = h * r;
+    const double e = fma(-hr, r, 0.5);
+    r = fma(r, e, r);
+  }
+  return (y > 0.0) ? r : ((y == 0.0) ? INFINITY : NAN);
+}
+
 TOG_HD double tog_jlmax(double a, double b) { return (a != a) ? a : ((b != b) ? b : fmax(a, b)); }
 TOG_HD double tog_jlmin(double a, double b) { return (a != a) ? a : ((b != b) ? b : fmin(a, b)); }
 

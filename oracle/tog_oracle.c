@@ -1061,24 +1061,31 @@ OC_EXPORT double oc_cond2(const double* A, int n) { return cond2(A, n); }
 /* the deterministic sin/cos shared with the GPU (include/tog_math.h), for tests */
 OC_EXPORT double oc_sin(double x) { return tog_sin(x); }
 OC_EXPORT double oc_cos(double x) { return tog_cos(x); }
+OC_EXPORT double oc_rsqrt(double x) { return tog_rsqrt(x); }
 OC_EXPORT void oc_qr_R(double* R, double* P, int rows, int cols) { qr_R(R, P, rows, cols); }
 
 /* chol_minus(A, B) (backward_pass.jl:186-192): Cholesky(copy(A), :U, 0) then
    lowrankdowndate!(C, B[i,:]) per row (Julia 1.1 LinearAlgebra cholesky.jl). Returns 0 or
    PosDefException index. */
 static int chol_minus(double* Uo, const double* A, int n, const double* B, int nb) {
-  double U[OM * OM], v[OM];
+  double U[OM * OM], v[OM], rd[OM];
   memcpy(U, A, sizeof(double) * n * n);
+  /* contract v4: the reciprocals of the diagonal are formed once and carried through the downdates
+     (1/(c A_ii) = (1/A_ii)(1/c)); 1/c = tog_rsqrt(1 - s^2) and c = (1 - s^2)(1/c) replace the
+     reference's sqrt and division by c (include/tog_math.h) */
+  for (int i = 0; i < n; i++) rd[i] = 1.0 / U[IDX(i, i, n)];
   for (int r = 0; r < nb; r++) {
     for (int j = 0; j < n; j++) v[j] = B[IDX(r, j, nb)];
     for (int i = 0; i < n; i++) {
       double Aii = U[IDX(i, i, n)];
-      double s = v[i] * (1.0 / Aii); /* contract v3: the reciprocal comes off the rotation's chain */
+      double s = v[i] * rd[i];
       double s2 = s * s;
       if (s2 > 1.0) return i + 1;
-      double c = sqrt(1.0 - s2);
-      double rc = 1.0 / c; /* contract v2: one division per rotation, (U_ij - s v_j)·(1/c) */
+      double y = 1.0 - s2;
+      double rc = tog_rsqrt(y);
+      double c = y * rc;
       U[IDX(i, i, n)] = c * Aii;
+      rd[i] = rd[i] * rc;
       for (int j = i + 1; j < n; j++) {
         double tmp = (U[IDX(i, j, n)] - s * v[j]) * rc;
         v[j] = c * v[j] - s * tmp;

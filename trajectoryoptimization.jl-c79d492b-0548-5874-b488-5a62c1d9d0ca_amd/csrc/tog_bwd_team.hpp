@@ -609,9 +609,10 @@ __global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuff
   const int team = threadIdx.x / Cfg::TEAM, tl = threadIdx.x % Cfg::TEAM;
   const int N = P->N;
   const long long idx = (long long)blockIdx.x * Cfg::TPW + team;
-  const long long b = idx / N;
-  const int k = (int)(idx - b * N);
-  if (b >= P->B) return;  // whole teams return together (DPP broadcasts stay within a team)
+  const long long slot = idx / N;
+  const int k = (int)(idx - slot * N);
+  const long long b = traj_of_slot(Bf, slot, P->B);
+  if (b < 0) return;  // whole teams return together (DPP broadcasts stay within a team)
   if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
   double* tlds = expand_lds + (size_t)team * expand_team_stride<M>(P->pmax);
   if (k == N - 1)
@@ -661,7 +662,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   static_assert(m <= n && n + 1 <= TEAM, "team layout");
   extern __shared__ double team_lds[];
   const int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
-  const long long b = (long long)blockIdx.x * Cfg::TPW + team;
+  const long long bs = traj_of_slot(Bf, (long long)blockIdx.x * Cfg::TPW + team, P->B);
+  const long long b = bs < 0 ? 0 : bs;
   const int N = P->N;
   const int stride = Bf.bwd_stride;
   constexpr int SREG = sreg_size<M>(SQRT);
@@ -679,7 +681,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     }
     __syncthreads();
   }
-  const bool live = (b < P->B) && Bf.st[b].active && !Bf.st[b].ls_pend;
+  const bool live = bs >= 0 && Bf.st[b].active && !Bf.st[b].ls_pend;
   const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
   const bool state_reg = (P->o.bp_reg_type == 1);
   const double dt = P->dt;
@@ -1410,52 +1412,81 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
           w[k] = 0.0;
           wn[k] = bus[TB + k];  // lane 0: row 0 of tmp1 (the other lanes ignore wn)
         }
-        double ru = 1.0 / u[0];  // contract v3: s = x_i·(1/R_ii), the reciprocal formed a step ahead
-        double* msg = bus2;  // [2][m][m] (8-lane teams)
+        // contract v4 (oracle chol_minus): s = x_i·(1/R_ii) with the diagonal reciprocal carried by
+        // products (1/(c R_ii) = (1/R_ii)(1/c)), 1/c = tog_rsqrt(1 - s²), c = (1 - s²)(1/c)
+        double ru = 1.0 / u[0];
         bool okd = true;
+        if constexpr (TEAM == 16) {
+          // Branch-free steps: every lane runs the rotation each step and keeps its row only while it
+          // holds an active (row r, column i) pair. Lane 0 takes row t of tmp1 from the bus (read a
+          // step ahead, the same address on every lane), the others lane i-1's x (DPP row_shr:1).
+          // A lane's travelling x is read by lane i+1 only on the step after one it was active on.
 #pragma unroll 1
-        for (int t = 0; t < n + m - 1; t++) {
-          const int r = t - tl;
-          double win[m];
-          if constexpr (TEAM == 16) {
+          for (int t = 0; t < n + m - 1; t++) {
+            const int r = t - tl;
+            const bool act = colu && r >= 0 && r < n;
+            double x[m];
 #pragma unroll
-            for (int k = 0; k + 1 < m; k++) win[k] = row_shr1(w[k + 1]);  // lane i-1's x from step t-1
-          }
-          if (colu && r >= 0 && r < n) {
-            if (tl == 0) {
+            for (int k = 0; k + 1 < m; k++) x[k] = row_shr1(w[k + 1]);  // lane i-1's x from step t-1
+            x[m - 1] = 0.0;
 #pragma unroll
-              for (int k = 0; k < m; k++) w[k] = wn[k];
-              const int rn = r + 1 < n ? r + 1 : r;  // prefetch the next row of tmp1
+            for (int k = 0; k < m; k++) x[k] = (tl == 0) ? wn[k] : x[k];
+            const int rn = t + 1 < n ? t + 1 : n - 1;  // lane 0's next row of tmp1
 #pragma unroll
-              for (int k = 0; k < m; k++) wn[k] = bus[TB + rn * m + k];
-            } else if constexpr (TEAM == 16) {
-#pragma unroll
-              for (int k = 0; k + 1 < m; k++) w[k] = win[k];
-            } else {
-              const double* in = msg + ((t - 1) & 1) * m * m + (tl - 1) * m;
-#pragma unroll
-              for (int k = 0; k + 1 < m; k++) w[k] = in[k + 1];
-            }
-            const double sn = w[0] * ru;
+            for (int k = 0; k < m; k++) wn[k] = bus[TB + rn * m + k];
+            const double sn = x[0] * ru;
             const double s2 = sn * sn;
-            if (s2 > 1.0) okd = false;
-            const double cs = sqrt(1.0 - s2);
-            const double rcs = 1.0 / cs;  // contract v2: one division per rotation
-            u[0] = cs * u[0];
-            ru = 1.0 / u[0];
+            okd = okd && !(act && s2 > 1.0);
+            const double y = 1.0 - s2;
+            const double rc = tog_rsqrt(y);
+            const double cs = y * rc;
+            w[0] = x[0];
 #pragma unroll
             for (int k = 1; k < m; k++) {
-              const double tmp = (u[k] - sn * w[k]) * rcs;
-              w[k] = cs * w[k] - sn * tmp;
-              u[k] = tmp;
+              const double tmp = (u[k] - sn * x[k]) * rc;
+              w[k] = cs * x[k] - sn * tmp;
+              u[k] = act ? tmp : u[k];
             }
-            if constexpr (TEAM != 16) {
+            u[0] = act ? cs * u[0] : u[0];
+            ru = act ? ru * rc : ru;
+          }
+        } else {
+          double* msg = bus2;  // [2][m][m]: lane i-1 -> lane i messages (8-lane teams)
+#pragma unroll 1
+          for (int t = 0; t < n + m - 1; t++) {
+            const int r = t - tl;
+            if (colu && r >= 0 && r < n) {
+              if (tl == 0) {
+#pragma unroll
+                for (int k = 0; k < m; k++) w[k] = wn[k];
+                const int rn = r + 1 < n ? r + 1 : r;  // prefetch the next row of tmp1
+#pragma unroll
+                for (int k = 0; k < m; k++) wn[k] = bus[TB + rn * m + k];
+              } else {
+                const double* in = msg + ((t - 1) & 1) * m * m + (tl - 1) * m;
+#pragma unroll
+                for (int k = 0; k + 1 < m; k++) w[k] = in[k + 1];
+              }
+              const double sn = w[0] * ru;
+              const double s2 = sn * sn;
+              if (s2 > 1.0) okd = false;
+              const double y = 1.0 - s2;
+              const double rc = tog_rsqrt(y);
+              const double cs = y * rc;
+              u[0] = cs * u[0];
+              ru = ru * rc;
+#pragma unroll
+              for (int k = 1; k < m; k++) {
+                const double tmp = (u[k] - sn * w[k]) * rc;
+                w[k] = cs * w[k] - sn * tmp;
+                u[k] = tmp;
+              }
               double* out = msg + (t & 1) * m * m + tl * m;
 #pragma unroll
               for (int k = 0; k < m; k++) out[k] = w[k];
             }
+            team_sync();
           }
-          if constexpr (TEAM != 16) team_sync();
         }
         const unsigned long long tmask = (TEAM >= 64 ? ~0ull : ((1ull << TEAM) - 1ull)) << (team * TEAM);
         const bool fail = (__ballot(!okd) & tmask) != 0ull;

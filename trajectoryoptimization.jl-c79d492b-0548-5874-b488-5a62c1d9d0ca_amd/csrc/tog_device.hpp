@@ -122,6 +122,7 @@ struct DevBuffers {
   int* lsok;    // (NC, B) speculative line-search trial rollout status
   int nc;       // candidates evaluated per trajectory per launch (<= 64)
   int* ls_list;   // (2, B) ping-pong lists of trajectories still undecided after a speculative round
+  int* ls_done;   // = ls_list + B: the trajectories whose inner solve finished this step (k_ls_book -> k_al_outer)
   int* ls_count;  // [LS_MAX_ROUNDS] list lengths, zeroed at the start of every forward pass
   int bwd_stride;     // k_bwd_team: per-team LDS stride (doubles) of the launch
   int bwd_shmem;      // k_bwd_team: dynamic LDS bytes per block of the launch
@@ -138,6 +139,10 @@ struct DevBuffers {
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū
   double* jws;        // staged RK3 Jacobian (Kuka): (2n duals, lanes) stage state between the kernels, or null
+  // compacted tail launches (tog_solve_step, k_list_active): the step's active trajectories and their
+  // count; null outside a tail step (launch slot = trajectory index)
+  int* act_list;
+  int* act_count;
   TrajState* st;
 };
 

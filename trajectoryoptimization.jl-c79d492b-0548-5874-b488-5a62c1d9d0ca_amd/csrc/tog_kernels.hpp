@@ -28,6 +28,18 @@ template <class M>
 __host__ __device__ constexpr int pcap_of() { return PCAP; }
 constexpr int WAVE = 64;
 
+// Compacted launches in the convergence tail (DevBuffers::act_list, built by k_list_active at the start
+// of a solve step): slot i of a launch is the i-th active trajectory of the step, -1 past the list's
+// end; without a list, slot i is trajectory i (-1 at or past B). Kernels then launch over
+// ceil(n_active) slots instead of the whole batch, and idle trajectories cost no empty blocks.
+__device__ __forceinline__ long long traj_of_slot(const DevBuffers& Bf, long long i, long long B) {
+  if (Bf.act_list) return i < (long long)*Bf.act_count ? (long long)Bf.act_list[i] : -1;
+  return i < B ? i : -1;
+}
+__device__ __forceinline__ long long slot_count(const DevBuffers& Bf, long long B) {
+  return Bf.act_list ? (long long)*Bf.act_count : B;
+}
+
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroups: s_barrier is ~free
 
 // candidate layout of the line search (k_ls_spec<CAND>): per knot the elements c of [ū_k (m) | x̄_k (n)]
@@ -354,8 +366,8 @@ k_jacobian(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   const int c = (int)(t % NCH);
   const long long bk = t / NCH;
   const int k = (int)(bk % (N - 1));
-  const long long b = bk / (N - 1);
-  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  const long long b = traj_of_slot(Bf, bk / (N - 1), P->B);
+  if (b < 0 || !Bf.st[b].active || Bf.st[b].ls_pend) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
   Dual<W> xd[n], ud[mb], xn[n];
@@ -409,8 +421,8 @@ k_jacobian_rk3_stage(const DevProblem* __restrict__ P, DevBuffers Bf, long long 
   const int c = (int)(t % NCH);
   const long long bk = t / NCH;
   const int k = (int)(bk % (N - 1));
-  const long long b = bk / (N - 1);
-  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  const long long b = traj_of_slot(Bf, bk / (N - 1), P->B);
+  if (b < 0 || !Bf.st[b].active || Bf.st[b].ls_pend) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
   const double dt = P->dt;
@@ -485,8 +497,8 @@ k_jacobian_mt(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) 
   const int c = (int)(t % NCH);
   const long long bk = t / NCH;
   const int k = (int)(bk % (N - 1));
-  const long long b = bk / (N - 1);
-  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  const long long b = traj_of_slot(Bf, bk / (N - 1), P->B);
+  if (b < 0 || !Bf.st[b].active || Bf.st[b].ls_pend) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
   const double h = u[mb];
@@ -979,10 +991,10 @@ __global__ void __launch_bounds__(64) k_backward(const DevProblem* __restrict__ 
   constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
   constexpr int n = M::n, m = M::m, L = n + m, NQ = nq_of<M>();
   __shared__ BwdLds<M, SQRT> sh;
-  const long long b = blockIdx.x;
+  const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
   const int lane = threadIdx.x;
   const int N = P->N;
-  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  if (b < 0 || !Bf.st[b].active || Bf.st[b].ls_pend) return;
   RegState s;
   s.rho = Bf.st[b].rho;
   s.drho = Bf.st[b].drho;
@@ -1342,20 +1354,24 @@ attempt:
         double* U = sh.Uc;
         double* v = sh.vv;
         for (int e = 0; e < m * m; e++) U[e] = sh.Quu[e];
+        double rdg[MMAX];  // contract v4 (oracle chol_minus): diagonal reciprocals carried by products
+        for (int i = 0; i < m; i++) rdg[i] = 1.0 / U[i + m * i];
         bool okd = true;
         for (int r = 0; r < n && okd; r++) {
           for (int j = 0; j < m; j++) v[j] = sh.tmp1[r + n * j];
           for (int i = 0; i < m; i++) {
             const double Aii = U[i + m * i];
-            const double sn = v[i] * (1.0 / Aii);  // contract v3 (oracle chol_minus)
+            const double sn = v[i] * rdg[i];
             const double s2 = sn * sn;
             if (s2 > 1.0) {
               okd = false;
               break;
             }
-            const double c = sqrt(1.0 - s2);
-            const double rc = 1.0 / c;
+            const double y = 1.0 - s2;
+            const double rc = tog_rsqrt(y);
+            const double c = y * rc;
             U[i + m * i] = c * Aii;
+            rdg[i] = rdg[i] * rc;
             for (int j = i + 1; j < m; j++) {
               const double tmp = (U[i + m * j] - sn * v[j]) * rc;
               v[j] = c * v[j] - sn * tmp;
@@ -1758,7 +1774,7 @@ template <class M, int INTEG, bool CAND>
 __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
                                                  int cnt, const int* __restrict__ list, const int* __restrict__ count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long nb = list ? (long long)*count : P->B;
+  const long long nb = list ? (long long)*count : slot_count(Bf, P->B);
   if ((long long)blockIdx.x * blockDim.x >= nb * cnt) return;  // block past the list: retire before LDS work
   extern __shared__ double spec_lds[];
   const RowTables RT =
@@ -1766,7 +1782,7 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
   const int NC = Bf.nc;
   if (t >= nb * cnt) return;
   const long long i = t / cnt;
-  const long long b = list ? (long long)list[i] : i;
+  const long long b = list ? (long long)list[i] : traj_of_slot(Bf, i, P->B);
   const TrajState& st = Bf.st[b];
   const int j = lo + st.ls_pend + (int)(t % cnt);  // a pending line search continues after its stored trials
   if (!st.active || j >= NC) return;
@@ -1794,11 +1810,11 @@ __global__ void __launch_bounds__(256) k_ls_compact(const DevProblem* __restrict
                                                     const int* __restrict__ in_list, const int* __restrict__ in_count,
                                                     int* __restrict__ out_list, int* __restrict__ out_count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long nb = in_list ? (long long)*in_count : P->B;
+  const long long nb = in_list ? (long long)*in_count : slot_count(Bf, P->B);
   bool und = false;
   long long b = 0;
   if (t < nb) {
-    b = in_list ? (long long)in_list[t] : t;
+    b = in_list ? (long long)in_list[t] : traj_of_slot(Bf, t, P->B);
     const TrajState& st = Bf.st[b];
     und = st.active && !ls_decided_within(P->o, Bf, b, Bf.nc, bookkeeping ? st.J : Jprev_in[b], st.dV0, st.dV1, hi);
   }
@@ -1825,12 +1841,12 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
                                                   int hi, const int* __restrict__ list, const int* __restrict__ count) {
   extern __shared__ double commit_lds[];
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long nb = (phase == 2) ? (long long)*count : P->B;
+  const long long nb = (phase == 2) ? (long long)*count : slot_count(Bf, P->B);
   if ((long long)blockIdx.x * blockDim.x >= nb) return;  // whole block past the list: retire early
   const RowTables RT =
       (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, commit_lds) : global_row_tables(P);
   if (t >= nb) return;
-  const long long b = (phase == 2) ? (long long)list[t] : t;
+  const long long b = (phase == 2) ? (long long)list[t] : traj_of_slot(Bf, t, P->B);
   if (!Bf.st[b].active) return;
   if (phase == 1 && !ls_decided_within(P->o, Bf, b, Bf.nc, bookkeeping ? Bf.st[b].J : Jprev_in[b], Bf.st[b].dV0,
                                        Bf.st[b].dV1, hi))
@@ -1933,11 +1949,11 @@ __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict_
                                                    const int* __restrict__ in_list, const int* __restrict__ in_count,
                                                    int* __restrict__ out_list, int* __restrict__ out_count, int pend) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long nb = in_list ? (long long)*in_count : P->B;
+  const long long nb = in_list ? (long long)*in_count : slot_count(Bf, P->B);
   bool und = false;
   long long b = 0;
   if (t < nb) {
-    b = in_list ? (long long)in_list[t] : t;
+    b = in_list ? (long long)in_list[t] : traj_of_slot(Bf, t, P->B);
     TrajState* st = Bf.st + b;
     if (st->active) {
       const tog_options& o = P->o;
@@ -2009,9 +2025,10 @@ __global__ void __launch_bounds__(256) k_ls_apply(const DevProblem* __restrict__
   const int N = P->N;
   const unsigned per = (unsigned)N * Q;
   const unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (unsigned long long)P->B * per) return;
-  const long long b = (long long)(t / per);
-  const unsigned r = (unsigned)(t - (unsigned long long)b * per);
+  const long long slot = (long long)(t / per);
+  if (slot >= slot_count(Bf, P->B)) return;
+  const long long b = traj_of_slot(Bf, slot, P->B);
+  const unsigned r = (unsigned)(t - (unsigned long long)slot * per);
   const int k = (int)(r / Q), q = (int)(r - (unsigned)k * Q);
   if (!Bf.st[b].active) return;
   const int w = Bf.ls_win[b];
@@ -2054,8 +2071,8 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const RowTables RT =
       (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, book_lds) : global_row_tables(P);
-  if (t >= P->B) return;
-  const long long b = t;
+  if (t >= slot_count(Bf, P->B)) return;
+  const long long b = traj_of_slot(Bf, t, P->B);
   if (!Bf.st[b].active) return;
   constexpr int n = M::n, m = M::m;
   const tog_options& o = P->o;
@@ -2105,7 +2122,7 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
       s.active = 0;  // reference: error("Cost increased during Forward Pass")
     } else if (inner_bookkeeping(P, s, J, grad, mode)) {
       // the AL outer update runs wave-parallel over the knots in k_al_outer
-      Bf.ls_list[P->B + atomicAdd(Bf.ls_count + 1, 1)] = (int)b;
+      Bf.ls_done[atomicAdd(Bf.ls_count + 1, 1)] = (int)b;
     }
   }
   Bf.st[b] = s;
@@ -2613,7 +2630,7 @@ struct ModelLaunch {
                        bk, Jp, Jo);
     if (bk && mode == TOG_MODE_AL) {
       const unsigned sm = (unsigned)(Bf.nknots * (2 * sizeof(double) + sizeof(int)));
-      hipLaunchKernelGGL((k_al_outer<M>), dim3((unsigned)B), dim3(64), sm, st, P, Bf, mode, Bf.ls_list + B,
+      hipLaunchKernelGGL((k_al_outer<M>), dim3((unsigned)B), dim3(64), sm, st, P, Bf, mode, Bf.ls_done,
                          Bf.ls_count + 1);
     }
   }

@@ -77,6 +77,8 @@ struct tog_handle {
   double* d_scratch2 = nullptr; // B doubles
   int* d_iscratch = nullptr;    // B ints
   double* d_stats = nullptr;    // 3 doubles
+  int* d_act_list = nullptr;    // B ints: the active trajectories of a compacted tail step
+  int* d_act_count = nullptr;
   std::vector<void*> allocs;
   // live per-kernel timing (tog_profile)
   bool profiling = false;
@@ -312,6 +314,22 @@ static __global__ void __launch_bounds__(1024) k_batch_stats(const TrajState* __
   }
 }
 
+
+// the active trajectories, for the compacted launches of a tail step (order immaterial: every
+// trajectory's computation is independent of its slot)
+static __global__ void __launch_bounds__(256) k_list_active(const TrajState* __restrict__ st, long long B, int* list,
+                                                            int* count) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool a = b < B && st[b].active;
+  const unsigned long long mask = __ballot(a);
+  if (mask == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(count, __popcll(mask));
+  base = __shfl(base, leader);
+  if (a) list[base + __popcll(mask & ((1ull << lane) - 1))] = (int)b;
+}
 
 __global__ void k_fill(double* p, size_t count, double v) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -702,12 +720,17 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
       (rc = dalloc(h, &b.Qscr, B * N * h->nq)) || (rc = dalloc(h, &b.st, B)) ||
       (rc = dalloc(h, &h->d_scratch, B)) || (rc = dalloc(h, &h->d_scratch2, B)) ||
       (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4)) ||
+      (rc = dalloc(h, &h->d_act_list, B)) || (rc = dalloc(h, &h->d_act_count, 1)) ||
       (rc = dalloc(h, &b.lsJ, B * 64)) || (rc = dalloc(h, &b.lsok, B * 64)) ||
       (rc = dalloc(h, &b.ls_list, 2 * B)) || (rc = dalloc(h, &b.ls_count, LS_MAX_ROUNDS)))
     return rc;
   b.Sdbg = nullptr;
   b.sdbg = nullptr;
   b.E = nullptr;
+  b.ls_done = b.ls_list + B;  // (the second half of ls_list; its offset is the full batch, never a
+                              //  compacted launch's slot count)
+  b.act_list = nullptr;  // set only in the launch view of a compacted tail step
+  b.act_count = nullptr;
   if (h->bwd_team) {  // expansion records of the team backward pass (k_expand_team)
     const size_t ne = (size_t)n + m + (size_t)m * m + (size_t)n * n;
     if ((rc = dalloc(h, &b.E, B * N * ne))) return rc;
@@ -1009,6 +1032,7 @@ int32_t tog_set_state(tog_handle* h, const double* x0, const double* U, const do
     });
   }
   HIPCHECK(hipSetDevice(h->device));
+  h->last_active = -1.0;  // every trajectory is active again
   const size_t n = h->n, m = h->m, N = h->N, B = h->B;
   HIPCHECK(hipMemcpyAsync(h->buf.x0, x0, sizeof(double) * B * n, hipMemcpyHostToDevice, h->stream));
   HIPCHECK(hipMemcpyAsync(h->buf.U, U, sizeof(double) * B * (N - 1) * m, hipMemcpyHostToDevice, h->stream));
@@ -1182,17 +1206,32 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps) {
   h->buf.ls_first = ((double)h->B <= few || (h->last_active >= 0.0 && h->last_active <= few)) ? h->buf.nc : LS_FIRST;
   // convergence tail (or a small batch): the latency-sized backward kernels (k_bwd_team WPE = 1)
   h->buf.tail = ((double)h->B <= TAIL_ACTIVE || (h->last_active >= 0.0 && h->last_active <= TAIL_ACTIVE)) ? 1 : 0;
+  // In the tail the kernels launch over the active trajectories only: k_list_active lists them once per
+  // call (trajectories only ever finish during a solve, so the list stays a superset of the active set
+  // for the call's steps, and every kernel still checks `active`), and each launch covers
+  // ceil(last n_active readback) slots instead of the whole batch (traj_of_slot, tog_kernels.hpp).
+  DevBuffers Bt = h->buf;
+  long long Bl = h->B;
+  if (h->buf.tail && h->last_active >= 0.0 && h->last_active < (double)h->B && !getenv("TOG_NO_COMPACT")) {
+    if (h->last_active == 0.0) return TOG_OK;  // nothing left to step
+    Bl = (long long)ceil(h->last_active);
+    HIPCHECK(hipMemsetAsync(h->d_act_count, 0, sizeof(int), h->stream));
+    hipLaunchKernelGGL(k_list_active, dim3((unsigned)((h->B + 255) / 256)), dim3(256), 0, h->stream, h->buf.st,
+                       (long long)h->B, h->d_act_list, h->d_act_count);
+    Bt.act_list = h->d_act_list;
+    Bt.act_count = h->d_act_count;
+  }
   for (int i = 0; i < nsteps; i++) {
-    timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, h->buf, h->B, h->N, h->integ, h->stream); });
+    timed(h, TOG_KERNEL_JACOBIAN, [&] { h->ops->jacobian(h->dP, Bt, Bl, h->N, h->integ, h->stream); });
     if (h->bwd_team)
       timed(h, TOG_KERNEL_EXPANSION, [&] {
-        h->ops->expand(h->dP, h->buf, h->B, h->N, h->pmax, h->opts.square_root, al, h->stream);
+        h->ops->expand(h->dP, Bt, Bl, h->N, h->pmax, h->opts.square_root, al, h->stream);
       });
     timed(h, TOG_KERNEL_BACKWARD,
-          [&] { h->ops->backward(h->dP, h->buf, h->B, h->opts.square_root, al, 0, h->bwd_team, h->stream); });
+          [&] { h->ops->backward(h->dP, Bt, Bl, h->opts.square_root, al, 0, h->bwd_team, h->stream); });
     timed(h, TOG_KERNEL_FORWARD,
           [&] {
-            h->ops->forward(h->dP, h->buf, h->B, h->integ, h->mode, 1, nullptr, nullptr, h->stream,
+            h->ops->forward(h->dP, Bt, Bl, h->integ, h->mode, 1, nullptr, nullptr, h->stream,
                             getenv("TOG_NO_OVERLAP") ? nullptr : &h->sp);
           });
   }
