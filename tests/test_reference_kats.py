@@ -317,3 +317,46 @@ def test_midpoint_jacobian_matches_central_differences(tog, oracle):
             fp = oracle.discrete_f(mid, tog.abi.MIDPOINT, (z + e)[:n], (z + e)[n:], 0.05)
             fm = oracle.discrete_f(mid, tog.abi.MIDPOINT, (z - e)[:n], (z - e)[n:], 0.05)
             assert np.allclose(S[:, j], (fp - fm) / 2e-6, rtol=1e-6, atol=1e-7), (mid, j)
+
+
+def _notebook_quadrotor(tog):
+    """examples/quadrotor/Quadrotor.ipynb cells 3-11: rk3(Dynamics.quadrotor), N = 101, dt = 0.1,
+    Q = R = 1e-2 I, Qf = 1000 I, x0 at the origin, xf = (0, 50, 0), hover controls, no constraints."""
+    n, m, N = 13, 4, 101
+    q0 = np.array([1.0, 0.0, 0.0, 0.0])
+    x0 = np.zeros(n)
+    x0[3:7] = q0
+    xf = np.zeros(n)
+    xf[0:3] = [0.0, 50.0, 0.0]
+    xf[3:7] = q0
+    obj = tog.LQRObjective(1e-2 * np.eye(n), 1e-2 * np.eye(m), 1000.0 * np.eye(n), xf, N)
+    U = 0.5 * 9.81 / 4.0 * np.ones((N - 1, m))
+    return tog.Problem(tog.rk3(tog.Dynamics.quadrotor), obj, U, x0=x0, xf=xf, N=N, dt=0.1)
+
+
+def test_quadrotor_notebook_final_cost(tog, oracle):
+    """The reference's own output for the quadrotor model: Quadrotor.ipynb cell 13 logs the converged
+    iLQR cost 18.17292526 (solve!(prob, iLQRSolverOptions{T}(verbose=true))). The oracle reaches
+    18.17294801 in 58 steps: 1.25e-6 relative. The notebook ran an older snapshot of the package (its
+    last logged step has α = 0.25, dJ = 2.36e-5, against α = 0.5, dJ = 5.9e-5 here), so iteration
+    counts are not comparable; the converged cost is, to within the cost tolerance's last step
+    (cost_tolerance = 1e-4 stops when 0 < dJ < 1e-4, i.e. within ~5.5e-6 relative of 18.17)."""
+    prob = _notebook_quadrotor(tog)
+    s = oracle.OracleSolver(prob, tog.iLQRSolverOptions())
+    s.solve()
+    J = s.get("stats")[tog.abi.STAT_J]
+    assert abs(J - 18.17292526) / 18.17292526 < 5e-6
+
+
+@pytest.mark.gpu
+def test_quadrotor_notebook_device(tog, gpu, oracle):
+    """The same notebook problem on the device equals the oracle (and so the notebook's cost)."""
+    prob = _notebook_quadrotor(tog)
+    s = oracle.OracleSolver(prob, tog.iLQRSolverOptions())
+    steps = s.solve()
+    gp = prob.copy()
+    solver = tog.solve_b(gp, tog.iLQRSolverOptions())
+    assert solver.stats["iterations_total"][0] == steps
+    assert np.abs(gp.X - s.get("X")).max() / max(1.0, np.abs(s.get("X")).max()) < 1e-6
+    assert np.abs(gp.U - s.get("U")).max() / max(1.0, np.abs(s.get("U")).max()) < 1e-6
+    assert abs(solver.stats["cost"][0] - 18.17292526) / 18.17292526 < 5e-6

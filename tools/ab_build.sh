@@ -1,10 +1,10 @@
 #!/bin/bash
-# Build an A/B variant of libtog.so with extra hipcc flags into build_ab/<name>/libtog.so
+# Build an A/B variant of libtog.so with extra hipcc flags into ab_libs/<name>/libtog.so
 # usage: tools/ab_build.sh <name> "<extra flags>"
 set -e
 name=$1; flags=$2
 src="$(cd "$(dirname "$0")/.." && pwd)/trajectoryoptimization.jl-c79d492b-0548-5874-b488-5a62c1d9d0ca_amd/csrc"
-out="$(cd "$(dirname "$0")/.." && pwd)/build_ab/$name"
+out="$(cd "$(dirname "$0")/.." && pwd)/ab_libs/$name"   # (gitignored; travels to the GPU box)
 mkdir -p "$out"
 cd "$out"
 for f in tog_runtime.cpp $(cd "$src" && ls k_*.hip); do

@@ -9,10 +9,9 @@ import sys
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 import __graft_entry__  # noqa: E402
 
-NAMES = ["terminal knot", "expand: Q.u += cu'g", "S [A B], Q.ux", "QR Q.uu", "QR Q.xx",
+NAMES = ["terminal knot", "expansion record loads", "S [A B], Q.ux", "QR Q.uu", "QR Q.xx",
          "regularise + cond", "gains solve", "K/d store, s, tmp1", "chol_minus", "S-update operands",
-         "QR S-update", "epilogue", "expand: cost terms (x/u loads)", "expand: team_rows (lam/mu, eval)",
-         "expand: chol_plus operands", "expand: chol_plus QR", "expand: Q.x += cx'g", "[A B] loads",
+         "QR S-update", "epilogue", "-", "-", "-", "-", "-", "[A B] loads",
          "-", "-"]
 pkg = __graft_entry__.load_package()
 abi = pkg.abi

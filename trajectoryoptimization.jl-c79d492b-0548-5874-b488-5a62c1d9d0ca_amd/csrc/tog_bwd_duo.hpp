@@ -1,0 +1,593 @@
+// tog_bwd_duo.hpp — the square-root backward pass of the convergence tail on two waves per trajectory.
+//
+// Reference: src/solvers/ilqr/backward_pass.jl:87-192 (_backwardpass_sqrt!, chol_plus, chol_minus).
+//
+// In the tail (few trajectories active, most SIMDs idle) a knot's time is the instruction stream of one
+// wave: k_bwd_team issues ~8-9 k instructions per knot at ~5 cycles each (profiles/r3g_ab_tail.txt).
+// Half of that work does not depend on the Q.xx chain, so here it runs on a second wave, on another
+// SIMD of the same CU:
+//   wave A (chain): S A -> qr([Q.xx; S A]) -> tmp1 = Q.xx' \ Q.ux' -> chol_minus(Q.uu, tmp1) ->
+//                   qr([Q.xx + tmp1 K; tmp2 K]) = S_k
+//   wave B (side):  Q.x/Q.u += [A B]'s -> S B -> Q.ux += (S B)'(S A) -> qr([Q.uu; S B]) ->
+//                   Quu_reg, cond, K, d, s_k, ΔV, the K/d stores
+// exchanging S A, Q.ux, Q.uu, K and the restart verdict through LDS at four workgroup barriers per knot:
+//   B1  S A on the bus (B's Q.ux needs it; S_{k+1}, s_{k+1} are no longer read)
+//   B2a Q.ux, Q.uu factor (A's tmp1 and chol_minus)
+//   B2b K, d and the regularisation verdict (A's S-update operands; both waves restart together)
+//   B3  S_k (the next knot's products)
+// Every value is produced by the same operations in the same order as k_bwd_team's (and the oracle's),
+// so the results are bit-identical; only the wave that computes them differs. One trajectory per
+// workgroup; the four 16-lane DPP rows of a wave compute the same team redundantly (identical values
+// to identical addresses), so every branch and barrier is wave- and workgroup-uniform.
+#pragma once
+
+namespace tog {
+
+template <class M>
+struct DuoLayout {  // doubles in the workgroup's LDS
+  static constexpr int n = M::n, m = M::m;
+  static constexpr int S = 0;                 // S_{k+1} (n*n, upper factor, zeros below) then s (n)
+  static constexpr int QU = n * n + n;        // Q.uu factor (m*m, column-major)
+  static constexpr int TX = QU + m * m;       // S A (n*n, column c from lane c of wave A)
+  static constexpr int QUX = TX + n * n;      // Q.ux (m*n, column c from lane c of wave B)
+  static constexpr int KB = QUX + m * n;      // K (m*n, column c from lane c of wave B)
+  static constexpr int BA = KB + m * n;       // wave A's bus: tmp1 rows at +32, chol_minus output after
+  static constexpr int BA_SIZE = 32 + n * m + 3 * m * m + 8;
+  static constexpr int BB = BA + BA_SIZE;     // wave B's bus: S B columns, :state B columns, cond scratch
+  static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
+  static constexpr int FLAGS = BB + BB_SIZE;  // [0] regularisation verdict (1 ok), [1] chol_minus failed
+  static constexpr int TOTAL = FLAGS + 2;
+};
+
+template <class M, int ALI>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1)))
+k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
+  using Cfg = TeamCfg<M>;
+  using D = DuoLayout<M>;
+  constexpr bool SQRT = true, AL = ALI != 0;
+  constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, NQ = nq_of<M>(), NE = ne_of<M>();
+  static_assert(TEAM == 16 && m <= n && n + 1 <= 16, "duo kernel: 16-lane DPP rows");
+  __shared__ double lds[D::TOTAL];
+  __shared__ int kcnt[TEAM_MAX_KNOTS], knx[TEAM_MAX_KNOTS];
+  const int wv = threadIdx.x >> 6;  // 0: chain wave A, 1: side wave B (wave-uniform)
+  const int tl = threadIdx.x & 15;  // column of this lane (each DPP row computes the whole team)
+  const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
+  if (b < 0) return;  // workgroup-uniform
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  const int N = P->N;
+  if (AL) {
+    for (int e = threadIdx.x; e < N; e += 128) {
+      kcnt[e] = P->knot_cnt[e];
+      knx[e] = P->knot_nx[e];
+    }
+  }
+  __syncthreads();
+  double* Sreg = lds + D::S;
+  double* QU = lds + D::QU;
+  double* TXb = lds + D::TX;
+  double* QUXb = lds + D::QUX;
+  double* KB = lds + D::KB;
+  double* busA = lds + D::BA;
+  double* busB = lds + D::BB;
+  int* flg = reinterpret_cast<int*>(lds + D::FLAGS);
+  constexpr int SOFF = n * n;
+  const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
+  const bool state_reg = (P->o.bp_reg_type == 1);
+  const double dt = P->dt;
+  const double* ABg = Bf.AB + (size_t)b * (N - 1) * n * L;
+  double* Kg = Bf.K + (size_t)b * (N - 1) * m * n;
+  double* dg = Bf.d + (size_t)b * (N - 1) * m;
+  double* Qs = Bf.Qscr + (size_t)b * N * NQ;
+  const double* Eg = Bf.E + (size_t)b * N * NE;
+  const bool colx = tl < n, colu = tl < m;
+  const int c = colx ? tl : 0, cu = colu ? tl : 0;
+  RegState s;  // (wave B's: ρ, dρ, flags)
+  s.rho = Bf.st[b].rho;
+  s.drho = Bf.st[b].drho;
+  s.flags = Bf.st[b].flags;
+  const double rho0 = s.rho, drho0 = s.drho;
+  int pd_flags = 0;  // (wave A's: chol_minus failures, merged at the end)
+  bool faithful = false;
+  int kmin = N - 1, restarts = 0;
+  double dV0 = 0.0, dV1 = 0.0;
+  bool done = false;
+  auto dense = [&](int k) { return knot_dense<SQRT, AL>(k, N, AL ? kcnt[k] : 0, AL ? knx[k] : 0); };
+
+  while (!done) {  // one attempt of the backward pass; a regularisation restart begins a new one
+    if (wv == 0) {  // S[N] = Q[N] (backward_pass.jl:100-101), from the terminal expansion record
+      const double* e = Eg + (size_t)(N - 1) * NE;
+      double Qxc[n];
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+      const double Qxs = e[c];
+      if (colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) Sreg[i + n * tl] = (i > tl) ? 0.0 : Qxc[i];
+        Sreg[SOFF + tl] = Qxs;
+      }
+      if (store_S && colx) {
+#pragma unroll
+        for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + (N - 1)) * n * n + i + n * tl] = Qxc[i];
+        Bf.sdbg[((size_t)b * N + (N - 1)) * n + tl] = Qxs;
+      }
+    }
+    __syncthreads();
+    dV0 = 0.0;
+    dV1 = 0.0;
+    bool restart = false;
+    for (int k = N - 2; k >= 0; k--) {
+      const bool replay = faithful && k >= kmin;
+      const double* e = Eg + (size_t)k * NE;
+      const double* q = Qs + (size_t)k * NQ;
+      // state carried across the knot's barriers: wave A's Q.xx column and S A column (T), wave B's
+      // Q.x entry, Q.u, Q.uu / Q.ux columns and S B column (T)
+      double Qxc[n], T[n];
+      double Qxs = 0.0, Qu[m], Quuc[m], Quxc[m];
+      // ------------------------------------------------------------------ phase 1: S A | Q.x, Q.u, S B
+      if (wv == 0) {
+        double Ac[n];
+        const double* abk = ABg + (size_t)k * n * L;
+#pragma unroll
+        for (int i = 0; i < n; i++) Ac[i] = abk[i + n * c];
+        if (replay) {
+#pragma unroll
+          for (int i = 0; i < n; i++) Qxc[i] = q[n + m + i + n * c];
+        } else if (dense(k)) {
+#pragma unroll
+          for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+        } else {
+#pragma unroll
+          for (int i = 0; i < n; i++) Qxc[i] = P->cQ[i + n * c];
+        }
+        // tmp_x = S A, l ascending, over the upper factor's nonzero rows (k_bwd_team TRI_SA)
+#pragma unroll
+        for (int i = 0; i < n; i++) T[i] = 0.0;
+        static_for<0, n>([&](auto lc) {
+          constexpr int l = decltype(lc)::value;
+          double sl[l + 1];
+#pragma unroll
+          for (int i = 0; i <= l; i++) sl[i] = Sreg[i + n * l];
+          TEAM_FENCE();
+#pragma unroll
+          for (int i = 0; i <= l; i++) T[i] = fma(sl[i], Ac[l], T[i]);
+        });
+        if (colx) {  // (wave B's Q.ux reads this copy; wave A keeps T for its QR)
+#pragma unroll
+          for (int i = 0; i < n; i++) TXb[i + n * tl] = T[i];
+        }
+      } else {
+        double Ac[n], Bc[n];
+        const double* abk = ABg + (size_t)k * n * L;
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          Ac[i] = abk[i + n * c];
+          Bc[i] = abk[i + n * (n + cu)];
+        }
+        if (replay) {
+          Qxs = q[c];
+#pragma unroll
+          for (int i = 0; i < m; i++) Qu[i] = q[n + i];
+#pragma unroll
+          for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
+        } else {
+          Qxs = e[c];
+#pragma unroll
+          for (int i = 0; i < m; i++) Qu[i] = e[n + i];
+#pragma unroll
+          for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;  // sqrt AL adds no Q.ux term (A.5)
+        }
+        // Q.x += A's ; Q.u += B's (backward_pass.jl:112-113)
+        {
+          double t = 0.0;
+#pragma unroll
+          for (int l = 0; l < n; l++) t = fma(Ac[l], Sreg[SOFF + l], t);
+          Qxs += t;
+          double tu = 0.0;
+#pragma unroll
+          for (int l = 0; l < n; l++) tu = fma(Bc[l], Sreg[SOFF + l], tu);
+          static_for<0, m>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            Qu[i] += row_bcast<i>(tu);
+          });
+        }
+        // tmp_u = S B
+#pragma unroll
+        for (int i = 0; i < n; i++) T[i] = 0.0;
+        static_for<0, n>([&](auto lc) {
+          constexpr int l = decltype(lc)::value;
+          double sl[l + 1];
+#pragma unroll
+          for (int i = 0; i <= l; i++) sl[i] = Sreg[i + n * l];
+          TEAM_FENCE();
+#pragma unroll
+          for (int i = 0; i <= l; i++) T[i] = fma(sl[i], Bc[l], T[i]);
+        });
+      }
+      __syncthreads();  // B1: S A on the bus; S_{k+1}, s_{k+1} fully read
+      // ------------------------------------------------------------------ phase 2: QR Q.xx | Q.ux, QR Q.uu
+      if (wv == 0) {
+        {  // Q.xx <- qr([Q.xx; tmp_x]).R (backward_pass.jl:116)
+          double a[2 * n];
+#pragma unroll
+          for (int i = 0; i < 2 * n; i++) a[i] = (i < n) ? Qxc[i] : T[i - n];
+          team_qr<2 * n, n, n, TEAM>(a, 2 * n, tl, busA);
+#pragma unroll
+          for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
+        }
+        if (faithful && colx) {
+#pragma unroll
+          for (int i = 0; i < n; i++) Qs[(size_t)k * NQ + n + m + i + n * tl] = Qxc[i];
+        }
+      } else {
+        {  // Q.ux += tmp_u' tmp_x (backward_pass.jl:118): tmp_u columns on wave B's bus, tmp_x from wave A
+          if (colu) {
+#pragma unroll
+            for (int i = 0; i < n; i++) busB[i + n * tl] = T[i];
+          }
+          team_sync();
+          double t[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) t[i] = 0.0;
+#pragma unroll 1
+          for (int l = 0; l < n; l++) {
+            double tu[m];
+            const double tx = TXb[l + n * c];
+#pragma unroll
+            for (int i = 0; i < m; i++) tu[i] = busB[l + n * i];
+            TEAM_FENCE();
+#pragma unroll
+            for (int i = 0; i < m; i++) t[i] = fma(tu[i], tx, t[i]);
+          }
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] += t[i];
+          team_sync();
+        }
+        {  // Q.uu <- qr([Q.uu; tmp_u]).R (backward_pass.jl:117)
+          double a[m + n];
+#pragma unroll
+          for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : T[i - m];
+          team_qr<m + n, m, m, TEAM>(a, m + n, tl, busB);
+#pragma unroll
+          for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+        }
+        if (colu) {
+#pragma unroll
+          for (int i = 0; i < m; i++) QU[i + m * tl] = Quuc[i];
+        }
+        if (colx) {
+#pragma unroll
+          for (int i = 0; i < m; i++) QUXb[i + m * tl] = Quxc[i];
+        }
+        if (faithful) {
+          double* qq = Qs + (size_t)k * NQ;
+          if (colx) {
+            qq[tl] = Qxs;
+#pragma unroll
+            for (int i = 0; i < m; i++) qq[n + m + n * n + m * m + i + m * tl] = Quxc[i];
+          }
+          if (colu) {
+#pragma unroll
+            for (int i = 0; i < m; i++) qq[n + m + n * n + i + m * tl] = Quuc[i];
+          }
+          if (tl == 0) {
+#pragma unroll
+            for (int i = 0; i < m; i++) qq[n + i] = Qu[i];
+          }
+        }
+      }
+      if (faithful) kmin = k < kmin ? k : kmin;
+      __syncthreads();  // B2a: Q.ux and the Q.uu factor on the bus
+      // ------------------------------------------------------------------ phase 3: tmp1, chol_minus | gains
+      bool pd_fail = false;
+      if (wv == 0) {
+        // tmp1 = (Q.xx') \ Q.ux' by distributed forward substitution: lane i owns row i of tmp1
+        double t1[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) t1[i] = QUXb[i + m * c];
+        double dgx = Qxc[0];
+#pragma unroll
+        for (int j = 1; j < n; j++)
+          if (tl == j) dgx = Qxc[j];
+        const double rdiag = 1.0 / dgx;
+        static_for<0, n>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if (tl == j) {
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = t1[i] * rdiag;
+          }
+          double xj[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) xj[i] = row_bcast<j>(t1[i]);
+          if (tl > j && colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = fma(-Qxc[j], xj[i], t1[i]);
+          }
+        });
+        constexpr int TB = 32;
+        if (colx) {
+#pragma unroll
+          for (int i = 0; i < m; i++) busA[TB + tl * m + i] = t1[i];
+        }
+        team_sync();
+        // tmp2 = chol_minus(Q.uu, tmp1) (backward_pass.jl:186-192), k_bwd_team's branch-free systolic
+        // schedule under contract v4
+        double* bus2 = busA + TB + n * m;
+        {
+          double u[m], w[m], wn[m];
+#pragma unroll
+          for (int kk = 0; kk < m; kk++) {
+            u[kk] = (colu && tl + kk < m) ? QU[tl + m * (tl + kk)] : 0.0;
+            w[kk] = 0.0;
+            wn[kk] = busA[TB + kk];
+          }
+          double ru = 1.0 / u[0];
+          bool okd = true;
+#pragma unroll 1
+          for (int t = 0; t < n + m - 1; t++) {
+            const int r = t - tl;
+            const bool act = colu && r >= 0 && r < n;
+            double x[m];
+#pragma unroll
+            for (int kk = 0; kk + 1 < m; kk++) x[kk] = row_shr1(w[kk + 1]);
+            x[m - 1] = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < m; kk++) x[kk] = (tl == 0) ? wn[kk] : x[kk];
+            const int rn = t + 1 < n ? t + 1 : n - 1;
+#pragma unroll
+            for (int kk = 0; kk < m; kk++) wn[kk] = busA[TB + rn * m + kk];
+            const double sn = x[0] * ru;
+            const double s2 = sn * sn;
+            okd = okd && !(act && s2 > 1.0);
+            const double y = 1.0 - s2;
+            const double rc = tog_rsqrt(y);
+            const double cs = y * rc;
+            w[0] = x[0];
+#pragma unroll
+            for (int kk = 1; kk < m; kk++) {
+              const double tmp = (u[kk] - sn * x[kk]) * rc;
+              w[kk] = cs * x[kk] - sn * tmp;
+              u[kk] = act ? tmp : u[kk];
+            }
+            u[0] = act ? cs * u[0] : u[0];
+            ru = act ? ru * rc : ru;
+          }
+          const unsigned long long rowmask = 0xFFFFull << (threadIdx.x & 48);
+          pd_fail = (__ballot(!okd) & rowmask) != 0ull;
+          if (colu) {
+#pragma unroll
+            for (int jj = 0; jj < m; jj++)
+              if (jj < tl) bus2[2 * m * m + tl + m * jj] = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < m; kk++)
+              if (tl + kk < m) bus2[2 * m * m + tl + m * (tl + kk)] = u[kk];
+          }
+        }
+      } else {
+        // regularise, test, gains (backward_pass.jl:120-145): Quu_reg = qr([Q.uu; sqrt(ρ) I]).R
+        // (:control) or qr([Q.uu; sqrt(ρ) B]).R (:state)
+        team_sync();
+        double F[m][m], rF[m];
+        {
+          const double sr = sqrt(s.rho);
+          auto qr_reg = [&](auto& a) {
+            constexpr int RR = sizeof(a) / sizeof(a[0]);
+#pragma unroll
+            for (int i = 0; i < RR; i++) {
+              double v = 0.0;
+              if (i < m) v = Quuc[i];
+              else if (state_reg) v = sr * ABg[(size_t)k * n * L + n * (n + cu) + (i - m)];
+              else if (i - m == tl) v = sr;
+              a[i] = v;
+            }
+            team_qr<RR, m, m, TEAM, true>(a, RR, tl, busB);
+            static_for<0, m>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+#pragma unroll
+              for (int i = 0; i < m; i++) F[i][j] = (i <= j) ? row_bcast<j>(a[i]) : 0.0;
+            });
+          };
+          if (state_reg) {
+            double a[m + n];
+            qr_reg(a);
+          } else {
+            double a[2 * m];
+            qr_reg(a);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < m; j++) rF[j] = 1.0 / F[j][j];
+        const bool ok = !cond_exceeds_team<m>(F, rF, 1e8, busB + 2 * n * m, tl);
+        if (ok) {
+          // right-hand side of this lane: Qux_reg column (state reg adds ρ B'A), or Q.u for lane n
+          double col[m];
+          if (state_reg) {  // (:state regularisation: the B columns on the bus)
+            if (colu) {
+              const double* bk = ABg + (size_t)k * n * L + n * (n + tl);
+#pragma unroll
+              for (int i = 0; i < n; i++) busB[n * m + i + n * tl] = bk[i];
+            }
+            team_sync();
+          }
+          if (colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) col[i] = Quxc[i];
+            if (state_reg) {
+              const double* ak = ABg + (size_t)k * n * L + n * c;
+              double t[m];
+#pragma unroll
+              for (int i = 0; i < m; i++) t[i] = 0.0;
+#pragma unroll 1
+              for (int l = 0; l < n; l++) {
+                const double a = ak[l];
+#pragma unroll
+                for (int i = 0; i < m; i++) t[i] = fma(busB[n * m + l + n * i], a, t[i]);
+              }
+#pragma unroll
+              for (int i = 0; i < m; i++) col[i] += s.rho * t[i];
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < m; i++) col[i] = Qu[i];
+          }
+          // K = -Quu_reg \ (Quu_reg' \ Qux_reg); contract v2: multiply by the diagonal reciprocals
+#pragma unroll
+          for (int j = 0; j < m; j++) {
+            const double xj = col[j] * rF[j];
+            col[j] = xj;
+#pragma unroll
+            for (int i = j + 1; i < m; i++) col[i] = fma(-F[j][i], xj, col[i]);
+          }
+#pragma unroll
+          for (int j = m - 1; j >= 0; j--) {
+            const double xj = col[j] * rF[j];
+            col[j] = xj;
+#pragma unroll
+            for (int i = j - 1; i >= 0; i--) col[i] = fma(-F[i][j], xj, col[i]);
+          }
+          double Kc[m], d[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) Kc[i] = -1.0 * col[i];
+#pragma unroll
+          for (int i = 0; i < m; i++) d[i] = row_bcast<n>(Kc[i]);
+          if (colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) {
+              Kg[(size_t)k * m * n + i + m * tl] = Kc[i];
+              KB[i + m * tl] = Kc[i];
+            }
+          }
+          if (tl == n) {
+#pragma unroll
+            for (int i = 0; i < m; i++) dg[(size_t)k * m + i] = Kc[i];
+          }
+          // s[c] = Q.x[c] + (K'Q.uu')(Q.uu d) + K'Q.u + Q.ux'd (backward_pass.jl:145)
+          double Ud[m], KtU[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < m; l++) t = fma(QU[i + m * l], d[l], t);
+            Ud[i] = t;
+          }
+#pragma unroll
+          for (int j = 0; j < m; j++) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < m; l++) t = fma(Kc[l], QU[j + m * l], t);
+            KtU[j] = t;
+          }
+          double sown;
+          {
+            double a = 0.0, b2 = 0.0, c2 = 0.0;
+#pragma unroll
+            for (int l = 0; l < m; l++) {
+              a = fma(KtU[l], Ud[l], a);
+              b2 = fma(Kc[l], Qu[l], b2);
+              c2 = fma(Quxc[l], d[l], c2);
+            }
+            sown = ((Qxs + a) + b2) + c2;
+          }
+          if (colx) Sreg[SOFF + tl] = sown;  // s_k (no wave reads s_{k+1} any more)
+          if (store_S && colx) Bf.sdbg[((size_t)b * N + k) * n + tl] = sown;
+          {  // ΔV += [d'Q.u, ½‖Q.uu d‖²] (backward_pass.jl:158-161)
+            double a = 0.0, b2 = 0.0;
+#pragma unroll
+            for (int i = 0; i < m; i++) a = fma(d[i], Qu[i], a);
+#pragma unroll
+            for (int i = 0; i < m; i++) b2 = fma(Ud[i], Ud[i], b2);
+            dV0 += a;
+            dV1 += 0.5 * b2;
+          }
+        }
+        if (threadIdx.x == 64) flg[0] = ok ? 1 : 0;
+      }
+      __syncthreads();  // B2b: K, d and the verdict on the bus
+      if (flg[0] == 0) {
+        // non-PD / cond > 1e8: increase ρ and restart at N-1; Q blocks are NOT re-expanded (A.1)
+        if (!faithful) {
+          faithful = true;  // replay this call from its start in faithful mode
+          s.rho = rho0;
+          s.drho = drho0;
+          restarts = 0;
+          kmin = N - 1;
+        } else {
+          reg_increase(P, s);
+          restarts++;
+          if (restarts > TOG_BP_MAX_RESTARTS) {
+            s.flags |= TOG_TRAJ_MAX_REG | TOG_TRAJ_BP_ABORTED;
+            done = true;
+          }
+        }
+        restart = true;
+        break;
+      }
+      // ------------------------------------------------------------------ phase 4: S_k = qr([Q.xx + tmp1 K; tmp2 K]).R
+      if (wv == 0) {
+        if (pd_fail) pd_flags |= TOG_TRAJ_SQRT_PD_FAIL;
+        constexpr int TB = 32;
+        double* bus2 = busA + TB + n * m;
+        const double* U2p = pd_fail ? QU : bus2 + 2 * m * m;  // tmp2, or Q.uu on failure
+        double Kc[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) Kc[i] = KB[i + m * c];
+        constexpr int RS = n + m;
+        double a[RS];
+        {
+          double v[n];
+#pragma unroll
+          for (int i = 0; i < n; i++) v[i] = 0.0;
+#pragma unroll
+          for (int l = 0; l < m; l++) {
+#pragma unroll
+            for (int i = 0; i < n; i++) v[i] = fma(busA[TB + i * m + l], Kc[l], v[i]);
+            TEAM_FENCE();
+          }
+#pragma unroll
+          for (int i = 0; i < n; i++) a[i] = Qxc[i] + v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          double v = 0.0;
+#pragma unroll
+          for (int l = 0; l < m; l++) v = fma(U2p[i + m * l], Kc[l], v);
+          a[n + i] = v;
+        }
+        team_sync();
+        team_qr<RS, n, 0, TEAM>(a, RS, tl, busA);
+        if (colx) {
+#pragma unroll
+          for (int i = 0; i < n; i++) Sreg[i + n * tl] = (i <= tl) ? a[i] : 0.0;
+        }
+        if (store_S && colx) {
+#pragma unroll
+          for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = (i <= tl) ? a[i] : 0.0;
+        }
+      }
+      __syncthreads();  // B3: S_k for the next knot
+    }
+    if (!restart) done = true;
+  }
+  if (wv == 0 && threadIdx.x == 0) flg[1] = pd_flags;
+  __syncthreads();
+  if (wv == 1) {
+    s.flags |= flg[1];
+    const bool aborted = (s.flags & TOG_TRAJ_BP_ABORTED) != 0;
+    if (!aborted) reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:166)
+    if (threadIdx.x == 64) {
+      TrajState& g = Bf.st[b];
+      g.rho = s.rho;
+      g.drho = s.drho;
+      g.flags = s.flags;
+      g.dV0 = aborted ? 0.0 : dV0;
+      g.dV1 = aborted ? 0.0 : dV1;
+      g.bp_restarts = restarts + (faithful ? 1 : 0);
+      if (aborted) g.active = 0;
+    }
+  }
+}
+
+}  // namespace tog

@@ -624,6 +624,12 @@ __global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuff
 #ifndef TOG_BWD_WAVES
 #define TOG_BWD_WAVES 2
 #endif
+#ifndef TOG_TAIL_PF
+#define TOG_TAIL_PF 0  // measured slower (profiles/r3g_ab_tail.txt): the prefetch buffer's registers spill
+#endif
+#ifndef TOG_TAIL_TRI
+#define TOG_TAIL_TRI 1
+#endif
 // Section timers of the knot loop (build with -DTOG_BWD_PROF; read with tog_bwd_prof_read): shader
 // clock deltas (s_memtime) summed per wave into SGPR accumulators, flushed once per wave.
 #ifdef TOG_BWD_PROF
@@ -706,6 +712,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   double dV0 = 0.0, dV1 = 0.0;
   double sown = 0.0;  // s[c] of the knot being produced
   bool done = !live;
+  // PF (TOG_TAIL_PF, the 1-wave/SIMD tail variant): knot k-1's [A|B] columns and expansion record
+  // loaded at the top of knot k. Off: measured 5 % slower at B = 1 (its buffer spills, and a spilled
+  // reload waits on every load in flight), and the loads are only ~3 % of a knot.
+  constexpr bool PF = (WPE == 1) && TOG_TAIL_PF;
+  // TRI_SA: S [A B] over the upper factor's nonzero rows only, fully unrolled (the 2-wave/SIMD variant
+  // keeps the rolled dense product: unrolled, its 256-register budget spills)
+  constexpr bool TRI_SA = (WPE == 1) && TOG_TAIL_TRI;
+  double pAc[n], pBc[n], pQxc[n], pQu[m], pQuuc[m], pQuxc[m], pQxs = 0.0;
+  int pk = -1;  // knot whose inputs the p* registers hold
   BPROF_DECL
 
   // Q blocks of knot k (terminal when TERM) from its expansion record (k_expand_team, ne_of):
@@ -775,7 +790,42 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       // the loop they would stay live across it and spill
       TEAM_FENCE();
       double Qxc[n], Quuc[m], Quxc[m], Qu[m], Qxs;
+      double Ac[n], Bc[n];  // this lane's columns of ∇F[k] = [A|B]
       const bool replay = faithful && k >= kmin;
+      const bool have_pf = PF && pk == k;  // knot k's inputs arrived during knot k+1 (neither its
+                                           // [A|B] nor its expansion record changes between attempts)
+      if (have_pf) {
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          Ac[i] = pAc[i];
+          Bc[i] = pBc[i];
+          Qxc[i] = pQxc[i];
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          Qu[i] = pQu[i];
+          Quuc[i] = pQuuc[i];
+          Quxc[i] = pQuxc[i];
+        }
+        Qxs = pQxs;
+      } else {
+        const double* abk = ABg + (size_t)k * n * L;
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          Ac[i] = abk[i + n * c];
+          Bc[i] = abk[i + n * (n + cu)];
+        }
+      }
+      if (PF && k > 0) {  // latency-sized variant: knot k-1's inputs load while knot k's chain runs
+        const double* abk = ABg + (size_t)(k - 1) * n * L;
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          pAc[i] = abk[i + n * c];
+          pBc[i] = abk[i + n * (n + cu)];
+        }
+        expand(k - 1, std::integral_constant<bool, false>{}, pQxs, pQu, pQxc, pQuuc, pQuxc);
+        pk = k - 1;
+      }
       if (replay) {
         const double* q = Qs + (size_t)k * NQ;
         Qxs = q[c];
@@ -787,20 +837,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
   #pragma unroll
         for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
-      } else {
+      } else if (!have_pf) {
         expand(k, std::integral_constant<bool, false>{}, Qxs, Qu, Qxc, Quuc, Quxc);
       }
-    BPROF(1)  // cost expansion remainder (Q.u += cu'g)
-    // ---------------------------------------------------------------- ∇F[k] = [A|B] columns
-    double Ac[n], Bc[n];
-    {
-      const double* abk = ABg + (size_t)k * n * L;
-#pragma unroll
-      for (int i = 0; i < n; i++) {
-        Ac[i] = abk[i + n * c];
-        Bc[i] = abk[i + n * (n + cu)];
-      }
-    }
+    BPROF(1)  // expansion record loads
 #ifdef TOG_BWD_PROF
     { volatile double sink_ = Ac[n - 1] + Bc[n - 1]; (void)sink_; }
 #endif
@@ -894,20 +934,39 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         TX[i] = 0.0;
         TU[i] = 0.0;
       }
-      // Column l of S is read from LDS in one burst (one wait per column, rolled loop: few live
-      // registers); dense as the oracle's operand (explicit zeros below the diagonal).
+      // Column l of S is read from LDS in one burst (one wait per column). S is the upper factor: its
+      // entries below the diagonal are exact +0.0, and the accumulators are never -0.0 (they start at
+      // +0.0 and an fma whose exact result is zero rounds to +0.0), so the oracle's dense terms
+      // fma(+0.0, a, t) == t for those rows are skipped (rows i <= l of column l only, ~half the work).
+      if constexpr (TRI_SA) {
+        static_for<0, n>([&](auto lc) {
+          constexpr int l = decltype(lc)::value;
+          double sl[l + 1];
+          const double* Sl = Sreg + n * l;
+#pragma unroll
+          for (int i = 0; i <= l; i++) sl[i] = Sl[i];
+          const double al = bus[l + n * c], bl = bus[l + n * (n + cu)];
+          TEAM_FENCE();
+#pragma unroll
+          for (int i = 0; i <= l; i++) {
+            TX[i] = fma(sl[i], al, TX[i]);
+            TU[i] = fma(sl[i], bl, TU[i]);
+          }
+        });
+      } else {
 #pragma unroll 1
-      for (int l = 0; l < n; l++) {
-        double sl[n];
-        const double* Sl = Sreg + n * l;
+        for (int l = 0; l < n; l++) {
+          double sl[n];
+          const double* Sl = Sreg + n * l;
 #pragma unroll
-        for (int i = 0; i < n; i++) sl[i] = Sl[i];
-        const double al = bus[l + n * c], bl = bus[l + n * (n + cu)];
-        TEAM_FENCE();
+          for (int i = 0; i < n; i++) sl[i] = Sl[i];
+          const double al = bus[l + n * c], bl = bus[l + n * (n + cu)];
+          TEAM_FENCE();
 #pragma unroll
-        for (int i = 0; i < n; i++) {
-          TX[i] = fma(sl[i], al, TX[i]);
-          TU[i] = fma(sl[i], bl, TU[i]);
+          for (int i = 0; i < n; i++) {
+            TX[i] = fma(sl[i], al, TX[i]);
+            TU[i] = fma(sl[i], bl, TU[i]);
+          }
         }
       }
       // Q.ux += tmp_u' tmp_x: tmp_u columns (lanes < m) then tmp_x columns go to region 1 ([A B]

@@ -2220,6 +2220,7 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
 // =============================================================================================
 }  // namespace tog
 #include "tog_bwd_team.hpp"
+#include "tog_bwd_duo.hpp"
 #include "tog_pn.hpp"
 namespace tog {
 
@@ -2556,10 +2557,19 @@ struct ModelLaunch {
           else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
         }
       };
-      if (Bf.tail)
+      if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && !getenv("TOG_NO_DUO")) {
+        // convergence tail, square-root pass: the chain and the side work on two waves (tog_bwd_duo.hpp),
+        // one trajectory per workgroup
+        if constexpr (TeamCfg<M>::TEAM == 16) {
+          const dim3 gd((unsigned)B), bd(128);
+          if (al) hipLaunchKernelGGL((k_bwd_duo<M, 1>), gd, bd, 0, st, P, Bf, flags);
+          else hipLaunchKernelGGL((k_bwd_duo<M, 0>), gd, bd, 0, st, P, Bf, flags);
+        }
+      } else if (Bf.tail) {
         launch(std::integral_constant<int, 1>{});
-      else
+      } else {
         launch(std::integral_constant<int, TOG_BWD_WAVES>{});
+      }
       return;
     }
     }

@@ -161,6 +161,19 @@ _CON_TEMPLATE = """
 """
 
 
+def _prune_stale_plugins(out_dir: pathlib.Path, hh: str):
+    """Remove generated plugins built against other libtog headers (their .hip records the hash):
+    tog_model_load / tog_generic_cost_load would refuse them anyway."""
+    for hip in out_dir.glob("gen_*.hip"):
+        try:
+            first = hip.read_text().split("\n", 1)[0]
+        except OSError:
+            continue
+        if first != f"// libtog header hash {hh}":
+            hip.with_suffix(".so").unlink(missing_ok=True)
+            hip.unlink(missing_ok=True)
+
+
 def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=None, con_body: str | None = None) -> Model:
     """``Model(f!, n, m)`` (src/model.jl:103-131) for user dynamics: ``f_body`` is the body of
     ``f(T* xd, const T* x, const T* u)`` in C++ over the scalar type ``T`` (double in rollouts,
@@ -182,9 +195,11 @@ def user_model(f_body: str, n: int, m: int, name: str = "UserModel", build_dir=N
     src = _PLUGIN_TEMPLATE.format(hdr=str(csrc / "tog_plugin.hpp"), name=name, n=int(n), m=int(m), body=body,
                                   con=con)
     hh = abi.header_hash()  # the plugin is compiled against (and cached under) libtog's header text
-    key = hashlib.sha1((src + hh).encode()).hexdigest()[:12]
+    src = f"// libtog header hash {hh}\n" + src
+    key = hashlib.sha1(src.encode()).hexdigest()[:12]
     so = out_dir / f"gen_{name}_{key}.so"
     if not so.exists():
+        _prune_stale_plugins(out_dir, hh)
         hip = out_dir / f"gen_{name}_{key}.hip"
         hip.write_text(src)
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-fPIC",
@@ -406,9 +421,11 @@ def generic_cost(stage_body: str, terminal_body: str, n: int, m: int, name: str 
     src = _COST_TEMPLATE.format(hdr=str(csrc / "tog_cost_plugin.hpp"), name=name, n=int(n), m=int(m),
                                 stage=ind(stage_body), term=ind(terminal_body))
     hh = abi.header_hash()  # the plugin is compiled against (and cached under) libtog's header text
-    key = hashlib.sha1((src + hh).encode()).hexdigest()[:12]
+    src = f"// libtog header hash {hh}\n" + src
+    key = hashlib.sha1(src.encode()).hexdigest()[:12]
     so = out_dir / f"gen_{name}_{key}.so"
     if not so.exists():
+        _prune_stale_plugins(out_dir, hh)
         hip = out_dir / f"gen_{name}_{key}.hip"
         hip.write_text(src)
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-fPIC",
