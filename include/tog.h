@@ -364,7 +364,7 @@ int32_t tog_backward_pass(tog_handle* h, int32_t sqrt, int32_t al, int32_t flags
    performs the same expansion fused, knot by knot, and does not read this field. */
 int32_t tog_cost_expansion(tog_handle* h, int32_t sqrt, int32_t al);
 /* solve!(prob, iLQRSolver) / solve!(prob, AugmentedLagrangianSolver) to completion:
-   tog_solve(h, TOG_MODE_ILQR | TOG_MODE_AL, iterations (x al_iterations) + 1) */
+   tog_solve(h, TOG_MODE_ILQR | TOG_MODE_AL, 0), i.e. with the tog_solve_budget step budget */
 int32_t tog_solve_ilqr(tog_handle* h);
 int32_t tog_solve_al(tog_handle* h);
 /* forwardpass! (forward_pass.jl:5-85) from the stored ΔV; J_prev (B) host pointer;
@@ -391,8 +391,13 @@ int32_t tog_batch_stats(tog_handle* h, double* out3);
 int32_t tog_batch_stats_device(tog_handle* h, void* dptr3);
 /* counter of step!s executed since tog_solve_init (device side, read blocking) */
 int32_t tog_total_steps(tog_handle* h, int64_t* out);
-/* full solves: run until no trajectory is active (or max_steps) */
+/* full solves: run until no trajectory is active (or max_steps batch steps; max_steps <= 0: the
+   tog_solve_budget default, which lets every trajectory reach its own iteration limit) */
 int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps);
+/* default batch-step budget of tog_solve: (iterations (x al_iterations) + 1) x the line-search rounds
+   an iteration may take when its trials are spread over batch steps (ceil(nc / 8) for batches large
+   enough to pend). Returns the budget (> 0) or a negative error code. */
+int32_t tog_solve_budget(tog_handle* h, int32_t mode);
 /* per-trajectory tog_traj_flag bits; flags_out: (B) int32 */
 int32_t tog_status(tog_handle* h, int32_t* flags_out);
 

@@ -346,9 +346,8 @@ function solve!(probs::Vector{<:Problem{T}}, s::BatchediLQRSolver{T}) where T
     togcheck(ccall((:tog_set_state, libtog), Int32, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
                    s.handle, x0, U, X))
     mode = s.opts.opts isa AugmentedLagrangianSolverOptions ? TOG_MODE_AL : TOG_MODE_ILQR
-    o = s.opts.opts
-    max_steps = s.opts.max_steps > 0 ? s.opts.max_steps :
-        (mode == TOG_MODE_AL ? o.opts_uncon.iterations * o.iterations + 1 : o.iterations + 1)
+    # 0: tog_solve_budget, the iteration budget x the line-search rounds of pending mode
+    max_steps = s.opts.max_steps > 0 ? s.opts.max_steps : 0
     togcheck(ccall((:tog_solve, libtog), Int32, (Ptr{Cvoid}, Int32, Int32), s.handle, mode, max_steps))
     togcheck(ccall((:tog_get, libtog), Int32, (Ptr{Cvoid}, Int32, Ptr{Float64}), s.handle, TOG_FIELD_X, X))
     togcheck(ccall((:tog_get, libtog), Int32, (Ptr{Cvoid}, Int32, Ptr{Float64}), s.handle, TOG_FIELD_U, U))

@@ -10,7 +10,7 @@
  *          goal = goal_constraint(xf) -> TOG_CON_GOAL (xf read from the closure)
  *   opts   AugmentedLagrangianSolverOptions(opts_uncon = iLQRSolverOptions(cost_tolerance=1e-5,
  *          square_root=true), constraint_tolerance=1e-3, cost_tolerance=1e-5, cost_tolerance_intermediate=1e-4)
- * then tog_create -> tog_set_state -> tog_solve (AL, iterations x al_iterations + 1) -> tog_get.
+ * then tog_create -> tog_set_state -> tog_solve (AL, default budget) -> tog_get.
  *
  *   test_capi_config3 --version           prints tog_version() (links the library, no device needed)
  *   test_capi_config3 <in.bin> <out.bin>  in: int64 B, x0 (13, B), U0 (4, 100, B); out: X (13, 101, B),
@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
   int rc = tog_create(&d, &o, 0, &h);
   if (rc) return fail_rc("tog_create", rc);
   if ((rc = tog_set_state(h, x0, U, NULL))) return fail_rc("tog_set_state", rc);
-  if ((rc = tog_solve(h, TOG_MODE_AL, o.iterations * o.al_iterations + 1))) return fail_rc("tog_solve", rc);
+  if ((rc = tog_solve(h, TOG_MODE_AL, 0))) return fail_rc("tog_solve", rc);  /* 0: tog_solve_budget */
   double* X = malloc(sizeof(double) * n * N * B);
   double* St = malloc(sizeof(double) * TOG_NSTATS * B);
   if ((rc = tog_get(h, TOG_FIELD_X, X)) || (rc = tog_get(h, TOG_FIELD_U, U)) || (rc = tog_get(h, TOG_FIELD_STATS, St)))

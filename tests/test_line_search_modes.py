@@ -64,3 +64,47 @@ def test_line_search_schedules_agree(tog, oracle, gpu, case):
         X, U = o.get("X"), o.get("U")
         assert np.max(np.abs(ref[0]._X[b] - X)) <= 1e-6 * max(1.0, np.max(np.abs(X)))
         assert np.max(np.abs(ref[0]._U[b] - U)) <= 1e-6 * max(1.0, np.max(np.abs(U)))
+
+
+def test_default_budget_covers_pending_rounds(tog, oracle, gpu):
+    """in pending mode an iteration can take ceil(nc / 8) batch steps, so the default
+    step budget (tog_solve_budget) must let every trajectory reach its own iteration limits. The old
+    budget of one iteration per step (iterations x al_iterations + 1) stops trajectories whose line
+    searches pended while they are still active; the default budget ends them all with their
+    iteration flags, as the reference's solve! loops (augmented_lagrangian_solve.jl / ilqr_solve.jl)
+    do, and matches the oracle. The maze's AL line searches backtrack past 8 trials as the penalties
+    grow; B = 8192 keeps the batch in pending mode for most of the solve."""
+    prob, opts = tog.Problems.config_quad_maze(B=8192)
+    il = opts.opts_uncon
+    il.iterations = 2                  # small caps that every trajectory reaches: dJ never
+    il.cost_tolerance = 0.0            # converges an inner solve, the constraints never converge
+    il.gradient_norm_tolerance = 0.0   # the AL solve: 15 outer iterations of one iLQR step each,
+    opts.iterations = 15               # the later ones backtracking past 8 trials (oracle: 19 of
+    opts.cost_tolerance = 0.0          # the first 32 trajectories need more than 31 batch steps)
+    opts.cost_tolerance_intermediate = 0.0
+    opts.constraint_tolerance = 0.0
+    mode = tog.abi.MODE_AL
+    old_budget = il.iterations * opts.iterations + 1
+
+    p_old = prob.copy()
+    s_old = tog.AbstractSolverFor(p_old, opts, device=0)
+    s_old.handle.solve(mode, max_steps=old_budget)
+    st_old = s_old.handle.status()
+    short = np.flatnonzero(st_old & tog.abi.TRAJ_ACTIVE)
+    assert short.size > 0, "no trajectory outlived the old budget: the case does not exercise it"
+
+    p = prob.copy()
+    solver = tog.solve_b(p, opts)
+    h = solver.handle
+    assert h.solve_budget(mode) == old_budget * -(-(il.iterations_linesearch + 1) // 8)
+    flags = solver.stats["flags"]
+    assert not np.any(flags & tog.abi.TRAJ_ACTIVE)
+    assert np.all(flags & (tog.abi.TRAJ_AL_MAX_ITERS | tog.abi.TRAJ_AL_CONVERGED))
+    for b in (int(short[0]), int(short[-1])):
+        o = oracle.OracleSolver(prob, opts, b=b)
+        steps = o.solve()
+        assert steps == int(solver.stats["iterations_total"][b]), b
+        assert int(o.get("stats")[tog.abi.STAT_FLAGS]) == int(flags[b]), b
+        X, U = o.get("X"), o.get("U")
+        assert np.max(np.abs(p._X[b] - X)) <= 1e-6 * max(1.0, np.max(np.abs(X))), b
+        assert np.max(np.abs(p._U[b] - U)) <= 1e-6 * max(1.0, np.max(np.abs(U))), b

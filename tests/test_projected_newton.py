@@ -86,6 +86,16 @@ def test_pn_rejects_infeasible_start(tog):
         tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
 
 
+def test_pn_rejects_min_time(tog):
+    """phase 2 on a minimum-time problem (altro_methods.jl:98-124) is refused, not
+    silently skipped."""
+    prob = tog.Problems.pendulum()
+    prob.tf = 0.0
+    with pytest.raises(NotImplementedError):
+        tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
+    tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=False))
+
+
 @pytest.mark.parametrize("ft,at", [(1e-6, 1e-3), (1e-10, 1e-3), (1e-10, 1e-4)])
 def test_oracle_projection_reaches_tolerance(tog, oracle, ft, at):
     """test/projected_newton_test.jl:111-120: after the projection every constraint is satisfied to

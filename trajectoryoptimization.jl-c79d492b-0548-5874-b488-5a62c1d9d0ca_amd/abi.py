@@ -260,6 +260,7 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_batch_stats_device.argtypes = [vp, vp]
     lib.tog_total_steps.argtypes = [vp, C.POINTER(C.c_int64)]
     lib.tog_solve.argtypes = [vp, C.c_int32, C.c_int32]
+    lib.tog_solve_budget.argtypes = [vp, C.c_int32]
     lib.tog_status.argtypes = [vp, _ip]
     lib.tog_profile.argtypes = [vp, C.c_int32]
     lib.tog_profile_read.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
@@ -283,8 +284,8 @@ def load_library(path: os.PathLike | None = None):
                  "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims", "tog_rollout_open_loop",
                  "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
                  "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
-                 "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile",
-                 "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
+                 "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_solve_budget", "tog_status",
+                 "tog_profile", "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
                  "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn", "tog_model_load", "tog_model_dims",
                  "tog_model_free", "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device",
                  "tog_generic_cost_free"):
@@ -302,8 +303,8 @@ EXPORTED_SYMBOLS = (
     "tog_synchronize", "tog_set_state", "tog_set", "tog_get", "tog_get_device_ptr", "tog_dims",
     "tog_rollout_open_loop", "tog_jacobians", "tog_update_constraints", "tog_cost", "tog_backward_pass",
     "tog_forward_pass", "tog_rollout", "tog_solve_init", "tog_solve_step", "tog_batch_stats",
-    "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_status", "tog_profile", "tog_profile_read",
-    "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
+    "tog_batch_stats_device", "tog_total_steps", "tog_solve", "tog_solve_budget", "tog_status", "tog_profile",
+    "tog_profile_read", "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
     "tog_solve_al", "tog_default_pn_options", "tog_solve_pn", "tog_model_load", "tog_model_dims", "tog_model_free",
     "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device", "tog_generic_cost_free",
 )

@@ -1117,12 +1117,29 @@ int32_t tog_cost_expansion(tog_handle* h, int32_t sq, int32_t al) {
 
 int32_t tog_solve_ilqr(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
-  return tog_solve(h, TOG_MODE_ILQR, h->opts.iterations + 1);
+  return tog_solve(h, TOG_MODE_ILQR, 0);
 }
 
 int32_t tog_solve_al(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
-  return tog_solve(h, TOG_MODE_AL, h->opts.iterations * h->opts.al_iterations + 1);
+  return tog_solve(h, TOG_MODE_AL, 0);
+}
+
+// Batch steps a solve to completion may take: the iteration budget (iterations, x al_iterations for AL,
+// + 1 for the final check) times the line-search rounds one iteration can spread over when its trials
+// are run LS_FIRST per batch step (pending mode, ceil(nc / LS_FIRST) rounds). A pending step does not
+// advance a trajectory's iteration counter, so a budget of one iteration per step would stop hard
+// trajectories before the device-side counters flag them MAX_ITERS. Steps beyond need are free:
+// tog_solve stops as soon as no trajectory is active.
+int32_t tog_solve_budget(tog_handle* h, int32_t mode) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  const tog_options& o = h->opts;
+  long long it = (long long)(o.iterations > 0 ? o.iterations : 0);
+  if (mode == TOG_MODE_AL) it *= (o.al_iterations > 0 ? o.al_iterations : 0);
+  const int nc = std::max(1, std::min(o.iterations_linesearch + 1, 64));
+  const long long rounds = getenv("TOG_LS_NOPEND") ? 1 : (nc + LS_FIRST - 1) / LS_FIRST;
+  const long long s = (it + 1) * rounds;
+  return (int32_t)std::min<long long>(s, INT32_MAX);
 }
 
 int32_t tog_backward_pass(tog_handle* h, int32_t sq, int32_t al, int32_t flags, double* dV_out) {
@@ -1302,6 +1319,7 @@ int32_t tog_total_steps(tog_handle* h, int64_t* out) {
 int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps) {
   int rc = tog_solve_init(h, mode);
   if (rc) return rc;
+  if (max_steps <= 0) max_steps = tog_solve_budget(h, mode);
   const int chunk = 4;
   double stats[3];
   for (int done = 0; done < max_steps; done += chunk) {
@@ -1387,6 +1405,18 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     W.SM = SM;
     W.nb = h->N + 1;
     const size_t blk = (size_t)B * W.nb * SM * SM, vec = (size_t)B * W.nb * SM;
+    const size_t pm = (size_t)(h->pmax > 0 ? h->pmax : 1);
+    // the whole workspace is sized before any allocation: a batch whose block factors do not fit the
+    // device's free memory is refused with TOG_ERR_NOMEM (solve it in slices, tog_create_multi)
+    const size_t need = sizeof(double) * (4 * blk + 5 * vec + 2 * (size_t)B * h->N * h->n) +
+                        sizeof(int) * ((size_t)B * h->N * pm + (size_t)B * h->N + (size_t)B * W.nb) +
+                        sizeof(PNState) * (size_t)B;
+    size_t fr = 0, tot = 0;
+    HIPCHECK(hipMemGetInfo(&fr, &tot));
+    if (need > fr)
+      return fail(TOG_ERR_NOMEM, "projected Newton workspace (" + std::to_string(need >> 20) + " MiB) exceeds free device memory (" +
+                                     std::to_string(fr >> 20) + " MiB)");
+    const size_t mark = h->allocs.size();
     int rc;
     if ((rc = dalloc(h, &W.Sd, blk)) || (rc = dalloc(h, &W.So, blk)) || (rc = dalloc(h, &W.Ld, blk)) ||
         (rc = dalloc(h, &W.Lo, blk)) || (rc = dalloc(h, &W.yv, vec)) || (rc = dalloc(h, &W.xv, vec)) ||
@@ -1394,8 +1424,13 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
         (rc = dalloc(h, &W.yd, (size_t)B * h->N * h->n)) || (rc = dalloc(h, &W.Xs, (size_t)B * h->N * h->n)) ||
         (rc = dalloc(h, &W.act, (size_t)B * h->N * (h->pmax > 0 ? h->pmax : 1))) ||
         (rc = dalloc(h, &W.na, (size_t)B * h->N)) || (rc = dalloc(h, &W.sz, (size_t)B * W.nb)) ||
-        (rc = dalloc(h, &W.st, (size_t)B)))
+        (rc = dalloc(h, &W.st, (size_t)B))) {
+      // partial failure: release what this call allocated, so a retry does not leak it
+      for (size_t i = mark; i < h->allocs.size(); i++) (void)hipFree(h->allocs[i]);
+      h->allocs.resize(mark);
+      (void)hipGetLastError();
       return rc;
+    }
     h->pn_alloc = true;
   }
   W.atol = opts->active_set_tolerance;

@@ -140,8 +140,16 @@ class BatchHandle:
     def solve_step(self, nsteps=1):
         abi.check(self.lib, self.lib.tog_solve_step(self.h, int(nsteps)))
 
-    def solve(self, mode, max_steps=10000):
-        abi.check(self.lib, self.lib.tog_solve(self.h, int(mode), int(max_steps)))
+    def solve_budget(self, mode):
+        """tog_solve_budget: default batch-step budget of a solve to completion."""
+        rc = self.lib.tog_solve_budget(self.h, int(mode))
+        if rc <= 0:
+            abi.check(self.lib, rc)
+        return int(rc)
+
+    def solve(self, mode, max_steps=None):
+        """tog_solve; max_steps None/0: the tog_solve_budget default"""
+        abi.check(self.lib, self.lib.tog_solve(self.h, int(mode), int(max_steps or 0)))
 
     def solve_pn(self, pn_opts: abi.tog_pn_options):
         """tog_solve_pn: returns the (B, PN_NSTATS) statistics rows."""

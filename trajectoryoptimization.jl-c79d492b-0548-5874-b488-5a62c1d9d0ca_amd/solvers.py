@@ -356,6 +356,10 @@ def AbstractSolverFor(prob, opts, **kw):
 def _altro_check(prob, opts):
     if opts.projected_newton and _altro_infeasible(prob):
         raise NotImplementedError("projected Newton on the infeasible-start problem (slack controls) is not built")
+    if opts.projected_newton and prob.tf == 0.0:
+        # altro_methods.jl:98-124 would run phase 2 on the minimum-time problem (the projection over
+        # [u; h]); the device projected Newton has no MinTime model, so refuse instead of skipping it
+        raise NotImplementedError("projected Newton on the minimum-time problem is not built")
 
 
 def _altro_pn_tolerances(opts):
@@ -399,9 +403,7 @@ def _solve_altro_infeasible(prob, opts, max_steps, device):
     solver = ALTROSolver(prob_inf, opts, device=device)
     h = solver.handle
     h.slack_controls()
-    o = to_tog_options(opts)
-    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None
-            else int(o.iterations) * int(o.al_iterations) + 1)
+    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None else h.solve_budget(abi.MODE_AL))
     h.download_state(prob_inf)
     solver.stats = h.stats_dict()
     solver.prob_infeasible = prob_inf
@@ -429,9 +431,7 @@ def _solve_altro_min_time(prob, opts, max_steps, device):
     pmt = minimum_time_problem(prob, opts.R_minimum_time, opts.dt_max, opts.dt_min)
     solver = ALTROSolver(pmt, opts, device=device)
     h = solver.handle
-    o = to_tog_options(opts)
-    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None
-            else int(o.iterations) * int(o.al_iterations) + 1)
+    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None else h.solve_budget(abi.MODE_AL))
     h.download_state(pmt)
     solver.stats = h.stats_dict()
     solver.prob_min_time = pmt
@@ -492,10 +492,9 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
 
 
 def _default_max_steps(solver):
-    o = to_tog_options(solver.opts)
-    if solver.mode == abi.MODE_AL:
-        return int(o.iterations) * int(o.al_iterations) + 1
-    return int(o.iterations) + 1
+    """tog_solve_budget: the iteration budget times the line-search rounds an iteration may spread
+    over in pending mode, so every trajectory reaches its own iteration limit (MAX_ITERS)."""
+    return solver.handle.solve_budget(solver.mode)
 
 
 def solve(prob, solver_or_opts, **kw):
