@@ -188,7 +188,7 @@ typedef struct tog_options {
   int32_t dJ_counter_limit;       /* 10   */
   int32_t square_root;            /* 0    */
   int32_t bp_reg_type;            /* 0 = :control, 1 = :state */
-  int32_t gradient_type;          /* 0 = :todorov, 1 = :feedforward */
+  int32_t gradient_type;          /* 0 = :todorov, 1 = :feedforward, 2 = :ℓ2, 3 = :ℓinf */
   int32_t iterations_linesearch;  /* 20   */
   double line_search_lower_bound; /* 1e-8 */
   double line_search_upper_bound; /* 10   */
@@ -249,7 +249,7 @@ enum tog_field {
 enum tog_stat {
   TOG_STAT_J = 0,           /* current cost (J_prev of the inner loop)              */
   TOG_STAT_DJ = 1,          /* last dJ                                              */
-  TOG_STAT_GRADIENT = 2,    /* last gradient (todorov / feedforward)                */
+  TOG_STAT_GRADIENT = 2,    /* last gradient (gradient_type's measure)              */
   TOG_STAT_ITERATIONS = 3,  /* iLQR stats[:iterations] (includes initial record)    */
   TOG_STAT_ZERO_COUNT = 4,  /* dJ_zero_counter                                      */
   TOG_STAT_ALPHA = 5,       /* last accepted step (logged 2*alpha)                  */

@@ -1149,6 +1149,7 @@ typedef struct oc_solver {
   /* per-iteration trace (for localisation) */
   int trace_len;
   double* trace; /* [J, alpha, rho, restarts, trials, z] per step */
+  int al_mode;   /* the current inner solve's objective is the AL one (compute_gradient's prob.obj) */
 } oc_solver;
 
 static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
@@ -2162,9 +2163,44 @@ OC_EXPORT double oc_forward(oc_solver* s, int al, double J_prev) {
 /* =====================================================================
  * Solves
  * ===================================================================== */
-/* gradient_todorov (ilqr_methods.jl:122-129) / gradient_feedforward (:135-137) */
+/* gradient_type :ℓ2 / :ℓinf (ilqr_methods.jl:96-99): norm(compute_gradient(prob, solver)) with
+   compute_gradient (:104-116) = vcat(Q[1].x, Q[1].u, ..., Q[N-1].x, Q[N-1].u, Q[N].x) of the plain
+   (not square-root) cost_expansion! of the current objective (the AL one inside AL solves) at the new
+   X, U; the AL terms use obj.C, the constraint values of the accepted trajectory (the last cost
+   evaluation, A.10). ℓinf is LinearAlgebra.generic_normInf (NaN propagates). ℓ2: Julia 1.1 hands
+   vectors of 32 or more Float64 to BLAS.nrm2, whose summation order and precision are the BLAS
+   build's; this restatement takes generic_norm2's unscaled double sum in index order (jl_norm2), so
+   the two agree to rounding (the convergence test grad < tol is unpinned within that rounding). */
+static double expansion_gradient_norm(oc_solver* s, int linf) {
+  int n = s->n, m = s->m, N = s->N;
+  oc_cost_expansion(s, 0, s->al_mode); /* overwrites solver.Q, as reset!(solver.Q) + cost_expansion! */
+  size_t len = (size_t)(N - 1) * (n + m) + n;
+  double* g = (double*)malloc(sizeof(double) * len);
+  size_t e = 0;
+  for (int k = 0; k < N - 1; k++) {
+    for (int i = 0; i < n; i++) g[e++] = s->Qx[(size_t)k * n + i];
+    for (int i = 0; i < m; i++) g[e++] = s->Qu[(size_t)k * m + i];
+  }
+  for (int i = 0; i < n; i++) g[e++] = s->Qx[(size_t)(N - 1) * n + i];
+  double r;
+  if (linf) {
+    r = fabs(g[0]);
+    for (size_t i = 1; i < len; i++) {
+      double v = fabs(g[i]);
+      r = (isnan(r) || r > v) ? r : v;
+    }
+  } else {
+    r = jl_norm2(g, (int)len);
+  }
+  free(g);
+  return r;
+}
+
+/* gradient_todorov (ilqr_methods.jl:122-129) / gradient_feedforward (:135-137) / ℓ2, ℓinf (above) */
 static double calc_gradient(oc_solver* s) {
   int m = s->m, N = s->N;
+  if (s->opts.gradient_type == 2 || s->opts.gradient_type == 3)
+    return expansion_gradient_norm(s, s->opts.gradient_type == 3);
   if (s->opts.gradient_type == 1) {
     double g = 0.0;
     for (int k = 0; k < N - 1; k++) {
@@ -2243,6 +2279,7 @@ static void ilqr_reset(oc_solver* s) { /* reset!(solver) ilqr_solver.jl:146-154 
 
 /* solve!(prob, iLQRSolver) ilqr_methods.jl:3-45 ; al selects the AL objective (inner solve) */
 static void ilqr_solve(oc_solver* s, int al, double cost_tol, double grad_tol) {
+  s->al_mode = al;
   ilqr_reset(s);
   oc_rollout_open_loop(s);
   double J_prev = cost(s, al, s->X, s->U);

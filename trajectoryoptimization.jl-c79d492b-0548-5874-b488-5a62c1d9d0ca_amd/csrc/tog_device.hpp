@@ -81,6 +81,35 @@ struct DevProblem {
   tog_options o;
 };
 
+// Read-only device tables seen through the constant address space. The row tables are read at the
+// same (knot, row) by every lane of a wave, so through these pointers a read is a scalar load
+// (lgkmcnt only). Through the generic pointers of DevProblem it is a flat load, whose wait also
+// drains every outstanding global load and store of the wave: in the rollouts that exposed a full
+// memory round trip per row and knot (k_ls_spec at B = 1: 6 µs per knot).
+template <class T>
+using cptr = const T __attribute__((address_space(4)))*;
+template <class T>
+__device__ __forceinline__ cptr<T> as_const(const T* p) {
+  return (cptr<T>)p;
+}
+__device__ __forceinline__ cptr<ConRow> knot_rows(const DevProblem* P, int k) {
+  return as_const(P->rows) + as_const(P->knot_off)[k];
+}
+__device__ __forceinline__ int knot_count(const DevProblem* P, int k) { return as_const(P->knot_cnt)[k]; }
+// a row read through either pointer kind (member-wise for the constant address space: the implicit
+// copy constructor takes a generic reference)
+__device__ __forceinline__ ConRow load_row(cptr<ConRow> p) {
+  ConRow r;
+  r.type = p->type;
+  r.idx = p->idx;
+  r.a = p->a;
+  r.b = p->b;
+  r.c = p->c;
+  r.r = p->r;
+  return r;
+}
+__device__ __forceinline__ ConRow load_row(const ConRow* p) { return *p; }
+
 // Per-trajectory solver state (the scalar fields of iLQRSolver/AugmentedLagrangianSolver and
 // their stats dicts, ilqr_solver.jl:93-154, augmented_lagrangian_solver.jl:101-140).
 struct TrajState {
@@ -128,7 +157,9 @@ struct DevBuffers {
   int bwd_shmem;      // k_bwd_team: dynamic LDS bytes per block of the launch
   int bwd_stride2[2]; // [std, sqrt] strides
   int bwd_shmem2[2];  // [std, sqrt] LDS bytes
-  int rows_shmem;     // LDS bytes of a block's copy of the row tables (rollout kernels)
+  int spec_tail_shmem; // LDS bytes of k_ls_spec_tail's chunk image (0: the tail uses k_ls_spec)
+  int cost_diag;       // DevProblem::diag_cost (host copy: kernel variants that inline the diagonal cost)
+  int rows_lds;        // LDS bytes of a block's copy of the row tables (bulk k_ls_spec; 0: global tables)
   int ls_first;       // width of the first speculative round (>= nc: one round)
   int nknots;         // N (host-side launch geometry)
   int ls_pend_ok;     // solve steps may carry an undecided line search over to the next step
@@ -1053,10 +1084,13 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
 // ---------------------------------------------------------------------------------------------
 // Costs (src/cost.jl:171-181), same association as the oracle. The outer loops are kept rolled:
 // fully unrolled, the compiler hoists all of Q into registers across the knot loop and spills.
-template <int n, int m>
+// DC: 0 = the cost's structure from P->diag_cost at run time; 1 = diagonal (the caller knows
+// P->diag_cost != 0); 2 = dense. A kernel that inlines only the diagonal form keeps x and u in registers
+// (the dense loops index them at run time).
+template <int n, int m, int DC = 0>
 __device__ __forceinline__ double stage_cost_dt(const DevProblem* P, const double* x, const double* u, double dt) {
   double xQx = 0.0, uRu = 0.0, qx = 0.0, ru = 0.0, uHx = 0.0;
-  if (P->diag_cost) {
+  if (DC == 1 || (DC == 0 && P->diag_cost)) {
 #pragma unroll
     for (int j = 0; j < n; j++) xQx = fma((0.5 * x[j]) * P->Q[j + n * j], x[j], xQx);
 #pragma unroll
@@ -1087,15 +1121,15 @@ __device__ __forceinline__ double stage_cost_dt(const DevProblem* P, const doubl
   for (int i = 0; i < m; i++) ru = fma(P->r[i], u[i], ru);
   return ((((xQx + uRu) + qx) + ru) + P->c + uHx) * dt;
 }
-template <int n, int m>
+template <int n, int m, int DC = 0>
 __device__ __forceinline__ double stage_cost(const DevProblem* P, const double* x, const double* u) {
-  return stage_cost_dt<n, m>(P, x, u, P->dt);
+  return stage_cost_dt<n, m, DC>(P, x, u, P->dt);
 }
 
-template <int n>
+template <int n, int DC = 0>
 __device__ __forceinline__ double terminal_cost(const DevProblem* P, const double* x) {
   double xQx = 0.0, qx = 0.0;
-  if (P->diag_cost) {
+  if (DC == 1 || (DC == 0 && P->diag_cost)) {
 #pragma unroll
     for (int j = 0; j < n; j++) xQx = fma((0.5 * x[j]) * P->Qf[j + n * j], x[j], xQx);
   } else {
@@ -1114,33 +1148,63 @@ __device__ __forceinline__ double terminal_cost(const DevProblem* P, const doubl
 // stage / terminal cost of model M: MinTimeCost for a minimum-time model (minimum_time.jl:148-149:
 // stage_cost(cost, x[1:n], u[1:m], h) + R_min_time u[end]^2 with dt = h = u[end]^2, terminal unchanged;
 // the zero-padded base matrices give the base cost of the leading parts bit for bit)
-template <class M>
+template <class M, int DC = 0>
 __device__ __forceinline__ double stage_cost_m(const DevProblem* P, const double* x, const double* u) {
   if constexpr (ModelTraits<M>::min_time) {
     const double h = u[M::m - 1];
-    return stage_cost_dt<M::n, M::m>(P, x, u, h * h) + P->R_min_time * (h * h);
+    return stage_cost_dt<M::n, M::m, DC>(P, x, u, h * h) + P->R_min_time * (h * h);
   } else {
-    return stage_cost<M::n, M::m>(P, x, u);
+    return stage_cost<M::n, M::m, DC>(P, x, u);
   }
 }
-template <class M>
+template <class M, int DC = 0>
 __device__ __forceinline__ double terminal_cost_m(const DevProblem* P, const double* x) {
-  return terminal_cost<M::n>(P, x);
+  return terminal_cost<M::n, DC>(P, x);
 }
 
 // constraint row value (u == nullptr at the terminal knot: only x rows exist there)
+// v[i] for a wave-uniform i in [0, NN) without an indexed register read: a chain of selects over
+// constant indices, so v stays in registers. An indexed read (s_set_gpr_idx) may read any register, so
+// the wait inserted before it drains every outstanding global load of the wave; in the rollouts, which
+// keep loads in flight across knots, that exposed a memory round trip per row.
+// (The empty asm makes each candidate an opaque value: without it the optimiser folds the chain of
+// selects over loads into one load from a selected address, and the array goes to scratch memory.)
+template <int NN>
+__device__ __forceinline__ double reg_at(const double* v, int i) {
+  double r = v[0];
+#pragma unroll
+  for (int j = 1; j < NN; j++) {
+    double t = v[j];
+    asm volatile("" : "+v"(t));
+    r = (i == j) ? t : r;
+  }
+  return r;
+}
+// x[i] / u[i] of a row: an indexed register move (IDX = 0: the backward kernels, which hold no loads in
+// flight there), or reg_at over the model's n / m (IDX = n, m: the rollouts)
+template <int NX, int NU>
+struct RowAt {
+  __device__ __forceinline__ static double x(const double* x, int i) {
+    if constexpr (NX > 0) return reg_at<NX>(x, i); else return x[i];
+  }
+  __device__ __forceinline__ static double u(const double* u, int i) {
+    if constexpr (NU > 0) return reg_at<NU>(u, i); else return u[i];
+  }
+};
+
 // SLACK = false compiles the infeasible-start slack row out (plain models never have it; the extra
 // case costs the team backward kernel registers)
-template <bool SLACK = true>
+template <bool SLACK = true, int NX = 0, int NU = 0>
 __device__ __forceinline__ double row_value(const ConRow& r, const double* x, const double* u) {
-  if (SLACK && r.type == ROW_USLACK) return u[r.idx];
-  if (r.type == ROW_MT_EQ) return u[(int)r.a] - x[r.idx];
+  using A = RowAt<NX, NU>;
+  if (SLACK && r.type == ROW_USLACK) return A::u(u, r.idx);
+  if (r.type == ROW_MT_EQ) return A::u(u, (int)r.a) - A::x(x, r.idx);
   switch (r.type) {
-    case ROW_XMAX: return x[r.idx] - r.a;
-    case ROW_UMAX: return u[r.idx] - r.a;
-    case ROW_XMIN: return r.a - x[r.idx];
-    case ROW_UMIN: return r.a - u[r.idx];
-    case ROW_GOAL: return x[r.idx] - r.a;
+    case ROW_XMAX: return A::x(x, r.idx) - r.a;
+    case ROW_UMAX: return A::u(u, r.idx) - r.a;
+    case ROW_XMIN: return r.a - A::x(x, r.idx);
+    case ROW_UMIN: return r.a - A::u(u, r.idx);
+    case ROW_GOAL: return A::x(x, r.idx) - r.a;
     case ROW_CIRCLE: {
       const double dx = x[0] - r.a, dy = x[1] - r.b;
       return -((dx * dx + dy * dy) - r.r * r.r);
@@ -1159,7 +1223,7 @@ __device__ __forceinline__ bool row_inequality(const ConRow& r) {
 // The same row seen by every lane of a wave (lanes iterate knots and rows in lockstep over the
 // shared row table): make its type and index wave-uniform so that the switch is a scalar branch
 // and x[idx] an indexed register move, not a per-lane chain of compares and selects.
-__device__ __forceinline__ ConRow uniform_row(const ConRow& r) {
+__device__ __forceinline__ ConRow uniform_row(ConRow r) {
   ConRow u = r;
   u.type = __builtin_amdgcn_readfirstlane(r.type);
   u.idx = __builtin_amdgcn_readfirstlane(r.idx);
@@ -1202,7 +1266,7 @@ __device__ __forceinline__ int row_grad(const ConRow& r, const double* x, int n,
 // Rows of a model: the built-in row types, plus the user constraint rows of a plugin model. A user
 // row evaluates the model's con(fid, c, x, u) (u = zeros at the terminal knot) and takes output idx;
 // its gradient over [x; u_base] comes from dual numbers with n + m_base partials (ForwardDiff).
-template <class M>
+template <class M, bool NOIDX = false>
 __device__ __forceinline__ double row_value_m(const ConRow& r, const double* x, const double* u) {
   if constexpr (HasCon<M>::value) {
     if (r.type == ROW_USER_INEQ || r.type == ROW_USER_EQ) {
@@ -1214,7 +1278,7 @@ __device__ __forceinline__ double row_value_m(const ConRow& r, const double* x, 
       return c[r.idx];
     }
   }
-  return row_value<(ModelTraits<M>::slack > 0)>(r, x, u);
+  return row_value<(ModelTraits<M>::slack > 0), NOIDX ? M::n : 0, NOIDX ? M::m : 0>(r, x, u);
 }
 template <class M>
 __host__ __device__ constexpr int row_grad_cap() {

@@ -70,8 +70,8 @@ __host__ __device__ constexpr int nq_of() {
 // AL terms λ'c + ½ c'Iμ c of one knot (augmented_lagrangian_methods.jl:298-313), rows in order. The
 // multipliers are loaded four rows at a time so their global loads overlap instead of serialising
 // one round trip per row. Ck (constraint values out) may be null.
-template <class M>
-__device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const double* lamk, const double* muk,
+template <class M, class RowPtr, bool NOIDX = false>
+__device__ __forceinline__ void al_knot_terms(RowPtr rows, int cnt, const double* lamk, const double* muk,
                                               const double* x, const double* u, double& lc, double& cIc,
                                               double* Ck) {
   for (int base = 0; base < cnt; base += 4) {
@@ -84,8 +84,8 @@ __device__ __forceinline__ void al_knot_terms(const ConRow* rows, int cnt, const
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       if (base + q < cnt) {
-        const ConRow r = uniform_row(rows[base + q]);
-        const double c = row_value_m<M>(r, x, u);
+        const ConRow r = uniform_row(load_row(rows + base + q));
+        const double c = row_value_m<M, NOIDX>(r, x, u);
         const double l = lv[q];
         const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
         const double w = a ? mv[q] : 0.0;
@@ -111,9 +111,9 @@ __device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& 
   const double* lam = Bf.lam + (size_t)b * N * pmax;
   const double* mu = Bf.mu + (size_t)b * N * pmax;
   for (int k = 0; k < N; k++) {
-    const int cnt = P->knot_cnt[k];
+    const int cnt = knot_count(P, k);
     if (cnt == 0) continue;
-    const ConRow* rows = P->rows + P->knot_off[k];
+    const cptr<ConRow> rows = knot_rows(P, k);
     const double* x = Xs + (size_t)k * n;
     const double* u = (k < N - 1) ? Us + (size_t)k * m : nullptr;
     double lc = 0.0, cIc = 0.0;
@@ -198,13 +198,127 @@ __device__ void traj_rollout_open(const DevProblem* __restrict__ P, const DevBuf
   }
 }
 
-// gradient_todorov (ilqr_methods.jl:122-129, A.3) / gradient_feedforward (:135-137)
+// compute_gradient (ilqr_methods.jl:104-116): the entries of vcat(Q[1].x, Q[1].u, ..., Q[N].x) of the plain
+// cost_expansion! (objective.jl:65-68, augmented_lagrangian_methods.jl:231-276 inside AL solves) at the
+// current X, U, in order, passed to visit(value). Same operations as the oracle's expansion_stage /
+// expansion_terminal / oc_cost_expansion(sq = 0); the AL terms use the constraint values of X, U (obj.C
+// after the accepted trajectory's cost evaluation, A.10) and add each row's gradient entries in row order
+// (the oracle's dense loops add exact zeros for the other rows). One lane per trajectory: gradient_type
+// :ℓ2 / :ℓinf only.
+template <class M, class F>
+__device__ void expansion_gradient_entries(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b,
+                                           bool al, F&& visit) {
+  constexpr int n = M::n, m = M::m, W = n + m;
+  constexpr bool MT = ModelTraits<M>::min_time;
+  const int N = P->N, pmax = P->pmax;
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  const double* lam = Bf.lam + (size_t)b * N * pmax;
+  const double* mu = Bf.mu + (size_t)b * N * pmax;
+  for (int k = 0; k < N; k++) {
+    const bool term = (k == N - 1);
+    const double* x = X + (size_t)k * n;
+    const double* u = term ? nullptr : U + (size_t)k * m;
+    double q[W];
+    if (!term) {
+      const double dt = MT ? u[m - 1] * u[m - 1] : P->dt;
+      double gx[n], gu[m];
+      for (int i = 0; i < n; i++) {
+        double a = 0.0, c = 0.0;
+        for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], x[j], a);
+        for (int j = 0; j < m; j++) c = fma(P->H[j + m * i], u[j], c);
+        gx[i] = (a + P->q[i]) + c;
+        q[i] = gx[i] * dt;
+      }
+      for (int i = 0; i < m; i++) {
+        double a = 0.0, c = 0.0;
+        for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], u[j], a);
+        for (int j = 0; j < n; j++) c = fma(P->H[i + m * j], x[j], c);
+        gu[i] = (a + P->r[i]) + c;
+        q[n + i] = gu[i] * dt;
+      }
+      if constexpr (MT) {  // MinTimeCost (minimum_time.jl:155-188): Q.u[end] = τ(2ℓ1 + R), Q.x[end] = R x[end]
+        const double R = P->R_min_time, tau = u[m - 1];
+        const double l1 = stage_cost_dt<n, m>(P, x, u, 1.0);
+        q[n + m - 1] = tau * (2.0 * l1 + R);
+        q[n - 1] = R * x[n - 1];
+      }
+    } else {
+      for (int i = 0; i < n; i++) {
+        double a = 0.0;
+        for (int j = 0; j < n; j++) a = fma(P->Qf[i + n * j], x[j], a);
+        q[i] = a + P->qf[i];
+      }
+      if constexpr (MT) q[n - 1] = P->R_min_time * x[n - 1];
+    }
+    const int p = al ? knot_count(P, k) : 0;
+    if (p > 0) {  // Q.x .+= cx'g ; Q.u .+= cu'g,  g = Iμ c + λ over the active set
+      const cptr<ConRow> rows = knot_rows(P, k);
+      double t[W];
+      for (int i = 0; i < W; i++) t[i] = 0.0;
+      for (int r = 0; r < p; r++) {
+        const ConRow row = load_row(rows + r);
+        const double c = row_value_m<M>(row, x, u);
+        const double l = lam[(size_t)k * pmax + r];
+        const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((c >= 0.0) || (l > 0.0)) : true;
+        const double w = a ? mu[(size_t)k * pmax + r] : 0.0;
+        const double g = w * c + l;
+        int idx[row_grad_cap<M>()];
+        double v[row_grad_cap<M>()];
+        const int nz = row_grad_m<M>(row, x, u, idx, v);
+        for (int z = 0; z < nz; z++)
+          if (!term || idx[z] < n) t[idx[z]] = fma(v[z], g, t[idx[z]]);
+      }
+      for (int i = 0; i < (term ? n : W); i++) q[i] += t[i];
+    }
+    for (int i = 0; i < (term ? n : W); i++) visit(q[i]);
+  }
+}
+
+// gradient_todorov (ilqr_methods.jl:122-129, A.3) / gradient_feedforward (:135-137) / :ℓ2, :ℓinf (:96-99:
+// LinearAlgebra.generic_normInf; for ℓ2 the unscaled sum of squares in index order of generic_norm2, the
+// oracle's jl_norm2 — Julia 1.1 passes these long vectors to BLAS.nrm2, whose accumulation the restatement
+// does not reproduce bit for bit)
 template <class M>
-__device__ double traj_gradient(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b) {
+__device__ double traj_gradient(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, bool al) {
   constexpr int m = M::m;
   const int N = P->N;
   const double* d = Bf.d + (size_t)b * (N - 1) * m;
   const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  if (P->o.gradient_type == 3) {
+    double r = NAN;
+    bool first = true;
+    expansion_gradient_entries<M>(P, Bf, b, al, [&](double g) {
+      const double v = fabs(g);
+      r = first ? v : ((isnan(r) || r > v) ? r : v);
+      first = false;
+    });
+    return r;
+  }
+  if (P->o.gradient_type == 2) {
+    double mx = 0.0;
+    long long len = 0;
+    expansion_gradient_entries<M>(P, Bf, b, al, [&](double g) {
+      mx = tog_jlmax(mx, fabs(g));
+      len++;
+    });
+    if (mx != mx || mx == 0.0 || isinf(mx)) return mx;
+    double s = 0.0;
+    bool first = true;
+    if (isfinite((double)len * mx * mx) && mx * mx != 0.0) {
+      expansion_gradient_entries<M>(P, Bf, b, al, [&](double g) {
+        s = first ? g * g : s + g * g;
+        first = false;
+      });
+      return sqrt(s);
+    }
+    expansion_gradient_entries<M>(P, Bf, b, al, [&](double g) {
+      const double t = fabs(g) / mx;
+      s = first ? t * t : s + t * t;
+      first = false;
+    });
+    return mx * sqrt(s);
+  }
   if (P->o.gradient_type == 1) {
     double g = 0.0;
     for (int k = 0; k < N - 1; k++) {
@@ -234,14 +348,14 @@ __device__ inline double traj_max_violation(const DevProblem* __restrict__ P, co
   const double* C = Bf.C + (size_t)b * N * pmax;
   double c_max = 0.0;
   for (int k = 0; k < N; k++) {
-    const int cnt = P->knot_cnt[k];
+    const int cnt = knot_count(P, k);
     if (cnt == 0) continue;
-    const ConRow* rows = P->rows + P->knot_off[k];
+    const cptr<ConRow> rows = knot_rows(P, k);
     double e = 0.0, im = -INFINITY;
     int ni = 0;
     for (int i = 0; i < cnt; i++) {
       const double c = C[(size_t)k * pmax + i];
-      if (row_inequality(rows[i])) {
+      if (row_inequality(load_row(rows + i))) {
         ni++;
         im = tog_jlmax(im, c);  // maximum(C.inequality): NaN propagates (Julia max)
       } else {
@@ -329,11 +443,11 @@ __global__ void __launch_bounds__(64) k_update_constraints(const DevProblem* __r
   const double* X = Bf.X + (size_t)b * N * n;
   const double* U = Bf.U + (size_t)b * (N - 1) * m;
   for (int k = 0; k < N; k++) {
-    const int cnt = P->knot_cnt[k];
-    const ConRow* rows = P->rows + P->knot_off[k];
+    const int cnt = knot_count(P, k);
+    const cptr<ConRow> rows = knot_rows(P, k);
     for (int i = 0; i < cnt; i++)
       Bf.C[((size_t)b * N + k) * pmax + i] =
-          row_value_m<M>(uniform_row(rows[i]), X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
+          row_value_m<M>(uniform_row(load_row(rows + i)), X + (size_t)k * n, k < N - 1 ? U + (size_t)k * m : nullptr);
   }
 }
 
@@ -1468,35 +1582,59 @@ __device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS tra
 // place into X, U (the accepted step; old X[k] is read before it is overwritten) and return the
 // todorov gradient of the new U (ilqr_methods.jl:122-129). WMODE 3: write the rolled-out trajectory
 // into the candidate slot `cw` (knot-major, n+m doubles per knot: x̄_k then ū_k), for k_ls_apply.
-// Constraint-row tables for the rollouts: the global ones, or a block's LDS copy (block_row_tables).
-struct RowTables {
-  const ConRow* rows;
-  const int* koff;
-  const int* kcnt;
+// Constraint-row tables of the rollouts. Every lane of a rollout kernel is at the same knot, so the row
+// reads are wave-uniform: through the constant address space (global_row_tables) they are scalar loads;
+// a block's LDS copy (block_row_tables, the bulk k_ls_spec: many waves read the same rows every knot)
+// is read through the local address space (ds_read). Either way lgkmcnt only: read through generic
+// pointers they were flat loads, whose waits also drain every outstanding global load and store.
+template <class T>
+using lptr = T __attribute__((address_space(3)))*;
+template <class RP, class IP>
+struct RowTablesT {
+  RP rows;
+  IP koff;
+  IP kcnt;
 };
+using RowTables = RowTablesT<cptr<ConRow>, cptr<int>>;
+using RowTablesL = RowTablesT<lptr<const ConRow>, lptr<const int>>;
 __device__ __forceinline__ RowTables global_row_tables(const DevProblem* P) {
-  return RowTables{P->rows, P->knot_off, P->knot_cnt};
+  return RowTables{as_const(P->rows), as_const(P->knot_off), as_const(P->knot_cnt)};
 }
-// Cooperative copy of the deduplicated row table and per-knot tables into dynamic LDS (all threads
-// of the block must call it). Needs P->nrows * sizeof(ConRow) + 2 * N * sizeof(int) bytes at `lds`.
-__device__ __forceinline__ RowTables block_row_tables(const DevProblem* P, void* lds) {
-  ConRow* rc = reinterpret_cast<ConRow*>(lds);
-  int* ko = reinterpret_cast<int*>(rc + P->nrows);
-  int* kc = ko + P->N;
+__device__ __forceinline__ ConRow load_row(lptr<const ConRow> p) {
+  ConRow r;
+  r.type = p->type;
+  r.idx = p->idx;
+  r.a = p->a;
+  r.b = p->b;
+  r.c = p->c;
+  r.r = p->r;
+  return r;
+}
+// LDS bytes of block_row_tables' copy; 0 when it exceeds the budget (the rollouts then use the global tables)
+__host__ __device__ constexpr int row_tables_bytes(int nrows, int N) {
+  return (int)(sizeof(ConRow) * nrows + sizeof(int) * 2 * N) <= 16 * 1024
+             ? (int)(sizeof(ConRow) * nrows + sizeof(int) * 2 * N)
+             : 0;
+}
+// Cooperative copy of the deduplicated row table and the per-knot tables into dynamic LDS at `lds` (all
+// threads of the block call it).
+__device__ __forceinline__ RowTablesL block_row_tables(const DevProblem* P, double* lds) {
   const double* src = reinterpret_cast<const double*>(P->rows);
-  double* dst = reinterpret_cast<double*>(rc);
-  for (int e = threadIdx.x; e < P->nrows * (int)(sizeof(ConRow) / 8); e += blockDim.x) dst[e] = src[e];
+  for (int e = threadIdx.x; e < P->nrows * (int)(sizeof(ConRow) / 8); e += blockDim.x) lds[e] = src[e];
+  int* ko = reinterpret_cast<int*>(lds + P->nrows * (int)(sizeof(ConRow) / 8));
+  int* kc = ko + P->N;
   for (int e = threadIdx.x; e < P->N; e += blockDim.x) {
     ko[e] = P->knot_off[e];
     kc[e] = P->knot_cnt[e];
   }
   __syncthreads();
-  return RowTables{rc, ko, kc};
+  return RowTablesL{(lptr<const ConRow>)(reinterpret_cast<const ConRow*>(lds)), (lptr<const int>)(ko),
+                    (lptr<const int>)(kc)};
 }
 
-template <class M, int INTEG, int WMODE>
+template <class M, int INTEG, int WMODE, class RT_T = RowTables>
 __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha,
-                             bool al, double& Jout, double* grad_out, const RowTables& RT,
+                             bool al, double& Jout, double* grad_out, const RT_T& RT,
                              double* __restrict__ cw = nullptr, int ncp = 0) {
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
@@ -1535,10 +1673,14 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (al) {
       const int cnt = RT.kcnt[k];
+      if (cnt > 0) {  // unconditional loads (clamped index), so no per-row branch splits the waits
 #pragma unroll
-      for (int q = 0; q < RB; q++) {
-        lp[q] = (q < cnt) ? lam[(size_t)k * pmax + q] : 0.0;
-        mp[q] = (q < cnt) ? mu[(size_t)k * pmax + q] : 0.0;
+        for (int q = 0; q < RB; q++) {
+          const size_t e = (size_t)k * pmax + (q < cnt ? q : 0);
+          const double lv = lam[e], mv = mu[e];
+          lp[q] = (q < cnt) ? lv : 0.0;
+          mp[q] = (q < cnt) ? mv : 0.0;
+        }
       }
     }
   };
@@ -1591,12 +1733,12 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     if (al) {
       const int cnt = RT.kcnt[k - 1];
       if (cnt) {
-        const ConRow* rows = RT.rows + RT.koff[k - 1];
+        const auto rows = RT.rows + RT.koff[k - 1];
         double lc = 0.0, cIc = 0.0;
 #pragma unroll
         for (int q = 0; q < RB; q++) {
           if (q < cnt) {
-            const ConRow r = uniform_row(rows[q]);
+            const ConRow r = uniform_row(load_row(rows + q));
             const double c = row_value_m<M>(r, xb, ub);
             const double l = lk[q];
             const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
@@ -1606,8 +1748,8 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
           }
         }
         if (cnt > RB)
-          al_knot_terms<M>(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB, mu + (size_t)(k - 1) * pmax + RB, xb,
-                        ub, lc, cIc, nullptr);
+          al_knot_terms<M>(rows + RB, cnt - RB, lam + (size_t)(k - 1) * pmax + RB,
+                                               mu + (size_t)(k - 1) * pmax + RB, xb, ub, lc, cIc, nullptr);
         Jc += lc + 0.5 * cIc;
       }
     }
@@ -1640,10 +1782,10 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
   if (al) {
     const int cnt = RT.kcnt[N - 1];
     if (cnt) {
-      const ConRow* rows = RT.rows + RT.koff[N - 1];
+      const auto rows = RT.rows + RT.koff[N - 1];
       double lc = 0.0, cIc = 0.0;
-      al_knot_terms<M>(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax, xb, nullptr, lc, cIc,
-                    nullptr);
+      al_knot_terms<M>(rows, cnt, lam + (size_t)(N - 1) * pmax, mu + (size_t)(N - 1) * pmax,
+                                           xb, nullptr, lc, cIc, nullptr);
       Jc += lc + 0.5 * cIc;
     }
     J = J + Jc;
@@ -1730,13 +1872,13 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
   (void)traj_cost<M>(P, Bf, b, X, U, true, C);  // J = cost(prob): updates C
   double mumax = 0.0;
   for (int k = 0; k < N; k++) {
-    const int cnt = P->knot_cnt[k];
-    const ConRow* rows = P->rows + P->knot_off[k];
+    const int cnt = knot_count(P, k);
+    const cptr<ConRow> rows = knot_rows(P, k);
     for (int i = 0; i < cnt; i++) {
       const size_t q = (size_t)k * pmax + i;
       double l = lam[q] + mu[q] * C[q];  // dual_update! (:107-118)
       l = tog_jlmax(o.dual_min, tog_jlmin(o.dual_max, l));
-      if (row_inequality(rows[i])) l = tog_jlmax(0.0, l);
+      if (row_inequality(load_row(rows + i))) l = tog_jlmax(0.0, l);
       lam[q] = l;
       mu[q] = fmax(0.0, fmin(o.penalty_max, o.penalty_scaling * mu[q]));  // penalty_update! (:121-126)
       mumax = fmax(mumax, mu[q]);
@@ -1770,33 +1912,219 @@ __device__ __forceinline__ bool ls_decided_within(const tog_options& o, const De
 // k_ls_compact (list != nullptr, length *count) — the earlier trials did not settle them. Lanes past
 // the list's end exit at once, so whole waves retire (the step-level path passes its J_prev through
 // Jprev_in).
-template <class M, int INTEG, bool CAND>
+// LRT: the rows are read from the block's LDS copy of the tables (AL mode, tables within
+// row_tables_bytes' budget), else through the constant address space.
+template <class M, int INTEG, bool CAND, bool LRT>
 __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
                                                  int cnt, const int* __restrict__ list, const int* __restrict__ count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nb = list ? (long long)*count : slot_count(Bf, P->B);
-  if ((long long)blockIdx.x * blockDim.x >= nb * cnt) return;  // block past the list: retire before LDS work
+  if ((long long)blockIdx.x * blockDim.x >= nb * cnt) return;  // block past the list: retire at once
   extern __shared__ double spec_lds[];
-  const RowTables RT =
-      (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, spec_lds) : global_row_tables(P);
-  const int NC = Bf.nc;
-  if (t >= nb * cnt) return;
-  const long long i = t / cnt;
-  const long long b = list ? (long long)list[i] : traj_of_slot(Bf, i, P->B);
-  const TrajState& st = Bf.st[b];
-  const int j = lo + st.ls_pend + (int)(t % cnt);  // a pending line search continues after its stored trials
-  if (!st.active || j >= NC) return;
-  double Jj = INFINITY;
-  bool ok;
-  if constexpr (CAND) {  // every trial keeps its rollout: the accepted one is copied, not replayed
-    double* cw = static_cast<double*>(
-        __builtin_assume_aligned(Bf.cand + ((size_t)b * P->N * cand_q<M>() * Bf.ncp + j) * 4, 32));
-    ok = rollout_cost<M, INTEG, 3>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw, Bf.ncp);
+  auto body = [&](const auto& RT) {
+    const int NC = Bf.nc;
+    if (t >= nb * cnt) return;
+    const long long i = t / cnt;
+    const long long b = list ? (long long)list[i] : traj_of_slot(Bf, i, P->B);
+    const TrajState& st = Bf.st[b];
+    const int j = lo + st.ls_pend + (int)(t % cnt);  // a pending line search continues after its stored trials
+    if (!st.active || j >= NC) return;
+    double Jj = INFINITY;
+    bool ok;
+    if constexpr (CAND) {  // every trial keeps its rollout: the accepted one is copied, not replayed
+      double* cw = static_cast<double*>(
+          __builtin_assume_aligned(Bf.cand + ((size_t)b * P->N * cand_q<M>() * Bf.ncp + j) * 4, 32));
+      ok = rollout_cost<M, INTEG, 3>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw, Bf.ncp);
+    } else {
+      ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
+    }
+    Bf.lsJ[b * NC + j] = Jj;
+    Bf.lsok[b * NC + j] = ok ? 1 : 0;
+  };
+  if constexpr (LRT) {
+    body(block_row_tables(P, spec_lds));
   } else {
-    ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
+    body(global_row_tables(P));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_ls_spec_tail: the speculative trials of the convergence tail (few trajectories, every trial in one
+// round, candidate slots). One wave per listed trajectory, lane j = trial j. The trials share the
+// trajectory's per-knot inputs (K_k, ū_k, d_k, λ_k, μ_k and the x_{k+1} of the current iterate), so the
+// wave stages them into LDS a chunk of spec_tail_tc knots at a time: coalesced loads for chunk c+1 are
+// issued into registers when chunk c starts and written to LDS when it ends, and the lanes read the
+// chunk's knots from LDS (broadcast reads). The serial knot loop then never waits on a global load; the
+// per-lane k_ls_spec, whose lanes each prefetch one knot ahead, waited a memory round trip per knot at
+// one trajectory per launch (601 µs for 100 knots). Same operations in the same order as rollout_cost
+// WMODE 3, so the trial costs, flags and candidate rollouts are bit-identical.
+// LDS image of one chunk (doubles, field-major): [K: TC·mn | ū: TC·m | d: TC·m | x: TC·n | λ: TC·p | μ: TC·p].
+__host__ __device__ constexpr int spec_tail_tc(int n, int m) { return (m * n <= 64) ? 16 : 8; }
+__host__ __device__ constexpr int spec_tail_rec(int n, int m, int pmax) { return m * n + 2 * m + n + 2 * pmax; }
+constexpr int SPEC_TAIL_PMAX = 16;  // larger row counts per knot take k_ls_spec
+
+template <class M, int INTEG, int DC>
+__global__ void __launch_bounds__(64) k_ls_spec_tail(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+                                                      int lo, int cnt) {
+  constexpr int n = M::n, m = M::m, MN = m * n;
+  constexpr int TC = spec_tail_tc(n, m);
+  constexpr int SREG = (TC * spec_tail_rec(n, m, SPEC_TAIL_PMAX) + WAVE - 1) / WAVE;  // staged doubles per lane
+  const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
+  if (b < 0) return;
+  const TrajState& st = Bf.st[b];
+  const int j = lo + st.ls_pend + (int)threadIdx.x;
+  if (!st.active || lo + st.ls_pend >= Bf.nc) return;  // (uniform over the block)
+  extern __shared__ double tl[];
+  const int lane = threadIdx.x;
+  const int N = P->N, pmax = P->pmax, NC = Bf.nc;
+  const bool al = (mode == TOG_MODE_AL);
+  const int PL = al ? pmax : 0;  // λ, μ are staged in AL mode only
+  const int OU = TC * MN, OD = OU + TC * m, OX = OD + TC * m, OL = OX + TC * n, OM = OL + TC * PL, TCR = OM + TC * PL;
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  const double* K = Bf.K + (size_t)b * (N - 1) * MN;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  const double* lam = Bf.lam + (size_t)b * N * pmax;
+  const double* mu = Bf.mu + (size_t)b * N * pmax;
+  // element e of chunk image starting at step s0 (steps s = k-1 in [0, N-1)); past the chunk's last step
+  // the address is clamped into the field (the value is never read)
+  auto src = [&](int e, int s0, int ns) -> const double* {
+    auto at = [&](const double* base, int sz, int off) {
+      const int r = e - off;  // element of this field in the chunk
+      return base + (size_t)s0 * sz + (r < ns * sz ? r : 0);
+    };
+    if (e < OU) return at(K, MN, 0);
+    if (e < OD) return at(U, m, OU);
+    if (e < OX) return at(d, m, OD);
+    if (e < OL) return at(X + n, n, OX);  // x_{s+1}: the next knot's x of the current iterate
+    if (e < OM) return at(lam, PL, OL);
+    return at(mu, PL, OM);
+  };
+  double sv[SREG];
+  auto stage_load = [&](int s0) {
+    const int ns = min(TC, N - 1 - s0);
+#pragma unroll
+    for (int i = 0; i < SREG; i++) {
+      const int e = lane + WAVE * i;
+      sv[i] = *src(e < TCR ? e : 0, s0, ns);
+    }
+  };
+  auto stage_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < SREG; i++) {
+      const int e = lane + WAVE * i;
+      if (e < TCR) tl[e] = sv[i];
+    }
+  };
+  // the terminal knot's λ, μ (AL mode) sit after the chunk image: [λ_N: p | μ_N: p], loaded with chunk 0
+  double tv = 0.0;
+  if (al) {
+    const int e = lane < 2 * PL ? lane : 0;
+    tv = (e < PL) ? lam[(size_t)(N - 1) * pmax + e] : mu[(size_t)(N - 1) * pmax + (e - PL)];
+  }
+  const bool on = (lane < cnt) && (j < NC);
+  double* cw = on ? static_cast<double*>(__builtin_assume_aligned(
+                        Bf.cand + ((size_t)b * N * cand_q<M>() * Bf.ncp + j) * 4, 32))
+                  : nullptr;
+  const int ncp = Bf.ncp;
+  const double alpha = ldexp(1.0, -j);
+  const double smax = P->o.max_state_value, umax = P->o.max_control_value;
+  const RowTables RT = global_row_tables(P);
+  double xb[n], xold[n], ub[m], xn[n];
+  double J = 0.0, Jc = 0.0;
+  bool live = on;
+#pragma unroll
+  for (int i = 0; i < n; i++) {
+    xb[i] = Bf.x0[(size_t)b * n + i];
+    xold[i] = X[i];
+  }
+  stage_load(0);
+#pragma unroll 1
+  for (int s0 = 0; s0 < N - 1; s0 += TC) {
+    if (s0 == 0 && lane < 2 * PL) tl[TCR + lane] = tv;
+    stage_store();  // chunk s0 (its loads were issued a chunk ago)
+    wsync();
+    const int ns = min(TC, N - 1 - s0);
+    if (s0 + TC < N - 1) stage_load(s0 + TC);
+    if (live) {
+#pragma unroll 1
+      for (int c = 0; c < ns; c++) {
+        const int k = s0 + c + 1;  // produces knot k from knot k-1
+        const double* Kk = tl + c * MN;
+#pragma unroll
+        for (int i = 0; i < m; i++) {
+          double t = 0.0;
+#pragma unroll
+          for (int jj = 0; jj < n; jj++) t = fma(Kk[i + m * jj], xb[jj] - xold[jj], t);
+          ub[i] = (tl[OU + c * m + i] + t) + alpha * tl[OD + c * m + i];
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) __builtin_nontemporal_store(ub[i], cw + cand_at(k - 1, i, cand_q<M>(), ncp));
+        J += stage_cost_m<M, DC>(P, xb, ub);
+        if (al) {
+          const int pc = RT.kcnt[k - 1];
+          if (pc) {
+            const auto rows = RT.rows + RT.koff[k - 1];
+            double lc = 0.0, cIc = 0.0;
+            for (int q = 0; q < pc; q++) {
+              const ConRow r = uniform_row(load_row(rows + q));
+              const double cv = row_value_m<M, true>(r, xb, ub);
+              const double l = tl[OL + c * PL + q];
+              const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((cv >= 0.0) || (l > 0.0)) : true;
+              const double w = a ? tl[OM + c * PL + q] : 0.0;
+              lc = fma(l, cv, lc);
+              cIc = fma(cv * w, cv, cIc);
+            }
+            Jc += lc + 0.5 * cIc;
+          }
+        }
+        discrete_step<M, INTEG>(xn, xb, ub, P->dt);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          xb[i] = xn[i];
+          ok = ok && (fabs(xn[i]) < smax);
+        }
+#pragma unroll
+        for (int i = 0; i < m; i++) ok = ok && (fabs(ub[i]) < umax);
+#pragma unroll
+        for (int i = 0; i < n; i++) xold[i] = tl[OX + c * n + i];
+#pragma unroll
+        for (int i = 0; i < n; i++) __builtin_nontemporal_store(xn[i], cw + cand_at(k, m + i, cand_q<M>(), ncp));
+        if (!ok) {
+          live = false;
+          break;
+        }
+      }
+    }
+    wsync();  // every lane is done with the chunk before the next one overwrites it
+  }
+  if (!on) return;
+  double Jj = INFINITY;
+  if (live) {
+    J += terminal_cost_m<M, DC>(P, xb);
+    if (al) {  // terminal rows (al_knot_terms' order), multipliers from LDS
+      const int pc = RT.kcnt[N - 1];
+      if (pc) {
+        const cptr<ConRow> rows = RT.rows + RT.koff[N - 1];
+        double lc = 0.0, cIc = 0.0;
+        for (int q = 0; q < pc; q++) {
+          const ConRow r = uniform_row(load_row(rows + q));
+          const double cv = row_value_m<M, true>(r, xb, nullptr);
+          const double l = tl[TCR + q];
+          const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((cv >= 0.0) || (l > 0.0)) : true;
+          const double w = a ? tl[TCR + PL + q] : 0.0;
+          lc = fma(l, cv, lc);
+          cIc = fma(cv * w, cv, cIc);
+        }
+        Jc += lc + 0.5 * cIc;
+      }
+      J = J + Jc;
+    }
+    Jj = J;
   }
   Bf.lsJ[b * NC + j] = Jj;
-  Bf.lsok[b * NC + j] = ok ? 1 : 0;
+  Bf.lsok[b * NC + j] = live ? 1 : 0;
 }
 
 // After trials [0, hi): list the active trajectories the acceptance logic has not settled yet
@@ -1839,12 +2167,10 @@ template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
                                                   int bookkeeping, const double* Jprev_in, double* Jout, int phase,
                                                   int hi, const int* __restrict__ list, const int* __restrict__ count) {
-  extern __shared__ double commit_lds[];
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nb = (phase == 2) ? (long long)*count : slot_count(Bf, P->B);
   if ((long long)blockIdx.x * blockDim.x >= nb) return;  // whole block past the list: retire early
-  const RowTables RT =
-      (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, commit_lds) : global_row_tables(P);
+  const RowTables RT = global_row_tables(P);
   if (t >= nb) return;
   const long long b = (phase == 2) ? (long long)list[t] : traj_of_slot(Bf, t, P->B);
   if (!Bf.st[b].active) return;
@@ -1902,7 +2228,7 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
     alpha_last = 0.0;
     reg_increase(P, s);
     s.rho += o.bp_reg_fp;
-    grad = traj_gradient<M>(P, Bf, b);
+    grad = traj_gradient<M>(P, Bf, b, al);
     copied = true;
   } else if (!bookkeeping) {
     double Jw;
@@ -1912,6 +2238,8 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
     rollout_cost<M, INTEG, 2>(P, Bf, b, alpha_last, al, Jw, &grad, RT);  // X, U <- X̄, Ū in place
     copied = true;
   }
+  // the rollout sums the todorov terms; the other gradient types need the new X, U (or d) whole
+  if (bookkeeping && copied && state != 2 && o.gradient_type != 0) grad = traj_gradient<M>(P, Bf, b, al);
   s.alpha = alpha_last;
   s.z = z;
   s.expected = expected;
@@ -2067,10 +2395,8 @@ __global__ void __launch_bounds__(256) k_ls_apply(const DevProblem* __restrict__
 template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
                                                 int bookkeeping, const double* Jprev_in, double* Jout) {
-  extern __shared__ double book_lds[];
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const RowTables RT =
-      (mode == TOG_MODE_AL && Bf.rows_shmem > 0) ? block_row_tables(P, book_lds) : global_row_tables(P);
+  const RowTables RT = global_row_tables(P);
   if (t >= slot_count(Bf, P->B)) return;
   const long long b = traj_of_slot(Bf, t, P->B);
   if (!Bf.st[b].active) return;
@@ -2097,7 +2423,7 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
     J = traj_cost<M>(P, Bf, b, X, U, al, al ? Bf.C + (size_t)b * N * P->pmax : nullptr);
     reg_increase(P, s);
     s.rho += o.bp_reg_fp;
-    grad = traj_gradient<M>(P, Bf, b);
+    grad = traj_gradient<M>(P, Bf, b, al);
     copied = true;
   } else if (win == -3) {
     double Jw;
@@ -2114,6 +2440,8 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
     grad = gsum / N;
     copied = true;
   }
+  // apply summed the todorov terms; the other gradient types need the new X, U (or d) whole
+  if (bookkeeping && copied && win != -2 && o.gradient_type != 0) grad = traj_gradient<M>(P, Bf, b, al);
   if (J > J_prev) s.flags |= TOG_TRAJ_COST_INCREASED;
   if (Jout) Jout[b] = J;
   (void)copied;
@@ -2158,13 +2486,13 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
     const double* x = X + (size_t)k * n;
     const double* u = (k < N - 1) ? U + (size_t)k * m : nullptr;
     sk[k] = (k < N - 1) ? stage_cost_m<M>(P, x, u) : terminal_cost_m<M>(P, x);
-    const int cnt = P->knot_cnt[k];
-    const ConRow* rows = P->rows + P->knot_off[k];
+    const int cnt = knot_count(P, k);
+    const cptr<ConRow> rows = knot_rows(P, k);
     double lc = 0.0, cIc = 0.0, e = 0.0, im = -INFINITY;
     int ni = 0;
     for (int i = 0; i < cnt; i++) {
       const size_t q = (size_t)k * pmax + i;
-      const ConRow r = rows[i];
+      const ConRow r = load_row(rows + i);
       const double c = row_value_m<M>(r, x, u);
       C[q] = c;
       const bool ineq = row_inequality<SL>(r);
@@ -2601,13 +2929,31 @@ struct ModelLaunch {
   template <int INTEG>
   static void spec(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int lo, int cnt, const int* list,
                    const int* count, hipStream_t st) {
+    if (Bf.tail && Bf.cand && Bf.spec_tail_shmem > 0 && !list && cnt <= WAVE) {  // one wave per trajectory
+      if (Bf.cost_diag)
+        hipLaunchKernelGGL((k_ls_spec_tail<M, INTEG, 1>), dim3((unsigned)B), dim3(WAVE), (unsigned)Bf.spec_tail_shmem,
+                           st, P, Bf, mode, lo, cnt);
+      else
+        hipLaunchKernelGGL((k_ls_spec_tail<M, INTEG, 0>), dim3((unsigned)B), dim3(WAVE), (unsigned)Bf.spec_tail_shmem,
+                           st, P, Bf, mode, lo, cnt);
+      return;
+    }
     const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
-    if (Bf.cand)
-      hipLaunchKernelGGL((k_ls_spec<M, INTEG, true>), dim3(gs), dim3(256), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
-                         lo, cnt, list, count);
-    else
-      hipLaunchKernelGGL((k_ls_spec<M, INTEG, false>), dim3(gs), dim3(256), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
-                         lo, cnt, list, count);
+    const unsigned rb = (mode == TOG_MODE_AL) ? (unsigned)Bf.rows_lds : 0u;
+    auto launch = [&](auto cand_c, auto lrt_c) {
+      constexpr bool CAND = decltype(cand_c)::value, LRT = decltype(lrt_c)::value;
+      hipLaunchKernelGGL((k_ls_spec<M, INTEG, CAND, LRT>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode, lo,
+                         cnt, list, count);
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (Bf.cand) {
+      if (rb) launch(T_{}, T_{});
+      else launch(T_{}, F_{});
+    } else {
+      if (rb) launch(F_{}, T_{});
+      else launch(F_{}, F_{});
+    }
   }
   // candidate-copy line search: one or two speculative rounds, each followed by its decisions, then the
   // copy of the accepted rollouts and the bookkeeping (no replay rollout on the critical path)
@@ -2636,7 +2982,7 @@ struct ModelLaunch {
     }
     const long long tot = B * (long long)Bf.nknots * cand_q<M>();
     hipLaunchKernelGGL((k_ls_apply<M>), dim3(grid(tot, 256)), dim3(256), 0, st, P, Bf, bk);
-    hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
+    hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode,
                        bk, Jp, Jo);
     if (bk && mode == TOG_MODE_AL) {
       const unsigned sm = (unsigned)(Bf.nknots * (2 * sizeof(double) + sizeof(int)));
@@ -2647,7 +2993,7 @@ struct ModelLaunch {
   template <int INTEG>
   static void commit(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
                      double* Jo, int phase, int hi, const int* list, const int* count, hipStream_t st) {
-    hipLaunchKernelGGL((k_ls_commit<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_shmem, st, P, Bf, mode,
+    hipLaunchKernelGGL((k_ls_commit<M, INTEG>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode,
                        bk, Jp, Jo, phase, hi, list, count);
   }
   template <int INTEG>

@@ -667,6 +667,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     for (int i = 0; pz && i < m * n; i++)
       if (std::signbit(P.H[i])) pz = false;
     P.diag_cost = diag ? (pz ? 2 : 1) : 0;
+    h->buf.cost_diag = P.diag_cost;
     if (opts->square_root && !ok) {
       return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
     }
@@ -697,14 +698,20 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     h->bwd_team = (!force_lds && !ops->min_time &&
                    team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
                       ? 1 : 0;
-    h->buf.rows_shmem = (int)(sizeof(ConRow) * rows.size() + sizeof(int) * 2 * (size_t)N);
-    if (h->buf.rows_shmem > 32 * 1024) h->buf.rows_shmem = 0;  // rollouts then read the global tables
     for (int sq = 0; sq < 2; sq++) {
       h->buf.bwd_stride2[sq] = ops->team_stride(h->pmax, sq);
       h->buf.bwd_shmem2[sq] = (int)bwd_team_shmem(h->buf.bwd_stride2[sq], ops->team_tpw, (int)rows.size(), N);
       if (h->buf.bwd_shmem2[sq] > 64 * 1024) h->bwd_team = 0;
     }
   }
+  // bulk k_ls_spec: a block's LDS copy of the row tables (TOG_SPEC_RT=global: the constant-space reads)
+  h->buf.rows_lds = getenv("TOG_SPEC_RT") && strcmp(getenv("TOG_SPEC_RT"), "global") == 0
+                        ? 0
+                        : row_tables_bytes((int)rows.size(), N);
+  // k_ls_spec_tail (tail rollouts staged through LDS): admissible up to SPEC_TAIL_PMAX rows per knot
+  h->buf.spec_tail_shmem = (h->pmax <= SPEC_TAIL_PMAX && !getenv("TOG_NO_SPEC_TAIL"))
+                               ? (int)(sizeof(double) * (spec_tail_tc(n, m) * spec_tail_rec(n, m, h->pmax) + 2 * h->pmax))
+                               : 0;
   P.knot_off = h->d_knot_off;
   P.knot_cnt = h->d_knot_cnt;
   P.knot_nx = h->d_knot_nx;
@@ -783,6 +790,8 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   if (!d || !opts || !out) return fail(TOG_ERR_ARG, "null argument");
   *out = nullptr;
   if (d->flags & ~(int32_t)(TOG_PROB_INFEASIBLE | TOG_PROB_MIN_TIME)) return fail(TOG_ERR_ARG, "unknown problem flags");
+  if (opts->gradient_type < 0 || opts->gradient_type > 3)
+    return fail(TOG_ERR_ARG, "gradient_type must be 0 (:todorov), 1 (:feedforward), 2 (:ℓ2) or 3 (:ℓinf)");
   if ((d->flags & TOG_PROB_MIN_TIME) && opts->square_root)
     return fail(TOG_ERR_UNSUPPORTED, "minimum time: MinTimeCost has no square-root expansion (std backward pass)");
   const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0, (d->flags & TOG_PROB_MIN_TIME) != 0,

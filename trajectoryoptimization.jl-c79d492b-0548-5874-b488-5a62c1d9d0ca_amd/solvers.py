@@ -24,6 +24,10 @@ from .problem import infeasible_problem
 
 # ----------------------------------------------------------------------------- options
 
+# gradient_type symbols (ilqr_solver.jl:20) -> tog_options.gradient_type; the ASCII spellings are accepted too
+GRADIENT_TYPES = {"todorov": 0, "feedforward": 1, "ℓ2": 2, "l2": 2, "ℓinf": 3, "linf": 3}
+
+
 @dataclass
 class iLQRSolverOptions:
     """src/solvers/ilqr/ilqr_solver.jl:7-81 (defaults identical)."""
@@ -160,9 +164,10 @@ def to_tog_options(opts) -> abi.tog_options:
     if il.bp_reg_type not in ("control", "state"):
         raise ValueError("bp_reg_type must be :control or :state")
     o.bp_reg_type = 0 if il.bp_reg_type == "control" else 1
-    if il.gradient_type not in ("todorov", "feedforward"):
-        raise NotImplementedError("gradient_type :ℓ2/:ℓinf are not built")
-    o.gradient_type = 0 if il.gradient_type == "todorov" else 1
+    # calculate_gradient (ilqr_methods.jl:91-102): :todorov, :feedforward, :ℓ2, :ℓinf
+    if il.gradient_type not in GRADIENT_TYPES:
+        raise ValueError(f"gradient_type must be one of {sorted(GRADIENT_TYPES)}")
+    o.gradient_type = GRADIENT_TYPES[il.gradient_type]
     o.iterations_linesearch = int(il.iterations_linesearch)
     o.line_search_lower_bound = il.line_search_lower_bound
     o.line_search_upper_bound = il.line_search_upper_bound
