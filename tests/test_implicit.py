@@ -55,8 +55,10 @@ def test_discretize_model_schemes(tog):
     assert tog.rk3_implicit(tog.Dynamics.cartpole).integration == tog.abi.RK3_IMPLICIT
     with pytest.raises(ValueError):
         tog.discretize_model(tog.Dynamics.pendulum, "bogus")
-    with pytest.raises(NotImplementedError):  # the device instantiates the Newton step for n <= 4
-        tog.discretize_model(tog.Dynamics.quadrotor, "midpoint_implicit")
+    # the device instantiates the Newton step for n <= 4 and the quadrotor (not the Kuka arm)
+    assert tog.discretize_model(tog.Dynamics.quadrotor, "midpoint_implicit").integration == tog.abi.MIDPOINT_IMPLICIT
+    with pytest.raises(NotImplementedError):
+        tog.discretize_model(tog.Dynamics.kuka, "midpoint_implicit")
 
 
 @pytest.mark.parametrize("scheme", SCHEMES)
@@ -147,7 +149,7 @@ def test_oracle_reference_pendulum_schemes(tog, oracle, scheme):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scheme", SCHEMES)
-@pytest.mark.parametrize("name", ["pendulum", "cartpole", "car", "doubleintegrator"])
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "car", "doubleintegrator", "quadrotor"])
 def test_gpu_implicit_jacobian_parity(tog, oracle, gpu, scheme, name):
     """k_jacobian through the device Newton step vs the oracle's dual restatement, bit for bit."""
     model = getattr(tog.Dynamics, name)
@@ -159,6 +161,9 @@ def test_gpu_implicit_jacobian_parity(tog, oracle, gpu, scheme, name):
     prob = tog.Problem(md, obj, 0.4 * rng.standard_normal((B, N - 1, m)), x0=0.3 * rng.standard_normal((B, n)), N=N,
                        dt=0.08)
     prob._X[...] = 0.5 * rng.standard_normal(prob._X.shape)
+    if name == "quadrotor":  # unit quaternions, controls about hover
+        prob._X[..., 3:7] = [1.0, 0.0, 0.0, 0.0]
+        prob._U[...] += 0.5 * 9.81 / 4
     solver = tog.iLQRSolver(prob, tog.iLQRSolverOptions())
     tog.jacobian_b(prob, solver)
     A = solver.handle.get(tog.abi.FIELD_A)
@@ -188,9 +193,40 @@ def test_gpu_implicit_pendulum_solve(tog, oracle, gpu, scheme):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scheme", SCHEMES)
+def test_gpu_implicit_quadrotor_solve(tog, oracle, gpu, scheme):
+    """The quadrotor (n = 13) under the implicit schemes: a short AL-iLQR solve (u bounds + goal, std
+    backward pass) on the device equals the oracle's, iterations included."""
+    base = tog.Problems.quadrotor_test("goal+bounds")
+    N = 21
+    xf = base.xf.copy()
+    xf[0:3] = [0.0, 2.0, 0.0]
+    n, m = 13, 4
+    cons = tog.Constraints(N)
+    bnd = tog.BoundConstraint(n, m, u_min=0.0, u_max=15.0)
+    for k in range(N - 1):
+        cons[k] += bnd
+    cons[N - 1] += tog.goal_constraint(xf)
+    obj = tog.LQRObjective(1e-2 * np.eye(n), 1e-2 * np.eye(m), 100.0 * np.eye(n), xf, N)
+    rng = np.random.default_rng(9)
+    U0 = 0.5 * 9.81 / 4 + 0.1 * rng.standard_normal((2, N - 1, m))
+    prob = tog.Problem(tog.discretize_model(tog.Dynamics.quadrotor, scheme), obj, U0, constraints=cons,
+                       x0=np.tile(base.x0[0], (2, 1)), xf=xf, N=N, dt=0.05)
+    opts = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(iterations=40), iterations=5,
+                                                constraint_tolerance=1e-3)
+    gp = prob.copy()
+    solver = tog.solve_b(gp, opts)
+    for b in range(prob.B):
+        o = oracle.OracleSolver(prob, opts, b=b)
+        steps = o.solve()
+        assert rel(gp._X[b], o.get("X")) < TOL_STEP and rel(gp._U[b], o.get("U")) < TOL_STEP, b
+        assert steps == solver.stats["iterations_total"][b]
+
+
+@pytest.mark.gpu
 def test_gpu_implicit_unsupported_model(tog, gpu):
     """tog_create rejects an implicit scheme on a model it is not instantiated for."""
-    prob = tog.Problems.pendulum("rk3")
-    prob.model = tog.Model(tog.abi.MODEL_QUADROTOR, 13, 4, "quadrotor", tog.abi.MIDPOINT_IMPLICIT)
+    prob = tog.Problems.kuka(N=5)
+    prob.model = tog.Model(tog.abi.MODEL_KUKA, 14, 7, "kuka", tog.abi.MIDPOINT_IMPLICIT)
     with pytest.raises(Exception):
         tog.iLQRSolver(prob, tog.iLQRSolverOptions())

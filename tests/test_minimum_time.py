@@ -128,3 +128,40 @@ def test_gpu_min_time_jacobian(tog, oracle, gpu):
     assert np.allclose(A, Ao, rtol=1e-13, atol=1e-15)
     assert np.allclose(B, Bo, rtol=1e-13, atol=1e-15)
     assert np.all(B[:, 3, 2] == 1.0) and np.all(A[:, 3, :] == 0.0)  # τ+ = h
+
+
+# minimum_time_problem on the remaining built-in models (the reference asserts only that the problem has
+# bounds, minimum_time.jl:2-8; its minimum-time tests cover the pendulum and the car, above). The device
+# is held to the oracle: equal iteration counts, X and U to the north-star bar. The Kuka case runs a short
+# horizon with control bounds added (its notebook problem has only the goal constraint).
+def _mt_model_case(tog, name):
+    al_opts = dict(opts_uncon=tog.iLQRSolverOptions(iterations=60), iterations=6, penalty_scaling=10.0)
+    if name == "quadrotor":
+        p = tog.Problems.quadrotor_test("goal+bounds")
+        return tog.minimum_time_problem(p, 5.0, 0.1, 1e-3), tog.AugmentedLagrangianSolverOptions(**al_opts)
+    if name == "cartpole":
+        p = tog.Problems.cartpole(constrained=True)
+        return tog.minimum_time_problem(p, 10.0, 0.1, 1e-3), tog.AugmentedLagrangianSolverOptions(**al_opts)
+    n, m, N = 14, 7, 11
+    base = tog.Problems.kuka(N=N, tf=0.5)
+    cons = tog.Constraints(N)
+    bnd = tog.BoundConstraint(n, m, u_min=-80.0, u_max=80.0)
+    for k in range(N - 1):
+        cons[k] += bnd
+    cons[N - 1] += tog.goal_constraint(base.xf)
+    p = tog.Problem(base.model, base.obj, base._U[0], constraints=cons, x0=base.x0[0], xf=base.xf, N=N, dt=base.dt)
+    al_opts["opts_uncon"] = tog.iLQRSolverOptions(iterations=25)
+    al_opts["iterations"] = 3
+    return tog.minimum_time_problem(p, 1.0, 0.1, 1e-3), tog.AugmentedLagrangianSolverOptions(**al_opts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["quadrotor", "cartpole", "kuka"])
+def test_gpu_min_time_models_equal_oracle(tog, oracle, gpu, name):
+    """MinTime<M> for the quadrotor, cartpole and Kuka models (add_min_time_controls, minimum_time.jl:83-104):
+    the AL solve of minimum_time_problem on the device (std backward pass, LDS kernel) equals the oracle."""
+    from test_gpu_parity import _solve_and_compare
+
+    pmt, opts = _mt_model_case(tog, name)
+    assert pmt.model.min_time and pmt.model.n == {"quadrotor": 14, "cartpole": 5, "kuka": 15}[name]
+    _solve_and_compare(tog, oracle, pmt, opts)

@@ -1,0 +1,10 @@
+// Kernel instantiation for the minimum-time quadrotor model, add_min_time_controls(model)
+// (src/solvers/altro/minimum_time.jl:83-104): state [x; τ], control [u; h], dt = h² (tog_device.hpp MinTime<M>).
+#include "tog_kernels.hpp"
+
+namespace tog {
+const ModelOps* ops_mt_quadrotor() {
+  static const ModelOps o = ModelLaunch<MinTime<Quadrotor>>::ops();
+  return &o;
+}
+}  // namespace tog

@@ -795,7 +795,7 @@ template <class M>
 struct ModelTraits {
   using Base = M;
   static constexpr int slack = 0;
-  static constexpr bool implicit_ok = M::n <= 4;  // implicit integrators instantiated
+  static constexpr bool implicit_ok = M::n <= 4 || M::id == TOG_MODEL_QUADROTOR;  // implicit integrators instantiated
   static constexpr bool min_time = false;
 };
 template <class Mb>
@@ -820,7 +820,8 @@ struct ModelTraits<Infeasible<Mb>> {
 // when T is a Dual, ∇g is formed at the values (∂f/∂x one Dual<1> column at a time), and
 // δy = (-∇g)\g by partial-pivoting LU. rk3_implicit reproduces the reference's aliasing of
 // fc1 = fc2 = fc3 (one array), so its residual is y - x - dt/6 F - 4/6 dt F - dt/6 F, F = f(Xm).
-// Built for models with n <= 4 (ModelTraits::implicit_ok); the reference's 1000-iteration error
+// Built for models with n <= 4 and the quadrotor (ModelTraits::implicit_ok; at n = 13 the real ∇g
+// and its LU live in scratch, several KB per lane); the reference's 1000-iteration error
 // becomes a NaN state (the rollout then fails as diverged).
 template <int n>
 __host__ __device__ __forceinline__ double jl_norm2(const double* g) {

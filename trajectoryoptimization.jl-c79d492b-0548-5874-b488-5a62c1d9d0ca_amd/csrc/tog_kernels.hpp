@@ -2929,13 +2929,11 @@ struct ModelLaunch {
   template <int INTEG>
   static void spec(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int lo, int cnt, const int* list,
                    const int* count, hipStream_t st) {
-    if (Bf.tail && Bf.cand && Bf.spec_tail_shmem > 0 && !list && cnt <= WAVE) {  // one wave per trajectory
-      if (Bf.cost_diag)
-        hipLaunchKernelGGL((k_ls_spec_tail<M, INTEG, 1>), dim3((unsigned)B), dim3(WAVE), (unsigned)Bf.spec_tail_shmem,
-                           st, P, Bf, mode, lo, cnt);
-      else
-        hipLaunchKernelGGL((k_ls_spec_tail<M, INTEG, 0>), dim3((unsigned)B), dim3(WAVE), (unsigned)Bf.spec_tail_shmem,
-                           st, P, Bf, mode, lo, cnt);
+    // the tail kernel inlines the diagonal cost only (the dense cost's run-time indexing of x, u would put
+    // them in scratch); dense costs take k_ls_spec
+    if (Bf.tail && Bf.cand && Bf.spec_tail_shmem > 0 && Bf.cost_diag && !list && cnt <= WAVE) {
+      hipLaunchKernelGGL((k_ls_spec_tail<M, INTEG, 1>), dim3((unsigned)B), dim3(WAVE), (unsigned)Bf.spec_tail_shmem, st,
+                         P, Bf, mode, lo, cnt);
       return;
     }
     const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early

@@ -36,6 +36,9 @@ const ModelOps* ops_inf_kuka();
 const ModelOps* ops_mt_pendulum();
 const ModelOps* ops_mt_car();
 const ModelOps* ops_mt_double_integrator();
+const ModelOps* ops_mt_quadrotor();
+const ModelOps* ops_mt_cartpole();
+const ModelOps* ops_mt_kuka();
 }  // namespace tog
 
 static thread_local std::string g_err;
@@ -143,6 +146,9 @@ static const ModelOps* ops_for(int model, bool infeasible, bool min_time, const 
       case TOG_MODEL_PENDULUM: return ops_mt_pendulum();
       case TOG_MODEL_CAR: return ops_mt_car();
       case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_mt_double_integrator();
+      case TOG_MODEL_QUADROTOR: return ops_mt_quadrotor();
+      case TOG_MODEL_CARTPOLE: return ops_mt_cartpole();
+      case TOG_MODEL_KUKA: return ops_mt_kuka();
     }
     return nullptr;
   }
@@ -805,7 +811,7 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
       d->integrator != TOG_RK3_IMPLICIT && d->integrator != TOG_MIDPOINT_IMPLICIT)
     return fail(TOG_ERR_UNSUPPORTED, "integrator");
   if ((d->integrator == TOG_RK3_IMPLICIT || d->integrator == TOG_MIDPOINT_IMPLICIT) && !ops->implicit)
-    return fail(TOG_ERR_UNSUPPORTED, "implicit integrators are built for models with n <= 4 (no slack controls)");
+    return fail(TOG_ERR_UNSUPPORTED, "implicit integrators are built for models with n <= 4 and the quadrotor (no slack controls)");
   int ndev = tog_device_count();
   if (device < 0 || device >= ndev) return fail(TOG_ERR_DEVICE, "no such HIP device");
   tog_handle* h = new tog_handle();
