@@ -280,11 +280,9 @@ __device__ void expansion_gradient_entries(const DevProblem* __restrict__ P, con
 // oracle's jl_norm2 — Julia 1.1 passes these long vectors to BLAS.nrm2, whose accumulation the restatement
 // does not reproduce bit for bit)
 template <class M>
-__device__ double traj_gradient(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, bool al) {
-  constexpr int m = M::m;
-  const int N = P->N;
-  const double* d = Bf.d + (size_t)b * (N - 1) * m;
-  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+__device__ __attribute__((noinline)) double traj_gradient_norm(const DevProblem* __restrict__ P,
+                                                               const DevBuffers& Bf, long long b, bool al) {
+  // (not inlined: its arrays would otherwise cost the bookkeeping kernels' common path registers)
   if (P->o.gradient_type == 3) {
     double r = NAN;
     bool first = true;
@@ -319,6 +317,16 @@ __device__ double traj_gradient(const DevProblem* __restrict__ P, const DevBuffe
     });
     return mx * sqrt(s);
   }
+  return 0.0;
+}
+
+template <class M>
+__device__ double traj_gradient(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, bool al) {
+  constexpr int m = M::m;
+  const int N = P->N;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  if (P->o.gradient_type >= 2) return traj_gradient_norm<M>(P, Bf, b, al);
   if (P->o.gradient_type == 1) {
     double g = 0.0;
     for (int k = 0; k < N - 1; k++) {
@@ -1582,54 +1590,51 @@ __device__ __forceinline__ void team_sync() {  // one-wave blocks: order LDS tra
 // place into X, U (the accepted step; old X[k] is read before it is overwritten) and return the
 // todorov gradient of the new U (ilqr_methods.jl:122-129). WMODE 3: write the rolled-out trajectory
 // into the candidate slot `cw` (knot-major, n+m doubles per knot: x̄_k then ū_k), for k_ls_apply.
-// Constraint-row tables of the rollouts. Every lane of a rollout kernel is at the same knot, so the row
-// reads are wave-uniform: through the constant address space (global_row_tables) they are scalar loads;
-// a block's LDS copy (block_row_tables, the bulk k_ls_spec: many waves read the same rows every knot)
-// is read through the local address space (ds_read). Either way lgkmcnt only: read through generic
-// pointers they were flat loads, whose waits also drain every outstanding global load and store.
-template <class T>
-using lptr = T __attribute__((address_space(3)))*;
+// Constraint-row tables of the rollouts: the global ones, or a block's LDS copy (block_row_tables), both
+// through generic pointers (the bulk rollout, k_ls_spec, measured 808 µs this way against 1,030 µs with
+// the copy read through the local address space or the tables through scalar loads: the flat loads'
+// waits cost less there than the serialised per-row LDS / scalar round trips). The tail rollout
+// (k_ls_spec_tail), one wave per trajectory with its inputs staged in LDS, reads the rows through the
+// constant address space (const_row_tables): a flat load's wait would drain its staging loads.
+struct RowTables {
+  const ConRow* rows;
+  const int* koff;
+  const int* kcnt;
+};
+__device__ __forceinline__ RowTables global_row_tables(const DevProblem* P) {
+  return RowTables{P->rows, P->knot_off, P->knot_cnt};
+}
 template <class RP, class IP>
 struct RowTablesT {
   RP rows;
   IP koff;
   IP kcnt;
 };
-using RowTables = RowTablesT<cptr<ConRow>, cptr<int>>;
-using RowTablesL = RowTablesT<lptr<const ConRow>, lptr<const int>>;
-__device__ __forceinline__ RowTables global_row_tables(const DevProblem* P) {
-  return RowTables{as_const(P->rows), as_const(P->knot_off), as_const(P->knot_cnt)};
-}
-__device__ __forceinline__ ConRow load_row(lptr<const ConRow> p) {
-  ConRow r;
-  r.type = p->type;
-  r.idx = p->idx;
-  r.a = p->a;
-  r.b = p->b;
-  r.c = p->c;
-  r.r = p->r;
-  return r;
+using RowTablesC = RowTablesT<cptr<ConRow>, cptr<int>>;
+__device__ __forceinline__ RowTablesC const_row_tables(const DevProblem* P) {
+  return RowTablesC{as_const(P->rows), as_const(P->knot_off), as_const(P->knot_cnt)};
 }
 // LDS bytes of block_row_tables' copy; 0 when it exceeds the budget (the rollouts then use the global tables)
 __host__ __device__ constexpr int row_tables_bytes(int nrows, int N) {
-  return (int)(sizeof(ConRow) * nrows + sizeof(int) * 2 * N) <= 16 * 1024
+  return (int)(sizeof(ConRow) * nrows + sizeof(int) * 2 * N) <= 32 * 1024
              ? (int)(sizeof(ConRow) * nrows + sizeof(int) * 2 * N)
              : 0;
 }
-// Cooperative copy of the deduplicated row table and the per-knot tables into dynamic LDS at `lds` (all
-// threads of the block call it).
-__device__ __forceinline__ RowTablesL block_row_tables(const DevProblem* P, double* lds) {
-  const double* src = reinterpret_cast<const double*>(P->rows);
-  for (int e = threadIdx.x; e < P->nrows * (int)(sizeof(ConRow) / 8); e += blockDim.x) lds[e] = src[e];
-  int* ko = reinterpret_cast<int*>(lds + P->nrows * (int)(sizeof(ConRow) / 8));
+// Cooperative copy of the deduplicated row table and per-knot tables into dynamic LDS (all threads of
+// the block must call it). Needs row_tables_bytes(P->nrows, P->N) bytes at `lds`.
+__device__ __forceinline__ RowTables block_row_tables(const DevProblem* P, void* lds) {
+  ConRow* rc = reinterpret_cast<ConRow*>(lds);
+  int* ko = reinterpret_cast<int*>(rc + P->nrows);
   int* kc = ko + P->N;
+  const double* src = reinterpret_cast<const double*>(P->rows);
+  double* dst = reinterpret_cast<double*>(rc);
+  for (int e = threadIdx.x; e < P->nrows * (int)(sizeof(ConRow) / 8); e += blockDim.x) dst[e] = src[e];
   for (int e = threadIdx.x; e < P->N; e += blockDim.x) {
     ko[e] = P->knot_off[e];
     kc[e] = P->knot_cnt[e];
   }
   __syncthreads();
-  return RowTablesL{(lptr<const ConRow>)(reinterpret_cast<const ConRow*>(lds)), (lptr<const int>)(ko),
-                    (lptr<const int>)(kc)};
+  return RowTables{rc, ko, kc};
 }
 
 template <class M, int INTEG, int WMODE, class RT_T = RowTables>
@@ -1673,14 +1678,10 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (al) {
       const int cnt = RT.kcnt[k];
-      if (cnt > 0) {  // unconditional loads (clamped index), so no per-row branch splits the waits
 #pragma unroll
-        for (int q = 0; q < RB; q++) {
-          const size_t e = (size_t)k * pmax + (q < cnt ? q : 0);
-          const double lv = lam[e], mv = mu[e];
-          lp[q] = (q < cnt) ? lv : 0.0;
-          mp[q] = (q < cnt) ? mv : 0.0;
-        }
+      for (int q = 0; q < RB; q++) {
+        lp[q] = (q < cnt) ? lam[(size_t)k * pmax + q] : 0.0;
+        mp[q] = (q < cnt) ? mu[(size_t)k * pmax + q] : 0.0;
       }
     }
   };
@@ -2029,7 +2030,7 @@ __global__ void __launch_bounds__(64) k_ls_spec_tail(const DevProblem* __restric
   const int ncp = Bf.ncp;
   const double alpha = ldexp(1.0, -j);
   const double smax = P->o.max_state_value, umax = P->o.max_control_value;
-  const RowTables RT = global_row_tables(P);
+  const RowTablesC RT = const_row_tables(P);
   double xb[n], xold[n], ub[m], xn[n];
   double J = 0.0, Jc = 0.0;
   bool live = on;
@@ -2170,7 +2171,9 @@ __global__ void __launch_bounds__(64) k_ls_commit(const DevProblem* __restrict__
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nb = (phase == 2) ? (long long)*count : slot_count(Bf, P->B);
   if ((long long)blockIdx.x * blockDim.x >= nb) return;  // whole block past the list: retire early
-  const RowTables RT = global_row_tables(P);
+  extern __shared__ double rt_lds[];
+  const RowTables RT =
+      (mode == TOG_MODE_AL && Bf.rows_lds > 0) ? block_row_tables(P, rt_lds) : global_row_tables(P);
   if (t >= nb) return;
   const long long b = (phase == 2) ? (long long)list[t] : traj_of_slot(Bf, t, P->B);
   if (!Bf.st[b].active) return;
@@ -2396,7 +2399,9 @@ template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
                                                 int bookkeeping, const double* Jprev_in, double* Jout) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const RowTables RT = global_row_tables(P);
+  extern __shared__ double rt_lds[];
+  const RowTables RT =
+      (mode == TOG_MODE_AL && Bf.rows_lds > 0) ? block_row_tables(P, rt_lds) : global_row_tables(P);
   if (t >= slot_count(Bf, P->B)) return;
   const long long b = traj_of_slot(Bf, t, P->B);
   if (!Bf.st[b].active) return;
@@ -2980,7 +2985,7 @@ struct ModelLaunch {
     }
     const long long tot = B * (long long)Bf.nknots * cand_q<M>();
     hipLaunchKernelGGL((k_ls_apply<M>), dim3(grid(tot, 256)), dim3(256), 0, st, P, Bf, bk);
-    hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode,
+    hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_lds, st, P, Bf, mode,
                        bk, Jp, Jo);
     if (bk && mode == TOG_MODE_AL) {
       const unsigned sm = (unsigned)(Bf.nknots * (2 * sizeof(double) + sizeof(int)));
@@ -2991,7 +2996,7 @@ struct ModelLaunch {
   template <int INTEG>
   static void commit(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
                      double* Jo, int phase, int hi, const int* list, const int* count, hipStream_t st) {
-    hipLaunchKernelGGL((k_ls_commit<M, INTEG>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf, mode,
+    hipLaunchKernelGGL((k_ls_commit<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_lds, st, P, Bf, mode,
                        bk, Jp, Jo, phase, hi, list, count);
   }
   template <int INTEG>
