@@ -131,7 +131,8 @@ enum tog_problem_flag {
 
 typedef struct tog_constraint {
   int32_t type;       /* tog_constraint_type */
-  int32_t count;      /* number of circles / spheres (ignored for BOUND/GOAL) */
+  int32_t count;      /* circles / spheres: their number; GOAL: rows x[1:count] (0 = n);
+                         BOUND: 0 = trim=true (infinite bounds dropped), 1 = trim=false */
   const double* data; /* see tog_constraint_type */
 } tog_constraint;
 

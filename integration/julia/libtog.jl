@@ -153,10 +153,11 @@ end
 "Rows of one constraint for tog_constraint: (type, count, data)."
 function tog_constraint_spec(con, n::Int, m::Int)
     if con isa BoundConstraint
-        # [x_max; x_min; u_max; u_min], ±Inf entries trimmed by the library (src/constraints.jl:173-181)
-        all(con.active.all) && !all(isfinite, [con.x_max; con.x_min; con.u_max; con.u_min]) &&
-            throw(ArgumentError("BoundConstraint(trim=false) with infinite bounds has no libtog rows"))
-        return TOG_CON_BOUND, Int32(0), Float64[con.x_max; con.x_min; con.u_max; con.u_min]
+        # [x_max; x_min; u_max; u_min]; count 0: ±Inf entries trimmed by the library (trim=true,
+        # src/constraints.jl:173-181), 1: every row kept (trim=false: an untrimmed constraint has every
+        # entry of `active.all` set)
+        untrimmed = all(con.active.all) && !all(isfinite, [con.x_max; con.x_min; con.u_max; con.u_min])
+        return TOG_CON_BOUND, Int32(untrimmed ? 1 : 0), Float64[con.x_max; con.x_min; con.u_max; con.u_min]
     elseif con isa Constraint && haskey(TOG_CONSTRAINTS, con.c)
         return TOG_CONSTRAINTS[con.c]
     elseif con isa Constraint{Equality} && con.label == :goal && hasfield(typeof(con.c), :xf)

@@ -1157,22 +1157,24 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
   oc->type = tc->type;
   switch (tc->type) {
     case TOG_CON_BOUND: {
-      /* src/constraints.jl:155-188, trim=true: active = isfinite.(bound) */
+      /* src/constraints.jl:155-188: trim=true (count 0): active = isfinite.(bound); trim=false (count 1):
+         every row active (an infinite bound then gives c = -Inf, and the AL terms NaN, as in the reference) */
       const double* D = tc->data;
+      const int keep = (tc->count == 1);
       int cx = 0, cu = 0, cxn = 0, cun = 0;
       for (int i = 0; i < n; i++) {
         oc->x_max[i] = D[i];
         oc->x_min[i] = D[n + i];
-        oc->ax_max[i] = isfinite(D[i]);
-        oc->ax_min[i] = isfinite(D[n + i]);
+        oc->ax_max[i] = keep || isfinite(D[i]);
+        oc->ax_min[i] = keep || isfinite(D[n + i]);
         cx += oc->ax_max[i];
         cxn += oc->ax_min[i];
       }
       for (int i = 0; i < m; i++) {
         oc->u_max[i] = D[2 * n + i];
         oc->u_min[i] = D[2 * n + m + i];
-        oc->au_max[i] = isfinite(D[2 * n + i]);
-        oc->au_min[i] = isfinite(D[2 * n + m + i]);
+        oc->au_max[i] = keep || isfinite(D[2 * n + i]);
+        oc->au_min[i] = keep || isfinite(D[2 * n + m + i]);
         cu += oc->au_max[i];
         cun += oc->au_min[i];
       }

@@ -294,10 +294,11 @@ def test_undefined_integration_raises(tog):
     prob = tog.Problems.pendulum()
     with pytest.raises(ValueError):
         tog.Problem(tog.Dynamics.pendulum, prob.obj, integration="bogus", N=prob.N, dt=prob.dt)
-    # the implicit Newton step is instantiated for models with n <= 4 (csrc/tog_device.hpp implicit_step)
+    # the implicit Newton step is instantiated for models with n <= 4 and the quadrotor
+    # (csrc/tog_device.hpp implicit_step), not the Kuka arm
     assert tog.discretize_model(tog.Dynamics.pendulum, "midpoint_implicit").integration == tog.abi.MIDPOINT_IMPLICIT
     with pytest.raises(NotImplementedError):
-        tog.discretize_model(tog.Dynamics.quadrotor, "midpoint_implicit")
+        tog.discretize_model(tog.Dynamics.kuka, "midpoint_implicit")
 
 
 def test_midpoint_jacobian_matches_central_differences(tog, oracle):
@@ -360,3 +361,77 @@ def test_quadrotor_notebook_device(tog, gpu, oracle):
     assert np.abs(gp.X - s.get("X")).max() / max(1.0, np.abs(s.get("X")).max()) < 1e-6
     assert np.abs(gp.U - s.get("U")).max() / max(1.0, np.abs(s.get("U")).max()) < 1e-6
     assert abs(solver.stats["cost"][0] - 18.17292526) / 18.17292526 < 5e-6
+
+
+# Untrimmed bounds (BoundConstraint(trim=false), src/constraints.jl:182-186). The reference's own KAT for
+# them is commented out in test/constraint_tests.jl:65-78; its values are the ones below.
+V_STAGE_UNTRIM = [-4, -3, -math.inf, -5, 5, -11, -7, -3, -5, -15]
+V_TERM_UNTRIM = [-4, -3, -math.inf, -11, -7, -3]
+
+
+def untrimmed_kat_problem(tog):
+    n, m, N = 3, 2, 2
+    bnd = tog.BoundConstraint(n, m, x_max=[5, 5, math.inf], x_min=[-10, -5, 0.0], u_min=-10.0, u_max=0.0, trim=False)
+    obj = tog.LQRObjective(np.eye(n), np.eye(m), np.eye(n), np.zeros(n), N)
+    cons = tog.Constraints([bnd], N)
+    prob = tog.Problem(tog.rk3(tog.Dynamics.car), obj, np.zeros((N - 1, m)), constraints=cons, x0=np.zeros(n),
+                       N=N, dt=0.1)
+    return prob, bnd
+
+
+def test_untrimmed_bound_kat_host(tog):
+    _, bnd = untrimmed_kat_problem(tog)
+    n, m = 3, 2
+    assert bnd.length("stage") == 2 * (n + m) and bnd.length("terminal") == 2 * n
+    assert list(bnd.evaluate(X_KAT, U_KAT)) == V_STAGE_UNTRIM
+    assert list(bnd.evaluate(X_KAT)) == V_TERM_UNTRIM
+    jac = bnd.jacobian(X_KAT, U_KAT)
+    assert np.array_equal(jac[:, :n], np.vstack([np.eye(n), np.zeros((m, n)), -np.eye(n), np.zeros((m, n))]))
+    assert np.array_equal(jac[:, n:], np.vstack([np.zeros((n, m)), np.eye(m), np.zeros((n, m)), -np.eye(m)]))
+
+
+def test_untrimmed_bound_kat_oracle(tog, oracle):
+    """The oracle keeps every row of an untrimmed bound (tog_constraint count = 1)."""
+    prob, _ = untrimmed_kat_problem(tog)
+    s = oracle.OracleSolver(prob, tog.AugmentedLagrangianSolverOptions())
+    s.set("X", np.stack([X_KAT, X_KAT]))
+    s.set("U", U_KAT[None, :])
+    s.update_constraints()
+    C = s.get("C")
+    assert list(C[0, :10]) == V_STAGE_UNTRIM
+    assert list(C[1, :6]) == V_TERM_UNTRIM
+    # an infinite bound's row makes the AL cost NaN (λ'c with λ = 0, c = -Inf), as in the reference
+    assert math.isnan(s.cost(al=True))
+
+
+def test_untrimmed_finite_bounds_solve_like_trimmed(tog, oracle):
+    """With every bound finite, trim=false changes nothing: the oracle's solves agree bit for bit."""
+    out = []
+    for trim in (True, False):
+        p = tog.Problems.pendulum("rk3")
+        n, m = p.model.n, p.model.m
+        cons = tog.Constraints(p.N)
+        bnd = tog.BoundConstraint(n, m, x_min=[-10.0, -10.0], x_max=[10.0, 10.0], u_min=-3.0, u_max=3.0, trim=trim)
+        for k in range(p.N - 1):
+            cons[k] += bnd
+        cons[p.N - 1] += tog.goal_constraint(p.xf)
+        q = tog.Problem(p.model, p.obj, p._U[0], constraints=cons, x0=p.x0[0], xf=p.xf, N=p.N, dt=p.dt)
+        o = oracle.OracleSolver(q, tog.AugmentedLagrangianSolverOptions(iterations=5), b=0)
+        steps = o.solve()
+        out.append((steps, o.get("X"), o.get("U")))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.gpu
+def test_gpu_untrimmed_bound_rows(tog, oracle, gpu):
+    """Device constraint values of the untrimmed KAT equal the oracle's (tog_update_constraints)."""
+    prob, _ = untrimmed_kat_problem(tog)
+    solver = tog.AugmentedLagrangianSolver(prob, tog.AugmentedLagrangianSolverOptions())
+    prob._X[0] = np.stack([X_KAT, X_KAT])
+    prob._U[0] = U_KAT[None, :]
+    solver.handle.upload_state(prob)
+    tog.update_constraints_b(prob, solver)
+    C = solver.handle.get(tog.abi.FIELD_C)[0]
+    assert list(C[0, :10]) == V_STAGE_UNTRIM
+    assert list(C[1, :6]) == V_TERM_UNTRIM

@@ -2128,6 +2128,242 @@ __global__ void __launch_bounds__(64) k_ls_spec_tail(const DevProblem* __restric
   Bf.lsok[b * NC + j] = live ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_ls_spec_tail2: k_ls_spec_tail on two waves (at most 32 trials). Wave A runs the dynamics chain
+// (ū + K δx + α d, the RK step, the divergence test) and hands each step's (x_s, u_s) to wave B through an
+// LDS ring of SPEC_RQ steps; wave B, one group of steps behind, adds the stage costs and AL row terms (in
+// rollout_cost's order), issues the candidate stores, and stages the next chunk of K, ū, d, x, λ, μ into
+// the other half of a double-buffered image. One workgroup barrier per group of SPEC_RQ steps. The
+// instructions off wave A's chain (rows, cost, stores, staging) are about a quarter of a step's.
+constexpr int SPEC_RQ = 4;      // steps per ring slot (and per barrier)
+constexpr int SPEC_LANES = 32;  // trials per workgroup
+__host__ __device__ constexpr int spec_tail2_doubles(int n, int m, int pmax) {
+  return 2 * (spec_tail_tc(n, m) * spec_tail_rec(n, m, pmax) + 2 * pmax) + 2 * SPEC_RQ * (n + m) * SPEC_LANES + 2;
+}
+
+template <class M, int INTEG, int DC>
+__global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+                                                        int lo, int cnt) {
+  constexpr int n = M::n, m = M::m, MN = m * n, W = n + m;
+  constexpr int TC = spec_tail_tc(n, m);
+  static_assert(TC % SPEC_RQ == 0, "a ring group never straddles two staging chunks");
+  constexpr int GPC = TC / SPEC_RQ;  // ring groups per staging chunk
+  static_assert(GPC >= 2, "the next chunk is stored while the previous one is still read");
+  constexpr int SREG = (TC * spec_tail_rec(n, m, SPEC_TAIL_PMAX) + WAVE - 1) / WAVE;
+  const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
+  if (b < 0) return;
+  const TrajState& st = Bf.st[b];
+  if (!st.active || lo + st.ls_pend >= Bf.nc) return;  // (uniform over the block)
+  extern __shared__ double tl2[];
+  const int wv = threadIdx.x >> 6;  // 0: chain wave A, 1: cost wave B
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int j = lo + st.ls_pend + lane;
+  const int N = P->N, pmax = P->pmax, NC = Bf.nc;
+  const bool al = (mode == TOG_MODE_AL);
+  const int PL = al ? pmax : 0;
+  const int OU = TC * MN, OD = OU + TC * m, OX = OD + TC * m, OL = OX + TC * n, OM = OL + TC * PL, TCR = OM + TC * PL;
+  const int IMG = TCR + 2 * PL;                 // one staging image, the terminal λ, μ after it
+  double* ring = tl2 + 2 * IMG;                 // [slot][step][element][lane]
+  int* live_out = reinterpret_cast<int*>(ring + 2 * SPEC_RQ * W * SPEC_LANES);
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  const double* K = Bf.K + (size_t)b * (N - 1) * MN;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  const double* lam = Bf.lam + (size_t)b * N * pmax;
+  const double* mu = Bf.mu + (size_t)b * N * pmax;
+  auto src = [&](int e, int s0, int ns) -> const double* {
+    auto at = [&](const double* base, int sz, int off) {
+      const int r = e - off;
+      return base + (size_t)s0 * sz + (r < ns * sz ? r : 0);
+    };
+    if (e < OU) return at(K, MN, 0);
+    if (e < OD) return at(U, m, OU);
+    if (e < OX) return at(d, m, OD);
+    if (e < OL) return at(X + n, n, OX);
+    if (e < OM) return at(lam, PL, OL);
+    return at(mu, PL, OM);
+  };
+  double sv[SREG];
+  auto stage_load = [&](int s0) {  // (wave B)
+    const int ns = min(TC, N - 1 - s0);
+#pragma unroll
+    for (int i = 0; i < SREG; i++) {
+      const int e = lane + WAVE * i;
+      sv[i] = *src(e < TCR ? e : 0, s0, ns);
+    }
+  };
+  auto stage_store = [&](double* img) {  // (wave B)
+#pragma unroll
+    for (int i = 0; i < SREG; i++) {
+      const int e = lane + WAVE * i;
+      if (e < TCR) img[e] = sv[i];
+    }
+  };
+  const bool on = (lane < cnt) && (j < NC);
+  const int NS = N - 1;                          // steps
+  const int G = (NS + SPEC_RQ - 1) / SPEC_RQ;    // ring groups
+  // chunk 0 and the terminal multipliers (both waves wait at the first barrier)
+  if (wv == 1) {
+    stage_load(0);
+    stage_store(tl2);
+    if (al && lane < 2 * PL)
+      tl2[TCR + lane] = (lane < PL) ? lam[(size_t)(N - 1) * pmax + lane] : mu[(size_t)(N - 1) * pmax + (lane - PL)];
+  }
+  __syncthreads();
+  if (wv == 0) {
+    // ---------------------------------------------------------------- wave A: the dynamics chain
+    const double alpha = ldexp(1.0, -j);
+    const double smax = P->o.max_state_value, umax = P->o.max_control_value;
+    double xb[n], xold[n], ub[m], xn[n];
+    bool live = on;
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+      xb[i] = Bf.x0[(size_t)b * n + i];
+      xold[i] = X[i];
+    }
+#pragma unroll 1
+    for (int g = 0; g <= G; g++) {
+      if (g < G && live) {
+        const double* img = tl2 + ((g / GPC) & 1) * IMG;
+        double* slot = ring + (size_t)(g & 1) * SPEC_RQ * W * SPEC_LANES;
+#pragma unroll 1
+        for (int q = 0; q < SPEC_RQ; q++) {
+          const int s = g * SPEC_RQ + q;
+          if (s >= NS) break;
+          const int c = s % TC;
+          const double* Kk = img + c * MN;
+#pragma unroll
+          for (int i = 0; i < m; i++) {
+            double t = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < n; jj++) t = fma(Kk[i + m * jj], xb[jj] - xold[jj], t);
+            ub[i] = (img[OU + c * m + i] + t) + alpha * img[OD + c * m + i];
+          }
+          double* e = slot + (size_t)q * W * SPEC_LANES + lane;
+#pragma unroll
+          for (int i = 0; i < n; i++) e[i * SPEC_LANES] = xb[i];  // x_s
+#pragma unroll
+          for (int i = 0; i < m; i++) e[(n + i) * SPEC_LANES] = ub[i];  // u_s
+          discrete_step<M, INTEG>(xn, xb, ub, P->dt);
+          bool ok = true;
+#pragma unroll
+          for (int i = 0; i < n; i++) {
+            xb[i] = xn[i];
+            ok = ok && (fabs(xn[i]) < smax);
+          }
+#pragma unroll
+          for (int i = 0; i < m; i++) ok = ok && (fabs(ub[i]) < umax);
+#pragma unroll
+          for (int i = 0; i < n; i++) xold[i] = img[OX + c * n + i];
+          if (!ok) {
+            live = false;
+            break;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // the final state and the verdict for wave B (x_{N-1} in ring slot 0, step 0)
+    if (lane < SPEC_LANES) {
+#pragma unroll
+      for (int i = 0; i < n; i++) ring[(size_t)i * SPEC_LANES + lane] = xb[i];
+      live_out[lane] = live ? 1 : 0;
+    }
+    __syncthreads();
+  } else {
+    // ---------------------------------------------------------------- wave B: costs, stores, staging
+    const RowTablesC RT = const_row_tables(P);
+    double* cw = on ? static_cast<double*>(__builtin_assume_aligned(
+                          Bf.cand + ((size_t)b * N * cand_q<M>() * Bf.ncp + j) * 4, 32))
+                    : nullptr;
+    const int ncp = Bf.ncp;
+    double J = 0.0, Jc = 0.0;
+#pragma unroll 1
+    for (int g = 0; g <= G; g++) {
+      // staging of the next chunk: loads in the chunk's second group, stores in its last one
+      const int cg = g % GPC, ch = g / GPC;
+      if (cg == (GPC > 1 ? 1 : 0) && (ch + 1) * TC < NS) stage_load((ch + 1) * TC);
+      if (g >= 1 && on) {
+        const int gp = g - 1;
+        const double* img = tl2 + ((gp / GPC) & 1) * IMG;
+        const double* slot = ring + (size_t)(gp & 1) * SPEC_RQ * W * SPEC_LANES;
+#pragma unroll 1
+        for (int q = 0; q < SPEC_RQ; q++) {
+          const int s = gp * SPEC_RQ + q;
+          if (s >= NS) break;
+          const int c = s % TC;
+          const double* e = slot + (size_t)q * W * SPEC_LANES + lane;
+          double x[n], u[m];
+#pragma unroll
+          for (int i = 0; i < n; i++) x[i] = e[i * SPEC_LANES];
+#pragma unroll
+          for (int i = 0; i < m; i++) u[i] = e[(n + i) * SPEC_LANES];
+#pragma unroll
+          for (int i = 0; i < m; i++) __builtin_nontemporal_store(u[i], cw + cand_at(s, i, cand_q<M>(), ncp));
+          if (s >= 1) {
+#pragma unroll
+            for (int i = 0; i < n; i++) __builtin_nontemporal_store(x[i], cw + cand_at(s, m + i, cand_q<M>(), ncp));
+          }
+          J += stage_cost_m<M, DC>(P, x, u);
+          if (al) {
+            const int pc = RT.kcnt[s];
+            if (pc) {
+              const cptr<ConRow> rows = RT.rows + RT.koff[s];
+              double lc = 0.0, cIc = 0.0;
+              for (int r = 0; r < pc; r++) {
+                const ConRow row = uniform_row(load_row(rows + r));
+                const double cv = row_value_m<M, true>(row, x, u);
+                const double l = img[OL + c * PL + r];
+                const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((cv >= 0.0) || (l > 0.0)) : true;
+                const double w = a ? img[OM + c * PL + r] : 0.0;
+                lc = fma(l, cv, lc);
+                cIc = fma(cv * w, cv, cIc);
+              }
+              Jc += lc + 0.5 * cIc;
+            }
+          }
+        }
+      }
+      if (cg == GPC - 1 && (ch + 1) * TC < NS) stage_store(tl2 + ((ch + 1) & 1) * IMG);
+      __syncthreads();
+    }
+    __syncthreads();  // wave A's final state and verdict
+    if (on) {
+      const bool live = live_out[lane] != 0;
+      double x[n];
+#pragma unroll
+      for (int i = 0; i < n; i++) x[i] = ring[(size_t)i * SPEC_LANES + lane];
+#pragma unroll
+      for (int i = 0; i < n; i++) __builtin_nontemporal_store(x[i], cw + cand_at(NS, m + i, cand_q<M>(), ncp));
+      double Jj = INFINITY;
+      if (live) {
+        J += terminal_cost_m<M, DC>(P, x);
+        if (al) {  // terminal rows (al_knot_terms' order), multipliers from the image
+          const int pc = RT.kcnt[N - 1];
+          if (pc) {
+            const cptr<ConRow> rows = RT.rows + RT.koff[N - 1];
+            double lc = 0.0, cIc = 0.0;
+            for (int r = 0; r < pc; r++) {
+              const ConRow row = uniform_row(load_row(rows + r));
+              const double cv = row_value_m<M, true>(row, x, nullptr);
+              const double l = tl2[TCR + r];
+              const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((cv >= 0.0) || (l > 0.0)) : true;
+              const double w = a ? tl2[TCR + PL + r] : 0.0;
+              lc = fma(l, cv, lc);
+              cIc = fma(cv * w, cv, cIc);
+            }
+            Jc += lc + 0.5 * cIc;
+          }
+          J = J + Jc;
+        }
+        Jj = J;
+      }
+      Bf.lsJ[b * NC + j] = Jj;
+      Bf.lsok[b * NC + j] = live ? 1 : 0;
+    }
+  }
+}
+
 // After trials [0, hi): list the active trajectories the acceptance logic has not settled yet
 // (input: every trajectory when in_list == nullptr, else in_list[0, *in_count)). One thread per
 // entry; a wave reserves its slots with one atomic (ballot + popcount). The list order varies from
@@ -2934,8 +3170,13 @@ struct ModelLaunch {
   template <int INTEG>
   static void spec(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int lo, int cnt, const int* list,
                    const int* count, hipStream_t st) {
-    // the tail kernel inlines the diagonal cost only (the dense cost's run-time indexing of x, u would put
+    // the tail kernels inline the diagonal cost only (the dense cost's run-time indexing of x, u would put
     // them in scratch); dense costs take k_ls_spec
+    if (Bf.tail && Bf.cand && Bf.spec_tail2_shmem > 0 && Bf.cost_diag && !list && cnt <= SPEC_LANES) {
+      hipLaunchKernelGGL((k_ls_spec_tail2<M, INTEG, 1>), dim3((unsigned)B), dim3(2 * WAVE),
+                         (unsigned)Bf.spec_tail2_shmem, st, P, Bf, mode, lo, cnt);
+      return;
+    }
     if (Bf.tail && Bf.cand && Bf.spec_tail_shmem > 0 && Bf.cost_diag && !list && cnt <= WAVE) {
       hipLaunchKernelGGL((k_ls_spec_tail<M, INTEG, 1>), dim3((unsigned)B), dim3(WAVE), (unsigned)Bf.spec_tail_shmem, st,
                          P, Bf, mode, lo, cnt);

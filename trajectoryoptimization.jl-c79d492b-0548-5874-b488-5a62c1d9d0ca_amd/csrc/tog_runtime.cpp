@@ -211,17 +211,19 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
       const double* D = con.data;
       switch (con.type) {
         case TOG_CON_BOUND: {
-          // data = [x_max(n), x_min(n), u_max(m), u_min(m)]; order [x_max; u_max; x_min; u_min]
+          // data = [x_max(n), x_min(n), u_max(m), u_min(m)]; order [x_max; u_max; x_min; u_min].
+          // count 0: trim = true (infinite bounds dropped); 1: trim = false (every row kept)
+          const bool keep = (con.count == 1);
           for (int i = 0; i < n; i++)
-            if (isfinite(D[i])) rows.push_back({ROW_XMAX, i, D[i], 0, 0, 0});
+            if (keep || isfinite(D[i])) rows.push_back({ROW_XMAX, i, D[i], 0, 0, 0});
           if (!term)
             for (int i = 0; i < m; i++)
-              if (isfinite(D[2 * n + i])) rows.push_back({ROW_UMAX, i, D[2 * n + i], 0, 0, 0});
+              if (keep || isfinite(D[2 * n + i])) rows.push_back({ROW_UMAX, i, D[2 * n + i], 0, 0, 0});
           for (int i = 0; i < n; i++)
-            if (isfinite(D[n + i])) rows.push_back({ROW_XMIN, i, D[n + i], 0, 0, 0});
+            if (keep || isfinite(D[n + i])) rows.push_back({ROW_XMIN, i, D[n + i], 0, 0, 0});
           if (!term)
             for (int i = 0; i < m; i++)
-              if (isfinite(D[2 * n + m + i])) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
+              if (keep || isfinite(D[2 * n + m + i])) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
           break;
         }
         case TOG_CON_GOAL: {  // count: rows x[1:count] - xf (the goal's inds); 0 = n
@@ -715,6 +717,11 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
                         ? 0
                         : row_tables_bytes((int)rows.size(), N);
   // k_ls_spec_tail (tail rollouts staged through LDS): admissible up to SPEC_TAIL_PMAX rows per knot
+  {  // k_ls_spec_tail2 (two waves): within 64 KB of LDS; TOG_NO_SPEC_TAIL2 keeps the one-wave kernel
+    const size_t b2 = sizeof(double) * (size_t)spec_tail2_doubles(n, m, h->pmax);
+    h->buf.spec_tail2_shmem =
+        (h->pmax <= SPEC_TAIL_PMAX && b2 <= 64 * 1024 && !getenv("TOG_NO_SPEC_TAIL2")) ? (int)b2 : 0;
+  }
   h->buf.spec_tail_shmem = (h->pmax <= SPEC_TAIL_PMAX && !getenv("TOG_NO_SPEC_TAIL"))
                                ? (int)(sizeof(double) * (spec_tail_tc(n, m) * spec_tail_rec(n, m, h->pmax) + 2 * h->pmax))
                                : 0;

@@ -500,7 +500,11 @@ class _Constraint:
 
 class BoundConstraint(_Constraint):
     """``BoundConstraint(n, m; x_min, x_max, u_min, u_max, trim=true)`` (src/constraints.jl:155-188).
-    Constraint vector order ``[x_max; u_max; x_min; u_min]`` with infinite bounds trimmed."""
+    Constraint vector order ``[x_max; u_max; x_min; u_min]``; ``trim=true`` drops the infinite bounds,
+    ``trim=false`` keeps every row (an infinite bound then evaluates to -Inf and the AL terms to NaN, as
+    in the reference). At the terminal knot the untrimmed rows are x_max and x_min (the reference's
+    untrimmed ``x_all`` mask, ``[trues(n); falses(m); trues(m); falses(m)]``, has the wrong length unless
+    n == m; its evident intent is taken)."""
 
     label = "bound"
 
@@ -508,10 +512,13 @@ class BoundConstraint(_Constraint):
         self.n, self.m = n, m
         self.u_max, self.u_min = _validate_bounds(u_max, u_min, m)
         self.x_max, self.x_min = _validate_bounds(x_max, x_min, n)
-        if not trim:
-            raise NotImplementedError("trim=false bounds are not built")
-        self.active = dict(x_max=np.isfinite(self.x_max), u_max=np.isfinite(self.u_max),
-                           x_min=np.isfinite(self.x_min), u_min=np.isfinite(self.u_min))
+        self.trim = bool(trim)
+        if self.trim:
+            self.active = dict(x_max=np.isfinite(self.x_max), u_max=np.isfinite(self.u_max),
+                               x_min=np.isfinite(self.x_min), u_min=np.isfinite(self.u_min))
+        else:
+            self.active = dict(x_max=np.ones(n, bool), u_max=np.ones(m, bool), x_min=np.ones(n, bool),
+                               u_min=np.ones(m, bool))
 
     def length(self, kind="stage"):
         a = self.active
@@ -542,8 +549,10 @@ class BoundConstraint(_Constraint):
         # an infeasible problem's controls are [u; slack]: the slack entries are unbounded
         # (trimmed), so the rows are those of the model controls (constraint_sets.jl:135-150)
         pad = np.full(0 if m is None else m - self.m, np.inf)
+        if pad.size and not self.trim:
+            raise NotImplementedError("trim=false bounds on an infeasible-start problem are not built")
         data = np.concatenate([self.x_max, self.x_min, self.u_max, pad, self.u_min, -pad])
-        return (abi.CON_BOUND, 0, data)
+        return (abi.CON_BOUND, 0 if self.trim else 1, data)
 
 
 class InfeasibleConstraint(_Constraint):
