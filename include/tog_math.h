@@ -86,7 +86,7 @@ TOG_HD double tog_cos(double x) {
  * contract v4): a bit-pattern seed (relative error below 3.5e-2) and four Newton
  * steps r += r (1/2 - (y/2) r^2) in fma form, so host and device produce the same bits; within 2 ulp
  * of the correctly rounded value for every normal y > 0 (tests/test_reference_kats.py checks 2^20
- * points). y == 0 gives +Inf, y < 0 or NaN gives NaN. One long dependent chain replaces the sqrt
+ * points). y == 0 gives +Inf, y == +Inf gives 0, y < 0 or NaN gives NaN. One long dependent chain replaces the sqrt
  * and the division of the reference's c = sqrt(1 - s^2), (.)/c. */
 TOG_HD double tog_rsqrt(double y) {
   long long i;
@@ -100,8 +100,12 @@ TOG_HD double tog_rsqrt(double y) {
     const double e = fma(-hr, r, 0.5);
     r = fma(r, e, r);
   }
-  return (y > 0.0) ? r : ((y == 0.0) ? INFINITY : NAN);
+  return (y > 0.0 && y < INFINITY) ? r : ((y == 0.0) ? INFINITY : ((y == INFINITY) ? 0.0 : NAN));
 }
+
+/* c = sqrt(y) of chol_minus as y * tog_rsqrt(y), with the reference's c = sqrt(0) = 0 at y == 0
+ * (s^2 == 1 exactly; y * rsqrt(y) would be 0 * Inf = NaN there). The reciprocal stays Inf. */
+TOG_HD double tog_rs_c(double y, double rc) { return (y == 0.0) ? 0.0 : y * rc; }
 
 TOG_HD double tog_jlmax(double a, double b) { return (a != a) ? a : ((b != b) ? b : fmax(a, b)); }
 TOG_HD double tog_jlmin(double a, double b) { return (a != a) ? a : ((b != b) ? b : fmin(a, b)); }

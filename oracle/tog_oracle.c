@@ -1083,7 +1083,7 @@ static int chol_minus(double* Uo, const double* A, int n, const double* B, int n
       if (s2 > 1.0) return i + 1;
       double y = 1.0 - s2;
       double rc = tog_rsqrt(y);
-      double c = y * rc;
+      double c = tog_rs_c(y, rc);
       U[IDX(i, i, n)] = c * Aii;
       rd[i] = rd[i] * rc;
       for (int j = i + 1; j < n; j++) {
@@ -1095,6 +1095,9 @@ static int chol_minus(double* Uo, const double* A, int n, const double* B, int n
   }
   memcpy(Uo, U, sizeof(double) * n * n);
   return 0;
+}
+OC_EXPORT int oc_chol_minus(double* Uo, const double* A, int n, const double* B, int nb) {
+  return chol_minus(Uo, A, n, B, nb);
 }
 
 /* =====================================================================

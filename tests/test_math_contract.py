@@ -1,0 +1,54 @@
+"""The shared arithmetic primitives of include/tog_math.h, run through the oracle build
+(host and device compile the same header): tog_rsqrt, the 1/sqrt of chol_minus contract v4, within
+2 ulp of the correctly rounded 1/sqrt on 2^20 points, and its boundary values; chol_minus at
+s^2 == 1 exactly, where the reference's c = sqrt(1 - s^2) is 0 (backward_pass.jl:186-192,
+lowrankdowndate!) and the diagonal must come out 0, not NaN."""
+import ctypes as C
+
+import numpy as np
+
+
+def _ulp_dist(a, b):
+    ia = a.view(np.int64)
+    ib = b.view(np.int64)
+    return np.abs(ia - ib)
+
+
+def test_rsqrt_within_2ulp_on_2pow20_points(oracle):
+    L = oracle.lib()
+    L.oc_rsqrt.restype = C.c_double
+    L.oc_rsqrt.argtypes = [C.c_double]
+    rng = np.random.default_rng(20)
+    # normal range, log-uniform over the exponent range plus dense sampling of [0, 1] (chol_minus's y)
+    y = np.concatenate([np.exp2(rng.uniform(-1020, 1020, 1 << 19)), rng.uniform(0, 1, 1 << 19)])
+    y = y[y > 0]
+    got = np.array([L.oc_rsqrt(float(v)) for v in y])
+    ref = 1.0 / np.sqrt(y.astype(np.longdouble))
+    ref = ref.astype(np.float64)
+    assert _ulp_dist(got, ref).max() <= 2
+
+
+def test_rsqrt_boundary_values(oracle):
+    L = oracle.lib()
+    L.oc_rsqrt.restype = C.c_double
+    L.oc_rsqrt.argtypes = [C.c_double]
+    assert L.oc_rsqrt(0.0) == np.inf
+    assert L.oc_rsqrt(np.inf) == 0.0
+    assert np.isnan(L.oc_rsqrt(-1.0))
+    assert np.isnan(L.oc_rsqrt(np.nan))
+
+
+def test_chol_minus_zero_cosine_gives_zero_diagonal(oracle):
+    L = oracle.lib()
+    dp = C.POINTER(C.c_double)
+    L.oc_chol_minus.restype = C.c_int
+    L.oc_chol_minus.argtypes = [dp, dp, C.c_int, dp, C.c_int]
+    # A = [[2]], downdate by the row [2]: s = 2 * (1/2) = 1 exactly, so c = 0 and the factor is 0
+    # (with more columns the reference's (A_ij - s x_j)/c then divides by zero and the next row's
+    # downdate throws PosDefException; that is the TOG_TRAJ_SQRT_PD_FAIL path)
+    A = np.array([[2.0]], order="F")
+    Bv = np.array([[2.0]], order="F")
+    U = np.full((1, 1), np.nan, order="F")
+    rc = L.oc_chol_minus(U.ctypes.data_as(dp), A.ctypes.data_as(dp), 1, Bv.ctypes.data_as(dp), 1)
+    assert rc == 0
+    assert U[0, 0] == 0.0

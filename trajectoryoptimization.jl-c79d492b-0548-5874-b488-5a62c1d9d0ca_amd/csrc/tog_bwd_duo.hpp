@@ -344,7 +344,7 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
             okd = okd && !(act && s2 > 1.0);
             const double y = 1.0 - s2;
             const double rc = tog_rsqrt(y);
-            const double cs = y * rc;
+            const double cs = tog_rs_c(y, rc);
             w[0] = x[0];
 #pragma unroll
             for (int kk = 1; kk < m; kk++) {

@@ -1498,7 +1498,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             okd = okd && !(act && s2 > 1.0);
             const double y = 1.0 - s2;
             const double rc = tog_rsqrt(y);
-            const double cs = y * rc;
+            const double cs = tog_rs_c(y, rc);
             w[0] = x[0];
 #pragma unroll
             for (int k = 1; k < m; k++) {
@@ -1531,7 +1531,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
               if (s2 > 1.0) okd = false;
               const double y = 1.0 - s2;
               const double rc = tog_rsqrt(y);
-              const double cs = y * rc;
+              const double cs = tog_rs_c(y, rc);
               u[0] = cs * u[0];
               ru = ru * rc;
 #pragma unroll

@@ -1491,7 +1491,7 @@ attempt:
             }
             const double y = 1.0 - s2;
             const double rc = tog_rsqrt(y);
-            const double c = y * rc;
+            const double c = tog_rs_c(y, rc);
             U[i + m * i] = c * Aii;
             rdg[i] = rdg[i] * rc;
             for (int j = i + 1; j < m; j++) {
@@ -2137,9 +2137,18 @@ __global__ void __launch_bounds__(64) k_ls_spec_tail(const DevProblem* __restric
 // instructions off wave A's chain (rows, cost, stores, staging) are about a quarter of a step's.
 constexpr int SPEC_RQ = 4;      // steps per ring slot (and per barrier)
 constexpr int SPEC_LANES = 32;  // trials per workgroup
-__host__ __device__ constexpr int spec_tail2_doubles(int n, int m, int pmax) {
-  return 2 * (spec_tail_tc(n, m) * spec_tail_rec(n, m, pmax) + 2 * pmax) + 2 * SPEC_RQ * (n + m) * SPEC_LANES + 2;
+// layout: two staging images (each with the terminal λ, μ after it), the ring, then SPEC_LANES ints of
+// wave A's verdicts (live_out), rounded up to whole doubles
+__host__ __device__ constexpr int spec_tail2_ring_off(int n, int m, int pmax) {
+  return 2 * (spec_tail_tc(n, m) * spec_tail_rec(n, m, pmax) + 2 * pmax);
 }
+__host__ __device__ constexpr int spec_tail2_doubles(int n, int m, int pmax) {
+  return spec_tail2_ring_off(n, m, pmax) + 2 * SPEC_RQ * (n + m) * SPEC_LANES +
+         (SPEC_LANES * (int)sizeof(int) + (int)sizeof(double) - 1) / (int)sizeof(double);
+}
+static_assert(spec_tail2_doubles(13, 4, 13) - spec_tail2_ring_off(13, 4, 13) - 2 * SPEC_RQ * 17 * SPEC_LANES ==
+                  SPEC_LANES / 2,
+              "live_out needs SPEC_LANES ints after the ring");
 
 template <class M, int INTEG, int DC>
 __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
@@ -2165,6 +2174,8 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
   const int IMG = TCR + 2 * PL;                 // one staging image, the terminal λ, μ after it
   double* ring = tl2 + 2 * IMG;                 // [slot][step][element][lane]
   int* live_out = reinterpret_cast<int*>(ring + 2 * SPEC_RQ * W * SPEC_LANES);
+  // (2 * IMG <= spec_tail2_ring_off(n, m, pmax): PL <= pmax, so live_out[SPEC_LANES) ends inside the
+  // spec_tail2_doubles(n, m, pmax) the runtime allocates)
   const double* X = Bf.X + (size_t)b * N * n;
   const double* U = Bf.U + (size_t)b * (N - 1) * m;
   const double* K = Bf.K + (size_t)b * (N - 1) * MN;

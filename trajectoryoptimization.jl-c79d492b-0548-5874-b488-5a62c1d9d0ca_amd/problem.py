@@ -67,9 +67,10 @@ def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) ->
               "midpoint_implicit": abi.MIDPOINT_IMPLICIT}
     if key not in integs:
         raise ValueError(f"Integration not defined: {discretizer!r}")  # src/model.jl:659
-    if integs[key] in (abi.RK3_IMPLICIT, abi.MIDPOINT_IMPLICIT) and model.n > 4 and model.name != "quadrotor":
-        # the device instantiates the implicit Newton step for n <= 4 and the quadrotor
-        # (ModelTraits::implicit_ok, csrc/tog_device.hpp)
+    builtin_implicit = model.plugin is None and model.model_id == abi.MODEL_QUADROTOR
+    if integs[key] in (abi.RK3_IMPLICIT, abi.MIDPOINT_IMPLICIT) and model.n > 4 and not builtin_implicit:
+        # the device instantiates the implicit Newton step for n <= 4 and the built-in quadrotor
+        # (ModelTraits::implicit_ok, csrc/tog_device.hpp), decided by model id as the runtime does
         raise NotImplementedError(f"implicit integration {discretizer!r} is built for models with n <= 4 "
                                   "and the quadrotor")
     return Model(model.model_id, model.n, model.m, model.name, integs[key], plugin=model.plugin)
