@@ -783,8 +783,9 @@ OC_EXPORT void oc_continuous_f(int model, double* xd, const double* x, const dou
 }
 
 /* ∇fd!(S, x, u, dt): ForwardDiff.jacobian!(S, fd_aug!, ẋ, [x;u;dt])  src/model.jl:491-512.
-   S is n x (n+m+1) column-major, partitioned xx | xu | xdt (src/model.jl:341). */
-OC_EXPORT void oc_discrete_jacobian(int model, int integ, double* S, const double* x, const double* u, double dt) {
+   S is n x (n+m+1) column-major, partitioned xx | xu | xdt (src/model.jl:341). Forward-mode duals
+   straight through the integrator. */
+static void discrete_jacobian_fd(int model, int integ, double* S, const double* x, const double* u, double dt) {
   int n = model_n[model], m = model_m[model];
   int L = n + m + 1;
   g_nd = L;
@@ -803,6 +804,97 @@ OC_EXPORT void oc_discrete_jacobian(int model, int integ, double* S, const doubl
   for (int j = 0; j < L; j++)
     for (int i = 0; i < n; i++) S[i + n * j] = XN[i].p[j];
   g_nd = 0;
+}
+
+/* The Kuka iiwa's RK3 Jacobian, "stage-chain" form (contract deviations): the same
+   derivative as forward-mode duals through rk3 (src/integration.jl:149-158), evaluated as
+     J_s = ∂f/∂[s; u] at each stage input s_1 = x, s_2 = x + k1/2, s_3 = (x - k1) + 2 k2 (dual numbers
+           seeded at the stage input, 21 partials; the primal stage inputs are discrete_step's),
+     K1 = J_1 dt,  T2 = I + K1/2,  F2 = J_2 [T2; E_u],  K2 = F2 dt,  T3 = (I - K1) + 2 K2,
+     F3 = J_3 [T3; E_u],  K3 = F3 dt,  [A B] = I + ((K1 + 4 K2) + K3)/6,
+   with RK3's elementwise operations in discrete_step's order and the two chain products as fma chains
+   over j = 0..13, started from J_s's u column (0 for the x columns): the accumulation order of the
+   fp64 matrix cores (v_mfma_f64_16x16x4_f64, k in order, tools/microbench/mfma_f64_order.hip) that
+   evaluate them on the device (k_kuka_chain). Rows 0..6 of f are q̇ = v, so F rows 0..6 are T rows
+   7..13. RigidBodyDynamics' own operation order is not reproduced either way; the
+   notebook pin (tests/test_kuka.py) holds for both forms. */
+static void kuka_rk3_jacobian_chain(double* S, const double* x, const double* u, double dt) {
+  enum { n = 14, m = 7, L = 21 };
+  const int save = g_nd;
+  double k1[n], t2[n], t3[n];
+  { /* primal stage inputs (discrete_f_dual's rk3 values) */
+    g_nd = 0;
+    dual X[n], U[m], F[n];
+    for (int i = 0; i < n; i++) X[i] = dc(x[i]);
+    for (int i = 0; i < m; i++) U[i] = dc(u[i]);
+    f_kuka(F, X, U);
+    for (int i = 0; i < n; i++) {
+      k1[i] = F[i].v * dt;
+      t2[i] = x[i] + k1[i] / 2.0;
+    }
+    for (int i = 0; i < n; i++) X[i] = dc(t2[i]);
+    f_kuka(F, X, U);
+    for (int i = 0; i < n; i++) t3[i] = (x[i] - k1[i]) + 2.0 * (F[i].v * dt);
+  }
+  double J[3][7][L]; /* rows 7..13 of J_s */
+  const double* pts[3] = {x, t2, t3};
+  g_nd = L;
+  for (int st = 0; st < 3; st++) {
+    dual Xs[n], Us[m], Fs[n];
+    for (int i = 0; i < n; i++) {
+      Xs[i] = dc(pts[st][i]);
+      Xs[i].p[i] = 1.0;
+    }
+    for (int i = 0; i < m; i++) {
+      Us[i] = dc(u[i]);
+      Us[i].p[n + i] = 1.0;
+    }
+    f_kuka(Fs, Xs, Us);
+    for (int i = 0; i < 7; i++)
+      for (int p = 0; p < L; p++) J[st][i][p] = Fs[7 + i].p[p];
+  }
+  g_nd = save;
+  static _Thread_local double K1[n][L], T[n][L], K2[n][L], Ssum[n][L];
+  for (int i = 0; i < n; i++)
+    for (int p = 0; p < L; p++) {
+      const double f1 = (i < 7) ? ((p == 7 + i) ? 1.0 : 0.0) : J[0][i - 7][p];
+      K1[i][p] = f1 * dt;
+      T[i][p] = ((i == p) ? 1.0 : 0.0) + K1[i][p] / 2.0;
+    }
+  for (int st = 1; st < 3; st++) {
+    double F[n][L];
+    for (int p = 0; p < L; p++)
+      for (int i = 0; i < n; i++) {
+        if (i < 7) {
+          F[i][p] = T[7 + i][p];
+        } else {
+          double acc = (p >= n) ? J[st][i - 7][p] : 0.0;
+          for (int j = 0; j < n; j++) acc = fma(J[st][i - 7][j], T[j][p], acc);
+          F[i][p] = acc;
+        }
+      }
+    for (int i = 0; i < n; i++)
+      for (int p = 0; p < L; p++) {
+        const double kk = F[i][p] * dt;
+        if (st == 1) {
+          K2[i][p] = kk;
+          T[i][p] = (((i == p) ? 1.0 : 0.0) - K1[i][p]) + 2.0 * kk;
+          Ssum[i][p] = K1[i][p] + 4.0 * kk;
+        } else {
+          Ssum[i][p] = Ssum[i][p] + kk;
+          S[i + n * p] = ((i == p) ? 1.0 : 0.0) + Ssum[i][p] / 6.0;
+        }
+      }
+  }
+}
+
+OC_EXPORT void oc_discrete_jacobian(int model, int integ, double* S, const double* x, const double* u, double dt) {
+  discrete_jacobian_fd(model, integ, S, x, u, dt); /* (the dt column) */
+  if (model == TOG_MODEL_KUKA && integ == TOG_RK3) kuka_rk3_jacobian_chain(S, x, u, dt);
+}
+/* forward-mode duals through the integrator for every model (tests: the stage-chain form against it) */
+OC_EXPORT void oc_discrete_jacobian_fd(int model, int integ, double* S, const double* x, const double* u, double dt) {
+  discrete_jacobian_fd(model, integ, S, x, u, dt);
 }
 
 OC_EXPORT int oc_model_n(int model) { return model_n[model]; }
@@ -1593,7 +1685,7 @@ static void traj_jacobian(const oc_solver* s, double* F, const double* x, const 
     const int nb = n - 1, mbb = m - 1;
     const double h = u[m - 1];
     double Z[16 * (16 + OM + 1)];
-    oc_discrete_jacobian(s->model, s->integ, Z, x, u, h * h); /* nb x (nb + mbb + 1) */
+    discrete_jacobian_fd(s->model, s->integ, Z, x, u, h * h); /* nb x (nb + mbb + 1) */
     memset(F, 0, sizeof(double) * n * (n + m + 1));
     for (int j = 0; j < nb; j++)
       for (int i = 0; i < nb; i++) F[i + n * j] = Z[i + nb * j];

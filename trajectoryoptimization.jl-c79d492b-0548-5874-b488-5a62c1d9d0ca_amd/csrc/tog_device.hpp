@@ -170,7 +170,10 @@ struct DevBuffers {
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū
-  double* jws;        // staged RK3 Jacobian (Kuka): (2n duals, lanes) stage state between the kernels, or null
+  double* jws;        // Kuka RK3 Jacobian workspace (stage-chain form: KJ_WSK doubles per knot slot; the
+                      // dual-staged A/B form: 2n duals per lane), or null
+  int jac_chain;      // Kuka RK3 Jacobian in stage-chain form (tog_kuka_jac.hpp; 0: TOG_KUKA_JAC=dual A/B)
+  int pad_jc;
   // compacted tail launches (tog_solve_step, k_list_active): the step's active trajectories and their
   // count; null outside a tail step (launch slot = trajectory index)
   int* act_list;
@@ -281,6 +284,14 @@ template <int W>
 __host__ __device__ __forceinline__ Dual<W> operator-(const Dual<W>& a, double s) {
   Dual<W> r = a;
   r.v = a.v - s;
+  return r;
+}
+template <int W>
+__host__ __device__ __forceinline__ Dual<W> operator-(double s, const Dual<W>& a) {  // a zero-tangent dual minus a
+  Dual<W> r;
+  r.v = s - a.v;
+#pragma unroll
+  for (int i = 0; i < W; i++) r.g[i] = -a.g[i];
   return r;
 }
 template <int W>
@@ -534,16 +545,18 @@ struct Kuka {
     for (int a = 0; a < 3; a++)
       y[a] = (x[0] * KT.R0[j][3 * a] + x[1] * KT.R0[j][3 * a + 1]) + x[2] * KT.R0[j][3 * a + 2];
   }
-  template <class T>
-  __host__ __device__ __forceinline__ static void E(int j, const T& c, const T& s, T* y, const T* x) {
+  // (c, s) may be plain doubles while x carries partials: TC * T is then the product a zero-tangent
+  // dual would give, fma(t.v, 0, c.v t.g) = c.v t.g (the stage-Jacobian lanes of tog_kuka_jac.hpp)
+  template <class TC, class T>
+  __host__ __device__ __forceinline__ static void E(int j, const TC& c, const TC& s, T* y, const T* x) {
     T t[3];
     r0t(j, t, x);
     y[0] = c * t[0] + s * t[1];
     y[1] = c * t[1] - s * t[0];
     y[2] = t[2];
   }
-  template <class T>
-  __host__ __device__ __forceinline__ static void Et(int j, const T& c, const T& s, T* y, const T* x) {
+  template <class TC, class T>
+  __host__ __device__ __forceinline__ static void Et(int j, const TC& c, const TC& s, T* y, const T* x) {
     T t[3];
     t[0] = c * x[0] - s * x[1];
     t[1] = s * x[0] + c * x[1];
@@ -582,11 +595,12 @@ struct Kuka {
     for (int a = 0; a < 3; a++) lin[a] = v[a] * KT.M[j] - hx[a];
   }
 
-  // dynamics_bias: RNEA with v̇ = 0 -> tau; also cos/sin of q for the mass matrix
-  template <class T>
-  __host__ __device__ __forceinline__ static void bias(T* tau, T* cq, T* sq, const T* q, const T* qd) {
-    const T z = cst_(0.0, q[0]);
-    T w[3] = {z, z, z}, v[3] = {z, z, z}, al[3] = {z, z, z}, ln[3] = {z, z, cst_(TOG_KUKA_GRAVITY, q[0])};
+  // dynamics_bias: RNEA with v̇ = 0 -> tau; also cos/sin of q for the mass matrix. TQ (q, cos, sin) may
+  // be double while T (q̇ and everything downstream) is a dual: the partials w.r.t. q̇ at fixed q.
+  template <class T, class TQ>
+  __host__ __device__ __forceinline__ static void bias(T* tau, TQ* cq, TQ* sq, const TQ* q, const T* qd) {
+    const T z = cst_(0.0, qd[0]);
+    T w[3] = {z, z, z}, v[3] = {z, z, z}, al[3] = {z, z, z}, ln[3] = {z, z, cst_(TOG_KUKA_GRAVITY, qd[0])};
     T nf[7][3], ff[7][3];
 #pragma unroll
     for (int j = 0; j < 7; j++) {
@@ -717,14 +731,9 @@ struct Kuka {
     }
   }
 
+  // Cholesky M = L Lᵀ in place (entry (i,j) of M is read once, before L[i][j] replaces it)
   template <class T>
-  __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
-    const T* q = x;
-    const T* qd = x + 7;
-    T tau[7], cq[7], sq[7], L[7][7], y[7];
-    bias(tau, cq, sq, q, qd);
-    mass(L, cq, sq);
-    // Cholesky M = L Lᵀ in place (entry (i,j) of M is read once, before L[i][j] replaces it)
+  __host__ __device__ __forceinline__ static void chol(T (*L)[7]) {
 #pragma unroll
     for (int j = 0; j < 7; j++) {
       T s = L[j][j];
@@ -739,20 +748,50 @@ struct Kuka {
         L[i][j] = t / L[j][j];
       }
     }
+  }
+  // t / L_ii with the dual quotient's partials, x.p * inv(y) (the divisor's partials are zero when L is
+  // a plain double: fma(x.p, 1/y, 0 * c2) = x.p * (1/y), not x.p / y)
+  __host__ __device__ __forceinline__ static double kdiv(double t, double l) { return t / l; }
+  template <int W>
+  __host__ __device__ __forceinline__ static Dual<W> kdiv(const Dual<W>& t, const Dual<W>& l) { return t / l; }
+  template <int W>
+  __host__ __device__ __forceinline__ static Dual<W> kdiv(const Dual<W>& t, double l) {
+    Dual<W> r;
+    r.v = t.v / l;
+    const double iy = 1.0 / l;
+#pragma unroll
+    for (int i = 0; i < W; i++) r.g[i] = t.g[i] * iy;
+    return r;
+  }
+  // v̇ = L⁻ᵀ L⁻¹ (u − τ): forward then backward substitution
+  template <class TL, class T, class TU>
+  __host__ __device__ __forceinline__ static void solve(T* vd, const TL (*L)[7], const TU* u, const T* tau) {
+    T y[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) {
       T t = u[i] - tau[i];
 #pragma unroll
       for (int k = 0; k < i; k++) t = t - L[i][k] * y[k];
-      y[i] = t / L[i][i];
+      y[i] = kdiv(t, L[i][i]);
     }
 #pragma unroll
     for (int i = 6; i >= 0; i--) {
       T t = y[i];
 #pragma unroll
-      for (int k = i + 1; k < 7; k++) t = t - L[k][i] * xd[7 + k];
-      xd[7 + i] = t / L[i][i];
+      for (int k = i + 1; k < 7; k++) t = t - L[k][i] * vd[k];
+      vd[i] = kdiv(t, L[i][i]);
     }
+  }
+
+  template <class T>
+  __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
+    const T* q = x;
+    const T* qd = x + 7;
+    T tau[7], cq[7], sq[7], L[7][7];
+    bias(tau, cq, sq, q, qd);
+    mass(L, cq, sq);
+    chol(L);
+    solve(xd + 7, L, u, tau);
 #pragma unroll
     for (int i = 0; i < 7; i++) xd[i] = qd[i];
   }

@@ -665,6 +665,10 @@ k_jacobian_mt(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) 
   }
 }
 
+}  // namespace tog
+#include "tog_kuka_jac.hpp"
+namespace tog {
+
 // =============================================================================================
 // Wave-level small dense linear algebra on LDS (column-major). All 64 lanes cooperate; sizes are
 // compile-time so every loop unrolls. Callers synchronise (wsync) between dependent steps.
@@ -3099,8 +3103,16 @@ struct ModelLaunch {
         constexpr int I = decltype(ic)::value;
         hipLaunchKernelGGL((k_jacobian_mt<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
       });
+    } else if (Mb::id == TOG_MODEL_KUKA && integ == TOG_RK3 && Bf.jws && Bf.jac_chain) {
+      if constexpr (Mb::id == TOG_MODEL_KUKA) {  // stage-chain form (tog_kuka_jac.hpp)
+        const long long total = B * (long long)(N - 1);
+        hipLaunchKernelGGL((k_kuka_points<M>), dim3(grid(total, 64)), dim3(64), 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_kuka_sjac<M, 0>), dim3(grid(total * 21, 256)), dim3(256), 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_kuka_sjac<M, 1>), dim3(grid(total * 21, 256)), dim3(256), 0, st, P, Bf, total);
+        hipLaunchKernelGGL((k_kuka_chain<M>), dim3((unsigned)total), dim3(64), 0, st, P, Bf, total);
+      }
     } else if (Mb::id == TOG_MODEL_KUKA && integ == TOG_RK3 && Bf.jws) {
-      if constexpr (Mb::id == TOG_MODEL_KUKA) {
+      if constexpr (Mb::id == TOG_MODEL_KUKA) {  // duals through the step, one launch per RK3 stage (A/B)
         constexpr int SW = TOG_JAC_STAGE_W, NCHS = (Mb::n + Mb::m + SW - 1) / SW;
         const long long total = B * (long long)(N - 1) * NCHS;
         const dim3 g(grid(total, 256)), blk(256);

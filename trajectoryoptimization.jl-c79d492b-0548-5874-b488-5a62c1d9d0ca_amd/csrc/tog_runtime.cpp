@@ -759,6 +759,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   if (b.nc < 1) b.nc = 1;
   b.nknots = N;
   b.jws = nullptr;
+  b.jac_chain = (getenv("TOG_KUKA_JAC") && strcmp(getenv("TOG_KUKA_JAC"), "dual") == 0) ? 0 : 1;
   // staged RK3 Jacobian (the RBD model): the stage state of every (knot, partial) lane
   if (ops->jws_per_lane > 0 && d->integrator == TOG_RK3 && !getenv("TOG_JAC_UNSTAGED")) {
     const size_t lanes = B * (size_t)(N - 1) * (size_t)(ops->n + ops->m - ops->slack);
