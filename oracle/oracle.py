@@ -14,6 +14,7 @@ import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
+LIB_LITERAL = HERE / "liboracle_literal.so"  # -DTOG_ORACLE_LITERAL: the reference's own arithmetic
 
 _pkg = sys.modules.get("trajopt_amd")
 if _pkg is None:  # pragma: no cover
@@ -24,6 +25,7 @@ if _pkg is None:  # pragma: no cover
 abi = _pkg.abi
 
 _lib = None
+_lib_literal = None
 
 FIELDS = {"X": abi.FIELD_X, "U": abi.FIELD_U, "Xbar": abi.FIELD_XBAR, "Ubar": abi.FIELD_UBAR, "K": abi.FIELD_K,
           "d": abi.FIELD_D, "A": abi.FIELD_A, "B": abi.FIELD_B, "S": abi.FIELD_S, "Sx": abi.FIELD_SX,
@@ -31,53 +33,62 @@ FIELDS = {"X": abi.FIELD_X, "U": abi.FIELD_U, "Xbar": abi.FIELD_XBAR, "Ubar": ab
           "x0": abi.FIELD_X0, "stats": abi.FIELD_STATS, "rho": abi.FIELD_RHO, "Q": abi.FIELD_Q}
 
 
-def lib():
-    global _lib
+def lib(literal=False):
+    """The contract build (default) or, with ``literal``, the literal-arithmetic build of the oracle."""
+    global _lib, _lib_literal
+    if literal:
+        if _lib_literal is None:
+            _lib_literal = _load(LIB_LITERAL)
+        return _lib_literal
     if _lib is None:
-        if not LIB.exists():
-            subprocess.run(["make"], cwd=HERE, check=True, capture_output=True)
-        L = C.CDLL(str(LIB))
-        vp, dp = C.c_void_p, C.POINTER(C.c_double)
-        L.oc_create.restype = vp
-        L.oc_create.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options)]
-        L.oc_destroy.argtypes = [vp]
-        L.oc_set_state.argtypes = [vp, dp, dp, dp]
-        L.oc_get.argtypes = [vp, C.c_int, dp]
-        L.oc_set.argtypes = [vp, C.c_int, dp]
-        L.oc_pmax.argtypes = [vp]
-        L.oc_rollout_open_loop.argtypes = [vp]
-        L.oc_slack_controls.argtypes = [vp]
-        L.oc_rollout.argtypes = [vp, C.c_double]
-        L.oc_jacobians.argtypes = [vp]
-        L.oc_cost_expansion.argtypes = [vp, C.c_int, C.c_int]
-        L.oc_backward.argtypes = [vp, C.c_int, dp]
-        L.oc_forward.argtypes = [vp, C.c_int, C.c_double]
-        L.oc_forward.restype = C.c_double
-        L.oc_cost.argtypes = [vp, C.c_int]
-        L.oc_cost.restype = C.c_double
-        L.oc_cost_bar.argtypes = [vp, C.c_int]
-        L.oc_cost_bar.restype = C.c_double
-        L.oc_solve_ilqr.argtypes = [vp]
-        L.oc_solve_al.argtypes = [vp]
-        L.oc_update_constraints.argtypes = [vp]
-        L.oc_max_violation.argtypes = [vp]
-        L.oc_max_violation.restype = C.c_double
-        L.oc_get_trace.argtypes = [vp, dp]
-        L.oc_discrete_f.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
-        L.oc_continuous_f.argtypes = [C.c_int, dp, dp, dp]
-        L.oc_discrete_jacobian.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
-        L.oc_cond2.argtypes = [dp, C.c_int]
-        L.oc_cond2.restype = C.c_double
-        L.oc_qr_R.argtypes = [dp, dp, C.c_int, C.c_int]
-        L.oc_solve_pn.argtypes = [vp, C.POINTER(abi.tog_pn_options), dp]
-        L.oc_solve_batch.restype = C.c_int64
-        L.oc_solve_batch.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp, dp,
-                                     C.c_int64, C.c_int]
-        L.oc_solve_batch_timed.restype = C.c_int64
-        L.oc_solve_batch_timed.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp,
-                                           dp, C.c_int64, C.c_int, C.POINTER(C.c_double)]
-        _lib = L
+        _lib = _load(LIB)
     return _lib
+
+
+def _load(path):
+    if not path.exists():
+        subprocess.run(["make"], cwd=HERE, check=True, capture_output=True)
+    L = C.CDLL(str(path))
+    vp, dp = C.c_void_p, C.POINTER(C.c_double)
+    L.oc_create.restype = vp
+    L.oc_create.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options)]
+    L.oc_destroy.argtypes = [vp]
+    L.oc_set_state.argtypes = [vp, dp, dp, dp]
+    L.oc_get.argtypes = [vp, C.c_int, dp]
+    L.oc_set.argtypes = [vp, C.c_int, dp]
+    L.oc_pmax.argtypes = [vp]
+    L.oc_rollout_open_loop.argtypes = [vp]
+    L.oc_slack_controls.argtypes = [vp]
+    L.oc_rollout.argtypes = [vp, C.c_double]
+    L.oc_jacobians.argtypes = [vp]
+    L.oc_cost_expansion.argtypes = [vp, C.c_int, C.c_int]
+    L.oc_backward.argtypes = [vp, C.c_int, dp]
+    L.oc_forward.argtypes = [vp, C.c_int, C.c_double]
+    L.oc_forward.restype = C.c_double
+    L.oc_cost.argtypes = [vp, C.c_int]
+    L.oc_cost.restype = C.c_double
+    L.oc_cost_bar.argtypes = [vp, C.c_int]
+    L.oc_cost_bar.restype = C.c_double
+    L.oc_solve_ilqr.argtypes = [vp]
+    L.oc_solve_al.argtypes = [vp]
+    L.oc_update_constraints.argtypes = [vp]
+    L.oc_max_violation.argtypes = [vp]
+    L.oc_max_violation.restype = C.c_double
+    L.oc_get_trace.argtypes = [vp, dp]
+    L.oc_discrete_f.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
+    L.oc_continuous_f.argtypes = [C.c_int, dp, dp, dp]
+    L.oc_discrete_jacobian.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
+    L.oc_cond2.argtypes = [dp, C.c_int]
+    L.oc_cond2.restype = C.c_double
+    L.oc_qr_R.argtypes = [dp, dp, C.c_int, C.c_int]
+    L.oc_solve_pn.argtypes = [vp, C.POINTER(abi.tog_pn_options), dp]
+    L.oc_solve_batch.restype = C.c_int64
+    L.oc_solve_batch.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp, dp,
+                                 C.c_int64, C.c_int]
+    L.oc_solve_batch_timed.restype = C.c_int64
+    L.oc_solve_batch_timed.argtypes = [C.POINTER(abi.tog_problem_desc), C.POINTER(abi.tog_options), C.c_int, dp,
+                                       dp, C.c_int64, C.c_int, C.POINTER(C.c_double)]
+    return L
 
 
 def _dp(a):
@@ -123,7 +134,8 @@ def qr_R(P):
 class OracleSolver:
     """Single-trajectory oracle solver for trajectory ``b`` of a (possibly batched) Problem."""
 
-    def __init__(self, prob, opts, b=0):
+    def __init__(self, prob, opts, b=0, literal=False):
+        self.L = lib(literal)
         self.prob = prob
         self.n, self.m, self.N = prob.model.n, prob.model.m, prob.N
         self.desc = prob.build_desc()
@@ -132,15 +144,15 @@ class OracleSolver:
         self.mode = abi.MODE_AL if (self.al_requested and prob.is_constrained()) else abi.MODE_ILQR
         if self.al_requested and not prob.is_constrained():
             self.opts = _pkg.to_tog_options(opts.opts_uncon if hasattr(opts, "opts_uncon") else opts.opts_al.opts_uncon)
-        self.s = lib().oc_create(C.byref(self.desc.desc), C.byref(self.opts))
-        self.pmax = lib().oc_pmax(self.s)
+        self.s = self.L.oc_create(C.byref(self.desc.desc), C.byref(self.opts))
+        self.pmax = self.L.oc_pmax(self.s)
         X = prob._X[b]
-        lib().oc_set_state(self.s, _dp(np.ascontiguousarray(prob.x0[b])), _dp(np.ascontiguousarray(prob._U[b])),
+        self.L.oc_set_state(self.s, _dp(np.ascontiguousarray(prob.x0[b])), _dp(np.ascontiguousarray(prob._U[b])),
                            _dp(np.ascontiguousarray(X)) if np.isfinite(X).all() else C.cast(None, C.POINTER(C.c_double)))
 
     def __del__(self):
         try:
-            lib().oc_destroy(self.s)
+            self.L.oc_destroy(self.s)
         except Exception:
             pass
 
@@ -153,7 +165,7 @@ class OracleSolver:
 
     def get(self, name):
         out = np.empty(self.shape(name))
-        lib().oc_get(self.s, FIELDS[name], _dp(out))
+        self.L.oc_get(self.s, FIELDS[name], _dp(out))
         if name in ("K", "A", "B", "S"):
             out = np.ascontiguousarray(np.swapaxes(out, -1, -2))
         return out
@@ -163,58 +175,58 @@ class OracleSolver:
         if name in ("K", "A", "B", "S"):
             v = np.swapaxes(v, -1, -2)
         v = np.ascontiguousarray(v.reshape(self.shape(name)))
-        lib().oc_set(self.s, FIELDS[name], _dp(v))
+        self.L.oc_set(self.s, FIELDS[name], _dp(v))
 
     # step level
     def rollout_open_loop(self):
-        lib().oc_rollout_open_loop(self.s)
+        self.L.oc_rollout_open_loop(self.s)
 
     def rollout(self, alpha):
-        return bool(lib().oc_rollout(self.s, alpha))
+        return bool(self.L.oc_rollout(self.s, alpha))
 
     def slack_controls(self):
-        lib().oc_slack_controls(self.s)
+        self.L.oc_slack_controls(self.s)
 
     def jacobians(self):
-        lib().oc_jacobians(self.s)
+        self.L.oc_jacobians(self.s)
 
     def update_constraints(self):
-        lib().oc_update_constraints(self.s)
+        self.L.oc_update_constraints(self.s)
 
     def cost_expansion(self, sqrt=False, al=False):
-        return lib().oc_cost_expansion(self.s, int(sqrt), int(al))
+        return self.L.oc_cost_expansion(self.s, int(sqrt), int(al))
 
     def backward(self, sqrt=False):
         dV = np.empty(2)
-        restarts = lib().oc_backward(self.s, int(sqrt), _dp(dV))
+        restarts = self.L.oc_backward(self.s, int(sqrt), _dp(dV))
         return dV, restarts
 
     def forward(self, J_prev, al=False):
-        return lib().oc_forward(self.s, int(al), float(J_prev))
+        return self.L.oc_forward(self.s, int(al), float(J_prev))
 
     def cost(self, al=False):
-        return lib().oc_cost(self.s, int(al))
+        return self.L.oc_cost(self.s, int(al))
 
     def solve(self):
         if self.mode == abi.MODE_AL:
-            return lib().oc_solve_al(self.s)
-        return lib().oc_solve_ilqr(self.s)
+            return self.L.oc_solve_al(self.s)
+        return self.L.oc_solve_ilqr(self.s)
 
     def max_violation(self):
-        return lib().oc_max_violation(self.s)
+        return self.L.oc_max_violation(self.s)
 
     def solve_pn(self, pn_opts):
         """solve!(prob, ProjectedNewtonSolver) (projected_newton.jl:6-20) on this trajectory's X, U;
         returns the TOG_PN_NSTATS statistics row."""
         out = np.zeros(abi.PN_NSTATS)
-        rc = lib().oc_solve_pn(self.s, C.byref(_pkg.to_tog_pn_options(pn_opts)), _dp(out))
+        rc = self.L.oc_solve_pn(self.s, C.byref(_pkg.to_tog_pn_options(pn_opts)), _dp(out))
         if rc != 0:
             raise NotImplementedError("projected Newton solve_type :optimal is not built")
         return out
 
     def trace(self):
         out = np.empty((4096, 6))
-        n = lib().oc_get_trace(self.s, _dp(out))
+        n = self.L.oc_get_trace(self.s, _dp(out))
         return out[:n]
 
 

@@ -890,7 +890,9 @@ static void kuka_rk3_jacobian_chain(double* S, const double* x, const double* u,
 
 OC_EXPORT void oc_discrete_jacobian(int model, int integ, double* S, const double* x, const double* u, double dt) {
   discrete_jacobian_fd(model, integ, S, x, u, dt); /* (the dt column) */
+#ifndef TOG_ORACLE_LITERAL /* literal: ForwardDiff through rk3, as the reference */
   if (model == TOG_MODEL_KUKA && integ == TOG_RK3) kuka_rk3_jacobian_chain(S, x, u, dt);
+#endif
 }
 /* forward-mode duals through the integrator for every model (tests: the stage-chain form against it) */
 OC_EXPORT void oc_discrete_jacobian_fd(int model, int integ, double* S, const double* x, const double* u, double dt) {
@@ -938,6 +940,44 @@ static void matmul(double* C, const double* A, int r, int k, const double* B, in
    costs one fma per row for v'y and one for the update. */
 static double sum4(const double* a) { return (a[0] + a[1]) + (a[2] + a[3]); }
 
+#ifdef TOG_ORACLE_LITERAL
+/* Literal mode (TOG_ORACLE_LITERAL, liboracle_literal.so): the reference's own arithmetic
+   where the contract deviates from it. Householder QR as LAPACK's unblocked dgeqr2: dlarfg's
+   normalised reflector (xnorm = dnrm2 as a plain sequential sum of squares, β = -sign(α) dlapy2(α,
+   xnorm), τ = (β-α)/β, x scaled by 1/(α-β)), dlarf's application (w = Cᵀv summed in row order,
+   C -= τ v wᵀ). Julia 1.1's qr(P) calls dgeqrt (compact WY): the same reflectors applied through
+   blocked updates, i.e. this is the reference up to the blocking's rounding. */
+static double dlapy2(double x, double y) {
+  const double xa = fabs(x), ya = fabs(y), w = xa > ya ? xa : ya, z = xa < ya ? xa : ya;
+  if (z == 0.0) return w;
+  const double q = z / w;
+  return w * sqrt(1.0 + q * q);
+}
+static void qr_R(double* R, double* P, int rows, int cols) {
+  int kmax = rows < cols ? rows : cols;
+  for (int j = 0; j < kmax; j++) {
+    double alpha = P[IDX(j, j, rows)];
+    double ss = 0.0;
+    for (int i = j + 1; i < rows; i++) ss = ss + P[IDX(i, j, rows)] * P[IDX(i, j, rows)];
+    const double xnorm = sqrt(ss);
+    if (xnorm == 0.0) continue; /* τ = 0, H = I */
+    const double beta = -copysign(dlapy2(alpha, xnorm), alpha);
+    const double tau = (beta - alpha) / beta;
+    const double sc = 1.0 / (alpha - beta);
+    for (int i = j + 1; i < rows; i++) P[IDX(i, j, rows)] = P[IDX(i, j, rows)] * sc;
+    P[IDX(j, j, rows)] = beta;
+    for (int c = j + 1; c < cols; c++) { /* dlarf: v = [1; x], w = C'v, C = C - τ v w' */
+      double w = P[IDX(j, c, rows)];
+      for (int i = j + 1; i < rows; i++) w = w + P[IDX(i, j, rows)] * P[IDX(i, c, rows)];
+      const double t = -tau * w;
+      P[IDX(j, c, rows)] = P[IDX(j, c, rows)] + t;
+      for (int i = j + 1; i < rows; i++) P[IDX(i, c, rows)] = P[IDX(i, c, rows)] + P[IDX(i, j, rows)] * t;
+    }
+  }
+  for (int j = 0; j < cols; j++)
+    for (int i = 0; i < cols; i++) R[IDX(i, j, cols)] = (i <= j && i < rows) ? P[IDX(i, j, rows)] : 0.0;
+}
+#else
 static void qr_R(double* R, double* P, int rows, int cols) {
   int kmax = rows < cols ? rows : cols;
   for (int j = 0; j < kmax; j++) {
@@ -962,16 +1002,22 @@ static void qr_R(double* R, double* P, int rows, int cols) {
   for (int j = 0; j < cols; j++)
     for (int i = 0; i < cols; i++) R[IDX(i, j, cols)] = (i <= j && i < rows) ? P[IDX(i, j, rows)] : 0.0;
 }
+#endif
 
 /* Triangular solves of the square-root backward pass (contract v2): the diagonal reciprocals are
    formed first (independent divisions) and every substitution step multiplies by them, so the
    dependent chain per step is one multiply instead of one division (x_j = b_j·(1/U_jj)). */
+#ifdef TOG_ORACLE_LITERAL
+#define TOG_RCP_STEP(b, j) ((b) / A[IDX(j, j, n)]) /* literal: substitution by division (BLAS dtrsm) */
+#else
+#define TOG_RCP_STEP(b, j) ((b) * r[j])
+#endif
 static void solve_upper_rcp(const double* A, int n, double* B, int nrhs) { /* A upper: A \ B */
   double r[OM > 16 ? OM : 16];
   for (int j = 0; j < n; j++) r[j] = 1.0 / A[IDX(j, j, n)];
   for (int c = 0; c < nrhs; c++)
     for (int j = n - 1; j >= 0; j--) {
-      double xj = B[IDX(j, c, n)] * r[j];
+      double xj = TOG_RCP_STEP(B[IDX(j, c, n)], j);
       B[IDX(j, c, n)] = xj;
       for (int i = j - 1; i >= 0; i--) B[IDX(i, c, n)] = fma(-A[IDX(i, j, n)], xj, B[IDX(i, c, n)]);
     }
@@ -981,7 +1027,7 @@ static void solve_uppert_rcp(const double* A, int n, double* B, int nrhs) { /* A
   for (int j = 0; j < n; j++) r[j] = 1.0 / A[IDX(j, j, n)];
   for (int c = 0; c < nrhs; c++)
     for (int j = 0; j < n; j++) {
-      double xj = B[IDX(j, c, n)] * r[j];
+      double xj = TOG_RCP_STEP(B[IDX(j, c, n)], j);
       B[IDX(j, c, n)] = xj;
       for (int i = j + 1; i < n; i++) B[IDX(i, c, n)] = fma(-A[IDX(j, i, n)], xj, B[IDX(i, c, n)]);
     }
@@ -1162,6 +1208,28 @@ OC_EXPORT void oc_qr_R(double* R, double* P, int rows, int cols) { qr_R(R, P, ro
 static int chol_minus(double* Uo, const double* A, int n, const double* B, int nb) {
   double U[OM * OM], v[OM], rd[OM];
   memcpy(U, A, sizeof(double) * n * n);
+#ifdef TOG_ORACLE_LITERAL
+  /* literal: lowrankdowndate! (Julia 1.1 LinearAlgebra cholesky.jl) as written: s = v_i / A_ii,
+     c = sqrt(1 - s^2), A_ii = c A_ii, tmp = (A_ij - s v_j) / c, v_j = c v_j - s tmp */
+  (void)rd;
+  for (int r = 0; r < nb; r++) {
+    for (int j = 0; j < n; j++) v[j] = B[IDX(r, j, nb)];
+    for (int i = 0; i < n; i++) {
+      const double s = v[i] / U[IDX(i, i, n)];
+      const double s2 = s * s;
+      if (s2 > 1.0) return i + 1;
+      const double c = sqrt(1.0 - s2);
+      U[IDX(i, i, n)] = c * U[IDX(i, i, n)];
+      for (int j = i + 1; j < n; j++) {
+        const double tmp = (U[IDX(i, j, n)] - s * v[j]) / c;
+        v[j] = c * v[j] - s * tmp;
+        U[IDX(i, j, n)] = tmp;
+      }
+    }
+  }
+  memcpy(Uo, U, sizeof(double) * n * n);
+  return 0;
+#endif
   /* contract v4: the reciprocals of the diagonal are formed once and carried through the downdates
      (1/(c A_ii) = (1/A_ii)(1/c)); 1/c = tog_rsqrt(1 - s^2) and c = (1 - s^2)(1/c) replace the
      reference's sqrt and division by c (include/tog_math.h) */
