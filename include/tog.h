@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define TOG_ABI_VERSION 2
+/* 3: tog_solve_altro / tog_altro_options, TOG_PROB_TF_MIN, TOG_NKERNELS = 4 (tog_profile_read fills 4
+      entries), tog_solve's max_steps <= 0 = the tog_solve_budget default */
+#define TOG_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status */
 enum tog_status_code {
@@ -126,7 +128,11 @@ enum tog_problem_flag {
      dt_k = h_k²), objective MinTimeCost with weight R_min_time (Q, R, H, q, r, Qf, qf the base cost's,
      zero-padded to n, m), constraints from mintime_constraints (h bounds in the BoundConstraint,
      TOG_CON_MIN_TIME_EQ rows). Std backward pass only (there is no sqrt MinTimeCost expansion). */
-  TOG_PROB_MIN_TIME = 2
+  TOG_PROB_MIN_TIME = 2,
+  /* tf = 0 (src/problem.jl:174-178): the final time is free and dt is the initial time step. Accepted by
+     tog_solve_altro only, which solves it as minimum_time_problem (ALTROSolverOptions R_minimum_time,
+     dt_max, dt_min); tog_create refuses it. */
+  TOG_PROB_TF_MIN = 4
 };
 
 typedef struct tog_constraint {
@@ -437,6 +443,41 @@ enum tog_pn_stat {
    of S + 1e-2 I, chord-method line searches with reg_solve refinement to |r| < 1e-8).
    out: (TOG_PN_NSTATS, B) host pointer or NULL. */
 int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out);
+
+/* ---- ALTRO (src/solvers/altro/altro_methods.jl:2-124) ---- */
+/* ALTROSolverOptions (src/solvers/altro/altro_solver.jl:6-65), its live fields; tog_default_altro_options
+   fills the reference defaults. opts_al is AugmentedLagrangianSolverOptions with its opts_uncon. */
+typedef struct tog_altro_options {
+  tog_options opts_al;
+  double R_inf;                         /* 1.0   infeasible_problem(prob, R_inf)                      */
+  double R_minimum_time;                /* 1.0   minimum_time_problem                                 */
+  double dt_max;                        /* 1.0                                                        */
+  double dt_min;                        /* 1e-3                                                       */
+  double projected_newton_tolerance;    /* 1e-3  AL constraint tolerance before projected Newton      */
+  int32_t dynamically_feasible_projection; /* 1 */
+  int32_t resolve_feasible_problem;     /* 1 */
+  int32_t projected_newton;             /* 0 */
+  int32_t reserved;
+  tog_pn_options opts_pn;
+} tog_altro_options;
+void tog_default_altro_options(tog_altro_options* opts);
+/* solve!(prob, ALTROSolverOptions) (altro_methods.jl:2-53): altro_problem (:98-124) transforms `desc`, the
+   original problem (flags 0 or TOG_PROB_TF_MIN), into the infeasible-start problem when X holds an initial
+   state trajectory (X not all NaN at the first knot, every trajectory of the batch or none;
+   infeasible_problem, infeasible.jl:2-33) or into the minimum-time problem when TOG_PROB_TF_MIN is set
+   (minimum_time_problem, minimum_time.jl:2-34); runs the AL solve on `device` (projected Newton after it
+   when opts->projected_newton), and process_results! (:56-95) writes the model states and controls back:
+   X (n, N, B) in/out (NULL: no initial trajectory), U (m, N-1, B) in/out, h (N-1, B) the time steps of a
+   minimum-time solve (dt_k = h_k^2) or NULL. With resolve_feasible_problem the infeasible solve is followed
+   by the feasible problem's solve from its controls. stats (TOG_NSTATS, B): the AL phase's statistics
+   (the infeasible / minimum-time problem's solve); stats_resolve (TOG_NSTATS, B): the feasible resolve;
+   stats_pn (TOG_PN_NSTATS, B): projected Newton; each may be NULL. Host pointers, blocking. A trajectory
+   whose forward pass reported TOG_TRAJ_COST_INCREASED (the reference's error) carries the flag in its
+   stats row. Not built: infeasible start + minimum time, projected Newton on those problems
+   (TOG_ERR_UNSUPPORTED). */
+int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
+                        const double* x0, double* X, double* U, double* h, double* stats, double* stats_resolve,
+                        double* stats_pn);
 
 /* per-kernel timing with HIP events recorded on the handle's stream around every launch issued by
    tog_solve_step (used by bench.py for the live roofline). */

@@ -19,14 +19,16 @@ using Parameters
 const libtog = get(ENV, "TOG_LIB", "libtog.so")
 
 # ------------------------------------------------------------------------ include/tog.h mirrors
+const TOG_ABI_VERSION = Int32(3)    # include/tog.h; checked against tog_version() at first use
 const TOG_OK = Int32(0)
 const TOG_RK3, TOG_RK4, TOG_MIDPOINT, TOG_RK3_IMPLICIT, TOG_MIDPOINT_IMPLICIT = Int32.(0:4)
 const TOG_CON_BOUND, TOG_CON_GOAL, TOG_CON_CIRCLES, TOG_CON_SPHERES, TOG_CON_INFEASIBLE, TOG_CON_USER,
       TOG_CON_MIN_TIME_EQ = Int32.(0:6)
-const TOG_PROB_INFEASIBLE, TOG_PROB_MIN_TIME = Int32(1), Int32(2)
+const TOG_PROB_INFEASIBLE, TOG_PROB_MIN_TIME, TOG_PROB_TF_MIN = Int32(1), Int32(2), Int32(4)
 const TOG_MODE_ILQR, TOG_MODE_AL = Int32(0), Int32(1)
 const TOG_FIELD_X, TOG_FIELD_U, TOG_FIELD_RHO, TOG_FIELD_STATS = Int32(0), Int32(1), Int32(16), Int32(15)
 const TOG_NSTATS = 14
+const TOG_PN_NSTATS = 7
 const TOG_STAT_J, TOG_STAT_ITERATIONS, TOG_STAT_C_MAX, TOG_STAT_AL_ITER, TOG_STAT_TOTAL_STEPS,
       TOG_STAT_FLAGS = 0, 3, 7, 8, 9, 12
 const TOG_TRAJ_COST_INCREASED = Int32(1 << 3)
@@ -51,6 +53,14 @@ struct TogProblemDesc
     user_model::Ptr{Cvoid}
     R_min_time::Float64
 end
+# Layout pins (tests/test_julia_layout.py checks these numbers, and the field lists below, against
+# include/tog.h compiled by gcc): sizeof and field offsets of the mirrored structs. tog_check_layout()
+# asserts them in Julia at first use.
+const TOG_LAYOUT = (tog_constraint = 16, tog_constraint_set = 16, tog_problem_desc = 152, tog_options = 200,
+                    tog_pn_options = 24, tog_altro_options = 280)
+const TOG_DESC_OFFSETS = (0, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64, 72, 80, 88, 96, 104, 112, 116, 120,
+                          128, 136, 144)
+
 mutable struct TogOptions          # field order = tog_options
     cost_tolerance::Float64; gradient_norm_tolerance::Float64
     iterations::Int32; dJ_counter_limit::Int32; square_root::Int32; bp_reg_type::Int32
@@ -67,6 +77,55 @@ mutable struct TogOptions          # field order = tog_options
         ccall((:tog_default_options, libtog), Cvoid, (Ref{TogOptions},), o)
         return o
     end
+end
+
+"The same fields, immutable (inline inside tog_altro_options)."
+struct TogOptionsI
+    cost_tolerance::Float64; gradient_norm_tolerance::Float64
+    iterations::Int32; dJ_counter_limit::Int32; square_root::Int32; bp_reg_type::Int32
+    gradient_type::Int32; iterations_linesearch::Int32
+    line_search_lower_bound::Float64; line_search_upper_bound::Float64
+    bp_reg_increase_factor::Float64; bp_reg_max::Float64; bp_reg_min::Float64; bp_reg_fp::Float64
+    max_cost_value::Float64; max_state_value::Float64; max_control_value::Float64
+    al_cost_tolerance::Float64; al_cost_tolerance_intermediate::Float64
+    al_gradient_norm_tolerance::Float64; al_gradient_norm_tolerance_intermediate::Float64
+    constraint_tolerance::Float64; dual_min::Float64; dual_max::Float64; penalty_max::Float64
+    penalty_initial::Float64; penalty_scaling::Float64; al_iterations::Int32; kickout_max_penalty::Int32
+end
+TogOptionsI(o::TogOptions) = TogOptionsI((getfield(o, f) for f in fieldnames(TogOptions))...)
+struct TogPNOptions                # = tog_pn_options
+    n_steps::Int32; solve_type::Int32; active_set_tolerance::Float64; feasibility_tolerance::Float64
+end
+mutable struct TogAltroOptions     # = tog_altro_options
+    opts_al::TogOptionsI
+    R_inf::Float64; R_minimum_time::Float64; dt_max::Float64; dt_min::Float64
+    projected_newton_tolerance::Float64
+    dynamically_feasible_projection::Int32; resolve_feasible_problem::Int32; projected_newton::Int32
+    reserved::Int32
+    opts_pn::TogPNOptions
+    function TogAltroOptions()
+        a = new()
+        ccall((:tog_default_altro_options, libtog), Cvoid, (Ref{TogAltroOptions},), a)
+        return a
+    end
+end
+
+const TOG_CHECKED = Ref(false)
+"ABI version and struct layouts, once per session."
+function tog_check_layout()
+    TOG_CHECKED[] && return nothing
+    v = ccall((:tog_version, libtog), Int32, ())
+    v == TOG_ABI_VERSION || error("libtog ABI version $v, this binding expects $TOG_ABI_VERSION")
+    sizeof(TogConstraint) == TOG_LAYOUT.tog_constraint || error("tog_constraint layout")
+    sizeof(TogConstraintSet) == TOG_LAYOUT.tog_constraint_set || error("tog_constraint_set layout")
+    sizeof(TogProblemDesc) == TOG_LAYOUT.tog_problem_desc || error("tog_problem_desc layout")
+    Tuple(Int(fieldoffset(TogProblemDesc, i)) for i = 1:fieldcount(TogProblemDesc)) == TOG_DESC_OFFSETS ||
+        error("tog_problem_desc field offsets")
+    sizeof(TogOptionsI) == TOG_LAYOUT.tog_options || error("tog_options layout")
+    sizeof(TogPNOptions) == TOG_LAYOUT.tog_pn_options || error("tog_pn_options layout")
+    sizeof(TogAltroOptions) == TOG_LAYOUT.tog_altro_options || error("tog_altro_options layout")
+    TOG_CHECKED[] = true
+    return nothing
 end
 
 togcheck(rc) = rc == TOG_OK ? nothing :
@@ -201,7 +260,8 @@ stage and terminal cost (column-major copies), and the per-knot ConstraintSets f
 tog_constraint entries in the order of the knot's constraint vector (labels in insertion order,
 src/constraint_sets.jl:64-94). Knots whose ConstraintSet is the same object share one table entry.
 """
-function tog_desc(prob::Problem; batch::Integer=1, R_min_time::Real=0.0)
+function tog_desc(prob::Problem; batch::Integer=1, R_min_time::Real=0.0, tf_min::Bool=false)
+    tog_check_layout()
     model = prob.model
     n, m, N = model.n, model.m, prob.N
     id, user, flags = tog_model_id(model)
@@ -232,6 +292,7 @@ function tog_desc(prob::Problem; batch::Integer=1, R_min_time::Real=0.0)
         knot_set[k] = set_ids[C]
     end
     push!(keep, sets); push!(keep, knot_set)
+    tf_min && (flags |= TOG_PROB_TF_MIN)   # tf = 0: tog_solve_altro builds minimum_time_problem
     d = TogProblemDesc(id, tog_integrator(model), Int32(n), Int32(m), Int32(N), flags, Int64(batch),
                        Float64(prob.dt), pointer(Q), pointer(R), pointer(H), pointer(q), pointer(r),
                        Float64(ℓ.c), pointer(Qf), pointer(qf), Float64(ℓN.c), Int32(length(sets)), Int32(0),
@@ -383,3 +444,75 @@ copy(s::BatchediLQRSolver{T}) where T = _tog_solver(s.desc, deepcopy(s.opts), s.
 size(s::BatchediLQRSolver) = (s.n, s.m, s.N)
 
 solver_name(::BatchediLQRSolverOptions) = "libtog batched iLQR"
+
+# ------------------------------------------------------------------------ ALTRO
+"ALTROSolverOptions (src/solvers/altro/altro_solver.jl:6-65) -> tog_altro_options."
+function tog_altro_options(opts::ALTROSolverOptions)
+    a = TogAltroOptions()
+    a.opts_al = TogOptionsI(tog_options(opts.opts_al))
+    a.R_inf = opts.R_inf; a.R_minimum_time = opts.R_minimum_time
+    a.dt_max = opts.dt_max; a.dt_min = opts.dt_min
+    a.projected_newton_tolerance = opts.projected_newton_tolerance
+    a.dynamically_feasible_projection = opts.dynamically_feasible_projection
+    a.resolve_feasible_problem = opts.resolve_feasible_problem
+    a.projected_newton = opts.projected_newton
+    pn = opts.opts_pn
+    pn.solve_type == :feasible || throw(ArgumentError("projected Newton solve_type $(pn.solve_type) is not built"))
+    a.opts_pn = TogPNOptions(Int32(pn.n_steps), Int32(0), pn.active_set_tolerance, pn.feasibility_tolerance)
+    return a
+end
+
+"Route solve!(prob, ::ALTROSolverOptions) to libtog (false: the reference's Julia solver)."
+const TOG_ALTRO = Ref(true)
+
+"""
+    solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float64})
+
+The reference's ALTRO entry (src/solvers/altro/altro_methods.jl:2-53; README.md:32-67's quick start),
+more specific than its `solve!(::Problem{T,Discrete}, ::ALTROSolverOptions)`, so a Float64 problem on a
+libtog model reaches tog_solve_altro: altro_problem (an initial state trajectory -> infeasible_problem; tf = 0
+-> minimum_time_problem), the AL solve on the GPU, projected Newton, process_results! and the feasible
+resolve run in libtog (csrc/tog_altro.cpp). prob.X, prob.U are written in place; a minimum-time solve leaves
+prob.U[k] = [u; u; h] as the reference's process_results! does. Returns solver stats in a Dict.
+"""
+function solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float64})
+    if !TOG_ALTRO[]
+        return invoke(solve!, Tuple{Problem{Float64,Discrete},ALTROSolverOptions}, prob, opts)
+    end
+    if opts.projected_newton   # altro_methods.jl:5-13 (mutates opts_al, as the reference does)
+        if opts.projected_newton_tolerance >= 0
+            opts.opts_al.constraint_tolerance = opts.projected_newton_tolerance
+        else
+            opts.opts_al.constraint_tolerance = 0
+            opts.opts_al.kickout_max_penalty = true
+        end
+    end
+    n, m, N = prob.model.n, prob.model.m, prob.N
+    tf_min = prob.tf == 0.0
+    desc = tog_desc(prob; batch=1, tf_min=tf_min)
+    a = tog_altro_options(opts)
+    x0 = Vector{Float64}(prob.x0)
+    X = Matrix{Float64}(undef, n, N)
+    for k = 1:N; X[:, k] = prob.X[k]; end      # all NaN (empty_state): no infeasible start
+    U = Matrix{Float64}(undef, m, N - 1)
+    for k = 1:N-1; U[:, k] = prob.U[k]; end
+    h = Vector{Float64}(undef, N - 1)
+    St, Sr = zeros(TOG_NSTATS), zeros(TOG_NSTATS)
+    Spn = zeros(TOG_PN_NSTATS)
+    togcheck(ccall((:tog_solve_altro, libtog), Int32,
+                   (Ref{TogProblemDesc}, Ref{TogAltroOptions}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                   desc.desc, a, Int32(0), x0, X, U, h, St, Sr, Spn))
+    copyto!(prob.X, [X[:, k] for k = 1:N])
+    if tf_min   # process_results! (altro_methods.jl:81-85): U[k] = [u; u; h]
+        for k = 1:N-1; prob.U[k] = [U[:, k]; U[:, k]; h[k]]; end
+    else
+        copyto!(prob.U, [U[:, k] for k = 1:N-1])
+    end
+    flags = Int32(St[TOG_STAT_FLAGS+1]) | Int32(Sr[TOG_STAT_FLAGS+1])
+    flags & TOG_TRAJ_COST_INCREASED != 0 && error("Cost increased during Forward Pass")  # forward_pass.jl:80-82
+    return Dict{Symbol,Any}(:iterations => Int(St[TOG_STAT_TOTAL_STEPS+1]), :cost => St[TOG_STAT_J+1],
+                            :c_max => St[TOG_STAT_C_MAX+1], :iterations_outer => Int(St[TOG_STAT_AL_ITER+1]),
+                            :flags => flags, :iterations_resolve => Int(Sr[TOG_STAT_TOTAL_STEPS+1]),
+                            :projected_newton => Spn)
+end

@@ -207,6 +207,10 @@ class OracleSolver:
     def cost(self, al=False):
         return self.L.oc_cost(self.s, int(al))
 
+    def cost_bar(self, al=False):
+        """cost of the last rollout's X̄, Ū"""
+        return self.L.oc_cost_bar(self.s, int(al))
+
     def solve(self):
         if self.mode == abi.MODE_AL:
             return self.L.oc_solve_al(self.s)

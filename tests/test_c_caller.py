@@ -11,6 +11,7 @@ import pytest
 
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 BIN = ROOT / "tests" / "c" / "test_capi_config3"
+BIN_ALTRO = ROOT / "tests" / "c" / "test_capi_altro"
 
 
 def test_c_caller_links_the_library(tog):
@@ -45,3 +46,37 @@ def test_c_caller_equals_python_path(tog, gpu, tmp_path):
     assert np.array_equal(X_c, gpu._X), np.max(np.abs(X_c - gpu._X))
     assert np.array_equal(U_c, gpu._U), np.max(np.abs(U_c - gpu._U))
     assert np.array_equal(St_c, St_py)
+
+
+@pytest.mark.gpu
+def test_c_caller_altro_equals_python_path(tog, gpu, tmp_path):
+    """tog_solve_altro from C (tests/c/test_capi_altro.c: the quadrotor_maze ALTRO case of
+    test/infeasible_tests.jl:57-76 as libtog.jl marshals it, an infeasible start from a state guess) equals
+    solve_b(prob, ALTROSolverOptions) from Python bit for bit, on B = 4 jittered way-point guesses."""
+    assert BIN_ALTRO.exists(), "tests/c/test_capi_altro not built: __graft_entry__.build() builds it"
+    B = 4
+    p0 = tog.Problems.quadrotor_maze()
+    n, m, N = 13, 4, p0.N
+    guesses = [tog.problems._maze_guess(N, 5.0, p0.x0[0], p0.xf, tog.problems._MAZE_WAYPOINTS + 0.5 *
+                                        np.random.default_rng(5000 + b).standard_normal((3, 5))) for b in range(B)]
+    prob = tog.Problem(p0.model, p0.obj, np.repeat(p0._U, B, axis=0), constraints=p0.constraints,
+                       x0=np.repeat(p0.x0, B, axis=0), xf=p0.xf, N=N, dt=p0.dt)
+    prob._X[...] = np.stack(guesses)
+    with open(tmp_path / "in.bin", "wb") as f:
+        f.write(np.int64(B).tobytes())
+        f.write(np.ascontiguousarray(prob.x0).tobytes())
+        f.write(np.ascontiguousarray(prob._U).tobytes())
+        f.write(np.ascontiguousarray(prob._X).tobytes())
+    r = subprocess.run([str(BIN_ALTRO), str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = np.fromfile(tmp_path / "out.bin", dtype=np.float64)
+    X_c = out[:B * N * n].reshape(B, N, n)
+    U_c = out[B * N * n:B * N * n + B * (N - 1) * m].reshape(B, N - 1, m)
+    St_c = out[B * N * n + B * (N - 1) * m:].reshape(B, tog.abi.NSTATS)
+    gp = prob.copy()
+    solver = tog.solve_b(gp, tog.Problems.maze_altro_options())
+    assert np.array_equal(X_c, gp._X), np.max(np.abs(X_c - gp._X))
+    assert np.array_equal(U_c, gp._U), np.max(np.abs(U_c - gp._U))
+    assert np.array_equal(St_c[:, tog.abi.STAT_TOTAL_STEPS], solver.stats["iterations_total"])
+    assert np.array_equal(St_c[:, tog.abi.STAT_FLAGS].astype(np.int64), solver.stats["flags"])

@@ -16,7 +16,7 @@ import numpy as np
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "csrc" / "libtog.so"
 
-TOG_ABI_VERSION = 2
+TOG_ABI_VERSION = 3
 
 # models (include/tog.h tog_model_id)
 MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM, MODEL_KUKA = range(6)
@@ -29,6 +29,7 @@ RK3, RK4, MIDPOINT, RK3_IMPLICIT, MIDPOINT_IMPLICIT = 0, 1, 2, 3, 4
 CON_BOUND, CON_GOAL, CON_CIRCLES, CON_SPHERES, CON_INFEASIBLE, CON_USER, CON_MIN_TIME_EQ = range(7)
 PROB_INFEASIBLE = 1  # tog_problem_flag
 PROB_MIN_TIME = 2
+PROB_TF_MIN = 4  # tf = 0: tog_solve_altro solves minimum_time_problem
 MODE_ILQR, MODE_AL = 0, 1
 
 (FIELD_X, FIELD_U, FIELD_XBAR, FIELD_UBAR, FIELD_K, FIELD_D, FIELD_A, FIELD_B, FIELD_S, FIELD_SX,
@@ -103,6 +104,14 @@ class tog_pn_options(C.Structure):
     """ProjectedNewtonSolverOptions (src/solvers/direct/direct_solvers.jl:14-30)."""
     _fields_ = [("n_steps", C.c_int32), ("solve_type", C.c_int32), ("active_set_tolerance", C.c_double),
                 ("feasibility_tolerance", C.c_double)]
+
+
+class tog_altro_options(C.Structure):
+    """ALTROSolverOptions (src/solvers/altro/altro_solver.jl:6-65), the live fields."""
+    _fields_ = [("opts_al", tog_options), ("R_inf", C.c_double), ("R_minimum_time", C.c_double),
+                ("dt_max", C.c_double), ("dt_min", C.c_double), ("projected_newton_tolerance", C.c_double),
+                ("dynamically_feasible_projection", C.c_int32), ("resolve_feasible_problem", C.c_int32),
+                ("projected_newton", C.c_int32), ("reserved", C.c_int32), ("opts_pn", tog_pn_options)]
 
 
 def default_options() -> tog_options:
@@ -272,6 +281,9 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_solve_al.argtypes = [vp]
     lib.tog_default_pn_options.argtypes = [C.POINTER(tog_pn_options)]
     lib.tog_solve_pn.argtypes = [vp, C.POINTER(tog_pn_options), _dp]
+    lib.tog_default_altro_options.argtypes = [C.POINTER(tog_altro_options)]
+    lib.tog_solve_altro.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_altro_options), C.c_int32, _dp, _dp,
+                                    _dp, _dp, _dp, _dp, _dp]
     lib.tog_model_load.argtypes = [C.c_char_p, C.POINTER(vp)]
     lib.tog_model_dims.argtypes = [vp, _ip, _ip]
     lib.tog_model_free.argtypes = [vp]
@@ -288,7 +300,7 @@ def load_library(path: os.PathLike | None = None):
                  "tog_profile", "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
                  "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn", "tog_model_load", "tog_model_dims",
                  "tog_model_free", "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device",
-                 "tog_generic_cost_free"):
+                 "tog_generic_cost_free", "tog_solve_altro"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -307,6 +319,7 @@ EXPORTED_SYMBOLS = (
     "tog_profile_read", "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
     "tog_solve_al", "tog_default_pn_options", "tog_solve_pn", "tog_model_load", "tog_model_dims", "tog_model_free",
     "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device", "tog_generic_cost_free",
+    "tog_default_altro_options", "tog_solve_altro",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD, KERNEL_EXPANSION = 0, 1, 2, 3
 NKERNELS = 4

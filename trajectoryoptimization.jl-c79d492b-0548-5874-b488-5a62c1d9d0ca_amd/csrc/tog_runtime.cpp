@@ -361,6 +361,8 @@ __global__ void k_reset_state(TrajState* st, long long B, double mu0) {
 extern "C" {
 
 int32_t tog_version(void) { return TOG_ABI_VERSION; }
+// (internal) the error path of tog_altro.cpp: records the message for tog_last_error
+int32_t tog__fail(int32_t code, const char* msg) { return fail(code, msg); }
 
 int32_t tog_model_load(const char* path, tog_model** out) {
   if (!path || !out) return fail(TOG_ERR_ARG, "null argument");

@@ -185,14 +185,18 @@ class BatchHandle:
         return f
 
     def stats_dict(self):
-        S = self.get(abi.FIELD_STATS)
-        return {
-            "cost": S[:, abi.STAT_J], "dJ": S[:, abi.STAT_DJ], "gradient": S[:, abi.STAT_GRADIENT],
-            "iterations": S[:, abi.STAT_ITERATIONS].astype(np.int64),
-            "dJ_zero_counter": S[:, abi.STAT_ZERO_COUNT].astype(np.int64),
-            "alpha": S[:, abi.STAT_ALPHA], "c_max": S[:, abi.STAT_C_MAX],
-            "iterations_outer": S[:, abi.STAT_AL_ITER].astype(np.int64),
-            "iterations_total": S[:, abi.STAT_TOTAL_STEPS].astype(np.int64),
-            "penalty_max": S[:, abi.STAT_PENALTY_MAX],
-            "flags": S[:, abi.STAT_FLAGS].astype(np.int64),
-        }
+        return stats_dict(self.get(abi.FIELD_STATS))
+
+
+def stats_dict(S):
+    """solver.stats from the (B, TOG_NSTATS) statistics rows (TOG_FIELD_STATS)."""
+    return {
+        "cost": S[:, abi.STAT_J], "dJ": S[:, abi.STAT_DJ], "gradient": S[:, abi.STAT_GRADIENT],
+        "iterations": S[:, abi.STAT_ITERATIONS].astype(np.int64),
+        "dJ_zero_counter": S[:, abi.STAT_ZERO_COUNT].astype(np.int64),
+        "alpha": S[:, abi.STAT_ALPHA], "c_max": S[:, abi.STAT_C_MAX],
+        "iterations_outer": S[:, abi.STAT_AL_ITER].astype(np.int64),
+        "iterations_total": S[:, abi.STAT_TOTAL_STEPS].astype(np.int64),
+        "penalty_max": S[:, abi.STAT_PENALTY_MAX],
+        "flags": S[:, abi.STAT_FLAGS].astype(np.int64),
+    }

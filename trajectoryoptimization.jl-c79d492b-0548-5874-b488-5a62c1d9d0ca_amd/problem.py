@@ -859,7 +859,9 @@ class Problem:
         return self.constraints.is_constrained()
 
     # ---- marshalling to the C ABI
-    def build_desc(self) -> abi.DescBuilder:
+    def build_desc(self, tf_min: bool = False) -> abi.DescBuilder:
+        """The C ABI's tog_problem_desc. ``tf_min``: mark a tf = 0 problem TOG_PROB_TF_MIN (the original
+        problem handed to tog_solve_altro, which builds minimum_time_problem itself)."""
         n, m, N = self.model.n, self.model.m, self.N
         stage, term = self.obj.stage, self.obj.terminal
         sets, knot_set, keys = [], [], {}
@@ -876,6 +878,8 @@ class Problem:
             knot_set.append(keys[key])
         R = stage.R if stage.R.size else np.zeros((m, m))
         flags = (abi.PROB_INFEASIBLE if self.model.slack else 0) | (abi.PROB_MIN_TIME if self.model.min_time else 0)
+        if tf_min and not self.model.min_time:
+            flags |= abi.PROB_TF_MIN
         return abi.DescBuilder(self.model.model_id, self.model.integration, n, m, N, self.dt, stage.Q, R, stage.H,
                                stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B,
                                flags=flags, user_model=self.model.plugin.ptr if self.model.plugin else None,

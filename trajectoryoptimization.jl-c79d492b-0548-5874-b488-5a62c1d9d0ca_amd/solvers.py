@@ -18,8 +18,9 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import abi
-from .device import BatchHandle
-from .problem import infeasible_problem
+import ctypes as C
+
+from .device import BatchHandle, stats_dict
 
 
 # ----------------------------------------------------------------------------- options
@@ -387,64 +388,64 @@ def _altro_infeasible(prob) -> bool:
     return bool(given.all())
 
 
-def _solve_altro_infeasible(prob, opts, max_steps, device):
-    """``solve!(prob, ::ALTROSolverOptions)`` with an initial state trajectory
-    (altro_methods.jl:2-124):
+def to_tog_altro_options(opts: ALTROSolverOptions) -> abi.tog_altro_options:
+    """ALTROSolverOptions -> the C ABI's ``tog_altro_options`` (its live fields)."""
+    a = abi.tog_altro_options()
+    a.opts_al = to_tog_options(opts.opts_al)
+    a.R_inf = float(opts.R_inf)
+    a.R_minimum_time = float(opts.R_minimum_time)
+    a.dt_max = float(opts.dt_max)
+    a.dt_min = float(opts.dt_min)
+    a.projected_newton_tolerance = float(opts.projected_newton_tolerance)
+    a.dynamically_feasible_projection = int(bool(opts.dynamically_feasible_projection))
+    a.resolve_feasible_problem = int(bool(opts.resolve_feasible_problem))
+    a.projected_newton = int(bool(opts.projected_newton))
+    a.opts_pn = to_tog_pn_options(opts.opts_pn) if opts.projected_newton else abi.tog_pn_options(1, 0, 1e-3, 1e-6)
+    return a
 
-    1. ``infeasible_problem(prob, R_inf)`` and its AL solve from the given X, with the slack controls
-       from ``slack_controls`` (computed on the device, infeasible.jl:63-80);
-    2. ``process_results!``: X and the model controls U[1:m] go back to ``prob``;
-    3. with ``resolve_feasible_problem``, the feasible problem is solved again by AL (iLQR when it
-       is unconstrained, augmented_lagrangian_methods.jl:33-36) from those controls. With
-       ``dynamically_feasible_projection`` it starts from ``projection!``'s trajectory. In this
-       snapshot ``projection!`` runs ``backwardpass!`` on a freshly constructed iLQR solver: ∇F and
-       the Q expansion are zero, so after one regularisation restart K = d = -0.0 and the α = 0
-       rollout is the open-loop rollout of U from x0 (ilqr_methods.jl:179-190, backward_pass.jl:9-85,
-       DESIGN.md §8). The device does exactly that: X = NaN triggers ``rollout!(prob)``.
-    Without resolve, ``prob`` keeps the infeasible solve's X (the projection is discarded).
-    """
-    m = prob.model.m
-    prob_inf = infeasible_problem(prob, opts.R_inf)
-    solver = ALTROSolver(prob_inf, opts, device=device)
-    h = solver.handle
-    h.slack_controls()
-    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None else h.solve_budget(abi.MODE_AL))
-    h.download_state(prob_inf)
-    solver.stats = h.stats_dict()
-    solver.prob_infeasible = prob_inf
-    prob._X[...] = prob_inf._X
-    prob._U[...] = prob_inf._U[:, :, :m]
-    if np.any(solver.stats["flags"] & abi.TRAJ_COST_INCREASED):
+
+def _solve_altro(prob, opts: ALTROSolverOptions, device: int):
+    """``solve!(prob, ::ALTROSolverOptions)`` (altro_methods.jl:2-124) through ``tog_solve_altro``: the C
+    ABI runs altro_problem (an initial state trajectory -> infeasible_problem, infeasible.jl:2-33; tf = 0 ->
+    minimum_time_problem, minimum_time.jl:2-34), the AL solve, projected Newton, process_results! and the
+    feasible resolve (csrc/tog_altro.cpp), so the Julia binding and C callers reach the same flow.
+
+    The returned solver carries ``stats`` (the AL phase: the infeasible / minimum-time problem's solve),
+    ``stats_feasible`` (the resolve of an infeasible start), ``stats_pn`` (projected Newton); a
+    minimum-time solve's time steps go to ``prob.h`` (the reference stores [u; u; h] in prob.U) and
+    ``total_time(prob)`` reads them."""
+    lib = abi.load_library()
+    infeasible = _altro_infeasible(prob)
+    desc = prob.build_desc(tf_min=prob.tf == 0.0)
+    a = to_tog_altro_options(opts)
+    B, N, n, m = prob.B, prob.N, prob.model.n, prob.model.m
+    x0 = np.ascontiguousarray(prob.x0, dtype=np.float64)
+    X = np.ascontiguousarray(prob._X, dtype=np.float64) if infeasible else np.full((B, N, n), np.nan)
+    U = np.ascontiguousarray(prob._U, dtype=np.float64)
+    h = np.zeros((B, N - 1))
+    St = np.zeros((B, abi.NSTATS))
+    St_res = np.zeros((B, abi.NSTATS))
+    pn = np.zeros((B, abi.PN_NSTATS))
+    abi.check(lib, lib.tog_solve_altro(C.byref(desc.desc), C.byref(a), int(device), abi.as_dp(x0), abi.as_dp(X),
+                                       abi.as_dp(U), abi.as_dp(h), abi.as_dp(St), abi.as_dp(St_res), abi.as_dp(pn)))
+    prob._X[...] = X
+    prob._U[...] = U
+    solver = ALTROSolver.__new__(ALTROSolver)
+    solver.opts, solver.handle = opts, None
+    solver.n, solver.m, solver.N = n, m, N
+    solver.stats = stats_dict(St)
+    if prob.tf == 0.0:
+        prob.h = h
+    if infeasible and opts.resolve_feasible_problem:
+        solver.stats_feasible = stats_dict(St_res)
+    flags = solver.stats["flags"] | (solver.stats_feasible["flags"] if hasattr(solver, "stats_feasible") else 0)
+    if np.any(flags & abi.TRAJ_COST_INCREASED):
         raise RuntimeError("Error: Cost increased during Forward Pass")
-    if opts.resolve_feasible_problem:
-        if opts.dynamically_feasible_projection:
-            prob._X[...] = np.nan
-        feasible = solve_b(prob, opts.opts_al, max_steps=max_steps, device=device)
-        solver.stats_feasible = feasible.stats
-    return solver
-
-
-def _solve_altro_min_time(prob, opts, max_steps, device):
-    """``solve!(prob, ::ALTROSolverOptions)`` for tf = 0 (altro_methods.jl:98-124, 55-95):
-    ``minimum_time_problem(prob, R_minimum_time, dt_max, dt_min)``, its AL solve (std backward pass:
-    MinTimeCost has no square-root expansion), then ``process_results!``: X[1:n] and U[1:m] go back to
-    ``prob``. The reference stores [u; u; h] in prob.U (its U[k][end] is h); here the time steps go to
-    ``prob.h`` and ``total_time(prob)`` reads them."""
-    from .problem import minimum_time_problem
-
-    n, m = prob.model.n, prob.model.m
-    pmt = minimum_time_problem(prob, opts.R_minimum_time, opts.dt_max, opts.dt_min)
-    solver = ALTROSolver(pmt, opts, device=device)
-    h = solver.handle
-    h.solve(abi.MODE_AL, max_steps=max_steps if max_steps is not None else h.solve_budget(abi.MODE_AL))
-    h.download_state(pmt)
-    solver.stats = h.stats_dict()
-    solver.prob_min_time = pmt
-    if np.any(solver.stats["flags"] & abi.TRAJ_COST_INCREASED):
-        raise RuntimeError("Error: Cost increased during Forward Pass")
-    prob._X[...] = pmt._X[:, :, :n]
-    prob._U[...] = pmt._U[:, :, :m]
-    prob.h = pmt._U[:, :, m].copy()
+    if opts.projected_newton:
+        solver.stats_pn = _pn_stats(pn, solver.stats["flags"])
+        if np.any(solver.stats["flags"] & abi.TRAJ_PN_ERROR):
+            raise RuntimeError("projected Newton: line search did not reduce the violation "
+                               "(the reference's _projection_linesearch! raises here)")
     return solver
 
 
@@ -463,13 +464,10 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
             return _solve_pn(prob, ProjectedNewtonSolver(prob, opts, device=device))
         if isinstance(opts, ALTROSolverOptions):
             _altro_check(prob, opts)
-            if prob.tf == 0.0:
-                if _altro_infeasible(prob):
-                    raise NotImplementedError("infeasible start + minimum time is not built")
-                return _solve_altro_min_time(prob, opts, max_steps, device)
-            if _altro_infeasible(prob):
-                return _solve_altro_infeasible(prob, opts, max_steps, device)
-            _altro_pn_tolerances(opts)
+            if prob.tf == 0.0 and _altro_infeasible(prob):
+                raise NotImplementedError("infeasible start + minimum time is not built")
+            _altro_pn_tolerances(opts)  # (mutates opts.opts_al, as the reference does)
+            return _solve_altro(prob, opts, device)
         if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
             # solve!(prob, ::AugmentedLagrangianSolverOptions) on an unconstrained problem
             # falls back to the unconstrained solver (augmented_lagrangian_methods.jl:33-36)
@@ -483,16 +481,6 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
     flags = solver.stats["flags"]
     if np.any(flags & abi.TRAJ_COST_INCREASED):
         raise RuntimeError("Error: Cost increased during Forward Pass")
-    if isinstance(solver_or_opts, ALTROSolverOptions) and solver_or_opts.projected_newton:
-        # phase 2 (altro_methods.jl:31-39): solver_pn.V = PrimalDual(prob_altro); solve! on the same
-        # device buffers (X, U of the AL solve are already resident)
-        pn = h.solve_pn(to_tog_pn_options(solver_or_opts.opts_pn))
-        h.download_state(prob)
-        flags = h.status()
-        solver.stats_pn = _pn_stats(pn, flags)
-        if np.any(flags & abi.TRAJ_PN_ERROR):
-            raise RuntimeError("projected Newton: line search did not reduce the violation "
-                               "(the reference's _projection_linesearch! raises here)")
     return solver
 
 
