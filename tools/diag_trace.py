@@ -104,3 +104,33 @@ elif which == "mt_kuka_ls":
         Jo = o.cost_bar(True)
         print(f"alpha {a:.4g}: ok dev {okd} orc {oko}; Xbar diff {np.nanmax(np.abs(Xd - Xo)):.3e} finite dev {np.isfinite(Xd).all()} orc {np.isfinite(Xo).all()};"
               f" max|x| dev {np.nanmax(np.abs(Xd)):.3e}; nan X at {np.argwhere(~np.isfinite(Xd))[:2].tolist()}; Ubar diff {np.nanmax(np.abs(Ud - Uo)):.3e}; J orc {Jo:.6e}")
+elif which == "mt_kuka_trials":
+    # the speculative trials of the failing step (index 19): device J / ok per trial vs the oracle's rollouts
+    import ctypes as C
+    sys.path.insert(0, str(ROOT / "tests"))
+    from test_minimum_time import _mt_model_case
+    prob, opts = _mt_model_case(tog, "kuka")
+    s = tog.AbstractSolverFor(prob.copy(), opts)
+    h = s.handle
+    h.solve_init(abi.MODE_AL)
+    for i in range(19):
+        h.solve_step(1)
+    st0 = {f: h.get(f, raw=True) for f in (abi.FIELD_X, abi.FIELD_U, abi.FIELD_LAMBDA, abi.FIELD_MU, abi.FIELD_RHO)}
+    S0 = h.get(abi.FIELD_STATS)[0]
+    h.solve_step(1)
+    nc = C.c_int32()
+    J = np.zeros(64); ok = np.zeros(64, dtype=np.int32)
+    h.lib.tog__debug_ls(h.h, J.ctypes.data_as(C.POINTER(C.c_double)), ok.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(nc))
+    S1 = h.get(abi.FIELD_STATS)[0]
+    print("J_prev", S0[abi.STAT_J], "-> J", S1[abi.STAT_J], "alpha", S1[abi.STAT_ALPHA], "trials", S1[abi.STAT_LS_TRIALS], "nc", nc.value)
+    o = orc.OracleSolver(prob, opts, b=0)
+    for f, nm in ((abi.FIELD_X, "X"), (abi.FIELD_U, "U"), (abi.FIELD_LAMBDA, "lambda"), (abi.FIELD_MU, "mu"), (abi.FIELD_RHO, "rho")):
+        o.set(nm, st0[f][0])
+    o.update_constraints(); o.jacobians()
+    assert o.cost_expansion(False, True) == 0
+    o.backward(False)
+    for j in range(nc.value):
+        a = 2.0 ** -j
+        oko = o.rollout(a)
+        Jo = o.cost_bar(True) if oko else float("nan")
+        print(f"trial {j:2d} alpha {a:.4g}: device ok {ok[j]} J {J[j]:.10e} | oracle ok {int(oko)} J {Jo:.10e}")

@@ -783,15 +783,47 @@ struct Kuka {
     }
   }
 
+  // f keeps its Cholesky and substitutions inline (the same operations as chol() and solve(), which the
+  // mixed-type stage-Jacobian lanes use): written through the helpers, the rollout kernels of the
+  // minimum-time Kuka (MinTime<Kuka>, 15 x 8) were compiled with a broken divergence test — trials
+  // with states beyond max_state_value, or NaN costs, came back accepted (round 4; the same source
+  // compiled for the host is bit-identical to the oracle). The inline form restores round 3's code.
   template <class T>
   __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
     const T* q = x;
     const T* qd = x + 7;
-    T tau[7], cq[7], sq[7], L[7][7];
+    T tau[7], cq[7], sq[7], L[7][7], y[7];
     bias(tau, cq, sq, q, qd);
     mass(L, cq, sq);
-    chol(L);
-    solve(xd + 7, L, u, tau);
+    // Cholesky M = L Lᵀ in place (entry (i,j) of M is read once, before L[i][j] replaces it)
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      T s = L[j][j];
+#pragma unroll
+      for (int k = 0; k < j; k++) s = s - L[j][k] * L[j][k];
+      L[j][j] = sqrt_(s);
+#pragma unroll
+      for (int i = j + 1; i < 7; i++) {
+        T t = L[i][j];
+#pragma unroll
+        for (int k = 0; k < j; k++) t = t - L[i][k] * L[j][k];
+        L[i][j] = t / L[j][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      T t = u[i] - tau[i];
+#pragma unroll
+      for (int k = 0; k < i; k++) t = t - L[i][k] * y[k];
+      y[i] = t / L[i][i];
+    }
+#pragma unroll
+    for (int i = 6; i >= 0; i--) {
+      T t = y[i];
+#pragma unroll
+      for (int k = i + 1; k < 7; k++) t = t - L[k][i] * xd[7 + k];
+      xd[7 + i] = t / L[i][i];
+    }
 #pragma unroll
     for (int i = 0; i < 7; i++) xd[i] = qd[i];
   }

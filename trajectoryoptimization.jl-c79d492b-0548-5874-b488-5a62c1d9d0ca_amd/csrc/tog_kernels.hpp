@@ -1920,8 +1920,8 @@ __device__ __forceinline__ bool ls_decided_within(const tog_options& o, const De
 // LRT: the rows are read from the block's LDS copy of the tables (AL mode, tables within
 // row_tables_bytes' budget), else through the constant address space.
 template <class M, int INTEG, bool CAND, bool LRT>
-__global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
-                                                 int cnt, const int* __restrict__ list, const int* __restrict__ count) {
+__device__ __forceinline__ void ls_spec_body(const DevProblem* __restrict__ P, const DevBuffers& Bf, int mode, int lo,
+                                             int cnt, const int* __restrict__ list, const int* __restrict__ count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nb = list ? (long long)*count : slot_count(Bf, P->B);
   if ((long long)blockIdx.x * blockDim.x >= nb * cnt) return;  // block past the list: retire at once
@@ -1951,6 +1951,22 @@ __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ 
   } else {
     body(global_row_tables(P));
   }
+}
+template <class M, int INTEG, bool CAND, bool LRT>
+__global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
+                                                 int cnt, const int* __restrict__ list, const int* __restrict__ count) {
+  ls_spec_body<M, INTEG, CAND, LRT>(P, Bf, mode, lo, cnt, list, count);
+}
+// The same rollouts for the models whose gain block exceeds 64 entries (the Kuka, its minimum-time and
+// infeasible variants, the infeasible quadrotor): one wave per SIMD may hold 512 registers (the
+// architectural file plus the accumulation registers as spill space). Their rollouts keep the RBD
+// evaluation's per-joint arrays live; at 256 registers they spilled to scratch (1,136 B per lane, round 4
+// profile), and their launches are at most a wave per SIMD anyway (B x 8 trials lanes).
+template <class M, int INTEG, bool CAND, bool LRT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_ls_spec_w1(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo, int cnt, const int* __restrict__ list,
+             const int* __restrict__ count) {
+  ls_spec_body<M, INTEG, CAND, LRT>(P, Bf, mode, lo, cnt, list, count);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3209,8 +3225,12 @@ struct ModelLaunch {
     const unsigned rb = (mode == TOG_MODE_AL) ? (unsigned)Bf.rows_lds : 0u;
     auto launch = [&](auto cand_c, auto lrt_c) {
       constexpr bool CAND = decltype(cand_c)::value, LRT = decltype(lrt_c)::value;
-      hipLaunchKernelGGL((k_ls_spec<M, INTEG, CAND, LRT>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode, lo,
-                         cnt, list, count);
+      if constexpr (M::n * M::m > 64)
+        hipLaunchKernelGGL((k_ls_spec_w1<M, INTEG, CAND, LRT>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode,
+                           lo, cnt, list, count);
+      else
+        hipLaunchKernelGGL((k_ls_spec<M, INTEG, CAND, LRT>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode, lo,
+                           cnt, list, count);
     };
     using T_ = std::true_type;
     using F_ = std::false_type;

@@ -1498,4 +1498,14 @@ int32_t tog_status(tog_handle* h, int32_t* flags_out) {
   return TOG_OK;
 }
 
+// (internal, diagnostics) the last forward pass's speculative trials: J (nc, B) and rollout status (nc, B)
+int32_t tog__debug_ls(tog_handle* h, double* J, int32_t* ok, int32_t* nc) {
+  if (!h || is_multi(h)) return fail(TOG_ERR_ARG, "tog__debug_ls: single-device handle");
+  *nc = h->buf.nc;
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  if (J) HIPCHECK(hipMemcpy(J, h->buf.lsJ, sizeof(double) * h->buf.nc * h->B, hipMemcpyDeviceToHost));
+  if (ok) HIPCHECK(hipMemcpy(ok, h->buf.lsok, sizeof(int) * h->buf.nc * h->B, hipMemcpyDeviceToHost));
+  return TOG_OK;
+}
+
 }  // extern "C"
