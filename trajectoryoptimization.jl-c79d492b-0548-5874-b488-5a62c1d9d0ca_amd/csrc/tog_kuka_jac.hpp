@@ -9,11 +9,11 @@
 //   K1 = J_1 dt, T2 = I + K1/2, F2 = J_2 [T2; E_u], K2 = F2 dt, T3 = (I - K1) + 2 K2, F3 = J_3 [T3; E_u],
 //   K3 = F3 dt, [A B] = I + ((K1 + 4 K2) + K3)/6.
 // Four launches per Jacobian, all over the knot slots of the active trajectories:
-//   k_kuka_points  one lane per knot: the primal stage inputs s_2, s_3 (two RNEA/CRBA/Cholesky solves), and
-//                  J_s's u columns: ∂v̇/∂u = M⁻¹ by two triangular solves per column from each stage's L;
+//   k_kuka_points  one lane per knot: the primal stage inputs s_2, s_3 (two RNEA/CRBA/Cholesky solves);
 //   k_kuka_sjac<Q> one lane per (knot, stage, q_p): the full dual RBD step, one partial;
-//   k_kuka_sjac<V> one lane per (knot, stage, v_p): at fixed q (no mass-matrix or Cholesky partials),
-//                  only the RNEA bias and the solve carry the partial;
+//   k_kuka_sjac<V> one lane per (knot, stage, p): the v_p partial at fixed q (no mass-matrix or Cholesky
+//                  partials, only the RNEA bias and the solve carry it), then the u_p column
+//                  ∂v̇/∂u_p = M⁻¹ e_p by two triangular solves with the lane's primal factor;
 //   k_kuka_chain   one wave per knot: the RK3 combination, the two 7x14 · 14x21 chain products on the fp64
 //                  matrix cores (v_mfma_f64_16x16x4_f64, k in order — the fma chain of the oracle) and
 //                  the store of [A B] (and the infeasible model's identity slack block).
@@ -38,32 +38,26 @@ __device__ __forceinline__ long long kj_traj(const DevBuffers& Bf, const DevProb
   return b;
 }
 
-// ∂v̇/∂u_p, p = 0..6, into J[i][14 + p]: the partials solve() carries when only u is seeded (u.p - τ.p =
-// e_p exactly; every L, τ partial is zero)
-__device__ __forceinline__ void kj_u_columns(double* J, const double (*L)[7]) {
-  double il[7];
+// ∂v̇/∂u_p into J[i][14 + p]: the partials solve() carries when only u_p is seeded (u.p - τ.p = e_p
+// exactly; every L, τ partial is zero; the quotient's partial is x.p * (1/L_ii), as kdiv)
+__device__ __forceinline__ void kj_u_column(double* J, const double (*L)[7], int p) {
+  double y[7], g[7];
 #pragma unroll
-  for (int i = 0; i < 7; i++) il[i] = 1.0 / L[i][i];
+  for (int i = 0; i < 7; i++) {
+    double t = (i == p) ? 1.0 : 0.0;
 #pragma unroll
-  for (int p = 0; p < 7; p++) {
-    double y[7], g[7];
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-      double t = (i == p) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < i; k++) t = t - L[i][k] * y[k];
-      y[i] = t * il[i];
-    }
-#pragma unroll
-    for (int i = 6; i >= 0; i--) {
-      double t = y[i];
-#pragma unroll
-      for (int k = i + 1; k < 7; k++) t = t - L[k][i] * g[k];
-      g[i] = t * il[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 7; i++) J[i * KJ_L + 14 + p] = g[i];
+    for (int k = 0; k < i; k++) t = t - L[i][k] * y[k];
+    y[i] = t * (1.0 / L[i][i]);
   }
+#pragma unroll
+  for (int i = 6; i >= 0; i--) {
+    double t = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 7; k++) t = t - L[k][i] * g[k];
+    g[i] = t * (1.0 / L[i][i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 7; i++) J[i * KJ_L + 14 + p] = g[i];
 }
 
 // primal f at (x, u): v̇ into vd, and the Cholesky factor of M(q)
@@ -95,7 +89,6 @@ __global__ void __launch_bounds__(64) k_kuka_points(const DevProblem* __restrict
   double* w = kj_slot(Bf, t);
   // stage 1 at x: k1 = f dt, s_2 = x + k1/2 (discrete_step's rk3)
   kj_primal(vd, L, x, u);
-  kj_u_columns(w + KJ_OFF_J, L);
 #pragma unroll
   for (int i = 0; i < n; i++) {
     k1[i] = (i < 7 ? x[7 + i] : vd[i - 7]) * dt;
@@ -104,7 +97,6 @@ __global__ void __launch_bounds__(64) k_kuka_points(const DevProblem* __restrict
   }
   // stage 2 at s_2: k2 = f dt, s_3 = (x - k1) + 2 k2
   kj_primal(vd, L, s, u);
-  kj_u_columns(w + KJ_OFF_J + 7 * KJ_L, L);
 #pragma unroll
   for (int i = 0; i < n; i++) {
     const double k2 = (i < 7 ? s[7 + i] : vd[i - 7]) * dt;
@@ -112,14 +104,6 @@ __global__ void __launch_bounds__(64) k_kuka_points(const DevProblem* __restrict
   }
 #pragma unroll
   for (int i = 0; i < n; i++) w[KJ_OFF_T3 + i] = s[i];
-  // stage 3 at s_3: only M(q)'s factor (for the u columns)
-  {
-    double tau[7], cq[7], sq[7];
-    Kuka::bias(tau, cq, sq, s, s + 7);
-    Kuka::mass(L, cq, sq);
-    Kuka::chol(L);
-  }
-  kj_u_columns(w + KJ_OFF_J + 14 * KJ_L, L);
 }
 
 // one lane per (knot, stage, direction p): TYPE 0 the q_p partial (full dual step), TYPE 1 the v_p partial
@@ -170,6 +154,7 @@ k_kuka_sjac(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
     Kuka::solve(vd, L, u, tau);
 #pragma unroll
     for (int i = 0; i < 7; i++) J[i * KJ_L + 7 + p] = vd[i].g[0];
+    kj_u_column(J, L, p);
   }
 }
 
