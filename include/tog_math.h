@@ -78,6 +78,26 @@ TOG_HD double tog_cos(double x) {
   }
 }
 
+/* (tog_sin(x), tog_cos(x)) from one reduction and one evaluation of each kernel polynomial, branch-free:
+ * bit-identical to the two calls (the same operations; the quadrant only selects and negates, which is
+ * exact). The reduction runs on 0 for non-finite x (a NaN or infinite fn must not reach the integer
+ * conversion) and its result is then discarded. Used where both are needed (the Kuka joints, and
+ * every dual sin/cos, whose partials need the other function). */
+TOG_HD void tog_sincos(double x, double* s, double* c) {
+  const int fin = isfinite(x);
+  double r;
+  int q = tog__rem_pio2(fin ? x : 0.0, &r);
+  if (fabs(x) < 7.85398163397448278999e-01) {
+    r = x;
+    q = 0;
+  }
+  const double ks = tog__ksin(r), kc = tog__kcos(r);
+  const double s0 = (q & 1) ? kc : ks, c0 = (q & 1) ? ks : kc;
+  const double sv = (q & 2) ? -s0 : s0, cv = ((q + 1) & 2) ? -c0 : c0;
+  *s = fin ? sv : x - x;
+  *c = fin ? cv : x - x;
+}
+
 /* Julia's max/min on floats (Base.max, Base.min): NaN in either argument propagates, unlike C's
  * fmax/fmin, which drop it. The AL bookkeeping uses them where the reference calls max/min/maximum/
  * norm(., Inf) (augmented_lagrangian_methods.jl:107-118, 171-184), so a NaN constraint value is

@@ -52,3 +52,50 @@ def test_chol_minus_zero_cosine_gives_zero_diagonal(oracle):
     rc = L.oc_chol_minus(U.ctypes.data_as(dp), A.ctypes.data_as(dp), 1, Bv.ctypes.data_as(dp), 1)
     assert rc == 0
     assert U[0, 0] == 0.0
+
+
+def test_sincos_bit_identical_to_sin_and_cos(tmp_path):
+    """tog_sincos (one reduction, both kernels, branch-free selection: the Kuka joints and every dual
+    sin/cos) against tog_sin / tog_cos bit for bit, host build, over 2^18 points spread over the
+    reduction's range plus the branch boundaries, signed zeros and non-finite values."""
+    import pathlib
+    import subprocess
+    root = pathlib.Path(__file__).resolve().parents[1]
+    src = tmp_path / "sc.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+#include "tog_math.h"
+int main(void) {
+  long bad = 0, n = 0;
+  const double sp[] = {0.0, -0.0, 7.85398163397448278999e-01, -7.85398163397448278999e-01,
+                       7.853981633974482e-01, 7.853981633974484e-01, 1.5707963267948966, 3.141592653589793,
+                       -3.141592653589793, 4.71238898038469, 1e-300, -1e-300, 5e5, -5e5,
+                       1.0 / 0.0, -1.0 / 0.0, 0.0 / 0.0};
+  uint64_t st = 88172645463325252ull;
+  for (long i = 0; i < (1L << 18) + (long)(sizeof(sp) / sizeof(sp[0])); i++) {
+    double x;
+    if (i < (long)(sizeof(sp) / sizeof(sp[0]))) x = sp[i];
+    else {
+      st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+      const double u = (double)(st >> 11) / 9007199254740992.0;
+      x = (i & 1) ? (u - 0.5) * 40.0 : (u - 0.5) * 4.0;
+    }
+    double s, c;
+    tog_sincos(x, &s, &c);
+    const double s0 = tog_sin(x), c0 = tog_cos(x);
+    n++;
+    if (memcmp(&s, &s0, 8) || memcmp(&c, &c0, 8)) {
+      if (!(s != s && s0 != s0 && c != c && c0 != c0)) bad++;
+    }
+  }
+  printf("%ld %ld\n", n, bad);
+  return 0;
+}
+''')
+    exe = tmp_path / "sc"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", str(root / "include"), str(src), "-o", str(exe), "-lm"],
+                   check=True)
+    n, bad = map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split())
+    assert n > 1 << 18 and bad == 0

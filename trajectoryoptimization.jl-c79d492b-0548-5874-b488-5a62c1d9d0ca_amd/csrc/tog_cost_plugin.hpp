@@ -220,12 +220,14 @@ __host__ __device__ __forceinline__ HDual<W> hunary(const HDual<W>& a, D1 fv, D1
 }
 template <int W>
 __host__ __device__ __forceinline__ HDual<W> sin_(const HDual<W>& a) {
-  const double s = tog_sin(a.v), c = tog_cos(a.v);
+  double s, c;
+  tog_sincos(a.v, &s, &c);
   return hunary(a, D1{s, c * a.t}, D1{c, (-s) * a.t});
 }
 template <int W>
 __host__ __device__ __forceinline__ HDual<W> cos_(const HDual<W>& a) {
-  const double s = tog_sin(a.v), c = tog_cos(a.v);
+  double s, c;
+  tog_sincos(a.v, &s, &c);
   return hunary(a, D1{c, (-s) * a.t}, D1{-s, (-c) * a.t});
 }
 template <int W>

@@ -185,6 +185,7 @@ struct DevBuffers {
 // Scalar helpers (double and Dual share names)
 __host__ __device__ __forceinline__ double sin_(double x) { return tog_sin(x); }
 __host__ __device__ __forceinline__ double cos_(double x) { return tog_cos(x); }
+__host__ __device__ __forceinline__ void sincos_(double x, double& s, double& c) { tog_sincos(x, &s, &c); }
 __host__ __device__ __forceinline__ double sqrt_(double x) { return sqrt(x); }
 __host__ __device__ __forceinline__ double inv_(double x) { return 1.0 / x; }
 __host__ __device__ __forceinline__ double val_(double x) { return x; }
@@ -315,8 +316,8 @@ __host__ __device__ __forceinline__ Dual<W> inv_(const Dual<W>& a) {
 template <int W>
 __host__ __device__ __forceinline__ Dual<W> sin_(const Dual<W>& a) {
   Dual<W> r;
-  r.v = tog_sin(a.v);
-  const double c = tog_cos(a.v);
+  double c;
+  tog_sincos(a.v, &r.v, &c);
 #pragma unroll
   for (int i = 0; i < W; i++) r.g[i] = c * a.g[i];
   return r;
@@ -324,11 +325,26 @@ __host__ __device__ __forceinline__ Dual<W> sin_(const Dual<W>& a) {
 template <int W>
 __host__ __device__ __forceinline__ Dual<W> cos_(const Dual<W>& a) {
   Dual<W> r;
-  r.v = tog_cos(a.v);
-  const double c = -tog_sin(a.v);
+  double sv;
+  tog_sincos(a.v, &sv, &r.v);
+  const double c = -sv;
 #pragma unroll
   for (int i = 0; i < W; i++) r.g[i] = c * a.g[i];
   return r;
+}
+// (sin_(a), cos_(a)) from one tog_sincos (bit-identical to the two calls)
+template <int W>
+__host__ __device__ __forceinline__ void sincos_(const Dual<W>& a, Dual<W>& s, Dual<W>& c) {
+  double sv, cv;
+  tog_sincos(a.v, &sv, &cv);
+  const double ns = -sv;
+  s.v = sv;
+  c.v = cv;
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    s.g[i] = cv * a.g[i];
+    c.g[i] = ns * a.g[i];
+  }
 }
 template <int W>
 __host__ __device__ __forceinline__ Dual<W> sqrt_(const Dual<W>& a) {
@@ -366,8 +382,10 @@ struct Car {  // dynamics/car.jl:3-8
   static constexpr int n = 3, m = 2, id = TOG_MODEL_CAR;
   template <class T>
   __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
-    xd[0] = u[0] * cos_(x[2]);
-    xd[1] = u[0] * sin_(x[2]);
+    T s, c;
+    sincos_(x[2], s, c);
+    xd[0] = u[0] * c;
+    xd[1] = u[0] * s;
     xd[2] = u[1];
   }
 };
@@ -379,8 +397,7 @@ struct Cartpole {  // dynamics/cartpole.jl:9-36 ; qdd = -H \ (C*qd + G - B*u), g
     const double mc = 1.0, mp = 0.2, l = 0.5, g = 9.81;
     T s, c;
     if (isfinite(val_(x[1]))) {
-      s = sin_(x[1]);
-      c = cos_(x[1]);
+      sincos_(x[1], s, c);
     } else {  // cartpole.jl:18-24
       s = cst_(INFINITY, x[1]);
       c = cst_(INFINITY, x[1]);
@@ -525,7 +542,11 @@ struct Kuka {
   static constexpr KukaTab KT{};
   // Joint index laundered through an SGPR at each use: the tables are then read from constant memory
   // (scalar loads) where they are used, instead of ~200 fp64 literals being materialised once and
-  // kept live in VGPRs across the three RK stages (which spilled 4 KB/lane in the Jacobian).
+  // kept live in VGPRs across the three RK stages (which spilled 4 KB/lane in the Jacobian). The plain
+  // double evaluation (rollouts, stage points: f<double>, LIT) takes the literals instead: the ±1 and 0
+  // entries fold into operand modifiers and inline constants, and no table value is loaded (in the
+  // rollout the hoisted scalar loads were spilled to VGPR lanes: 2.09 -> 1.71 ms for the 4096 x 8
+  // rollouts alone, tools/microbench/kuka_f_bench.hip).
   __host__ __device__ __forceinline__ static int lj(int j) {
 #ifdef __HIP_DEVICE_COMPILE__
     asm volatile("" : "+s"(j));
@@ -597,16 +618,15 @@ struct Kuka {
 
   // dynamics_bias: RNEA with v̇ = 0 -> tau; also cos/sin of q for the mass matrix. TQ (q, cos, sin) may
   // be double while T (q̇ and everything downstream) is a dual: the partials w.r.t. q̇ at fixed q.
-  template <class T, class TQ>
+  template <class T, class TQ, bool LIT = false>
   __host__ __device__ __forceinline__ static void bias(T* tau, TQ* cq, TQ* sq, const TQ* q, const T* qd) {
     const T z = cst_(0.0, qd[0]);
     T w[3] = {z, z, z}, v[3] = {z, z, z}, al[3] = {z, z, z}, ln[3] = {z, z, cst_(TOG_KUKA_GRAVITY, qd[0])};
     T nf[7][3], ff[7][3];
 #pragma unroll
     for (int j = 0; j < 7; j++) {
-      const int jl = Kuka::lj(j);
-      cq[j] = cos_(q[j]);
-      sq[j] = sin_(q[j]);
+      const int jl = LIT ? j : Kuka::lj(j);
+      sincos_(q[j], sq[j], cq[j]);
       T t[3], tv[3], wj[3], vj[3], aj[3], lj[3];
       cross_dc(t, w, KT.P[jl]);
 #pragma unroll
@@ -645,7 +665,7 @@ struct Kuka {
       tau[j] = nf[j][2];
       if (j > 0) {
         T fp[3], np[3], rx[3];
-        const int jl = Kuka::lj(j);
+        const int jl = LIT ? j : Kuka::lj(j);
         Et(jl, cq[j], sq[j], fp, ff[j]);
         Et(jl, cq[j], sq[j], np, nf[j]);
         cross_cd(rx, KT.P[jl], fp);
@@ -660,7 +680,7 @@ struct Kuka {
   }
 
   // mass_matrix by CRBA; lower triangle M[i][j], i >= j
-  template <class T>
+  template <class T, bool LIT = false>
   __host__ __device__ __forceinline__ static void mass(T (*M)[7], const T* cq, const T* sq) {
     double mc = KT.M[6];
     T hc[3], Ic[3][3];
@@ -682,7 +702,7 @@ struct Kuka {
 #pragma unroll
       for (int k = j; k >= 1; k--) {
         T fl[3], fa[3], rx[3];
-        const int kl = Kuka::lj(k);
+        const int kl = LIT ? k : Kuka::lj(k);
         Et(kl, cq[k], sq[k], fl, Fl);
         Et(kl, cq[k], sq[k], fa, Fa);
         cross_cd(rx, KT.P[kl], fl);
@@ -694,7 +714,7 @@ struct Kuka {
         M[j][k - 1] = Fa[2];
       }
       if (j > 0) {
-        const int jl = Kuka::lj(j), jp = Kuka::lj(j - 1);
+        const int jl = LIT ? j : Kuka::lj(j), jp = LIT ? j - 1 : Kuka::lj(j - 1);
         const double* r = KT.P[jl];
         T hr[3], W[3][3], col[3], row[3], Ir[3][3];
         Et(jl, cq[j], sq[j], hr, hc);
@@ -788,13 +808,13 @@ struct Kuka {
   // minimum-time Kuka (MinTime<Kuka>, 15 x 8) were compiled with a broken divergence test — trials
   // with states beyond max_state_value, or NaN costs, came back accepted (round 4; the same source
   // compiled for the host is bit-identical to the oracle). The inline form restores round 3's code.
-  template <class T>
+  template <class T, bool LIT = std::is_same<T, double>::value>
   __host__ __device__ __forceinline__ static void f(T* xd, const T* x, const T* u) {
     const T* q = x;
     const T* qd = x + 7;
     T tau[7], cq[7], sq[7], L[7][7], y[7];
-    bias(tau, cq, sq, q, qd);
-    mass(L, cq, sq);
+    bias<T, T, LIT>(tau, cq, sq, q, qd);
+    mass<T, LIT>(L, cq, sq);
     // Cholesky M = L Lᵀ in place (entry (i,j) of M is read once, before L[i][j] replaces it)
 #pragma unroll
     for (int j = 0; j < 7; j++) {

@@ -1641,7 +1641,7 @@ __device__ __forceinline__ RowTables block_row_tables(const DevProblem* P, void*
   return RowTables{rc, ko, kc};
 }
 
-template <class M, int INTEG, int WMODE, class RT_T = RowTables>
+template <class M, int INTEG, int WMODE, int DC = 0, class RT_T = RowTables>
 __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, double alpha,
                              bool al, double& Jout, double* grad_out, const RT_T& RT,
                              double* __restrict__ cw = nullptr, int ncp = 0) {
@@ -1734,7 +1734,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       gsum += mx;
     }
     // stage cost and AL terms of knot k-1 (x̄_{k-1}, ū_{k-1})
-    J += stage_cost_m<M>(P, xb, ub);
+    J += stage_cost_m<M, DC>(P, xb, ub);
     if (al) {
       const int cnt = RT.kcnt[k - 1];
       if (cnt) {
@@ -1783,7 +1783,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
     }
     if (!ok) return false;
   }
-  J += terminal_cost_m<M>(P, xb);
+  J += terminal_cost_m<M, DC>(P, xb);
   if (al) {
     const int cnt = RT.kcnt[N - 1];
     if (cnt) {
@@ -1919,7 +1919,7 @@ __device__ __forceinline__ bool ls_decided_within(const tog_options& o, const De
 // Jprev_in).
 // LRT: the rows are read from the block's LDS copy of the tables (AL mode, tables within
 // row_tables_bytes' budget), else through the constant address space.
-template <class M, int INTEG, bool CAND, bool LRT>
+template <class M, int INTEG, bool CAND, bool LRT, int DC>
 __device__ __forceinline__ void ls_spec_body(const DevProblem* __restrict__ P, const DevBuffers& Bf, int mode, int lo,
                                              int cnt, const int* __restrict__ list, const int* __restrict__ count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1939,9 +1939,9 @@ __device__ __forceinline__ void ls_spec_body(const DevProblem* __restrict__ P, c
     if constexpr (CAND) {  // every trial keeps its rollout: the accepted one is copied, not replayed
       double* cw = static_cast<double*>(
           __builtin_assume_aligned(Bf.cand + ((size_t)b * P->N * cand_q<M>() * Bf.ncp + j) * 4, 32));
-      ok = rollout_cost<M, INTEG, 3>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw, Bf.ncp);
+      ok = rollout_cost<M, INTEG, 3, DC>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT, cw, Bf.ncp);
     } else {
-      ok = rollout_cost<M, INTEG, 0>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
+      ok = rollout_cost<M, INTEG, 0, DC>(P, Bf, b, ldexp(1.0, -j), mode == TOG_MODE_AL, Jj, nullptr, RT);
     }
     Bf.lsJ[b * NC + j] = Jj;
     Bf.lsok[b * NC + j] = ok ? 1 : 0;
@@ -1952,21 +1952,23 @@ __device__ __forceinline__ void ls_spec_body(const DevProblem* __restrict__ P, c
     body(global_row_tables(P));
   }
 }
-template <class M, int INTEG, bool CAND, bool LRT>
+// DC: the cost's structure (stage_cost_dt): 1 when the launch knows the cost is diagonal (x̄, ū then stay
+// in registers; the dense loops index them at run time), else 0
+template <class M, int INTEG, bool CAND, bool LRT, int DC>
 __global__ void __launch_bounds__(256) k_ls_spec(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo,
                                                  int cnt, const int* __restrict__ list, const int* __restrict__ count) {
-  ls_spec_body<M, INTEG, CAND, LRT>(P, Bf, mode, lo, cnt, list, count);
+  ls_spec_body<M, INTEG, CAND, LRT, DC>(P, Bf, mode, lo, cnt, list, count);
 }
 // The same rollouts for the models whose gain block exceeds 64 entries (the Kuka, its minimum-time and
 // infeasible variants, the infeasible quadrotor): one wave per SIMD may hold 512 registers (the
 // architectural file plus the accumulation registers as spill space). Their rollouts keep the RBD
 // evaluation's per-joint arrays live; at 256 registers they spilled to scratch (1,136 B per lane, round 4
 // profile), and their launches are at most a wave per SIMD anyway (B x 8 trials lanes).
-template <class M, int INTEG, bool CAND, bool LRT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <class M, int INTEG, bool CAND, bool LRT, int DC>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_ls_spec_w1(const DevProblem* __restrict__ P, DevBuffers Bf, int mode, int lo, int cnt, const int* __restrict__ list,
              const int* __restrict__ count) {
-  ls_spec_body<M, INTEG, CAND, LRT>(P, Bf, mode, lo, cnt, list, count);
+  ls_spec_body<M, INTEG, CAND, LRT, DC>(P, Bf, mode, lo, cnt, list, count);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3223,23 +3225,31 @@ struct ModelLaunch {
     }
     const unsigned gs = grid(B * (long long)cnt, 256);  // one lane per (trajectory, trial); list rounds exit early
     const unsigned rb = (mode == TOG_MODE_AL) ? (unsigned)Bf.rows_lds : 0u;
-    auto launch = [&](auto cand_c, auto lrt_c) {
+    auto launch = [&](auto cand_c, auto lrt_c, auto dc_c) {
       constexpr bool CAND = decltype(cand_c)::value, LRT = decltype(lrt_c)::value;
-      if constexpr (M::n * M::m > 64)
-        hipLaunchKernelGGL((k_ls_spec_w1<M, INTEG, CAND, LRT>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode,
-                           lo, cnt, list, count);
+      constexpr int DC = decltype(dc_c)::value;
+      if constexpr (M::n * M::m > 64)  // (64-lane workgroups spread the waves over every CU: 5% on the Kuka's)
+        hipLaunchKernelGGL((k_ls_spec_w1<M, INTEG, CAND, LRT, DC>), dim3(grid(B * (long long)cnt, 64)), dim3(64),
+                           LRT ? rb : 0u, st, P, Bf, mode, lo, cnt, list, count);
       else
-        hipLaunchKernelGGL((k_ls_spec<M, INTEG, CAND, LRT>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode, lo,
-                           cnt, list, count);
+        hipLaunchKernelGGL((k_ls_spec<M, INTEG, CAND, LRT, DC>), dim3(gs), dim3(256), LRT ? rb : 0u, st, P, Bf, mode,
+                           lo, cnt, list, count);
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    if (Bf.cand) {
-      if (rb) launch(T_{}, T_{});
-      else launch(T_{}, F_{});
+    using D0 = std::integral_constant<int, 0>;
+    using D1 = std::integral_constant<int, 1>;
+    if (Bf.cand) {  // (the candidate-copy line search is the default path: its kernels know the diagonal cost)
+      if (rb) {
+        if (Bf.cost_diag) launch(T_{}, T_{}, D1{});
+        else launch(T_{}, T_{}, D0{});
+      } else {
+        if (Bf.cost_diag) launch(T_{}, F_{}, D1{});
+        else launch(T_{}, F_{}, D0{});
+      }
     } else {
-      if (rb) launch(F_{}, T_{});
-      else launch(F_{}, F_{});
+      if (rb) launch(F_{}, T_{}, D0{});
+      else launch(F_{}, F_{}, D0{});
     }
   }
   // candidate-copy line search: one or two speculative rounds, each followed by its decisions, then the
