@@ -25,11 +25,11 @@ s = pkg.AbstractSolverFor(prob, opts)
 s.handle.solve_init(abi.MODE_AL)
 s.handle.solve_step(1)
 s.handle.synchronize()
-buf = (ctypes.c_ulonglong * 20)()
+buf = (ctypes.c_ulonglong * 32)()
 read(buf)
 s.handle.solve_step(steps)
 s.handle.synchronize()
-assert read(buf) == 20
+assert read(buf) in (20, 32)
 tot = sum(buf)
 waves = (B + 3) // 4
 print(f"B={B} steps={steps}: cycles per wave-knot = {tot / (waves * steps * (prob.N - 1)):.0f}")

@@ -214,8 +214,14 @@ __device__ __forceinline__ double row_shr1(double v) {
 // block (the Cholesky factor being updated), rows j+1..TOP-1 of column j are exact zeros throughout
 // the sweep (no reflector touches them), so they are skipped: their terms are fma(0, y, t) == t.
 // FULL: rows == ROWS is known at compile time (no per-entry liveness selects).
-template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16, bool FULL = false>
-__device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus) {
+struct QrNoPost {
+  template <class J, class A>
+  __device__ __forceinline__ void operator()(J, const A&) const {}
+};
+// POST (16-lane path): called after column step j as post(integral_constant j, a); row j of R is final
+// then (no later reflector touches it), so a consumer may take R's rows as they are released.
+template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16, bool FULL = false, class POST = QrNoPost>
+__device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus, const POST& post = POST{}) {
 #define TQ_LIVE(i, j) ((FULL || TEAMW == 16 || (i) < rows) && !((i) > (j) && (i) < TOP))
   if constexpr (TEAMW == 16) {
     // Reflectors broadcast by DPP row_newbcast (the team is one DPP row). The lane-predicated parts
@@ -259,6 +265,7 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
         for (int i = j + 1; i < ROWS; i++)
           if (TQ_LIVE(i, j)) a[i] = fma(v[i], p, a[i]);
       }
+      post(jc, a);
     });
     return;
   }
@@ -630,31 +637,7 @@ __global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuff
 #ifndef TOG_TAIL_TRI
 #define TOG_TAIL_TRI 1
 #endif
-// Section timers of the knot loop (build with -DTOG_BWD_PROF; read with tog_bwd_prof_read): shader
-// clock deltas (s_memtime) summed per wave into SGPR accumulators, flushed once per wave.
-#ifdef TOG_BWD_PROF
-constexpr int BPROF_N = 20;
-static __device__ unsigned long long tog_bwd_prof[BPROF_N];
-// per-block LDS accumulators (non-returning ds_add_u64: no wait), only the last stamp in SGPRs
-#define BPROF_DECL                                             \
-  __shared__ unsigned long long bp_lds[BPROF_N];               \
-  if (threadIdx.x < BPROF_N) bp_lds[threadIdx.x] = 0ull;       \
-  __syncthreads();                                             \
-  unsigned long long bp_t = __builtin_amdgcn_s_memtime();
-#define BPROF(id)                                                        \
-  {                                                                      \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
-    if (threadIdx.x == 0) atomicAdd(&bp_lds[id], t_ - bp_t);             \
-    bp_t = t_;                                                           \
-  }
-#define BPROF_FLUSH                                                      \
-  __syncthreads();                                                       \
-  if (threadIdx.x < BPROF_N) atomicAdd(&tog_bwd_prof[threadIdx.x], bp_lds[threadIdx.x]);
-#else
-#define BPROF_DECL
-#define BPROF(id) {}
-#define BPROF_FLUSH
-#endif
+// (section timers: BPROF_DECL / BPROF / BPROF_FLUSH, defined in tog_kernels.hpp)
 // WPE: waves per SIMD the register budget is sized for. The full batch runs WPE = TOG_BWD_WAVES (2:
 // 256 registers, latency hidden by the second wave); the convergence tail -- few trajectories, most
 // SIMDs idle -- runs WPE = 1 (512 registers, no spills on the serial chain; DevBuffers::tail).

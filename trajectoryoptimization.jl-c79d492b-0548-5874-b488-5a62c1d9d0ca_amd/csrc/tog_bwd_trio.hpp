@@ -1,62 +1,61 @@
-// tog_bwd_duo.hpp — the square-root backward pass of the convergence tail on two waves per trajectory.
+// tog_bwd_trio.hpp — the square-root backward pass of the convergence tail on three waves per trajectory.
 //
 // Reference: src/solvers/ilqr/backward_pass.jl:87-192 (_backwardpass_sqrt!, chol_plus, chol_minus).
 //
-// In the tail (few trajectories active, most SIMDs idle) a knot's time is the instruction stream of one
-// wave: k_bwd_team issues ~8-9 k instructions per knot at ~5 cycles each (profiles/r3g_ab_tail.txt).
-// Half of that work does not depend on the Q.xx chain, so here it runs on a second wave, on another
-// SIMD of the same CU:
-//   wave A (chain): qr([Q.xx; S A]) -> tmp1 = Q.xx' \ Q.ux' -> chol_minus(Q.uu, tmp1) ->
-//                   qr([Q.xx + tmp1 K; tmp2 K]) = S_k, releasing S_k's rows as the QR finalises them
-//   wave B (side):  Q.x/Q.u += [A B]'s -> Q.ux += (S B)'(S A) -> qr([Q.uu; S B]) ->
-//                   Quu_reg, cond, K, d, s_k, ΔV, the K/d stores; then the next knot's products
-//                   S_k A_{k-1} and S_k B_{k-1}, row i as soon as wave A releases S_k's row i
-// Row i of the R factor is final after column step i of the Householder sweep (no later reflector
-// touches it), so wave A stores it to LDS and tags it with the knot's sequence number; wave B waits on
-// the tag and forms row i of S A and S B while the sweep goes on. The chain wave then starts each knot
-// with its QR (the products are on the bus), and the knot has three workgroup barriers:
-//   B2a Q.ux, Q.uu factor (A's tmp1 and chol_minus)
-//   B2b K, d and the regularisation verdict (A's S-update operands; both waves restart together)
-//   B3  S_k released whole, S_k A_{k-1} on the bus (the next knot)
-// (The row tags need no fence: a wave's LDS operations are performed in issue order, so a tag is never
-// visible before the row stored ahead of it; the reader's acquire load orders its row reads after the tag.)
-// Every value is produced by the same operations in the same order as k_bwd_team's (and the oracle's),
-// so the results are bit-identical; only the wave that computes them differs. One trajectory per
-// workgroup; the four 16-lane DPP rows of a wave compute the same team redundantly (identical values
-// to identical addresses), so every branch and barrier is wave- and workgroup-uniform.
+// k_bwd_duo (tog_bwd_duo.hpp) with the downdate taken off the chain wave. In the duo kernel a knot is
+// qr([Q.xx; S A]) -> tmp1 -> chol_minus -> qr([Q.xx + tmp1 K; tmp2 K]) back to back on wave A. But
+// row j of tmp1 = Q.xx' \ Q.ux' needs only rows 0..j of the new Q.xx factor, and step t of the
+// systolic chol_minus needs only rows 0..t of tmp1, so both can follow the first QR row by row:
+//   wave A (QRs):  qr([Q.xx; S A]) releasing the factor's rows; after B2b the S-update operands and
+//                  qr([Q.xx + tmp1 K; tmp2 K]) = S_k releasing S_k's rows
+//   wave B (side): Q.x/Q.u += [A B]'s -> qr([Q.uu; S B]) (released to C) -> Quu_reg, cond -> K, d,
+//                  s_k, ΔV, the K/d stores (with C's Q.ux); then the next knot's S_k A_{k-1} and
+//                  S_k B_{k-1} from S_k's released rows
+//   wave C (downdate): Q.ux += (S B)'(S A) (released to B), then per released row j of the Q.xx factor
+//                  one step of the forward substitution for tmp1 and one systolic step of
+//                  chol_minus(Q.uu, tmp1), then the downdate's last m - 1 steps
+// Two workgroup barriers per knot: B2b (K, d, verdict, tmp1, tmp2 on the bus; all three waves restart
+// together) and B3 (S_k whole, S_k A_{k-1} and S_k B_{k-1} on the bus). Everything else passes through
+// LDS tagged with the knot's sequence number: a wave's LDS operations are performed in issue order, so a
+// tag stored after its data is never visible before the data, and the reader's acquire load orders its
+// reads after the tag. Every value is computed by the same operations in the same order as k_bwd_duo's
+// and k_bwd_team's (and the oracle's): the results are bit-identical.
 #pragma once
 
 namespace tog {
 
 template <class M>
-struct DuoLayout {  // doubles in the workgroup's LDS
+struct TrioLayout {  // doubles in the workgroup's LDS
   static constexpr int n = M::n, m = M::m;
   static constexpr int S = 0;                 // S_{k+1} (n*n, upper factor, zeros below) then s (n)
-  static constexpr int QU = n * n + n;        // Q.uu factor (m*m, column-major)
-  static constexpr int TX = QU + m * m;       // S A (n*n, column c from lane c of wave A)
-  static constexpr int QUX = TX + n * n;      // Q.ux (m*n, column c from lane c of wave B)
+  static constexpr int QU = n * n + n;        // Q.uu factor (m*m, column-major; B -> C, B's s_k)
+  static constexpr int TX = QU + m * m;       // S A (n*n, column c from lane c of wave B)
+  static constexpr int TU = TX + n * n;       // S B (n*m, column c from lane c of wave B)
+  static constexpr int QUX = TU + n * m;      // Q.ux (m*n, column c from lane c of wave C)
   static constexpr int KB = QUX + m * n;      // K (m*n, column c from lane c of wave B)
-  static constexpr int BA = KB + m * n;       // wave A's bus: tmp1 rows at +32, chol_minus output after
+  static constexpr int RX = KB + m * n;       // the new Q.xx factor's released rows (n*n, A -> C)
+  static constexpr int BA = RX + n * n;       // wave C's bus: tmp1 rows at +32, chol_minus output after
   static constexpr int BA_SIZE = 32 + n * m + 3 * m * m + 8;
-  static constexpr int BB = BA + BA_SIZE;     // wave B's bus: S B columns, :state B columns, cond scratch
+  static constexpr int BB = BA + BA_SIZE;     // wave B's bus: :state B columns, cond scratch
   static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
-  static constexpr int FLAGS = BB + BB_SIZE;  // [0] regularisation verdict (1 ok), [1] chol_minus failed
-  static constexpr int RF = FLAGS + 2;        // n ints: the knot sequence number of S_k's released rows
-  static constexpr int TOTAL = RF + (n + 1) / 2;
+  static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] verdict (1 ok), [1] chol_minus failures at the
+                                              // end, [2] this knot's chol_minus failure (C -> A)
+  static constexpr int TAGS = FLAGS + 2;      // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux
+  static constexpr int NTAGS = 2 * n + 2;
+  static constexpr int TOTAL = TAGS + (NTAGS + 1) / 2;
 };
 
-
 template <class M, int ALI>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1)))
-k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1)))
+k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
   using Cfg = TeamCfg<M>;
-  using D = DuoLayout<M>;
+  using D = TrioLayout<M>;
   constexpr bool SQRT = true, AL = ALI != 0;
   constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, NQ = nq_of<M>(), NE = ne_of<M>();
-  static_assert(TEAM == 16 && m <= n && n + 1 <= 16, "duo kernel: 16-lane DPP rows");
+  static_assert(TEAM == 16 && m <= n && n + 1 <= 16, "trio kernel: 16-lane DPP rows");
   __shared__ double lds[D::TOTAL];
   __shared__ int kcnt[TEAM_MAX_KNOTS], knx[TEAM_MAX_KNOTS];
-  const int wv = threadIdx.x >> 6;  // 0: chain wave A, 1: side wave B (wave-uniform)
+  const int wv = threadIdx.x >> 6;  // 0: QR wave A, 1: side wave B, 2: downdate wave C (wave-uniform)
   const int tl = threadIdx.x & 15;  // column of this lane (each DPP row computes the whole team)
   const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
   if (b < 0) return;  // workgroup-uniform
@@ -64,23 +63,31 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
   BPROF_DECL
   const int N = P->N;
   if (AL) {
-    for (int e = threadIdx.x; e < N; e += 128) {
+    for (int e = threadIdx.x; e < N; e += 192) {
       kcnt[e] = P->knot_cnt[e];
       knx[e] = P->knot_nx[e];
     }
   }
-  int* rowf = reinterpret_cast<int*>(lds + D::RF);
-  if (threadIdx.x < n) rowf[threadIdx.x] = 0;
+  int* tags = reinterpret_cast<int*>(lds + D::TAGS);
+  int* rowf = tags;           // S_k's rows (A -> B)
+  int* rxf = tags + n;        // the new Q.xx factor's rows (A -> C)
+  int* quf = tags + 2 * n;    // the Q.uu factor (B -> C)
+  int* quxf = quf + 1;        // Q.ux (C -> B)
+  if (threadIdx.x < D::NTAGS) tags[threadIdx.x] = 0;
   __syncthreads();
   double* Sreg = lds + D::S;
   double* QU = lds + D::QU;
   double* TXb = lds + D::TX;
+  double* TUb = lds + D::TU;
   double* QUXb = lds + D::QUX;
   double* KB = lds + D::KB;
+  double* RX = lds + D::RX;
   double* busA = lds + D::BA;
   double* busB = lds + D::BB;
   int* flg = reinterpret_cast<int*>(lds + D::FLAGS);
   constexpr int SOFF = n * n;
+  constexpr int TB = 32;
+  double* bus2 = busA + TB + n * m;
   const bool store_S = (flags & TOG_BP_STORE_S) && Bf.Sdbg;
   const bool state_reg = (P->o.bp_reg_type == 1);
   const double dt = P->dt;
@@ -102,7 +109,15 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
   double dV0 = 0.0, dV1 = 0.0;
   bool done = false;
   auto dense = [&](int k) { return knot_dense<SQRT, AL>(k, N, AL ? kcnt[k] : 0, AL ? knx[k] : 0); };
-  int seq = 0;  // knot sequence number (both waves count alike): tags S_k's released rows
+  int seq = 0;  // knot sequence number (every wave counts alike): the tags' value for this knot
+  auto tag_store = [&](int* t) {
+    asm volatile("" ::: "memory");  // (after the tagged data; the hardware keeps the order)
+    if (tl == 0) __hip_atomic_store(t, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto tag_wait = [&](int* t) {
+    while (__hip_atomic_load(t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq) {
+    }
+  };
   // wave A: the Q.xx column entering knot kk's QR (the replayed one in faithful mode), loaded a knot ahead
   auto load_qxx = [&](int kk, double (&Qx)[n]) {
     if (faithful && kk >= kmin) {
@@ -141,6 +156,7 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
       tu = fma(sr[l - i], Bc[l], tu);
     }
     if (colx) TXb[i + n * tl] = tx;
+    if (colu) TUb[i + n * tl] = tu;
     Tb[i] = tu;
   };
 
@@ -167,7 +183,7 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
     double Qxn[n], Ac[n], Bc[n], Tb[n];
     if (wv == 0) {
       load_qxx(N - 2, Qxn);
-    } else {  // the first knot's products, from the whole terminal factor
+    } else if (wv == 1) {  // the first knot's products, from the whole terminal factor
       load_ab(N - 2, Ac, Bc);
       static_for<0, n>([&](auto ic) { row_products(ic, Ac, Bc, Tb); });
     }
@@ -180,11 +196,8 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
       const bool replay = faithful && k >= kmin;
       const double* e = Eg + (size_t)k * NE;
       const double* q = Qs + (size_t)k * NQ;
-      // state carried across the knot's barriers: wave A's Q.xx column, wave B's Q.x entry, Q.u,
-      // Q.uu / Q.ux columns
-      double Qxc[n];
-      double Qxs = 0.0, Qu[m], Quuc[m], Quxc[m];
-      // ------------------------------------------------------------------ phase 1: QR Q.xx | Q.ux, QR Q.uu
+      double Qxc[n];  // (wave A's Q.xx factor column, kept for the S-update operands)
+      // ------------------------------------------------------------------ A: qr([Q.xx; S A]), rows released
       if (wv == 0) {
         {  // Q.xx <- qr([Q.xx; tmp_x]).R (backward_pass.jl:116), tmp_x = S A from wave B's bus
           double a[2 * n];
@@ -194,7 +207,12 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
             a[n + i] = TXb[i + n * c];
           }
           DPROF(0);
-          team_qr<2 * n, n, n, TEAM>(a, 2 * n, tl, busA);
+          auto release = [&](auto jc, const double (&r)[2 * n]) {
+            constexpr int j = decltype(jc)::value;
+            if (colx) RX[j + n * tl] = (j <= tl) ? r[j] : 0.0;
+            tag_store(&rxf[j]);
+          };
+          team_qr<2 * n, n, n, TEAM, false>(a, 2 * n, tl, busA, release);
 #pragma unroll
           for (int i = 0; i < n; i++) Qxc[i] = (i <= tl) ? a[i] : 0.0;
         }
@@ -203,24 +221,35 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
           for (int i = 0; i < n; i++) Qs[(size_t)k * NQ + n + m + i + n * tl] = Qxc[i];
         }
         DPROF(2);
-      } else {
+      } else if (wv == 1) {
+        // ---------------------------------------------------------------- B: Q.x, Q.u, qr([Q.uu; S B]), gains
+        double Qxs, Qu[m], Quuc[m], Quxc[m];
         if (replay) {
           Qxs = q[c];
 #pragma unroll
           for (int i = 0; i < m; i++) Qu[i] = q[n + i];
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
-#pragma unroll
-          for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
         } else {
           Qxs = e[c];
 #pragma unroll
           for (int i = 0; i < m; i++) Qu[i] = e[n + i];
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
-#pragma unroll
-          for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;  // sqrt AL adds no Q.ux term (A.5)
         }
+        {  // Q.uu <- qr([Q.uu; tmp_u]).R (backward_pass.jl:117), released to wave C
+          double a[m + n];
+#pragma unroll
+          for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : Tb[i - m];
+          team_qr<m + n, m, m, TEAM>(a, m + n, tl, busB);
+#pragma unroll
+          for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+        }
+        if (colu) {
+#pragma unroll
+          for (int i = 0; i < m; i++) QU[i + m * tl] = Quuc[i];
+        }
+        tag_store(quf);
         // Q.x += A's ; Q.u += B's (backward_pass.jl:112-113)
         {
           double t = 0.0;
@@ -235,54 +264,9 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
             Qu[i] += row_bcast<i>(tu);
           });
         }
-        DPROF(10);
-        {  // Q.ux += tmp_u' tmp_x (backward_pass.jl:118): tmp_u columns on wave B's bus, tmp_x on the bus
-          if (colu) {
-#pragma unroll
-            for (int i = 0; i < n; i++) busB[i + n * tl] = Tb[i];
-          }
-          team_sync();
-          double t[m];
-#pragma unroll
-          for (int i = 0; i < m; i++) t[i] = 0.0;
-#pragma unroll 1
-          for (int l = 0; l < n; l++) {
-            double tu[m];
-            const double tx = TXb[l + n * c];
-#pragma unroll
-            for (int i = 0; i < m; i++) tu[i] = busB[l + n * i];
-            TEAM_FENCE();
-#pragma unroll
-            for (int i = 0; i < m; i++) t[i] = fma(tu[i], tx, t[i]);
-          }
-#pragma unroll
-          for (int i = 0; i < m; i++) Quxc[i] += t[i];
-          team_sync();
-        }
-        DPROF(12);
-        {  // Q.uu <- qr([Q.uu; tmp_u]).R (backward_pass.jl:117)
-          double a[m + n];
-#pragma unroll
-          for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : Tb[i - m];
-          team_qr<m + n, m, m, TEAM>(a, m + n, tl, busB);
-#pragma unroll
-          for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
-        }
-        if (colu) {
-#pragma unroll
-          for (int i = 0; i < m; i++) QU[i + m * tl] = Quuc[i];
-        }
-        if (colx) {
-#pragma unroll
-          for (int i = 0; i < m; i++) QUXb[i + m * tl] = Quxc[i];
-        }
         if (faithful) {
           double* qq = Qs + (size_t)k * NQ;
-          if (colx) {
-            qq[tl] = Qxs;
-#pragma unroll
-            for (int i = 0; i < m; i++) qq[n + m + n * n + m * m + i + m * tl] = Quxc[i];
-          }
+          if (colx) qq[tl] = Qxs;
           if (colu) {
 #pragma unroll
             for (int i = 0; i < m; i++) qq[n + m + n * n + i + m * tl] = Quuc[i];
@@ -292,102 +276,9 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
             for (int i = 0; i < m; i++) qq[n + i] = Qu[i];
           }
         }
-      }
-      if (faithful) kmin = k < kmin ? k : kmin;
-      DPROF(wv ? 13 : 19);
-      __syncthreads();  // B2a: Q.ux and the Q.uu factor on the bus
-      DPROF(wv ? 14 : 3);
-      // ------------------------------------------------------------------ phase 3: tmp1, chol_minus | gains
-      bool pd_fail = false;
-      if (wv == 0) {
-        // tmp1 = (Q.xx') \ Q.ux' by distributed forward substitution: lane i owns row i of tmp1
-        double t1[m];
-#pragma unroll
-        for (int i = 0; i < m; i++) t1[i] = QUXb[i + m * c];
-        double dgx = Qxc[0];
-#pragma unroll
-        for (int j = 1; j < n; j++)
-          if (tl == j) dgx = Qxc[j];
-        const double rdiag = 1.0 / dgx;
-        static_for<0, n>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          if (tl == j) {
-#pragma unroll
-            for (int i = 0; i < m; i++) t1[i] = t1[i] * rdiag;
-          }
-          double xj[m];
-#pragma unroll
-          for (int i = 0; i < m; i++) xj[i] = row_bcast<j>(t1[i]);
-          if (tl > j && colx) {
-#pragma unroll
-            for (int i = 0; i < m; i++) t1[i] = fma(-Qxc[j], xj[i], t1[i]);
-          }
-        });
-        constexpr int TB = 32;
-        if (colx) {
-#pragma unroll
-          for (int i = 0; i < m; i++) busA[TB + tl * m + i] = t1[i];
-        }
-        team_sync();
-        DPROF(4);
-        // tmp2 = chol_minus(Q.uu, tmp1) (backward_pass.jl:186-192), k_bwd_team's branch-free systolic
-        // schedule under contract v4
-        double* bus2 = busA + TB + n * m;
-        {
-          double u[m], w[m], wn[m];
-#pragma unroll
-          for (int kk = 0; kk < m; kk++) {
-            u[kk] = (colu && tl + kk < m) ? QU[tl + m * (tl + kk)] : 0.0;
-            w[kk] = 0.0;
-            wn[kk] = busA[TB + kk];
-          }
-          double ru = 1.0 / u[0];
-          bool okd = true;
-#pragma unroll 1
-          for (int t = 0; t < n + m - 1; t++) {
-            const int r = t - tl;
-            const bool act = colu && r >= 0 && r < n;
-            double x[m];
-#pragma unroll
-            for (int kk = 0; kk + 1 < m; kk++) x[kk] = row_shr1(w[kk + 1]);
-            x[m - 1] = 0.0;
-#pragma unroll
-            for (int kk = 0; kk < m; kk++) x[kk] = (tl == 0) ? wn[kk] : x[kk];
-            const int rn = t + 1 < n ? t + 1 : n - 1;
-#pragma unroll
-            for (int kk = 0; kk < m; kk++) wn[kk] = busA[TB + rn * m + kk];
-            const double sn = x[0] * ru;
-            const double s2 = sn * sn;
-            okd = okd && !(act && s2 > 1.0);
-            const double y = 1.0 - s2;
-            const double rc = tog_rsqrt(y);
-            const double cs = tog_rs_c(y, rc);
-            w[0] = x[0];
-#pragma unroll
-            for (int kk = 1; kk < m; kk++) {
-              const double tmp = (u[kk] - sn * x[kk]) * rc;
-              w[kk] = cs * x[kk] - sn * tmp;
-              u[kk] = act ? tmp : u[kk];
-            }
-            u[0] = act ? cs * u[0] : u[0];
-            ru = act ? ru * rc : ru;
-          }
-          const unsigned long long rowmask = 0xFFFFull << (threadIdx.x & 48);
-          pd_fail = (__ballot(!okd) & rowmask) != 0ull;
-          if (colu) {
-#pragma unroll
-            for (int jj = 0; jj < m; jj++)
-              if (jj < tl) bus2[2 * m * m + tl + m * jj] = 0.0;
-#pragma unroll
-            for (int kk = 0; kk < m; kk++)
-              if (tl + kk < m) bus2[2 * m * m + tl + m * (tl + kk)] = u[kk];
-          }
-        }
-        DPROF(5);
-      } else {
+        DPROF(13);
         // regularise, test, gains (backward_pass.jl:120-145): Quu_reg = qr([Q.uu; sqrt(ρ) I]).R
         // (:control) or qr([Q.uu; sqrt(ρ) B]).R (:state)
-        team_sync();
         double F[m][m], rF[m];
         {
           const double sr = sqrt(s.rho);
@@ -420,6 +311,10 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
         for (int j = 0; j < m; j++) rF[j] = 1.0 / F[j][j];
         const bool ok = !cond_exceeds_team<m>(F, rF, 1e8, busB + 2 * n * m, tl);
         DPROF(15);
+        tag_wait(quxf);
+#pragma unroll
+        for (int i = 0; i < m; i++) Quxc[i] = QUXb[i + m * c];
+        DPROF(14);
         if (ok) {
           // right-hand side of this lane: Qux_reg column (state reg adds ρ B'A), or Q.u for lane n
           double col[m];
@@ -524,9 +419,127 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
         }
         if (threadIdx.x == 64) flg[0] = ok ? 1 : 0;
         DPROF(16);
+      } else {
+        // ---------------------------------------------------------------- C: Q.ux, tmp1, chol_minus
+        double Quxc[m];
+        if (replay) {
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
+        } else {
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;  // sqrt AL adds no Q.ux term (A.5)
+        }
+        {  // Q.ux += tmp_u' tmp_x (backward_pass.jl:118): both products from wave B's bus
+          double t[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) t[i] = 0.0;
+#pragma unroll 1
+          for (int l = 0; l < n; l++) {
+            double tu[m];
+            const double tx = TXb[l + n * c];
+#pragma unroll
+            for (int i = 0; i < m; i++) tu[i] = TUb[l + n * i];
+            TEAM_FENCE();
+#pragma unroll
+            for (int i = 0; i < m; i++) t[i] = fma(tu[i], tx, t[i]);
+          }
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] += t[i];
+        }
+        if (colx) {
+#pragma unroll
+          for (int i = 0; i < m; i++) QUXb[i + m * tl] = Quxc[i];
+        }
+        tag_store(quxf);
+        if (faithful && colx) {
+#pragma unroll
+          for (int i = 0; i < m; i++) Qs[(size_t)k * NQ + n + m + n * n + m * m + i + m * tl] = Quxc[i];
+        }
+        DPROF(1);
+        // tmp1 = (Q.xx') \ Q.ux' (lane i owns row i of tmp1) and tmp2 = chol_minus(Q.uu, tmp1)
+        // (backward_pass.jl:186-192, contract v4), fused: step j of the substitution finalises row j of
+        // tmp1, which enters the systolic downdate at its step j (lane 0; the rows move one lane per step)
+        double t1[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) t1[i] = Quxc[i];
+        tag_wait(quf);
+        DPROF(3);
+        double u[m], w[m], x0[m];
+#pragma unroll
+        for (int kk = 0; kk < m; kk++) {
+          u[kk] = (colu && tl + kk < m) ? QU[tl + m * (tl + kk)] : 0.0;
+          w[kk] = 0.0;
+        }
+        double ru = 1.0 / u[0];
+        bool okd = true;
+        auto chol_step = [&](int t) {
+          const int r = t - tl;
+          const bool act = colu && r >= 0 && r < n;
+          double x[m];
+#pragma unroll
+          for (int kk = 0; kk + 1 < m; kk++) x[kk] = row_shr1(w[kk + 1]);
+          x[m - 1] = 0.0;
+#pragma unroll
+          for (int kk = 0; kk < m; kk++) x[kk] = (tl == 0) ? x0[kk] : x[kk];
+          const double sn = x[0] * ru;
+          const double s2 = sn * sn;
+          okd = okd && !(act && s2 > 1.0);
+          const double y = 1.0 - s2;
+          const double rc = tog_rsqrt(y);
+          const double cs = tog_rs_c(y, rc);
+          w[0] = x[0];
+#pragma unroll
+          for (int kk = 1; kk < m; kk++) {
+            const double tmp = (u[kk] - sn * x[kk]) * rc;
+            w[kk] = cs * x[kk] - sn * tmp;
+            u[kk] = act ? tmp : u[kk];
+          }
+          u[0] = act ? cs * u[0] : u[0];
+          ru = act ? ru * rc : ru;
+        };
+        static_for<0, n>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          tag_wait(&rxf[j]);
+          const double rj = RX[j + n * c];  // row j of the factor: R[j][j] on lane j, R[j][c] on lane c
+          if (tl == j) {
+            const double rdiag = 1.0 / rj;
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = t1[i] * rdiag;
+          }
+          double xj[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) xj[i] = row_bcast<j>(t1[i]);
+          if (tl > j && colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = fma(-rj, xj[i], t1[i]);
+          }
+          if (tl == j) {
+#pragma unroll
+            for (int i = 0; i < m; i++) busA[TB + j * m + i] = t1[i];
+          }
+#pragma unroll
+          for (int i = 0; i < m; i++) x0[i] = xj[i];
+          chol_step(j);
+        });
+        DPROF(4);
+#pragma unroll 1
+        for (int t = n; t < n + m - 1; t++) chol_step(t);  // (lane 0 idle: its input stays row n-1)
+        const unsigned long long rowmask = 0xFFFFull << (threadIdx.x & 48);
+        const bool pd_fail = (__ballot(!okd) & rowmask) != 0ull;
+        if (colu) {
+#pragma unroll
+          for (int jj = 0; jj < m; jj++)
+            if (jj < tl) bus2[2 * m * m + tl + m * jj] = 0.0;
+#pragma unroll
+          for (int kk = 0; kk < m; kk++)
+            if (tl + kk < m) bus2[2 * m * m + tl + m * (tl + kk)] = u[kk];
+        }
+        if (threadIdx.x == 128) flg[2] = pd_fail ? 1 : 0;
+        DPROF(5);
       }
-      __syncthreads();  // B2b: K, d and the verdict on the bus
-      DPROF(wv ? 17 : 6);
+      if (faithful) kmin = k < kmin ? k : kmin;
+      __syncthreads();  // B2b: K, d, the verdict, tmp1 and tmp2 on the bus
+      DPROF(wv == 0 ? 6 : (wv == 1 ? 17 : 12));
       if (flg[0] == 0) {
         // non-PD / cond > 1e8: increase ρ and restart at N-1; Q blocks are NOT re-expanded (A.1)
         if (!faithful) {
@@ -546,12 +559,11 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
         restart = true;
         break;
       }
-      // ------------------------------------------------------------------ phase 4: S_k = qr([Q.xx + tmp1 K; tmp2 K]).R
+      // ------------------------------------------------------------------ S_k = qr([Q.xx + tmp1 K; tmp2 K]).R
       if (wv == 0) {
+        const bool pd_fail = flg[2] != 0;
         if (pd_fail) pd_flags |= TOG_TRAJ_SQRT_PD_FAIL;
         if (k > 0) load_qxx(k - 1, Qxn);  // (in flight during the S-update)
-        constexpr int TB = 32;
-        double* bus2 = busA + TB + n * m;
         const double* U2p = pd_fail ? QU : bus2 + 2 * m * m;  // tmp2, or Q.uu on failure
         double Kc[m];
 #pragma unroll
@@ -578,14 +590,12 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
           for (int l = 0; l < m; l++) v = fma(U2p[i + m * l], Kc[l], v);
           a[n + i] = v;
         }
-        team_sync();
         DPROF(7);
         // release row j of S_k after column step j: the row (zeros left of the diagonal), then its tag
         auto release = [&](auto jc, const double (&r)[RS]) {
           constexpr int j = decltype(jc)::value;
           if (colx) Sreg[j + n * tl] = (j <= tl) ? r[j] : 0.0;
-          asm volatile("" ::: "memory");
-          if (tl == 0) __hip_atomic_store(&rowf[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          tag_store(&rowf[j]);
         };
         team_qr<RS, n, 0, TEAM, false>(a, RS, tl, busA, release);
         if (store_S && colx) {
@@ -593,18 +603,17 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
           for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = (i <= tl) ? a[i] : 0.0;
         }
         DPROF(8);
-      } else if (k > 0) {  // the next knot's S_k A_{k-1} (to the bus) and S_k B_{k-1}, row by row
+      } else if (wv == 1 && k > 0) {  // the next knot's S_k A_{k-1} and S_k B_{k-1}, row by row
         load_ab(k - 1, Ac, Bc);
         static_for<0, n>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
-          while (__hip_atomic_load(&rowf[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq) {
-          }
+          tag_wait(&rowf[i]);
           row_products(ic, Ac, Bc, Tb);
         });
         DPROF(11);
       }
-      __syncthreads();  // B3: S_k for the next knot, S_k A_{k-1} on the bus
-      DPROF(wv ? 18 : 9);
+      __syncthreads();  // B3: S_k for the next knot, S_k A_{k-1} and S_k B_{k-1} on the bus
+      DPROF(wv == 0 ? 9 : (wv == 1 ? 18 : 19));
     }
     if (!restart) done = true;
   }

@@ -18,6 +18,7 @@
 #pragma once
 
 #include "tog_device.hpp"
+#include <string.h>
 
 namespace tog {
 
@@ -1575,6 +1576,44 @@ attempt:
 // acceptance logic over (ok_j, J_j) in order -- bit-identical decisions -- and the accepted α is
 // replayed once more, writing the new trajectory in place. One round covers iterations_linesearch=20.
 // =============================================================================================
+// Section timers of the knot loop (build with -DTOG_BWD_PROF; read with tog_bwd_prof_read): shader
+// clock deltas (s_memtime) summed per wave into SGPR accumulators, flushed once per wave.
+#ifdef TOG_BWD_PROF
+constexpr int BPROF_N = 32;  // 0-19 the backward kernels, 20-27 the tail rollouts
+static __device__ unsigned long long tog_bwd_prof[BPROF_N];
+// per-block LDS accumulators (non-returning ds_add_u64: no wait), only the last stamp in SGPRs
+#define BPROF_DECL                                             \
+  __shared__ unsigned long long bp_lds[BPROF_N];               \
+  if (threadIdx.x < BPROF_N) bp_lds[threadIdx.x] = 0ull;       \
+  __syncthreads();                                             \
+  unsigned long long bp_t = __builtin_amdgcn_s_memtime();
+#define BPROF(id)                                                        \
+  {                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+    if (threadIdx.x == 0) atomicAdd(&bp_lds[id], t_ - bp_t);             \
+    bp_t = t_;                                                           \
+  }
+#define BPROF_FLUSH                                                      \
+  __syncthreads();                                                       \
+  if (threadIdx.x < BPROF_N) atomicAdd(&tog_bwd_prof[threadIdx.x], bp_lds[threadIdx.x]);
+#else
+#define BPROF_DECL
+#define BPROF(id) {}
+#define BPROF_FLUSH
+#endif
+
+// Per-wave section timers (tools/duo_prof.py): shader-clock deltas summed by lane 0 of each wave.
+#ifdef TOG_BWD_PROF
+#define DPROF(id)                                                        \
+  {                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&bp_lds[id], t_ - bp_t);      \
+    bp_t = t_;                                                           \
+  }
+#else
+#define DPROF(id) {}
+#endif
+
 constexpr int FTEAM = 32;
 constexpr int LS_MAX_ROUNDS = 2;  // speculative line-search rounds per forward pass
 #ifndef TOG_LS_FIRST
@@ -2186,6 +2225,7 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
   const TrajState& st = Bf.st[b];
   if (!st.active || lo + st.ls_pend >= Bf.nc) return;  // (uniform over the block)
   extern __shared__ double tl2[];
+  BPROF_DECL
   const int wv = threadIdx.x >> 6;  // 0: chain wave A, 1: cost wave B
   const int lane = threadIdx.x & (WAVE - 1);
   const int j = lo + st.ls_pend + lane;
@@ -2294,7 +2334,9 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
           }
         }
       }
+      DPROF(20);
       __syncthreads();
+      DPROF(21);
     }
     // the final state and the verdict for wave B (x_{N-1} in ring slot 0, step 0)
     if (lane < SPEC_LANES) {
@@ -2357,8 +2399,11 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
           }
         }
       }
+      DPROF(22);
       if (cg == GPC - 1 && (ch + 1) * TC < NS) stage_store(tl2 + ((ch + 1) & 1) * IMG);
+      DPROF(23);
       __syncthreads();
+      DPROF(24);
     }
     __syncthreads();  // wave A's final state and verdict
     if (on) {
@@ -2395,6 +2440,7 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
       Bf.lsok[b * NC + j] = live ? 1 : 0;
     }
   }
+  BPROF_FLUSH
 }
 
 // After trials [0, hi): list the active trajectories the acceptance logic has not settled yet
@@ -2823,6 +2869,7 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
 }  // namespace tog
 #include "tog_bwd_team.hpp"
 #include "tog_bwd_duo.hpp"
+#include "tog_bwd_trio.hpp"
 #include "tog_pn.hpp"
 namespace tog {
 
@@ -3167,13 +3214,25 @@ struct ModelLaunch {
           else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
         }
       };
-      if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && !getenv("TOG_NO_DUO")) {
-        // convergence tail, square-root pass: the chain and the side work on two waves (tog_bwd_duo.hpp),
-        // one trajectory per workgroup
+      // TOG_BWD_TAIL: "trio" (default), "duo", or "team" (the one-wave team kernel), for A/B checks
+      static const int tail_kind = [] {
+        const char* v = getenv("TOG_BWD_TAIL");
+        if (getenv("TOG_NO_DUO") || (v && !strcmp(v, "team"))) return 0;
+        return (v && !strcmp(v, "duo")) ? 2 : 3;
+      }();
+      if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && tail_kind) {
+        // convergence tail, square-root pass, one trajectory per workgroup: the QRs, the side work and
+        // the downdate on three waves (tog_bwd_trio.hpp), or the chain and the side work on two
+        // (tog_bwd_duo.hpp)
         if constexpr (TeamCfg<M>::TEAM == 16) {
-          const dim3 gd((unsigned)B), bd(128);
-          if (al) hipLaunchKernelGGL((k_bwd_duo<M, 1>), gd, bd, 0, st, P, Bf, flags);
-          else hipLaunchKernelGGL((k_bwd_duo<M, 0>), gd, bd, 0, st, P, Bf, flags);
+          const dim3 gd((unsigned)B);
+          if (tail_kind == 3) {
+            if (al) hipLaunchKernelGGL((k_bwd_trio<M, 1>), gd, dim3(192), 0, st, P, Bf, flags);
+            else hipLaunchKernelGGL((k_bwd_trio<M, 0>), gd, dim3(192), 0, st, P, Bf, flags);
+          } else {
+            if (al) hipLaunchKernelGGL((k_bwd_duo<M, 1>), gd, dim3(128), 0, st, P, Bf, flags);
+            else hipLaunchKernelGGL((k_bwd_duo<M, 0>), gd, dim3(128), 0, st, P, Bf, flags);
+          }
         }
       } else if (Bf.tail) {
         launch(std::integral_constant<int, 1>{});
