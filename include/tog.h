@@ -49,10 +49,14 @@ enum tog_traj_flag {
   TOG_TRAJ_COST_INCREASED = 1 << 3,  /* error("Cost increased") forward_pass.jl:80-82           */
   TOG_TRAJ_COST_BLOWUP = 1 << 4,     /* J > max_cost_value, ilqr_methods.jl:25-28              */
   TOG_TRAJ_MAX_REG = 1 << 5,         /* @warn "Max regularization exceeded" ilqr_methods.jl:169 */
-  TOG_TRAJ_SQRT_PD_FAIL = 1 << 6,    /* lowrankdowndate!/cholesky PosDefException (sqrt BP)     */
+  TOG_TRAJ_SQRT_PD_FAIL = 1 << 6,    /* lowrankdowndate! PosDefException in the sqrt BP: like the
+                                        reference's exception it ends the trajectory's solve (with
+                                        BP_ABORTED; solve_b raises LinAlgError after the batch) */
   TOG_TRAJ_AL_CONVERGED = 1 << 7,    /* c_max < constraint_tolerance                            */
   TOG_TRAJ_AL_MAX_ITERS = 1 << 8,    /* AL outer loop exhausted                                 */
-  TOG_TRAJ_SINGULAR = 1 << 9,        /* SingularException path (pinv fallback) hit in sqrt BP   */
+  TOG_TRAJ_SINGULAR = 1 << 9,        /* zero on the diagonal of the sqrt BP's Q.xx factor (the
+                                        reference's SingularException -> pinv path; unreachable
+                                        for PD cost Hessians)                     */
   TOG_TRAJ_BP_ABORTED = 1 << 10      /* more than TOG_BP_MAX_RESTARTS regularisation restarts in
                                         one backward pass: the trajectory stops (with MAX_REG).
                                         The reference would keep restarting (backward_pass.jl:52-62,

@@ -2244,8 +2244,11 @@ static void backward_sqrt(oc_solver* s) {
     /* tmp2 = chol_minus(Q.uu, tmp1) */
     double tmp2[OM * OM];
     if (chol_minus(tmp2, Quu, m, tmp1, n)) {
-      s->flags |= TOG_TRAJ_SQRT_PD_FAIL;
-      memcpy(tmp2, Quu, sizeof(double) * m * m); /* the reference throws here */
+      /* lowrankdowndate! throws PosDefException (backward_pass.jl:186-192): the solve of this
+         trajectory stops here, like the restart cap (no :decrease, ΔV = 0) */
+      s->flags |= TOG_TRAJ_SQRT_PD_FAIL | TOG_TRAJ_BP_ABORTED;
+      s->dV[0] = s->dV[1] = 0.0;
+      return;
     }
     /* S[k].xx = chol_plus(Q.xx + tmp1*K, tmp2*K) */
     {

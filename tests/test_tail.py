@@ -51,3 +51,19 @@ def test_compacted_tail_equals_full_launches(tog, gpu, oracle):
         X, U = ref.get("X"), ref.get("U")
         assert np.abs(a._X[bi] - X).max() / max(1.0, np.abs(X).max()) < TOL_SOLVE
         assert np.abs(a._U[bi] - U).max() / max(1.0, np.abs(U).max()) < TOL_SOLVE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["duo", "team"])
+def test_tail_backward_kernels_agree(tog, gpu, kind):
+    """The three tail backward kernels (k_bwd_trio, the default; k_bwd_duo; the one-wave k_bwd_team,
+    TOG_BWD_TAIL) perform the same operations in the same order: a batch solved with each equals the
+    others bit for bit (X, U, every per-trajectory statistic). B = 24 keeps every step in the tail
+    mode, and the restarts of the config-3 solves exercise the faithful replays."""
+    B = 24
+    _, _, a, Sa = _solve(tog, B, {"TOG_BWD_TAIL": None})
+    _, _, b, Sb = _solve(tog, B, {"TOG_BWD_TAIL": kind})
+    assert np.array_equal(a._X, b._X)
+    assert np.array_equal(a._U, b._U)
+    assert np.array_equal(Sa, Sb)
+    assert Sa[:, tog.abi.STAT_BP_RESTARTS].max() >= 0

@@ -40,7 +40,7 @@ struct DuoLayout {  // doubles in the workgroup's LDS
   static constexpr int BA_SIZE = 32 + n * m + 3 * m * m + 8;
   static constexpr int BB = BA + BA_SIZE;     // wave B's bus: S B columns, :state B columns, cond scratch
   static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
-  static constexpr int FLAGS = BB + BB_SIZE;  // [0] regularisation verdict (1 ok), [1] chol_minus failed
+  static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] regularisation verdict (1 ok), [2] chol_minus failed
   static constexpr int RF = FLAGS + 2;        // n ints: the knot sequence number of S_k's released rows
   static constexpr int TOTAL = RF + (n + 1) / 2;
 };
@@ -96,7 +96,6 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
   s.drho = Bf.st[b].drho;
   s.flags = Bf.st[b].flags;
   const double rho0 = s.rho, drho0 = s.drho;
-  int pd_flags = 0;  // (wave A's: chol_minus failures, merged at the end)
   bool faithful = false;
   int kmin = N - 1, restarts = 0;
   double dV0 = 0.0, dV1 = 0.0;
@@ -374,6 +373,7 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
           }
           const unsigned long long rowmask = 0xFFFFull << (threadIdx.x & 48);
           pd_fail = (__ballot(!okd) & rowmask) != 0ull;
+          if (threadIdx.x == 0) flg[2] = pd_fail ? 1 : 0;
           if (colu) {
 #pragma unroll
             for (int jj = 0; jj < m; jj++)
@@ -546,13 +546,18 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
         restart = true;
         break;
       }
+      if (flg[2]) {  // lowrankdowndate! throws PosDefException: this trajectory's solve stops
+        s.flags |= TOG_TRAJ_SQRT_PD_FAIL | TOG_TRAJ_BP_ABORTED;
+        done = true;
+        restart = true;
+        break;
+      }
       // ------------------------------------------------------------------ phase 4: S_k = qr([Q.xx + tmp1 K; tmp2 K]).R
       if (wv == 0) {
-        if (pd_fail) pd_flags |= TOG_TRAJ_SQRT_PD_FAIL;
         if (k > 0) load_qxx(k - 1, Qxn);  // (in flight during the S-update)
         constexpr int TB = 32;
         double* bus2 = busA + TB + n * m;
-        const double* U2p = pd_fail ? QU : bus2 + 2 * m * m;  // tmp2, or Q.uu on failure
+        const double* U2p = bus2 + 2 * m * m;  // tmp2
         double Kc[m];
 #pragma unroll
         for (int i = 0; i < m; i++) Kc[i] = KB[i + m * c];
@@ -608,10 +613,7 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
     }
     if (!restart) done = true;
   }
-  if (wv == 0 && threadIdx.x == 0) flg[1] = pd_flags;
-  __syncthreads();
   if (wv == 1) {
-    s.flags |= flg[1];
     const bool aborted = (s.flags & TOG_TRAJ_BP_ABORTED) != 0;
     if (!aborted) reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:166)
     if (threadIdx.x == 64) {

@@ -1445,7 +1445,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       // the travelling x in a frame shifted by i (u[k] = R[i][i+k], w[k] = x[i+k]; slots k >= m-i
       // carry don't-care values), so the pivot is always u[0], w[0] with no per-lane selects, and
       // lane i-1 hands lane i its w[1..] (DPP row_shr:1 on 16-lane teams).
-      const double* U2p;  // tmp2 (column-major): the downdated factor, or Q.uu on failure
+      const double* U2p;  // tmp2 (column-major): the downdated factor
+      bool pd_abort = false;
       {
         double u[m], w[m], wn[m];
 #pragma unroll
@@ -1541,10 +1542,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             if (tl + k < m) bus2[2 * m * m + tl + m * (tl + k)] = u[k];
         }
         team_sync();
-        U2p = fail ? QU : bus2 + 2 * m * m;
-        if (fail) s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
+        U2p = bus2 + 2 * m * m;
+        pd_abort = fail;
       }
       BPROF(8)  // chol_minus
+      if (pd_abort) {  // lowrankdowndate! throws PosDefException: this trajectory's solve stops
+        s.flags |= TOG_TRAJ_SQRT_PD_FAIL | TOG_TRAJ_BP_ABORTED;
+        done = true;
+        restart = true;
+        break;
+      }
       // S[k] = qr([Q.xx + tmp1 K; tmp2 K]).R
       {
         constexpr int RS = n + m;

@@ -38,8 +38,7 @@ struct TrioLayout {  // doubles in the workgroup's LDS
   static constexpr int BA_SIZE = 32 + n * m + 3 * m * m + 8;
   static constexpr int BB = BA + BA_SIZE;     // wave B's bus: :state B columns, cond scratch
   static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
-  static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] verdict (1 ok), [1] chol_minus failures at the
-                                              // end, [2] this knot's chol_minus failure (C -> A)
+  static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] verdict (1 ok), [2] this knot's chol_minus failure (C -> all)
   static constexpr int TAGS = FLAGS + 2;      // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux
   static constexpr int NTAGS = 2 * n + 2;
   static constexpr int TOTAL = TAGS + (NTAGS + 1) / 2;
@@ -103,7 +102,6 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
   s.drho = Bf.st[b].drho;
   s.flags = Bf.st[b].flags;
   const double rho0 = s.rho, drho0 = s.drho;
-  int pd_flags = 0;  // (wave A's: chol_minus failures, merged at the end)
   bool faithful = false;
   int kmin = N - 1, restarts = 0;
   double dV0 = 0.0, dV1 = 0.0;
@@ -559,12 +557,16 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
         restart = true;
         break;
       }
+      if (flg[2]) {  // lowrankdowndate! throws PosDefException: this trajectory's solve stops
+        s.flags |= TOG_TRAJ_SQRT_PD_FAIL | TOG_TRAJ_BP_ABORTED;
+        done = true;
+        restart = true;
+        break;
+      }
       // ------------------------------------------------------------------ S_k = qr([Q.xx + tmp1 K; tmp2 K]).R
       if (wv == 0) {
-        const bool pd_fail = flg[2] != 0;
-        if (pd_fail) pd_flags |= TOG_TRAJ_SQRT_PD_FAIL;
         if (k > 0) load_qxx(k - 1, Qxn);  // (in flight during the S-update)
-        const double* U2p = pd_fail ? QU : bus2 + 2 * m * m;  // tmp2, or Q.uu on failure
+        const double* U2p = bus2 + 2 * m * m;  // tmp2
         double Kc[m];
 #pragma unroll
         for (int i = 0; i < m; i++) Kc[i] = KB[i + m * c];
@@ -617,10 +619,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
     }
     if (!restart) done = true;
   }
-  if (wv == 0 && threadIdx.x == 0) flg[1] = pd_flags;
-  __syncthreads();
   if (wv == 1) {
-    s.flags |= flg[1];
     const bool aborted = (s.flags & TOG_TRAJ_BP_ABORTED) != 0;
     if (!aborted) reg_decrease(P, s);  // regularization_update!(solver, :decrease) (backward_pass.jl:166)
     if (threadIdx.x == 64) {

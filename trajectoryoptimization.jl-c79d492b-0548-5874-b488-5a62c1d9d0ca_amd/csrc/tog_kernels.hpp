@@ -1506,10 +1506,6 @@ attempt:
             }
           }
         }
-        if (!okd) {
-          s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
-          for (int e = 0; e < m * m; e++) U[e] = sh.Quu[e];
-        }
         for (int e = 0; e < m * m; e++) sh.tmp2[e] = U[e];
         // ΔV
         double a = 0.0, bb = 0.0;
@@ -1520,7 +1516,10 @@ attempt:
         sh.flag = okd ? 1 : 0;
       }
       wsync();
-      if (!sh.flag) s.flags |= TOG_TRAJ_SQRT_PD_FAIL;
+      if (!sh.flag) {  // lowrankdowndate! throws PosDefException: this trajectory's solve stops
+        s.flags |= TOG_TRAJ_SQRT_PD_FAIL | TOG_TRAJ_BP_ABORTED;
+        break;
+      }
       // S[k].xx = qr([Q.xx + tmp1*K; tmp2*K]).R
       {
         constexpr int rows = n + m;
@@ -3215,11 +3214,9 @@ struct ModelLaunch {
         }
       };
       // TOG_BWD_TAIL: "trio" (default), "duo", or "team" (the one-wave team kernel), for A/B checks
-      static const int tail_kind = [] {
-        const char* v = getenv("TOG_BWD_TAIL");
-        if (getenv("TOG_NO_DUO") || (v && !strcmp(v, "team"))) return 0;
-        return (v && !strcmp(v, "duo")) ? 2 : 3;
-      }();
+      // (read per launch: tests switch it within one process)
+      const char* tk = getenv("TOG_BWD_TAIL");
+      const int tail_kind = (getenv("TOG_NO_DUO") || (tk && !strcmp(tk, "team"))) ? 0 : ((tk && !strcmp(tk, "duo")) ? 2 : 3);
       if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && tail_kind) {
         // convergence tail, square-root pass, one trajectory per workgroup: the QRs, the side work and
         // the downdate on three waves (tog_bwd_trio.hpp), or the chain and the side work on two

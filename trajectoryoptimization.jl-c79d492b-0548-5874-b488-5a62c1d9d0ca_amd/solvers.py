@@ -8,7 +8,11 @@ reference's ``solve!`` and ``solve(prob, opts)`` its copying variant (src/solver
 
 Errors follow the reference: invalid arguments raise ``ValueError`` (ArgumentError),
 ``Cost increased during Forward Pass`` raises ``RuntimeError`` when a trajectory reports it
-(forward_pass.jl:80-82); the ``@warn``s become per-trajectory status flags in ``solver.stats``.
+(forward_pass.jl:80-82), and a ``PosDefException`` of the square-root backward pass's
+``lowrankdowndate!`` (backward_pass.jl:186-192) raises ``PosDefException`` (a
+``numpy.linalg.LinAlgError``); a batch raises after every trajectory has finished (the failed ones
+stop where the reference's exception would, flagged ``TRAJ_SQRT_PD_FAIL | TRAJ_BP_ABORTED``). The
+``@warn``s become per-trajectory status flags in ``solver.stats``.
 """
 from __future__ import annotations
 
@@ -21,6 +25,25 @@ from . import abi
 import ctypes as C
 
 from .device import BatchHandle, stats_dict
+
+
+class PosDefException(np.linalg.LinAlgError):
+    """LinearAlgebra.PosDefException: a trajectory's square-root backward pass hit a downdate that is
+    not positive definite (chol_minus, backward_pass.jl:186-192). ``trajectories`` lists them."""
+
+    def __init__(self, trajectories):
+        self.trajectories = list(trajectories)
+        super().__init__(f"PosDefException in chol_minus (lowrankdowndate!) for trajectories {self.trajectories}")
+
+
+def _raise_trajectory_errors(flags):
+    """The reference's exceptions, after the batch: cost increase (forward_pass.jl:80-82) and the
+    downdate's PosDefException."""
+    flags = np.asarray(flags)
+    if np.any(flags & abi.TRAJ_SQRT_PD_FAIL):
+        raise PosDefException(np.nonzero(flags & abi.TRAJ_SQRT_PD_FAIL)[0].tolist())
+    if np.any(flags & abi.TRAJ_COST_INCREASED):
+        raise RuntimeError("Error: Cost increased during Forward Pass")
 
 
 # ----------------------------------------------------------------------------- options
@@ -439,8 +462,7 @@ def _solve_altro(prob, opts: ALTROSolverOptions, device: int):
     if infeasible and opts.resolve_feasible_problem:
         solver.stats_feasible = stats_dict(St_res)
     flags = solver.stats["flags"] | (solver.stats_feasible["flags"] if hasattr(solver, "stats_feasible") else 0)
-    if np.any(flags & abi.TRAJ_COST_INCREASED):
-        raise RuntimeError("Error: Cost increased during Forward Pass")
+    _raise_trajectory_errors(flags)
     if opts.projected_newton:
         solver.stats_pn = _pn_stats(pn, solver.stats["flags"])
         if np.any(solver.stats["flags"] & abi.TRAJ_PN_ERROR):
@@ -478,9 +500,7 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
     h.solve(mode, max_steps=max_steps if max_steps is not None else _default_max_steps(solver))
     h.download_state(prob)
     solver.stats = h.stats_dict()
-    flags = solver.stats["flags"]
-    if np.any(flags & abi.TRAJ_COST_INCREASED):
-        raise RuntimeError("Error: Cost increased during Forward Pass")
+    _raise_trajectory_errors(solver.stats["flags"])
     return solver
 
 
