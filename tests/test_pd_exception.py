@@ -6,8 +6,8 @@ thrown (TRAJ_SQRT_PD_FAIL | TRAJ_BP_ABORTED, no forward pass, its X and U as the
 the batch finishes, and solve_b then raises PosDefException (a numpy LinAlgError). The cases: a cost
 with a cross term H large enough that the Schur complement R - H Q⁻¹ H' of the stage Hessian is
 indefinite — at the first backward pass (h = 2) or after one accepted iteration (quadrotor, h = 1.1);
-h = 1 converges. The device (every backward kernel: the bulk team kernel, and the tail's trio, duo and
-one-wave team kernels) must stop at the same step as the oracle with the same X, U and flags."""
+h = 1 converges. The device (every backward kernel: the bulk team kernel, and the tail's quad, trio, duo
+and one-wave team kernels) must stop at the same step as the oracle with the same X, U and flags."""
 import os
 
 import numpy as np
@@ -61,7 +61,7 @@ def test_posdef_exception_is_a_linalg_error(tog):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", [None, "duo", "team"])
+@pytest.mark.parametrize("kind", [None, "trio", "duo", "team"])
 @pytest.mark.parametrize("model,hval", [("di", 2.0), ("quad", 1.1), ("quad", 2.0)])
 def test_device_stops_like_the_oracle(tog, gpu, oracle, kind, model, hval):
     abi = tog.abi

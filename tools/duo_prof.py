@@ -11,8 +11,19 @@ import time
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 import __graft_entry__  # noqa: E402
 
-KIND = sys.argv[2] if len(sys.argv) > 2 else "trio"
-if KIND == "trio":  # tog_bwd_trio.hpp's DPROF ids
+KIND = sys.argv[2] if len(sys.argv) > 2 else "quad"
+if KIND == "quad":  # tog_bwd_quad.hpp's DPROF ids
+    NAMES = {0: "A: knot start", 1: "A: QR [Q.xx; S A] (rows released)", 2: "A: wait K, tmp1",
+             3: "A: top operands Q.xx + tmp1 K", 4: "A: wait B2b", 5: "A: bottom operands + QR S-update",
+             25: "A: wait B3",
+             6: "B: loads, QR [Q.uu; S B], Q.x/Q.u", 7: "B: regularise + cond", 8: "B: wait Q.ux",
+             9: "B: gains, K/d, s, dV", 10: "B: wait B2b", 11: "B: S A, S B rows (with waits)", 12: "B: wait B3",
+             13: "C: Q.ux", 14: "C: tmp1 rows (with waits)", 15: "C: wait B2b", 16: "C: wait B3",
+             17: "D: wait Q.uu", 18: "D: chol_minus rows (with waits)", 19: "D: chol_minus tail",
+             26: "D: wait B2b", 27: "D: wait B3"}
+    WAVES = {"A": [0, 1, 2, 3, 4, 5, 25], "B": [6, 7, 8, 9, 10, 11, 12], "C": [13, 14, 15, 16],
+             "D": [17, 18, 19, 26, 27]}
+elif KIND == "trio":  # tog_bwd_trio.hpp's DPROF ids
     NAMES = {0: "A: knot start", 2: "A: QR [Q.xx; S A] (rows released)", 6: "A: wait B2b",
              7: "A: S-update operands", 8: "A: QR S-update (rows released)", 9: "A: wait B3",
              13: "B: loads, QR [Q.uu; S B], Q.x/Q.u", 15: "B: regularise + cond", 14: "B: wait Q.ux",

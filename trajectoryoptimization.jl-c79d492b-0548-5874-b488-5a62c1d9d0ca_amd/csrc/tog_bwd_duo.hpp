@@ -589,8 +589,7 @@ k_bwd_duo(const DevProblem* P, DevBuffers Bf, int flags) {
         auto release = [&](auto jc, const double (&r)[RS]) {
           constexpr int j = decltype(jc)::value;
           if (colx) Sreg[j + n * tl] = (j <= tl) ? r[j] : 0.0;
-          asm volatile("" ::: "memory");
-          if (tl == 0) __hip_atomic_store(&rowf[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (tl == 0) __hip_atomic_store(&rowf[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WAVEFRONT);
         };
         team_qr<RS, n, 0, TEAM, false>(a, RS, tl, busA, release);
         if (store_S && colx) {

@@ -1,31 +1,32 @@
-// tog_bwd_trio.hpp — the square-root backward pass of the convergence tail on three waves per trajectory.
+// tog_bwd_quad.hpp — the square-root backward pass of the convergence tail on four waves per trajectory.
 //
 // Reference: src/solvers/ilqr/backward_pass.jl:87-192 (_backwardpass_sqrt!, chol_plus, chol_minus).
 //
-// k_bwd_duo (tog_bwd_duo.hpp) with the downdate taken off the chain wave. In the duo kernel a knot is
-// qr([Q.xx; S A]) -> tmp1 -> chol_minus -> qr([Q.xx + tmp1 K; tmp2 K]) back to back on wave A. But
-// row j of tmp1 = Q.xx' \ Q.ux' needs only rows 0..j of the new Q.xx factor, and step t of the
-// systolic chol_minus needs only rows 0..t of tmp1, so both can follow the first QR row by row:
-//   wave A (QRs):  qr([Q.xx; S A]) releasing the factor's rows; after B2b the S-update operands and
-//                  qr([Q.xx + tmp1 K; tmp2 K]) = S_k releasing S_k's rows
-//   wave B (side): Q.x/Q.u += [A B]'s -> qr([Q.uu; S B]) (released to C) -> Quu_reg, cond -> K, d,
-//                  s_k, ΔV, the K/d stores (with C's Q.ux); then the next knot's S_k A_{k-1} and
-//                  S_k B_{k-1} from S_k's released rows
-//   wave C (downdate): Q.ux += (S B)'(S A) (released to B), then per released row j of the Q.xx factor
-//                  one step of the forward substitution for tmp1 and one systolic step of
-//                  chol_minus(Q.uu, tmp1), then the downdate's last m - 1 steps
-// Two workgroup barriers per knot: B2b (K, d, verdict, tmp1, tmp2 on the bus; all three waves restart
-// together) and B3 (S_k whole, S_k A_{k-1} and S_k B_{k-1} on the bus). Everything else passes through
-// LDS tagged with the knot's sequence number: a wave's LDS operations are performed in issue order, so a
-// tag stored after its data is never visible before the data, and the reader's acquire load orders its
-// reads after the tag. Every value is computed by the same operations in the same order as k_bwd_duo's
-// and k_bwd_team's (and the oracle's): the results are bit-identical.
+// k_bwd_trio (tog_bwd_trio.hpp) with its downdate wave split in two. In the trio kernel wave C ran
+// Q.ux, then per released row of the new Q.xx factor one substitution step and one systolic
+// chol_minus step (≈ 820 cycles a row against the QR's ≈ 650), so the chain waited on C
+// (profiles/r4o_trio_sections_b1.txt). Here
+//   wave A (QRs):   qr([Q.xx; S A]) releasing the factor's rows; as soon as K (B) and tmp1 (C) are out,
+//                   the top rows Q.xx + tmp1 K of the S-update operand; after B2b its bottom rows
+//                   tmp2 K and qr([Q.xx + tmp1 K; tmp2 K]) = S_k releasing S_k's rows
+//   wave B (side):  Q.x/Q.u += [A B]'s, qr([Q.uu; S B]) (released to D), Quu_reg, cond, K, d, s_k, ΔV
+//                   and the K/d stores (with C's Q.ux; K released to A); then the next knot's S_k A_{k-1}
+//                   and S_k B_{k-1} from S_k's released rows
+//   wave C (tmp1):  Q.ux += (S B)'(S A) (released to B), then tmp1 = Q.xx' \ Q.ux' one row per released
+//                   row of the Q.xx factor, each row released to D (and to A)
+//   wave D (chol):  chol_minus(Q.uu, tmp1), systolic step t as row t of tmp1 is released
+// Two workgroup barriers per knot: B2b (tmp2, the verdict, the downdate's failure flag; all four waves
+// restart or stop together) and B3 (S_k whole, S_k A_{k-1} and S_k B_{k-1} on the bus). Everything else
+// passes through LDS tagged with the knot's sequence number (tog_bwd_trio.hpp: a wave's LDS operations
+// are performed in issue order, so a tag stored after its data is never visible before the data). Every
+// value is computed by the same operations in the same order as the other backward kernels (and the
+// oracle): the results are bit-identical.
 #pragma once
 
 namespace tog {
 
 template <class M>
-struct TrioLayout {  // doubles in the workgroup's LDS
+struct QuadLayout {  // doubles in the workgroup's LDS
   static constexpr int n = M::n, m = M::m;
   static constexpr int S = 0;                 // S_{k+1} (n*n, upper factor, zeros below) then s (n)
   static constexpr int QU = n * n + n;        // Q.uu factor (m*m, column-major; B -> C, B's s_k)
@@ -39,22 +40,23 @@ struct TrioLayout {  // doubles in the workgroup's LDS
   static constexpr int BB = BA + BA_SIZE;     // wave B's bus: :state B columns, cond scratch
   static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
   static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] verdict (1 ok), [2] this knot's chol_minus failure (C -> all)
-  static constexpr int TAGS = FLAGS + 2;      // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux
-  static constexpr int NTAGS = 2 * n + 2;
+  static constexpr int TAGS = FLAGS + 2;      // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux,
+                                              // tmp1 rows (n), K
+  static constexpr int NTAGS = 3 * n + 3;
   static constexpr int TOTAL = TAGS + (NTAGS + 1) / 2;
 };
 
 template <class M, int ALI>
-__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1)))
-k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   using Cfg = TeamCfg<M>;
-  using D = TrioLayout<M>;
+  using D = QuadLayout<M>;
   constexpr bool SQRT = true, AL = ALI != 0;
   constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, NQ = nq_of<M>(), NE = ne_of<M>();
-  static_assert(TEAM == 16 && m <= n && n + 1 <= 16, "trio kernel: 16-lane DPP rows");
+  static_assert(TEAM == 16 && m <= n && n + 1 <= 16, "quad kernel: 16-lane DPP rows");
   __shared__ double lds[D::TOTAL];
   __shared__ int kcnt[TEAM_MAX_KNOTS], knx[TEAM_MAX_KNOTS];
-  const int wv = threadIdx.x >> 6;  // 0: QR wave A, 1: side wave B, 2: downdate wave C (wave-uniform)
+  const int wv = threadIdx.x >> 6;  // 0: QR wave A, 1: side wave B, 2: tmp1 wave C, 3: chol wave D (uniform)
   const int tl = threadIdx.x & 15;  // column of this lane (each DPP row computes the whole team)
   const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
   if (b < 0) return;  // workgroup-uniform
@@ -62,7 +64,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
   BPROF_DECL
   const int N = P->N;
   if (AL) {
-    for (int e = threadIdx.x; e < N; e += 192) {
+    for (int e = threadIdx.x; e < N; e += 256) {
       kcnt[e] = P->knot_cnt[e];
       knx[e] = P->knot_nx[e];
     }
@@ -72,6 +74,8 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
   int* rxf = tags + n;        // the new Q.xx factor's rows (A -> C)
   int* quf = tags + 2 * n;    // the Q.uu factor (B -> C)
   int* quxf = quf + 1;        // Q.ux (C -> B)
+  int* t1f = quxf + 1;        // tmp1's rows (C -> D, A)
+  int* kf = t1f + n;          // K (B -> A)
   if (threadIdx.x < D::NTAGS) tags[threadIdx.x] = 0;
   __syncthreads();
   double* Sreg = lds + D::S;
@@ -102,6 +106,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
   s.drho = Bf.st[b].drho;
   s.flags = Bf.st[b].flags;
   const double rho0 = s.rho, drho0 = s.drho;
+  constexpr int RS = n + m;  // rows of the S-update operand
   bool faithful = false;
   int kmin = N - 1, restarts = 0;
   double dV0 = 0.0, dV1 = 0.0;
@@ -198,6 +203,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
       const double* e = Eg + (size_t)k * NE;
       const double* q = Qs + (size_t)k * NQ;
       double Qxc[n];  // (wave A's Q.xx factor column, kept for the S-update operands)
+      double a2[RS], Kc[m];  // (wave A's S-update operand column and K column, across B2b)
       // ------------------------------------------------------------------ A: qr([Q.xx; S A]), rows released
       if (wv == 0) {
         {  // Q.xx <- qr([Q.xx; tmp_x]).R (backward_pass.jl:116), tmp_x = S A from wave B's bus
@@ -221,7 +227,28 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
 #pragma unroll
           for (int i = 0; i < n; i++) Qs[(size_t)k * NQ + n + m + i + n * tl] = Qxc[i];
         }
+        DPROF(1);
+        // the top rows of the S-update operand, Q.xx + tmp1 K, as soon as K and all of tmp1 are out (a
+        // knot that restarts leaves K unwritten: the rows are then discarded)
+        tag_wait(kf);
+        tag_wait(&t1f[n - 1]);
         DPROF(2);
+#pragma unroll
+        for (int i = 0; i < m; i++) Kc[i] = KB[i + m * c];
+        {
+          double v[n];
+#pragma unroll
+          for (int i = 0; i < n; i++) v[i] = 0.0;
+#pragma unroll
+          for (int l = 0; l < m; l++) {
+#pragma unroll
+            for (int i = 0; i < n; i++) v[i] = fma(busA[TB + i * m + l], Kc[l], v[i]);
+            TEAM_FENCE();
+          }
+#pragma unroll
+          for (int i = 0; i < n; i++) a2[i] = Qxc[i] + v[i];
+        }
+        DPROF(3);
       } else if (wv == 1) {
         // ---------------------------------------------------------------- B: Q.x, Q.u, qr([Q.uu; S B]), gains
         double Qxs, Qu[m], Quuc[m], Quxc[m];
@@ -277,7 +304,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
             for (int i = 0; i < m; i++) qq[n + i] = Qu[i];
           }
         }
-        DPROF(13);
+        DPROF(6);
         // regularise, test, gains (backward_pass.jl:120-145): Quu_reg = qr([Q.uu; sqrt(ρ) I]).R
         // (:control) or qr([Q.uu; sqrt(ρ) B]).R (:state)
         double F[m][m], rF[m];
@@ -311,11 +338,11 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
 #pragma unroll
         for (int j = 0; j < m; j++) rF[j] = 1.0 / F[j][j];
         const bool ok = !cond_exceeds_team<m>(F, rF, 1e8, busB + 2 * n * m, tl);
-        DPROF(15);
+        DPROF(7);
         tag_wait(quxf);
 #pragma unroll
         for (int i = 0; i < m; i++) Quxc[i] = QUXb[i + m * c];
-        DPROF(14);
+        DPROF(8);
         if (ok) {
           // right-hand side of this lane: Qux_reg column (state reg adds ρ B'A), or Q.u for lane n
           double col[m];
@@ -419,9 +446,10 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
           }
         }
         if (threadIdx.x == 64) flg[0] = ok ? 1 : 0;
-        DPROF(16);
-      } else {
-        // ---------------------------------------------------------------- C: Q.ux, tmp1, chol_minus
+        tag_store(kf);
+        DPROF(9);
+      } else if (wv == 2) {
+        // ---------------------------------------------------------------- C: Q.ux, tmp1
         double Quxc[m];
         if (replay) {
 #pragma unroll
@@ -430,20 +458,20 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
 #pragma unroll
           for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;  // sqrt AL adds no Q.ux term (A.5)
         }
-        {  // Q.ux += tmp_u' tmp_x (backward_pass.jl:118): both products from wave B's bus
-          double t[m];
+        {  // Q.ux += tmp_u' tmp_x (backward_pass.jl:118): both products from wave B's bus, read up front
+          double tx[n], tu[n][m], t[m];
+#pragma unroll
+          for (int l = 0; l < n; l++) {
+            tx[l] = TXb[l + n * c];
+#pragma unroll
+            for (int i = 0; i < m; i++) tu[l][i] = TUb[l + n * i];
+          }
 #pragma unroll
           for (int i = 0; i < m; i++) t[i] = 0.0;
-#pragma unroll 1
-          for (int l = 0; l < n; l++) {
-            double tu[m];
-            const double tx = TXb[l + n * c];
 #pragma unroll
-            for (int i = 0; i < m; i++) tu[i] = TUb[l + n * i];
-            TEAM_FENCE();
+          for (int l = 0; l < n; l++)
 #pragma unroll
-            for (int i = 0; i < m; i++) t[i] = fma(tu[i], tx, t[i]);
-          }
+            for (int i = 0; i < m; i++) t[i] = fma(tu[l][i], tx[l], t[i]);
 #pragma unroll
           for (int i = 0; i < m; i++) Quxc[i] += t[i];
         }
@@ -456,15 +484,41 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
 #pragma unroll
           for (int i = 0; i < m; i++) Qs[(size_t)k * NQ + n + m + n * n + m * m + i + m * tl] = Quxc[i];
         }
-        DPROF(1);
-        // tmp1 = (Q.xx') \ Q.ux' (lane i owns row i of tmp1) and tmp2 = chol_minus(Q.uu, tmp1)
-        // (backward_pass.jl:186-192, contract v4), fused: step j of the substitution finalises row j of
-        // tmp1, which enters the systolic downdate at its step j (lane 0; the rows move one lane per step)
+        DPROF(13);
+        // tmp1 = (Q.xx') \ Q.ux' by distributed forward substitution (lane i owns row i), step j as row j
+        // of the factor is released; row j of tmp1 is final after step j and released in turn
         double t1[m];
 #pragma unroll
         for (int i = 0; i < m; i++) t1[i] = Quxc[i];
+        static_for<0, n>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          tag_wait(&rxf[j]);
+          const double rj = RX[j + n * c];  // row j of the factor: R[j][j] on lane j, R[j][c] on lane c
+          if (tl == j) {
+            const double rdiag = 1.0 / rj;
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = t1[i] * rdiag;
+          }
+          double xj[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) xj[i] = row_bcast<j>(t1[i]);
+          if (tl > j && colx) {
+#pragma unroll
+            for (int i = 0; i < m; i++) t1[i] = fma(-rj, xj[i], t1[i]);
+          }
+          if (tl == j) {
+#pragma unroll
+            for (int i = 0; i < m; i++) busA[TB + j * m + i] = t1[i];
+          }
+          tag_store(&t1f[j]);
+        });
+        DPROF(14);
+      } else {
+        // ---------------------------------------------------------------- D: tmp2 = chol_minus(Q.uu, tmp1)
+        // (backward_pass.jl:186-192, contract v4): k_bwd_team's systolic schedule, step t as row t of
+        // tmp1 is released (lane 0 takes it; the rows move one lane per step)
         tag_wait(quf);
-        DPROF(3);
+        DPROF(17);
         double u[m], w[m], x0[m];
 #pragma unroll
         for (int kk = 0; kk < m; kk++) {
@@ -498,31 +552,14 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
           u[0] = act ? cs * u[0] : u[0];
           ru = act ? ru * rc : ru;
         };
-        static_for<0, n>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          tag_wait(&rxf[j]);
-          const double rj = RX[j + n * c];  // row j of the factor: R[j][j] on lane j, R[j][c] on lane c
-          if (tl == j) {
-            const double rdiag = 1.0 / rj;
+        static_for<0, n>([&](auto tc) {
+          constexpr int t = decltype(tc)::value;
+          tag_wait(&t1f[t]);
 #pragma unroll
-            for (int i = 0; i < m; i++) t1[i] = t1[i] * rdiag;
-          }
-          double xj[m];
-#pragma unroll
-          for (int i = 0; i < m; i++) xj[i] = row_bcast<j>(t1[i]);
-          if (tl > j && colx) {
-#pragma unroll
-            for (int i = 0; i < m; i++) t1[i] = fma(-rj, xj[i], t1[i]);
-          }
-          if (tl == j) {
-#pragma unroll
-            for (int i = 0; i < m; i++) busA[TB + j * m + i] = t1[i];
-          }
-#pragma unroll
-          for (int i = 0; i < m; i++) x0[i] = xj[i];
-          chol_step(j);
+          for (int kk = 0; kk < m; kk++) x0[kk] = busA[TB + t * m + kk];
+          chol_step(t);
         });
-        DPROF(4);
+        DPROF(18);
 #pragma unroll 1
         for (int t = n; t < n + m - 1; t++) chol_step(t);  // (lane 0 idle: its input stays row n-1)
         const unsigned long long rowmask = 0xFFFFull << (threadIdx.x & 48);
@@ -535,12 +572,12 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
           for (int kk = 0; kk < m; kk++)
             if (tl + kk < m) bus2[2 * m * m + tl + m * (tl + kk)] = u[kk];
         }
-        if (threadIdx.x == 128) flg[2] = pd_fail ? 1 : 0;
-        DPROF(5);
+        if (threadIdx.x == 192) flg[2] = pd_fail ? 1 : 0;
+        DPROF(19);
       }
       if (faithful) kmin = k < kmin ? k : kmin;
-      __syncthreads();  // B2b: K, d, the verdict, tmp1 and tmp2 on the bus
-      DPROF(wv == 0 ? 6 : (wv == 1 ? 17 : 12));
+      __syncthreads();  // B2b: tmp2, the verdict and the downdate's failure flag on the bus
+      DPROF(wv == 0 ? 4 : (wv == 1 ? 10 : (wv == 2 ? 15 : 26)));
       if (flg[0] == 0) {
         // non-PD / cond > 1e8: increase ρ and restart at N-1; Q blocks are NOT re-expanded (A.1)
         if (!faithful) {
@@ -570,24 +607,9 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
       if (wv == 0) {
         if (k > 0) load_qxx(k - 1, Qxn);  // (in flight during the S-update)
         const double* U2p = bus2 + 2 * m * m;  // tmp2
-        double Kc[m];
-#pragma unroll
-        for (int i = 0; i < m; i++) Kc[i] = KB[i + m * c];
-        constexpr int RS = n + m;
         double a[RS];
-        {
-          double v[n];
 #pragma unroll
-          for (int i = 0; i < n; i++) v[i] = 0.0;
-#pragma unroll
-          for (int l = 0; l < m; l++) {
-#pragma unroll
-            for (int i = 0; i < n; i++) v[i] = fma(busA[TB + i * m + l], Kc[l], v[i]);
-            TEAM_FENCE();
-          }
-#pragma unroll
-          for (int i = 0; i < n; i++) a[i] = Qxc[i] + v[i];
-        }
+        for (int i = 0; i < n; i++) a[i] = a2[i];
 #pragma unroll
         for (int i = 0; i < m; i++) {
           double v = 0.0;
@@ -595,7 +617,6 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
           for (int l = 0; l < m; l++) v = fma(U2p[i + m * l], Kc[l], v);
           a[n + i] = v;
         }
-        DPROF(7);
         // release row j of S_k after column step j: the row (zeros left of the diagonal), then its tag
         auto release = [&](auto jc, const double (&r)[RS]) {
           constexpr int j = decltype(jc)::value;
@@ -607,7 +628,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
 #pragma unroll
           for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = (i <= tl) ? a[i] : 0.0;
         }
-        DPROF(8);
+        DPROF(5);
       } else if (wv == 1 && k > 0) {  // the next knot's S_k A_{k-1} and S_k B_{k-1}, row by row
         load_ab(k - 1, Ac, Bc);
         static_for<0, n>([&](auto ic) {
@@ -618,7 +639,7 @@ k_bwd_trio(const DevProblem* P, DevBuffers Bf, int flags) {
         DPROF(11);
       }
       __syncthreads();  // B3: S_k for the next knot, S_k A_{k-1} and S_k B_{k-1} on the bus
-      DPROF(wv == 0 ? 9 : (wv == 1 ? 18 : 19));
+      DPROF(wv == 0 ? 25 : (wv == 1 ? 12 : (wv == 2 ? 16 : 27)));
     }
     if (!restart) done = true;
   }

@@ -2869,6 +2869,7 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
 #include "tog_bwd_team.hpp"
 #include "tog_bwd_duo.hpp"
 #include "tog_bwd_trio.hpp"
+#include "tog_bwd_quad.hpp"
 #include "tog_pn.hpp"
 namespace tog {
 
@@ -3213,17 +3214,22 @@ struct ModelLaunch {
           else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
         }
       };
-      // TOG_BWD_TAIL: "trio" (default), "duo", or "team" (the one-wave team kernel), for A/B checks
-      // (read per launch: tests switch it within one process)
+      // TOG_BWD_TAIL: "quad" (default), "trio", "duo", or "team" (the one-wave team kernel), for A/B
+      // checks (read per launch: tests switch it within one process)
       const char* tk = getenv("TOG_BWD_TAIL");
-      const int tail_kind = (getenv("TOG_NO_DUO") || (tk && !strcmp(tk, "team"))) ? 0 : ((tk && !strcmp(tk, "duo")) ? 2 : 3);
+      const int tail_kind = (getenv("TOG_NO_DUO") || (tk && !strcmp(tk, "team")))
+                                ? 0
+                                : (tk && !strcmp(tk, "duo")) ? 2 : (tk && !strcmp(tk, "trio")) ? 3 : 4;
       if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && tail_kind) {
-        // convergence tail, square-root pass, one trajectory per workgroup: the QRs, the side work and
-        // the downdate on three waves (tog_bwd_trio.hpp), or the chain and the side work on two
-        // (tog_bwd_duo.hpp)
+        // convergence tail, square-root pass, one trajectory per workgroup: the QRs, the side work, tmp1
+        // and the downdate on four waves (tog_bwd_quad.hpp), the last two on one (tog_bwd_trio.hpp), or
+        // the chain and the side work on two (tog_bwd_duo.hpp)
         if constexpr (TeamCfg<M>::TEAM == 16) {
           const dim3 gd((unsigned)B);
-          if (tail_kind == 3) {
+          if (tail_kind == 4) {
+            if (al) hipLaunchKernelGGL((k_bwd_quad<M, 1>), gd, dim3(256), 0, st, P, Bf, flags);
+            else hipLaunchKernelGGL((k_bwd_quad<M, 0>), gd, dim3(256), 0, st, P, Bf, flags);
+          } else if (tail_kind == 3) {
             if (al) hipLaunchKernelGGL((k_bwd_trio<M, 1>), gd, dim3(192), 0, st, P, Bf, flags);
             else hipLaunchKernelGGL((k_bwd_trio<M, 0>), gd, dim3(192), 0, st, P, Bf, flags);
           } else {
