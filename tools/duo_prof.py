@@ -69,7 +69,7 @@ for wname, ids in WAVES.items():
     for i in ids:
         print(f"  {NAMES.get(i, '-'):40s} {100.0 * buf[i] / max(tot, 1):6.2f}%  {buf[i] / knots:9.1f} cyc/knot")
 # the tail rollouts (k_ls_spec_tail2), per solver step
-T2 = {20: "rollout A: dynamics (per ring group)", 21: "rollout A: wait for B", 22: "rollout B: costs, rows, stores",
+T2 = {20: "rollout A: dynamics (per ring group)", 21: "rollout A: wait for B", 22: "rollout B: stage costs, stores",
       23: "rollout B: staging", 24: "rollout B: wait for A"}
 tot2 = sum(buf[i] for i in T2)
 print(f"tail rollouts: {tot2 / steps:.0f} cyc/step (both waves)")

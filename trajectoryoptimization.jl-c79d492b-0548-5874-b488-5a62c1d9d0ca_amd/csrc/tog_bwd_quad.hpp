@@ -40,7 +40,9 @@ struct QuadLayout {  // doubles in the workgroup's LDS
   static constexpr int BB = BA + BA_SIZE;     // wave B's bus: :state B columns, cond scratch
   static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
   static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] verdict (1 ok), [2] this knot's chol_minus failure (C -> all)
-  static constexpr int TAGS = FLAGS + 2;      // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux,
+  static constexpr int PAD = FLAGS + 2;       // 16 doubles: where the lanes past the team's columns store
+                                              // their part of a released row (no per-lane branch)
+  static constexpr int TAGS = PAD + 16;       // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux,
                                               // tmp1 rows (n), K
   static constexpr int NTAGS = 3 * n + 3;
   static constexpr int TOTAL = TAGS + (NTAGS + 1) / 2;
@@ -87,6 +89,7 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   double* RX = lds + D::RX;
   double* busA = lds + D::BA;
   double* busB = lds + D::BB;
+  double* pad = lds + D::PAD;
   int* flg = reinterpret_cast<int*>(lds + D::FLAGS);
   constexpr int SOFF = n * n;
   constexpr int TB = 32;
@@ -117,9 +120,8 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   // scope, because the hardware needs no wait for the order (a wave's LDS operations are performed in
   // issue order) -- and unlike a compiler barrier it leaves the scheduler free to move arithmetic
   // across the release.
-  auto tag_store = [&](int* t) {
-    if (tl == 0) __hip_atomic_store(t, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WAVEFRONT);
-  };
+  // (every lane stores the same tag: no exec-mask change splits the scheduling region)
+  auto tag_store = [&](int* t) { __hip_atomic_store(t, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WAVEFRONT); };
   auto tag_wait = [&](int* t) {
     while (__hip_atomic_load(t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq) {
     }
@@ -137,6 +139,24 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
     } else {
 #pragma unroll
       for (int i = 0; i < n; i++) Qx[i] = P->cQ[i + n * c];
+    }
+  };
+  // wave B: knot kk's Q.x entry, Q.u and Q.uu column (the replayed ones in faithful mode), a knot ahead
+  auto load_b = [&](int kk, double& xs, double (&qu)[m], double (&quu)[m]) {
+    if (faithful && kk >= kmin) {
+      const double* qk = Qs + (size_t)kk * NQ;
+      xs = qk[c];
+#pragma unroll
+      for (int i = 0; i < m; i++) qu[i] = qk[n + i];
+#pragma unroll
+      for (int i = 0; i < m; i++) quu[i] = qk[n + m + n * n + i + m * cu];
+    } else {
+      const double* ek = Eg + (size_t)kk * NE;
+      xs = ek[c];
+#pragma unroll
+      for (int i = 0; i < m; i++) qu[i] = ek[n + i];
+#pragma unroll
+      for (int i = 0; i < m; i++) quu[i] = ek[n + m + i + m * cu];
     }
   };
   // wave B: this lane's columns of A_kk and B_kk
@@ -186,11 +206,12 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
     }
     __syncthreads();
     // carried across knots: wave A's next Q.xx column; wave B's A_k, B_k columns and S_{k+1} B_k
-    double Qxn[n], Ac[n], Bc[n], Tb[n];
+    double Qxn[n], Ac[n], Bc[n], Tb[n], Bxs, Bqu[m], Bquu[m];
     if (wv == 0) {
       load_qxx(N - 2, Qxn);
     } else if (wv == 1) {  // the first knot's products, from the whole terminal factor
       load_ab(N - 2, Ac, Bc);
+      load_b(N - 2, Bxs, Bqu, Bquu);
       static_for<0, n>([&](auto ic) { row_products(ic, Ac, Bc, Tb); });
     }
     __syncthreads();
@@ -200,7 +221,6 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
     for (int k = N - 2; k >= 0; k--) {
       seq++;
       const bool replay = faithful && k >= kmin;
-      const double* e = Eg + (size_t)k * NE;
       const double* q = Qs + (size_t)k * NQ;
       double Qxc[n];  // (wave A's Q.xx factor column, kept for the S-update operands)
       double a2[RS], Kc[m];  // (wave A's S-update operand column and K column, across B2b)
@@ -216,7 +236,7 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
           DPROF(0);
           auto release = [&](auto jc, const double (&r)[2 * n]) {
             constexpr int j = decltype(jc)::value;
-            if (colx) RX[j + n * tl] = (j <= tl) ? r[j] : 0.0;
+            *(colx ? RX + j + n * tl : pad + tl) = (j <= tl) ? r[j] : 0.0;
             tag_store(&rxf[j]);
           };
           team_qr<2 * n, n, n, TEAM, false>(a, 2 * n, tl, busA, release);
@@ -251,19 +271,11 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         DPROF(3);
       } else if (wv == 1) {
         // ---------------------------------------------------------------- B: Q.x, Q.u, qr([Q.uu; S B]), gains
-        double Qxs, Qu[m], Quuc[m], Quxc[m];
-        if (replay) {
-          Qxs = q[c];
+        double Qxs = Bxs, Qu[m], Quuc[m], Quxc[m];
 #pragma unroll
-          for (int i = 0; i < m; i++) Qu[i] = q[n + i];
-#pragma unroll
-          for (int i = 0; i < m; i++) Quuc[i] = q[n + m + n * n + i + m * cu];
-        } else {
-          Qxs = e[c];
-#pragma unroll
-          for (int i = 0; i < m; i++) Qu[i] = e[n + i];
-#pragma unroll
-          for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
+        for (int i = 0; i < m; i++) {
+          Qu[i] = Bqu[i];
+          Quuc[i] = Bquu[i];
         }
         {  // Q.uu <- qr([Q.uu; tmp_u]).R (backward_pass.jl:117), released to wave C
           double a[m + n];
@@ -532,10 +544,8 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
           const bool act = colu && r >= 0 && r < n;
           double x[m];
 #pragma unroll
-          for (int kk = 0; kk + 1 < m; kk++) x[kk] = row_shr1(w[kk + 1]);
-          x[m - 1] = 0.0;
-#pragma unroll
-          for (int kk = 0; kk < m; kk++) x[kk] = (tl == 0) ? x0[kk] : x[kk];
+          for (int kk = 0; kk + 1 < m; kk++) x[kk] = row_shr1_or(w[kk + 1], x0[kk]);  // (lane 0: x0)
+          x[m - 1] = (tl == 0) ? x0[m - 1] : 0.0;
           const double sn = x[0] * ru;
           const double s2 = sn * sn;
           okd = okd && !(act && s2 > 1.0);
@@ -620,7 +630,7 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         // release row j of S_k after column step j: the row (zeros left of the diagonal), then its tag
         auto release = [&](auto jc, const double (&r)[RS]) {
           constexpr int j = decltype(jc)::value;
-          if (colx) Sreg[j + n * tl] = (j <= tl) ? r[j] : 0.0;
+          *(colx ? Sreg + j + n * tl : pad + tl) = (j <= tl) ? r[j] : 0.0;
           tag_store(&rowf[j]);
         };
         team_qr<RS, n, 0, TEAM, false>(a, RS, tl, busA, release);
@@ -631,6 +641,7 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         DPROF(5);
       } else if (wv == 1 && k > 0) {  // the next knot's S_k A_{k-1} and S_k B_{k-1}, row by row
         load_ab(k - 1, Ac, Bc);
+        load_b(k - 1, Bxs, Bqu, Bquu);
         static_for<0, n>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
           tag_wait(&rowf[i]);

@@ -197,6 +197,15 @@ __device__ __forceinline__ double row_bcast(double v) {
   return __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(v), v, 0x150 + L, 0xF, 0xF, true);
 }
 
+// Lane i of each DPP row receives lane i-1's value, lane 0 of the row `old` (row_shr:1 with bound_ctrl
+// off: the lane without a source keeps the old operand)
+__device__ __forceinline__ double row_shr1_or(double v, double old) {
+  const long long x = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(x & 0xffffffffll), 0x111, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(x >> 32), 0x111, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // Lane i of each DPP row receives lane i-1's value (row_shr:1, two 32-bit DPP moves: 64-bit DPP
 // only has row_newbcast); lane 0 of the row receives 0.
 __device__ __forceinline__ double row_shr1(double v) {

@@ -2189,12 +2189,14 @@ __global__ void __launch_bounds__(64) k_ls_spec_tail(const DevProblem* __restric
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_ls_spec_tail2: k_ls_spec_tail on two waves (at most 32 trials). Wave A runs the dynamics chain
-// (ū + K δx + α d, the RK step, the divergence test) and hands each step's (x_s, u_s) to wave B through an
-// LDS ring of SPEC_RQ steps; wave B, one group of steps behind, adds the stage costs and AL row terms (in
-// rollout_cost's order), issues the candidate stores, and stages the next chunk of K, ū, d, x, λ, μ into
-// the other half of a double-buffered image. One workgroup barrier per group of SPEC_RQ steps. The
-// instructions off wave A's chain (rows, cost, stores, staging) are about a quarter of a step's.
+// k_ls_spec_tail2: k_ls_spec_tail on three waves (at most 32 trials). Wave A runs the dynamics chain
+// (ū + K δx + α d, the RK step, the divergence test) and hands each step's (x_s, u_s) to the cost waves
+// through an LDS ring of SPEC_RQ steps; one group of steps behind, wave B adds the stage costs, issues the
+// candidate stores and stages the next chunk of K, ū, d, x, λ, μ into the other half of a double-buffered
+// image, and wave C adds the AL row terms. The two running sums are rollout_cost's own (J over the stage
+// costs, Jc over the row terms, J + Jc at the end), each in knot order, so splitting them between waves
+// keeps every bit. One workgroup barrier per group of SPEC_RQ steps. (With the rows on wave B as well,
+// wave A waited on B for a fifth of the rollout: profiles/r4o_trio_sections_b1.txt.)
 constexpr int SPEC_RQ = 4;      // steps per ring slot (and per barrier)
 constexpr int SPEC_LANES = 32;  // trials per workgroup
 // layout: two staging images (each with the terminal λ, μ after it), the ring, then SPEC_LANES ints of
@@ -2204,14 +2206,14 @@ __host__ __device__ constexpr int spec_tail2_ring_off(int n, int m, int pmax) {
 }
 __host__ __device__ constexpr int spec_tail2_doubles(int n, int m, int pmax) {
   return spec_tail2_ring_off(n, m, pmax) + 2 * SPEC_RQ * (n + m) * SPEC_LANES +
-         (SPEC_LANES * (int)sizeof(int) + (int)sizeof(double) - 1) / (int)sizeof(double);
+         (SPEC_LANES * (int)sizeof(int) + (int)sizeof(double) - 1) / (int)sizeof(double) + SPEC_LANES;
 }
 static_assert(spec_tail2_doubles(13, 4, 13) - spec_tail2_ring_off(13, 4, 13) - 2 * SPEC_RQ * 17 * SPEC_LANES ==
-                  SPEC_LANES / 2,
-              "live_out needs SPEC_LANES ints after the ring");
+                  SPEC_LANES / 2 + SPEC_LANES,
+              "live_out needs SPEC_LANES ints after the ring, then SPEC_LANES doubles for wave C's Jc");
 
 template <class M, int INTEG, int DC>
-__global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
+__global__ void __launch_bounds__(192) k_ls_spec_tail2(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
                                                         int lo, int cnt) {
   constexpr int n = M::n, m = M::m, MN = m * n, W = n + m;
   constexpr int TC = spec_tail_tc(n, m);
@@ -2225,7 +2227,7 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
   if (!st.active || lo + st.ls_pend >= Bf.nc) return;  // (uniform over the block)
   extern __shared__ double tl2[];
   BPROF_DECL
-  const int wv = threadIdx.x >> 6;  // 0: chain wave A, 1: cost wave B
+  const int wv = threadIdx.x >> 6;  // 0: chain wave A, 1: cost wave B, 2: row wave C
   const int lane = threadIdx.x & (WAVE - 1);
   const int j = lo + st.ls_pend + lane;
   const int N = P->N, pmax = P->pmax, NC = Bf.nc;
@@ -2235,6 +2237,7 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
   const int IMG = TCR + 2 * PL;                 // one staging image, the terminal λ, μ after it
   double* ring = tl2 + 2 * IMG;                 // [slot][step][element][lane]
   int* live_out = reinterpret_cast<int*>(ring + 2 * SPEC_RQ * W * SPEC_LANES);
+  double* jc_out = ring + 2 * SPEC_RQ * W * SPEC_LANES + (SPEC_LANES * (int)sizeof(int) + 7) / 8;  // (wave C's Jc)
   // (2 * IMG <= spec_tail2_ring_off(n, m, pmax): PL <= pmax, so live_out[SPEC_LANES) ends inside the
   // spec_tail2_doubles(n, m, pmax) the runtime allocates)
   const double* X = Bf.X + (size_t)b * N * n;
@@ -2337,21 +2340,21 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
       __syncthreads();
       DPROF(21);
     }
-    // the final state and the verdict for wave B (x_{N-1} in ring slot 0, step 0)
+    // the final state and the verdict for the cost waves (x_{N-1} in ring slot 0, step 0)
     if (lane < SPEC_LANES) {
 #pragma unroll
       for (int i = 0; i < n; i++) ring[(size_t)i * SPEC_LANES + lane] = xb[i];
       live_out[lane] = live ? 1 : 0;
     }
     __syncthreads();
-  } else {
-    // ---------------------------------------------------------------- wave B: costs, stores, staging
-    const RowTablesC RT = const_row_tables(P);
+    __syncthreads();  // (wave C's Jc to wave B)
+  } else if (wv == 1) {
+    // ---------------------------------------------------------------- wave B: stage costs, stores, staging
     double* cw = on ? static_cast<double*>(__builtin_assume_aligned(
                           Bf.cand + ((size_t)b * N * cand_q<M>() * Bf.ncp + j) * 4, 32))
                     : nullptr;
     const int ncp = Bf.ncp;
-    double J = 0.0, Jc = 0.0;
+    double J = 0.0;
 #pragma unroll 1
     for (int g = 0; g <= G; g++) {
       // staging of the next chunk: loads in the chunk's second group, stores in its last one
@@ -2359,13 +2362,11 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
       if (cg == (GPC > 1 ? 1 : 0) && (ch + 1) * TC < NS) stage_load((ch + 1) * TC);
       if (g >= 1 && on) {
         const int gp = g - 1;
-        const double* img = tl2 + ((gp / GPC) & 1) * IMG;
         const double* slot = ring + (size_t)(gp & 1) * SPEC_RQ * W * SPEC_LANES;
 #pragma unroll 1
         for (int q = 0; q < SPEC_RQ; q++) {
           const int s = gp * SPEC_RQ + q;
           if (s >= NS) break;
-          const int c = s % TC;
           const double* e = slot + (size_t)q * W * SPEC_LANES + lane;
           double x[n], u[m];
 #pragma unroll
@@ -2379,23 +2380,6 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
             for (int i = 0; i < n; i++) __builtin_nontemporal_store(x[i], cw + cand_at(s, m + i, cand_q<M>(), ncp));
           }
           J += stage_cost_m<M, DC>(P, x, u);
-          if (al) {
-            const int pc = RT.kcnt[s];
-            if (pc) {
-              const cptr<ConRow> rows = RT.rows + RT.koff[s];
-              double lc = 0.0, cIc = 0.0;
-              for (int r = 0; r < pc; r++) {
-                const ConRow row = uniform_row(load_row(rows + r));
-                const double cv = row_value_m<M, true>(row, x, u);
-                const double l = img[OL + c * PL + r];
-                const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((cv >= 0.0) || (l > 0.0)) : true;
-                const double w = a ? img[OM + c * PL + r] : 0.0;
-                lc = fma(l, cv, lc);
-                cIc = fma(cv * w, cv, cIc);
-              }
-              Jc += lc + 0.5 * cIc;
-            }
-          }
         }
       }
       DPROF(22);
@@ -2405,39 +2389,90 @@ __global__ void __launch_bounds__(128) k_ls_spec_tail2(const DevProblem* __restr
       DPROF(24);
     }
     __syncthreads();  // wave A's final state and verdict
+    double x[n];
+    bool live = false;
     if (on) {
-      const bool live = live_out[lane] != 0;
-      double x[n];
+      live = live_out[lane] != 0;
 #pragma unroll
       for (int i = 0; i < n; i++) x[i] = ring[(size_t)i * SPEC_LANES + lane];
 #pragma unroll
       for (int i = 0; i < n; i++) __builtin_nontemporal_store(x[i], cw + cand_at(NS, m + i, cand_q<M>(), ncp));
+      if (live) J += terminal_cost_m<M, DC>(P, x);
+    }
+    __syncthreads();  // wave C's Jc
+    if (on) {
       double Jj = INFINITY;
-      if (live) {
-        J += terminal_cost_m<M, DC>(P, x);
-        if (al) {  // terminal rows (al_knot_terms' order), multipliers from the image
-          const int pc = RT.kcnt[N - 1];
-          if (pc) {
-            const cptr<ConRow> rows = RT.rows + RT.koff[N - 1];
-            double lc = 0.0, cIc = 0.0;
-            for (int r = 0; r < pc; r++) {
-              const ConRow row = uniform_row(load_row(rows + r));
-              const double cv = row_value_m<M, true>(row, x, nullptr);
-              const double l = tl2[TCR + r];
-              const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((cv >= 0.0) || (l > 0.0)) : true;
-              const double w = a ? tl2[TCR + PL + r] : 0.0;
-              lc = fma(l, cv, lc);
-              cIc = fma(cv * w, cv, cIc);
-            }
-            Jc += lc + 0.5 * cIc;
-          }
-          J = J + Jc;
-        }
-        Jj = J;
-      }
+      if (live) Jj = al ? J + jc_out[lane] : J;
       Bf.lsJ[b * NC + j] = Jj;
       Bf.lsok[b * NC + j] = live ? 1 : 0;
     }
+  } else {
+    // ---------------------------------------------------------------- wave C: the AL row terms
+    const RowTablesC RT = const_row_tables(P);
+    double Jc = 0.0;
+    auto row_terms = [&](const cptr<ConRow> rows, int pc, const double* x, const double* u, const double* lp,
+                         const double* mp) {
+      double lc = 0.0, cIc = 0.0;
+      constexpr int RU = 8;  // the first RU rows unrolled (their table loads issue together)
+#pragma unroll
+      for (int r = 0; r < RU; r++) {
+        if (r < pc) {
+          const ConRow row = uniform_row(load_row(rows + r));
+          const double cv = row_value_m<M, true>(row, x, u);
+          const double l = lp[r];
+          const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((cv >= 0.0) || (l > 0.0)) : true;
+          const double w = a ? mp[r] : 0.0;
+          lc = fma(l, cv, lc);
+          cIc = fma(cv * w, cv, cIc);
+        }
+      }
+      for (int r = RU; r < pc; r++) {
+        const ConRow row = uniform_row(load_row(rows + r));
+        const double cv = row_value_m<M, true>(row, x, u);
+        const double l = lp[r];
+        const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(row) ? ((cv >= 0.0) || (l > 0.0)) : true;
+        const double w = a ? mp[r] : 0.0;
+        lc = fma(l, cv, lc);
+        cIc = fma(cv * w, cv, cIc);
+      }
+      Jc += lc + 0.5 * cIc;
+    };
+#pragma unroll 1
+    for (int g = 0; g <= G; g++) {
+      if (al && g >= 1 && on) {
+        const int gp = g - 1;
+        const double* img = tl2 + ((gp / GPC) & 1) * IMG;
+        const double* slot = ring + (size_t)(gp & 1) * SPEC_RQ * W * SPEC_LANES;
+#pragma unroll 1
+        for (int q = 0; q < SPEC_RQ; q++) {
+          const int s = gp * SPEC_RQ + q;
+          if (s >= NS) break;
+          const int pc = RT.kcnt[s];
+          if (!pc) continue;
+          const int c = s % TC;
+          const double* e = slot + (size_t)q * W * SPEC_LANES + lane;
+          double x[n], u[m];
+#pragma unroll
+          for (int i = 0; i < n; i++) x[i] = e[i * SPEC_LANES];
+#pragma unroll
+          for (int i = 0; i < m; i++) u[i] = e[(n + i) * SPEC_LANES];
+          row_terms(RT.rows + RT.koff[s], pc, x, u, img + OL + c * PL, img + OM + c * PL);
+        }
+      }
+      __syncthreads();
+    }
+    __syncthreads();  // wave A's final state and verdict
+    if (al && on && live_out[lane] != 0) {  // terminal rows (al_knot_terms' order), multipliers from the image
+      const int pc = RT.kcnt[N - 1];
+      if (pc) {
+        double x[n];
+#pragma unroll
+        for (int i = 0; i < n; i++) x[i] = ring[(size_t)i * SPEC_LANES + lane];
+        row_terms(RT.rows + RT.koff[N - 1], pc, x, nullptr, tl2 + TCR, tl2 + TCR + PL);
+      }
+      jc_out[lane] = Jc;
+    }
+    __syncthreads();
   }
   BPROF_FLUSH
 }
@@ -3276,7 +3311,7 @@ struct ModelLaunch {
     // the tail kernels inline the diagonal cost only (the dense cost's run-time indexing of x, u would put
     // them in scratch); dense costs take k_ls_spec
     if (Bf.tail && Bf.cand && Bf.spec_tail2_shmem > 0 && Bf.cost_diag && !list && cnt <= SPEC_LANES) {
-      hipLaunchKernelGGL((k_ls_spec_tail2<M, INTEG, 1>), dim3((unsigned)B), dim3(2 * WAVE),
+      hipLaunchKernelGGL((k_ls_spec_tail2<M, INTEG, 1>), dim3((unsigned)B), dim3(3 * WAVE),
                          (unsigned)Bf.spec_tail2_shmem, st, P, Bf, mode, lo, cnt);
       return;
     }
