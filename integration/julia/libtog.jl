@@ -15,6 +15,7 @@
 # tog_desc below does and is checked bit for bit against the Python path on the GPU.
 
 using Parameters
+using LinearAlgebra: PosDefException
 
 const libtog = get(ENV, "TOG_LIB", "libtog.so")
 
@@ -32,6 +33,7 @@ const TOG_PN_NSTATS = 7
 const TOG_STAT_J, TOG_STAT_ITERATIONS, TOG_STAT_C_MAX, TOG_STAT_AL_ITER, TOG_STAT_TOTAL_STEPS,
       TOG_STAT_FLAGS = 0, 3, 7, 8, 9, 12
 const TOG_TRAJ_COST_INCREASED = Int32(1 << 3)
+const TOG_TRAJ_SQRT_PD_FAIL = Int32(1 << 6)     # lowrankdowndate! PosDefException (the trajectory stopped)
 const TOG_MODEL_USER = Int32(100)
 
 struct TogConstraint
@@ -425,7 +427,10 @@ function solve!(probs::Vector{<:Problem{T}}, s::BatchediLQRSolver{T}) where T
     s.stats[:c_max] = St[TOG_STAT_C_MAX+1, :]
     s.stats[:iterations_outer] = Int.(St[TOG_STAT_AL_ITER+1, :])
     s.stats[:flags] = flags
-    any(f -> f & TOG_TRAJ_COST_INCREASED != 0, flags) && error("Cost increased during Forward Pass")  # forward_pass.jl:80-82
+    # the reference's exceptions, after the batch: chol_minus's PosDefException (backward_pass.jl:186-192),
+    # then the cost increase (forward_pass.jl:80-82)
+    any(f -> f & TOG_TRAJ_SQRT_PD_FAIL != 0, flags) && throw(PosDefException(0))
+    any(f -> f & TOG_TRAJ_COST_INCREASED != 0, flags) && error("Cost increased during Forward Pass")
     return s
 end
 
@@ -510,6 +515,7 @@ function solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float6
         copyto!(prob.U, [U[:, k] for k = 1:N-1])
     end
     flags = Int32(St[TOG_STAT_FLAGS+1]) | Int32(Sr[TOG_STAT_FLAGS+1])
+    flags & TOG_TRAJ_SQRT_PD_FAIL != 0 && throw(PosDefException(0))   # backward_pass.jl:186-192
     flags & TOG_TRAJ_COST_INCREASED != 0 && error("Cost increased during Forward Pass")  # forward_pass.jl:80-82
     return Dict{Symbol,Any}(:iterations => Int(St[TOG_STAT_TOTAL_STEPS+1]), :cost => St[TOG_STAT_J+1],
                             :c_max => St[TOG_STAT_C_MAX+1], :iterations_outer => Int(St[TOG_STAT_AL_ITER+1]),
