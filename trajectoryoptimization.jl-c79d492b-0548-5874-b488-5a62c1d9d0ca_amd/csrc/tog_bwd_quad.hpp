@@ -40,11 +40,13 @@ struct QuadLayout {  // doubles in the workgroup's LDS
   static constexpr int BB = BA + BA_SIZE;     // wave B's bus: :state B columns, cond scratch
   static constexpr int BB_SIZE = 2 * n * m + m * m + 8;
   static constexpr int FLAGS = BB + BB_SIZE;  // ints: [0] verdict (1 ok), [2] this knot's chol_minus failure (C -> all)
-  static constexpr int PAD = FLAGS + 2;       // 16 doubles: where the lanes past the team's columns store
+  static constexpr int QXT = FLAGS + 2;       // (S B)'(S A) for the next knot's Q.ux (m*n, column c from
+                                              // lane c of wave B, summed as S's rows were released)
+  static constexpr int PAD = QXT + m * n;     // 16 doubles: where the lanes past the team's columns store
                                               // their part of a released row (no per-lane branch)
-  static constexpr int TAGS = PAD + 16;       // ints: S_k rows (n), Q.xx factor rows (n), Q.uu, Q.ux,
+  static constexpr int TAGS = PAD + 16;       // ints: S_k rows (n), Q.xx factor rows (n), Q.uu rows (m), Q.ux,
                                               // tmp1 rows (n), K
-  static constexpr int NTAGS = 3 * n + 3;
+  static constexpr int NTAGS = 3 * n + m + 2;
   static constexpr int TOTAL = TAGS + (NTAGS + 1) / 2;
 };
 
@@ -74,8 +76,8 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   int* tags = reinterpret_cast<int*>(lds + D::TAGS);
   int* rowf = tags;           // S_k's rows (A -> B)
   int* rxf = tags + n;        // the new Q.xx factor's rows (A -> C)
-  int* quf = tags + 2 * n;    // the Q.uu factor (B -> C)
-  int* quxf = quf + 1;        // Q.ux (C -> B)
+  int* qurf = tags + 2 * n;   // the Q.uu factor's rows (B -> D)
+  int* quxf = qurf + m;       // Q.ux (C -> B)
   int* t1f = quxf + 1;        // tmp1's rows (C -> D, A)
   int* kf = t1f + n;          // K (B -> A)
   if (threadIdx.x < D::NTAGS) tags[threadIdx.x] = 0;
@@ -83,13 +85,13 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   double* Sreg = lds + D::S;
   double* QU = lds + D::QU;
   double* TXb = lds + D::TX;
-  double* TUb = lds + D::TU;
   double* QUXb = lds + D::QUX;
   double* KB = lds + D::KB;
   double* RX = lds + D::RX;
   double* busA = lds + D::BA;
   double* busB = lds + D::BB;
   double* pad = lds + D::PAD;
+  double* QXT = lds + D::QXT;
   int* flg = reinterpret_cast<int*>(lds + D::FLAGS);
   constexpr int SOFF = n * n;
   constexpr int TB = 32;
@@ -110,6 +112,31 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   s.flags = Bf.st[b].flags;
   const double rho0 = s.rho, drho0 = s.drho;
   constexpr int RS = n + m;  // rows of the S-update operand
+  // Registers carried across knots, one array shared by the wave roles (they are wave-exclusive; the
+  // compiler cannot know it, so separate arrays would all stay live in every wave and spill):
+  //   A: [0, n) the next knot's Q.xx column; [n, 2n) its Q.xx factor column, [2n, 2n+RS) the S-update
+  //      operand column and [2n+RS, 2n+RS+m) K's column (within a knot)
+  //   B: [0, n) A_k column, [n, 2n) B_k column, [2n, 3n) (S B) column, then Q.u (m), Q.uu column (m),
+  //      the Q.x entry
+  //   C: [0, m) the replayed Q.ux column, [m, 2m) H dt's column
+  constexpr int NR = (2 * n + RS + m) > (3 * n + 2 * m + 1) ? (2 * n + RS + m) : (3 * n + 2 * m + 1);
+  double R[NR];
+#pragma unroll
+  for (int i = 0; i < NR; i++) R[i] = 0.0;
+  auto view = [&](auto off_c, auto len_c) -> double (&)[decltype(len_c)::value] {
+    return *reinterpret_cast<double(*)[decltype(len_c)::value]>(R + decltype(off_c)::value);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using In = std::integral_constant<int, n>;
+  using I2n = std::integral_constant<int, 2 * n>;
+  using I3n = std::integral_constant<int, 3 * n>;
+  using Im = std::integral_constant<int, m>;
+  using IRS = std::integral_constant<int, RS>;
+  double(&Hdt)[m] = view(Im{}, Im{});  // (wave C) H dt's column, the Q.ux every non-replayed knot starts from
+  if (wv == 2) {
+#pragma unroll
+    for (int i = 0; i < m; i++) Hdt[i] = P->H[i + m * c] * dt;
+  }
   bool faithful = false;
   int kmin = N - 1, restarts = 0;
   double dV0 = 0.0, dV1 = 0.0;
@@ -170,7 +197,9 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   };
   // wave B: row i of tmp_x = S A and tmp_u = S B for this lane's columns, l ascending over the upper
   // factor's nonzero entries (the order of k_bwd_team's TRI_SA products: each entry is the same fma chain)
-  auto row_products = [&](auto ic, const double (&Ac)[n], const double (&Bc)[n], double (&Tb)[n]) {
+  // The next knot's tmp_u' tmp_x (backward_pass.jl:118) is accumulated here too, row i's terms as row i
+  // comes: t[ii] = fma(tmp_u[i][ii], tmp_x[i][c], t[ii]), i ascending -- the order of the Q.ux sum.
+  auto row_products = [&](auto ic, const double (&Ac)[n], const double (&Bc)[n], double (&Tb)[n], double (&tq)[m]) {
     constexpr int i = decltype(ic)::value;
     double sr[n - i];
 #pragma unroll
@@ -182,8 +211,17 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
       tu = fma(sr[l - i], Bc[l], tu);
     }
     if (colx) TXb[i + n * tl] = tx;
-    if (colu) TUb[i + n * tl] = tu;
     Tb[i] = tu;
+    static_for<0, m>([&](auto iic) {
+      constexpr int ii = decltype(iic)::value;
+      tq[ii] = fma(row_bcast<ii>(tu), tx, tq[ii]);
+    });
+  };
+  auto products_done = [&](const double (&tq)[m]) {
+    if (colx) {
+#pragma unroll
+      for (int ii = 0; ii < m; ii++) QXT[ii + m * tl] = tq[ii];
+    }
   };
 
   while (!done) {  // one attempt of the backward pass; a regularisation restart begins a new one
@@ -206,13 +244,30 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
     }
     __syncthreads();
     // carried across knots: wave A's next Q.xx column; wave B's A_k, B_k columns and S_{k+1} B_k
-    double Qxn[n], Ac[n], Bc[n], Tb[n], Bxs, Bqu[m], Bquu[m];
+    double(&Qxn)[n] = view(I0{}, In{});
+    double(&Ac)[n] = view(I0{}, In{});
+    double(&Bc)[n] = view(In{}, In{});
+    double(&Tb)[n] = view(I2n{}, In{});
+    double(&Bqu)[m] = view(I3n{}, Im{});
+    double(&Bquu)[m] = view(std::integral_constant<int, 3 * n + m>{}, Im{});
+    double& Bxs = R[3 * n + 2 * m];
+    double(&Cqr)[m] = view(I0{}, Im{});  // (wave C's replayed Q.ux)
+    auto load_cqr = [&](int kk) {
+      if (faithful && kk >= kmin) {
+        const double* qk = Qs + (size_t)kk * NQ;
+#pragma unroll
+        for (int i = 0; i < m; i++) Cqr[i] = qk[n + m + n * n + m * m + i + m * c];
+      }
+    };
+    if (wv == 2) load_cqr(N - 2);
     if (wv == 0) {
       load_qxx(N - 2, Qxn);
     } else if (wv == 1) {  // the first knot's products, from the whole terminal factor
       load_ab(N - 2, Ac, Bc);
       load_b(N - 2, Bxs, Bqu, Bquu);
-      static_for<0, n>([&](auto ic) { row_products(ic, Ac, Bc, Tb); });
+      double tq[m] = {};
+      static_for<0, n>([&](auto ic) { row_products(ic, Ac, Bc, Tb, tq); });
+      products_done(tq);
     }
     __syncthreads();
     dV0 = 0.0;
@@ -222,8 +277,9 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
       seq++;
       const bool replay = faithful && k >= kmin;
       const double* q = Qs + (size_t)k * NQ;
-      double Qxc[n];  // (wave A's Q.xx factor column, kept for the S-update operands)
-      double a2[RS], Kc[m];  // (wave A's S-update operand column and K column, across B2b)
+      double(&Qxc)[n] = view(In{}, In{});  // (wave A's Q.xx factor column, kept for the S-update operands)
+      double(&a2)[RS] = view(I2n{}, IRS{});  // (wave A's S-update operand column and K column, across B2b)
+      double(&Kc)[m] = view(std::integral_constant<int, 2 * n + RS>{}, Im{});
       // ------------------------------------------------------------------ A: qr([Q.xx; S A]), rows released
       if (wv == 0) {
         {  // Q.xx <- qr([Q.xx; tmp_x]).R (backward_pass.jl:116), tmp_x = S A from wave B's bus
@@ -277,19 +333,19 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
           Qu[i] = Bqu[i];
           Quuc[i] = Bquu[i];
         }
-        {  // Q.uu <- qr([Q.uu; tmp_u]).R (backward_pass.jl:117), released to wave C
+        {  // Q.uu <- qr([Q.uu; tmp_u]).R (backward_pass.jl:117), its rows released to wave D
           double a[m + n];
 #pragma unroll
           for (int i = 0; i < m + n; i++) a[i] = (i < m) ? Quuc[i] : Tb[i - m];
-          team_qr<m + n, m, m, TEAM>(a, m + n, tl, busB);
+          auto release = [&](auto jc, const double (&r)[m + n]) {
+            constexpr int j = decltype(jc)::value;
+            *(colu ? QU + j + m * tl : pad + tl) = (j <= tl) ? r[j] : 0.0;
+            tag_store(&qurf[j]);
+          };
+          team_qr<m + n, m, m, TEAM, false>(a, m + n, tl, busB, release);
 #pragma unroll
           for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
         }
-        if (colu) {
-#pragma unroll
-          for (int i = 0; i < m; i++) QU[i + m * tl] = Quuc[i];
-        }
-        tag_store(quf);
         // Q.x += A's ; Q.u += B's (backward_pass.jl:112-113)
         {
           double t = 0.0;
@@ -463,30 +519,11 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
       } else if (wv == 2) {
         // ---------------------------------------------------------------- C: Q.ux, tmp1
         double Quxc[m];
-        if (replay) {
 #pragma unroll
-          for (int i = 0; i < m; i++) Quxc[i] = q[n + m + n * n + m * m + i + m * c];
-        } else {
+        for (int i = 0; i < m; i++) Quxc[i] = replay ? Cqr[i] : Hdt[i];  // sqrt AL adds no Q.ux term (A.5)
+        // Q.ux += tmp_u' tmp_x (backward_pass.jl:118), the sum wave B formed from S_{k+1}'s rows
 #pragma unroll
-          for (int i = 0; i < m; i++) Quxc[i] = P->H[i + m * c] * dt;  // sqrt AL adds no Q.ux term (A.5)
-        }
-        {  // Q.ux += tmp_u' tmp_x (backward_pass.jl:118): both products from wave B's bus, read up front
-          double tx[n], tu[n][m], t[m];
-#pragma unroll
-          for (int l = 0; l < n; l++) {
-            tx[l] = TXb[l + n * c];
-#pragma unroll
-            for (int i = 0; i < m; i++) tu[l][i] = TUb[l + n * i];
-          }
-#pragma unroll
-          for (int i = 0; i < m; i++) t[i] = 0.0;
-#pragma unroll
-          for (int l = 0; l < n; l++)
-#pragma unroll
-            for (int i = 0; i < m; i++) t[i] = fma(tu[l][i], tx[l], t[i]);
-#pragma unroll
-          for (int i = 0; i < m; i++) Quxc[i] += t[i];
-        }
+        for (int i = 0; i < m; i++) Quxc[i] += QXT[i + m * c];
         if (colx) {
 #pragma unroll
           for (int i = 0; i < m; i++) QUXb[i + m * tl] = Quxc[i];
@@ -529,12 +566,13 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         // ---------------------------------------------------------------- D: tmp2 = chol_minus(Q.uu, tmp1)
         // (backward_pass.jl:186-192, contract v4): k_bwd_team's systolic schedule, step t as row t of
         // tmp1 is released (lane 0 takes it; the rows move one lane per step)
-        tag_wait(quf);
+        // lane i's row of the Q.uu factor is first used at step i (its first active step): it is loaded
+        // there, as row i is released (the lanes' earlier results are never consumed)
         DPROF(17);
         double u[m], w[m], x0[m];
 #pragma unroll
         for (int kk = 0; kk < m; kk++) {
-          u[kk] = (colu && tl + kk < m) ? QU[tl + m * (tl + kk)] : 0.0;
+          u[kk] = 0.0;
           w[kk] = 0.0;
         }
         double ru = 1.0 / u[0];
@@ -564,14 +602,21 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         };
         static_for<0, n>([&](auto tc) {
           constexpr int t = decltype(tc)::value;
+          if constexpr (t < m) {
+            tag_wait(&qurf[t]);
+            if (tl == t) {
+#pragma unroll
+              for (int kk = 0; kk < m; kk++) u[kk] = (t + kk < m) ? QU[t + m * (t + kk)] : 0.0;
+              ru = 1.0 / u[0];
+            }
+          }
           tag_wait(&t1f[t]);
 #pragma unroll
           for (int kk = 0; kk < m; kk++) x0[kk] = busA[TB + t * m + kk];
           chol_step(t);
         });
         DPROF(18);
-#pragma unroll 1
-        for (int t = n; t < n + m - 1; t++) chol_step(t);  // (lane 0 idle: its input stays row n-1)
+        static_for<n, n + m - 1>([&](auto tc) { chol_step(decltype(tc)::value); });  // (lane 0 idle: input row n-1)
         const unsigned long long rowmask = 0xFFFFull << (threadIdx.x & 48);
         const bool pd_fail = (__ballot(!okd) & rowmask) != 0ull;
         if (colu) {
@@ -639,14 +684,18 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
           for (int i = 0; i < n; i++) Bf.Sdbg[((size_t)b * N + k) * n * n + i + n * tl] = (i <= tl) ? a[i] : 0.0;
         }
         DPROF(5);
+      } else if (wv == 2 && k > 0) {
+        load_cqr(k - 1);
       } else if (wv == 1 && k > 0) {  // the next knot's S_k A_{k-1} and S_k B_{k-1}, row by row
         load_ab(k - 1, Ac, Bc);
         load_b(k - 1, Bxs, Bqu, Bquu);
+        double tq[m] = {};
         static_for<0, n>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
           tag_wait(&rowf[i]);
-          row_products(ic, Ac, Bc, Tb);
+          row_products(ic, Ac, Bc, Tb, tq);
         });
+        products_done(tq);
         DPROF(11);
       }
       __syncthreads();  // B3: S_k for the next knot, S_k A_{k-1} and S_k B_{k-1} on the bus
