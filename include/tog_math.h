@@ -78,6 +78,21 @@ TOG_HD double tog_cos(double x) {
   }
 }
 
+/* x / 6, correctly rounded, without the division sequence (the RK3 and RK4 steps end with one per state
+ * entry, src/integration.jl:122,157): Markstein's correction -- q0 = RN(x r) with r = RN(1/6) is faithful,
+ * the remainder x - 6 q0 is exact under fma, and RN(q0 + (x - 6 q0) r) is RN(x / 6). Equal to x / 6.0 bit
+ * for bit on every x with 2^-1000 <= |x| <= DBL_MAX (tests/test_math_contract.py checks 4e8 values); zeros,
+ * the subnormal range, infinities and NaN take the division. */
+TOG_HD double tog_div6(double x) {
+  const double r = 0.16666666666666666;
+  const double q0 = x * r;
+  const double e = fma(-q0, 6.0, x);
+  const double q = fma(e, r, q0);
+  const double ax = fabs(x);
+  if (__builtin_expect(!(ax >= 0x1p-1000 && ax <= 1.7976931348623157e308), 0)) return x / 6.0;
+  return q;
+}
+
 /* (tog_sin(x), tog_cos(x)) from one reduction and one evaluation of each kernel polynomial, branch-free:
  * bit-identical to the two calls (the same operations; the quadrant only selects and negates, which is
  * exact). The reduction runs on 0 for non-finite x (a NaN or infinite fn must not reach the integer

@@ -90,6 +90,12 @@ static inline dual ddivc(dual a, double s) { /* Dual / Real */
   for (int i = 0; i < g_nd; i++) r.p[i] = a.p[i] / s;
   return r;
 }
+static inline dual ddiv6(dual a) { /* Dual / 6 (tog_div6: the correctly rounded quotient) */
+  dual r;
+  r.v = tog_div6(a.v);
+  for (int i = 0; i < g_nd; i++) r.p[i] = tog_div6(a.p[i]);
+  return r;
+}
 /* ForwardDiff: x/y -> Dual(xv/yv, x.p*inv(yv) + y.p*(-(xv/(yv*yv)))) */
 static inline dual ddiv(dual a, dual b) {
   dual r;
@@ -741,7 +747,7 @@ static void discrete_f_dual(int model, int integ, int n, dual* xn, const dual* x
     /* x + (k1 + 2*k2 + 2*k3 + k4)/6 */
     for (int i = 0; i < n; i++) {
       dual s = dadd(dadd(dadd(k1[i], dscale(k2[i], 2.0)), dscale(k3[i], 2.0)), k4[i]);
-      xn[i] = dadd(x[i], ddivc(s, 6.0));
+      xn[i] = dadd(x[i], ddiv6(s));
     }
   } else {
     /* k3 = f(x - k1 + 2*k2) */
@@ -751,7 +757,7 @@ static void discrete_f_dual(int model, int integ, int n, dual* xn, const dual* x
     /* x + (k1 + 4*k2 + k3)/6 */
     for (int i = 0; i < n; i++) {
       dual s = dadd(dadd(k1[i], dscale(k2[i], 4.0)), k3[i]);
-      xn[i] = dadd(x[i], ddivc(s, 6.0));
+      xn[i] = dadd(x[i], ddiv6(s));
     }
   }
 }
@@ -882,7 +888,7 @@ static void kuka_rk3_jacobian_chain(double* S, const double* x, const double* u,
           Ssum[i][p] = K1[i][p] + 4.0 * kk;
         } else {
           Ssum[i][p] = Ssum[i][p] + kk;
-          S[i + n * p] = ((i == p) ? 1.0 : 0.0) + Ssum[i][p] / 6.0;
+          S[i + n * p] = ((i == p) ? 1.0 : 0.0) + tog_div6(Ssum[i][p]);
         }
       }
   }

@@ -591,7 +591,7 @@ k_jacobian_rk3_stage(const DevProblem* __restrict__ P, DevBuffers Bf, long long 
 #pragma unroll
       for (int i = 0; i < n; i++) {
         kk[i] = kk[i] * dt;
-        const Dual<W> xn = xd[i] + (sv[i] + kk[i]) / 6.0;
+        const Dual<W> xn = xd[i] + div6_(sv[i] + kk[i]);
 #pragma unroll
         for (int w = 0; w < W; w++)
           if (c * W + w < Lb) out[i + n * (c * W + w)] = xn.g[w];

@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(64) k_kuka_chain(const DevProblem* __restrict_
     if (e < KJ_E) {
       const double f3 = (i < 7) ? T[p * 16 + 7 + i] : stash[(i - 7) + 7 * p];
       const double s = Ss[r] + f3 * dt;
-      out[e] = ((i == p) ? 1.0 : 0.0) + s / 6.0;
+      out[e] = ((i == p) ? 1.0 : 0.0) + tog_div6(s);
     }
   }
   if constexpr (L > KJ_L) {  // add_slack_controls: ∂x⁺/∂s = I (src/model.jl:771-774)
