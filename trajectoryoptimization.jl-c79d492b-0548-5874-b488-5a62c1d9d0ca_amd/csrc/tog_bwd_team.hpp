@@ -197,6 +197,24 @@ __device__ __forceinline__ double row_bcast(double v) {
   return __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(v), v, 0x150 + L, 0xF, 0xF, true);
 }
 
+// Broadcast lane L of each 4-lane group to the group (quad_perm [L,L,L,L], two 32-bit DPP moves)
+template <int L>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(0), (int)(x & 0xffffffffll), L * 0x55,
+                                             0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(0), (int)(x >> 32), L * 0x55, 0xF, 0xF,
+                                             true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+// lane L of the team to the team: a 16-lane team is a DPP row, a 4-lane team a quad
+template <int TW, int L>
+__device__ __forceinline__ double team_bcast(double v) {
+  static_assert(TW == 16 || TW == 4, "DPP team broadcasts: 16- or 4-lane teams");
+  if constexpr (TW == 16) return row_bcast<L>(v);
+  else return quad_bcast<L>(v);
+}
+
 // Lane i of each DPP row receives lane i-1's value, lane 0 of the row `old` (row_shr:1 with bound_ctrl
 // off: the lane without a source keeps the old operand)
 __device__ __forceinline__ double row_shr1_or(double v, double old) {
@@ -231,9 +249,9 @@ struct QrNoPost {
 // then (no later reflector touches it), so a consumer may take R's rows as they are released.
 template <int ROWS, int COLS, int TOP = 0, int TEAMW = 16, bool FULL = false, class POST = QrNoPost>
 __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, double* bus, const POST& post = POST{}) {
-#define TQ_LIVE(i, j) ((FULL || TEAMW == 16 || (i) < rows) && !((i) > (j) && (i) < TOP))
-  if constexpr (TEAMW == 16) {
-    // Reflectors broadcast by DPP row_newbcast (the team is one DPP row). The lane-predicated parts
+#define TQ_LIVE(i, j) ((FULL || TEAMW == 16 || TEAMW == 4 || (i) < rows) && !((i) > (j) && (i) < TOP))
+  if constexpr (TEAMW == 16 || TEAMW == 4) {
+    // Reflectors broadcast by DPP row_newbcast (the team is one DPP row; a 4-lane team: quad_perm). The lane-predicated parts
     // are written branch-free: every lane runs the reflector arithmetic on its own column (SIMT
     // issues it once either way) and lane j's results are selected once per step, and the update
     // uses w = 0 on lanes <= j, which leaves their live entries unchanged (x - 0, fma(v, 0, x)) and
@@ -258,11 +276,11 @@ __device__ __forceinline__ void team_qr(double (&a)[ROWS], int rows, int tl, dou
       const double vd = alpha - beta;
       const double rd = (ss != 0.0) ? 1.0 / (beta * vd) : 0.0;  // 0: tau = 0, H = I
       if (tq == j && ss != 0.0) a[j] = beta;
-      const double rdj = row_bcast<j>(rd), vdj = row_bcast<j>(vd);
+      const double rdj = team_bcast<TEAMW, j>(rd), vdj = team_bcast<TEAMW, j>(vd);
       double v[ROWS];
 #pragma unroll
       for (int i = j + 1; i < ROWS; i++)
-        if (TQ_LIVE(i, j)) v[i] = row_bcast<j>(a[i]);
+        if (TQ_LIVE(i, j)) v[i] = team_bcast<TEAMW, j>(a[i]);
       if (tq > j && tq < COLS && rdj != 0.0) {
         double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -618,23 +636,171 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   }
 }
 
+// mode 0: every knot; 1: only the dense ones (the others are on k_expand_u); 2: only the terminal knot
+// (one team per trajectory: no stage knot is dense)
 template <class M, int SQRTI, int ALI>
-__global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuffers Bf) {
+__global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuffers Bf, int mode) {
   using Cfg = TeamCfg<M>;
   extern __shared__ double expand_lds[];
   const int team = threadIdx.x / Cfg::TEAM, tl = threadIdx.x % Cfg::TEAM;
   const int N = P->N;
   const long long idx = (long long)blockIdx.x * Cfg::TPW + team;
-  const long long slot = idx / N;
-  const int k = (int)(idx - slot * N);
+  const long long slot = (mode == 2) ? idx : idx / N;
+  const int k = (mode == 2) ? N - 1 : (int)(idx - slot * N);
   const long long b = traj_of_slot(Bf, slot, P->B);
   if (b < 0) return;  // whole teams return together (DPP broadcasts stay within a team)
   if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  if (mode == 1 && k < N - 1 && !(ALI && P->knot_nx[k] > 0)) return;
   double* tlds = expand_lds + (size_t)team * expand_team_stride<M>(P->pmax);
   if (k == N - 1)
     team_expand<M, SQRTI != 0, ALI != 0, true>(P, Bf, b, k, tlds, tl, team);
   else
     team_expand<M, SQRTI != 0, ALI != 0, false>(P, Bf, b, k, tlds, tl, team);
+}
+
+// k_expand_u: the square-root expansion of the knots whose Q.xx is the problem constant (stage knots
+// without a state-gradient row: the record carries Q.x, Q.u and the Q.uu factor only) on 4-lane teams,
+// 16 knots per wave. team_expand gives such a knot a 16-lane team of which only the m <= 4 Q.uu
+// columns work; here lane c owns Q.uu's column c and Q.x's entries c, c + 4, ..., and every value is
+// formed by team_expand's operations in its order (the Q.uu factor by the same column-distributed QR,
+// its broadcasts within the quad). The dense knots (the terminal one, knots with state rows) stay on
+// k_expand_team.
+template <class M, bool AL>
+__device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffers& Bf, long long b, int k,
+                                            double* tlds, int tl, int team) {
+  using Cfg = TeamCfg<M>;
+  constexpr int n = M::n, m = M::m, PU = Cfg::PU, NE = ne_of<M>(), TQ = 4;
+  static_assert(m <= TQ, "quad_expand: at most 4 controls");
+  const int N = P->N, pmax = P->pmax;
+  const double dt = P->dt;
+  const bool colu = tl < m;
+  const int cu = colu ? tl : 0;
+  const double* xg = Bf.X + ((size_t)b * N + k) * n;
+  const double* ug = Bf.U + ((size_t)b * (N - 1) + k) * m;
+  constexpr int NXL = (n + TQ - 1) / TQ;  // Q.x entries of this lane: tl + TQ j
+  double Qxs[NXL], Quuc[m], Qu[m];
+  const int diag_mode = P->diag_cost;
+  if (diag_mode == 2) {
+#pragma unroll
+    for (int j = 0; j < NXL; j++) {
+      const int cc = tl + TQ * j < n ? tl + TQ * j : 0;
+      Qxs[j] = ((fma(P->Q[cc + n * cc], xg[cc], 0.0) + P->q[cc]) + 0.0) * dt;
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) Qu[i] = ((fma(P->R[i + m * i], ug[i], 0.0) + P->r[i]) + 0.0) * dt;
+    const double rd = P->cR[cu + m * cu];
+#pragma unroll
+    for (int i = 0; i < m; i++) Quuc[i] = (i == cu) ? rd : 0.0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < NXL; j++) {
+      const int cc = tl + TQ * j < n ? tl + TQ * j : 0;
+      double a = 0.0, bq = 0.0;
+      if (diag_mode) {
+        a = fma(P->Q[cc + n * cc], xg[cc], 0.0);
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < n; jj++) a = fma(P->Q[cc + n * jj], xg[jj], a);
+#pragma unroll
+        for (int jj = 0; jj < m; jj++) bq = fma(P->H[jj + m * cc], ug[jj], bq);
+      }
+      Qxs[j] = ((a + P->q[cc]) + bq) * dt;
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) {
+      double a2 = 0.0, b2 = 0.0;
+      if (diag_mode) {
+        a2 = fma(P->R[i + m * i], ug[i], 0.0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
+#pragma unroll
+        for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
+      }
+      Qu[i] = ((a2 + P->r[i]) + b2) * dt;
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) Quuc[i] = P->cR[i + m * cu];
+  }
+  const int p = AL ? P->knot_cnt[k] : 0;
+  if (AL && p > 0) {
+    RowInfo* rows = reinterpret_cast<RowInfo*>(tlds + 48);
+    int* xr = reinterpret_cast<int*>(rows + pmax);
+    int* ur = xr + pmax;
+    double* xs = reinterpret_cast<double*>(ur + pmax);
+    double* us = xs + n;
+#pragma unroll
+    for (int j = 0; j < NXL; j++)
+      if (tl + TQ * j < n) xs[tl + TQ * j] = xg[tl + TQ * j];
+    if (colu) us[tl] = ug[tl];
+    team_sync();
+    int nx, nu;
+    team_rows<M>(Bf, b, k, N, pmax, p, P->rows + P->knot_off[k], xs, us, rows, xr, ur, nx, nu, team, tl, TQ);
+    team_sync();
+    // chol_plus!(Q.uu, Iμ_sqrt cu) (no state rows here: nx == 0)
+    if (nu > 0) {
+      double a[m + PU];
+#pragma unroll
+      for (int i = 0; i < m + PU; i++) {
+        if (i < m) {
+          a[i] = Quuc[i];
+        } else if (i - m < nu) {
+          const RowInfo& ri = rows[ur[i - m]];
+          a[i] = ri.ws * ((ri.idx[0] == n + cu) ? ri.v[0] : 0.0);
+        } else {
+          a[i] = 0.0;
+        }
+      }
+      team_qr<m + PU, m, m, TQ, true>(a, m + PU, tl, tlds);
+#pragma unroll
+      for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
+    }
+    // Q.u .+= cu'g (Q.x .+= cx'g has no rows here)
+    double tu[m];
+#pragma unroll
+    for (int i = 0; i < m; i++) tu[i] = 0.0;
+    for (int z = 0; z < nu; z++) {
+      const RowInfo& ri = rows[ur[z]];
+      const int id = ri.idx[0];
+#pragma unroll
+      for (int i = 0; i < m; i++)
+        if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < m; i++) Qu[i] += tu[i];
+    {  // Q.x .+= 0 (team_expand adds the empty sum: tx = 0.0)
+#pragma unroll
+      for (int j = 0; j < NXL; j++) Qxs[j] += 0.0;
+    }
+  }
+  double* e = Bf.E + ((size_t)b * N + k) * NE;
+#pragma unroll
+  for (int j = 0; j < NXL; j++)
+    if (tl + TQ * j < n) e[tl + TQ * j] = Qxs[j];
+  if (colu) {
+    double qu = Qu[0];
+#pragma unroll
+    for (int i = 1; i < m; i++)
+      if (tl == i) qu = Qu[i];
+    e[n + tl] = qu;
+#pragma unroll
+    for (int i = 0; i < m; i++) e[n + m + i + m * tl] = Quuc[i];
+  }
+}
+
+template <class M, int ALI>
+__global__ void __launch_bounds__(64) k_expand_u(const DevProblem* P, DevBuffers Bf) {
+  extern __shared__ double expand_lds[];
+  const int team = threadIdx.x / 4, tl = threadIdx.x % 4;
+  const int N = P->N;
+  const long long idx = (long long)blockIdx.x * 16 + team;
+  const long long slot = idx / (N - 1);
+  const int k = (int)(idx - slot * (N - 1));
+  const long long b = traj_of_slot(Bf, slot, P->B);
+  if (b < 0) return;  // whole teams return together (DPP broadcasts stay within a quad)
+  if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
+  if (ALI && P->knot_nx[k] > 0) return;  // a dense knot: k_expand_team
+  quad_expand<M, ALI != 0>(P, Bf, b, k, expand_lds + (size_t)team * expand_team_stride<M>(P->pmax), tl, team);
 }
 
 #ifndef TOG_BWD_WAVES

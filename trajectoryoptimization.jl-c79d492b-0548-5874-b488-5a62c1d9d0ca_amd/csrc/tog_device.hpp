@@ -173,7 +173,7 @@ struct DevBuffers {
   double* jws;        // Kuka RK3 Jacobian workspace (stage-chain form: KJ_WSK doubles per knot slot; the
                       // dual-staged A/B form: 2n duals per lane), or null
   int jac_chain;      // Kuka RK3 Jacobian in stage-chain form (tog_kuka_jac.hpp; 0: TOG_KUKA_JAC=dual A/B)
-  int pad_jc;
+  int dense_stage_knots;  // some stage knot has a state-gradient row (k_expand_u / k_expand_team split)
   // compacted tail launches (tog_solve_step, k_list_active): the step's active trajectories and their
   // count; null outside a tail step (launch slot = trajectory index)
   int* act_list;

@@ -3293,15 +3293,29 @@ struct ModelLaunch {
                      hipStream_t st) {
     if constexpr (M::m <= M::n && M::n + 1 <= 16 && !ModelTraits<M>::min_time) {
       constexpr int TPW = TeamCfg<M>::TPW;
-      const long long teams = B * (long long)N;
-      const dim3 g((unsigned)((teams + TPW - 1) / TPW)), blk(64);
       const unsigned sm = (unsigned)(sizeof(double) * TPW * expand_team_stride<M>(pmax));
+      // square root, at most 4 controls, 16-lane teams: the knots with a constant Q.xx on 4-lane teams
+      // (k_expand_u), the dense ones on k_expand_team (only the terminal knot when no stage knot has a
+      // state row); TOG_EXPAND_QUAD=0 keeps every knot on k_expand_team, for A/B checks
+      int mode = 0;
+      if constexpr (M::m <= 4 && TeamCfg<M>::TEAM == 16) {
+        const char* eq = getenv("TOG_EXPAND_QUAD");
+        if (sq && !(eq && eq[0] == '0')) {
+          const long long qteams = B * (long long)(N - 1);
+          const unsigned smq = (unsigned)(sizeof(double) * 16 * expand_team_stride<M>(pmax));
+          if (al) hipLaunchKernelGGL((k_expand_u<M, 1>), dim3((unsigned)((qteams + 15) / 16)), dim3(64), smq, st, P, Bf);
+          else hipLaunchKernelGGL((k_expand_u<M, 0>), dim3((unsigned)((qteams + 15) / 16)), dim3(64), smq, st, P, Bf);
+          mode = (al && Bf.dense_stage_knots) ? 1 : 2;
+        }
+      }
+      const long long teams = (mode == 2) ? B : B * (long long)N;
+      const dim3 g((unsigned)((teams + TPW - 1) / TPW)), blk(64);
       if (sq) {
-        if (al) hipLaunchKernelGGL((k_expand_team<M, 1, 1>), g, blk, sm, st, P, Bf);
-        else hipLaunchKernelGGL((k_expand_team<M, 1, 0>), g, blk, sm, st, P, Bf);
+        if (al) hipLaunchKernelGGL((k_expand_team<M, 1, 1>), g, blk, sm, st, P, Bf, mode);
+        else hipLaunchKernelGGL((k_expand_team<M, 1, 0>), g, blk, sm, st, P, Bf, mode);
       } else {
-        if (al) hipLaunchKernelGGL((k_expand_team<M, 0, 1>), g, blk, sm, st, P, Bf);
-        else hipLaunchKernelGGL((k_expand_team<M, 0, 0>), g, blk, sm, st, P, Bf);
+        if (al) hipLaunchKernelGGL((k_expand_team<M, 0, 1>), g, blk, sm, st, P, Bf, mode);
+        else hipLaunchKernelGGL((k_expand_team<M, 0, 0>), g, blk, sm, st, P, Bf, mode);
       }
     }
   }
