@@ -108,6 +108,13 @@ __host__ __device__ inline int expand_team_stride(int pmax) {
   int s = 48 + pmax * 8 + pmax + M::n + M::m;
   return s + (s & 1);
 }
+// k_expand_u's per-team LDS (doubles): no bus (its 4-lane QR broadcasts by DPP), the row table sized
+// for its knots (pu = DevBuffers::expand_u_pmax) -- the LDS per block bounds its occupancy
+template <class M>
+__host__ __device__ inline int expand_u_stride(int pu) {
+  int s = pu * 8 + pu + M::n + M::m;
+  return s + (s & 1);
+}
 
 // Host-side admissibility of the team kernel for a problem (otherwise the LDS kernel runs).
 constexpr int TEAM_MAX_ROWS = 128;   // deduplicated row table cached in LDS
@@ -671,7 +678,7 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
   using Cfg = TeamCfg<M>;
   constexpr int n = M::n, m = M::m, PU = Cfg::PU, NE = ne_of<M>(), TQ = 4;
   static_assert(m <= TQ, "quad_expand: at most 4 controls");
-  const int N = P->N, pmax = P->pmax;
+  const int N = P->N, pmax = P->pmax, pu = Bf.expand_u_pmax;  // (pmax: the λ/μ layout; pu: the LDS table)
   const double dt = P->dt;
   const bool colu = tl < m;
   const int cu = colu ? tl : 0;
@@ -724,10 +731,10 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
   }
   const int p = AL ? P->knot_cnt[k] : 0;
   if (AL && p > 0) {
-    RowInfo* rows = reinterpret_cast<RowInfo*>(tlds + 48);
-    int* xr = reinterpret_cast<int*>(rows + pmax);
-    int* ur = xr + pmax;
-    double* xs = reinterpret_cast<double*>(ur + pmax);
+    RowInfo* rows = reinterpret_cast<RowInfo*>(tlds);
+    int* xr = reinterpret_cast<int*>(rows + pu);
+    int* ur = xr + pu;
+    double* xs = reinterpret_cast<double*>(ur + pu);
     double* us = xs + n;
 #pragma unroll
     for (int j = 0; j < NXL; j++)
@@ -800,7 +807,7 @@ __global__ void __launch_bounds__(64) k_expand_u(const DevProblem* P, DevBuffers
   if (b < 0) return;  // whole teams return together (DPP broadcasts stay within a quad)
   if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
   if (ALI && P->knot_nx[k] > 0) return;  // a dense knot: k_expand_team
-  quad_expand<M, ALI != 0>(P, Bf, b, k, expand_lds + (size_t)team * expand_team_stride<M>(P->pmax), tl, team);
+  quad_expand<M, ALI != 0>(P, Bf, b, k, expand_lds + (size_t)team * expand_u_stride<M>(Bf.expand_u_pmax), tl, team);
 }
 
 #ifndef TOG_BWD_WAVES
