@@ -108,13 +108,6 @@ __host__ __device__ inline int expand_team_stride(int pmax) {
   int s = 48 + pmax * 8 + pmax + M::n + M::m;
   return s + (s & 1);
 }
-// k_expand_u's per-team LDS (doubles): no bus (its 4-lane QR broadcasts by DPP), the row table sized
-// for its knots (pu = DevBuffers::expand_u_pmax) -- the LDS per block bounds its occupancy
-template <class M>
-__host__ __device__ inline int expand_u_stride(int pu) {
-  int s = pu * 8 + pu + M::n + M::m;
-  return s + (s & 1);
-}
 
 // Host-side admissibility of the team kernel for a problem (otherwise the LDS kernel runs).
 constexpr int TEAM_MAX_ROWS = 128;   // deduplicated row table cached in LDS
@@ -673,12 +666,11 @@ __global__ void __launch_bounds__(64) k_expand_team(const DevProblem* P, DevBuff
 // its broadcasts within the quad). The dense knots (the terminal one, knots with state rows) stay on
 // k_expand_team.
 template <class M, bool AL>
-__device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffers& Bf, long long b, int k,
-                                            double* tlds, int tl, int team) {
+__device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffers& Bf, long long b, int k, int tl) {
   using Cfg = TeamCfg<M>;
   constexpr int n = M::n, m = M::m, PU = Cfg::PU, NE = ne_of<M>(), TQ = 4;
   static_assert(m <= TQ, "quad_expand: at most 4 controls");
-  const int N = P->N, pmax = P->pmax, pu = Bf.expand_u_pmax;  // (pmax: the λ/μ layout; pu: the LDS table)
+  const int N = P->N, pmax = P->pmax;
   const double dt = P->dt;
   const bool colu = tl < m;
   const int cu = colu ? tl : 0;
@@ -731,34 +723,57 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
   }
   const int p = AL ? P->knot_cnt[k] : 0;
   if (AL && p > 0) {
-    RowInfo* rows = reinterpret_cast<RowInfo*>(tlds);
-    int* xr = reinterpret_cast<int*>(rows + pu);
-    int* ur = xr + pu;
-    double* xs = reinterpret_cast<double*>(ur + pu);
-    double* us = xs + n;
+    // The knot's rows, all control bounds (no state rows here, so team_rows' control-row list is the
+    // row order itself and nu = p <= PU): row r on lane r % 4, evaluated as team_rows evaluates it, in
+    // registers; lane c then takes row i's (√w, gradient entry, its index, g) from lane i % 4 by a quad
+    // DPP broadcast. No LDS: the launch's occupancy is its register count's.
+    constexpr int QR = (PU + TQ - 1) / TQ;
+    const ConRow* cr = P->rows + P->knot_off[k];
+    const double* lam = Bf.lam + ((size_t)b * N + k) * pmax;
+    const double* mu = Bf.mu + ((size_t)b * N + k) * pmax;
+    double rws[QR], rv[QR], rg[QR];
+    int rid[QR];
 #pragma unroll
-    for (int j = 0; j < NXL; j++)
-      if (tl + TQ * j < n) xs[tl + TQ * j] = xg[tl + TQ * j];
-    if (colu) us[tl] = ug[tl];
-    team_sync();
-    int nx, nu;
-    team_rows<M>(Bf, b, k, N, pmax, p, P->rows + P->knot_off[k], xs, us, rows, xr, ur, nx, nu, team, tl, TQ);
-    team_sync();
-    // chol_plus!(Q.uu, Iμ_sqrt cu) (no state rows here: nx == 0)
-    if (nu > 0) {
+    for (int q = 0; q < QR; q++) {
+      const int r = tl + TQ * q;
+      rws[q] = 0.0;
+      rv[q] = 0.0;
+      rg[q] = 0.0;
+      rid[q] = -1;
+      if (r < p) {
+        const ConRow row = cr[r];
+        const double c = row_value<false>(row, xg, ug);
+        const double l = lam[r];
+        const bool act = row_inequality<false>(row) ? ((c >= 0.0) || (l > 0.0)) : true;
+        const double w = act ? mu[r] : 0.0;
+        rws[q] = act ? sqrt(mu[r]) : 0.0;
+        rg[q] = w * c + l;
+        int gi[3];
+        double gv[3];
+        row_grad<false>(row, xg, n, gi, gv);
+        rid[q] = gi[0];
+        rv[q] = gv[0];
+      }
+    }
+    const int nu = p;
+    // row i's values on every lane of the quad (broadcast where used, so that no table stays live)
+    auto idx_of = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      return __builtin_amdgcn_update_dpp(__builtin_nondeterministic_value(0), rid[i / TQ], (i % TQ) * 0x55, 0xF, 0xF,
+                                         true);
+    };
+    // chol_plus!(Q.uu, Iμ_sqrt cu)
+    {
       double a[m + PU];
 #pragma unroll
-      for (int i = 0; i < m + PU; i++) {
-        if (i < m) {
-          a[i] = Quuc[i];
-        } else if (i - m < nu) {
-          const RowInfo& ri = rows[ur[i - m]];
-          a[i] = ri.ws * ((ri.idx[0] == n + cu) ? ri.v[0] : 0.0);
-        } else {
-          a[i] = 0.0;
-        }
-      }
-      team_qr<m + PU, m, m, TQ, true>(a, m + PU, tl, tlds);
+      for (int i = 0; i < m; i++) a[i] = Quuc[i];
+      static_for<0, PU>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const double ws = quad_bcast<i % TQ>(rws[i / TQ]), v = quad_bcast<i % TQ>(rv[i / TQ]);
+        const int id = idx_of(ic);
+        a[m + i] = (i < nu) ? ws * ((id == n + cu) ? v : 0.0) : 0.0;
+      });
+      team_qr<m + PU, m, m, TQ, true>(a, m + PU, tl, nullptr);
 #pragma unroll
       for (int i = 0; i < m; i++) Quuc[i] = (i <= tl) ? a[i] : 0.0;
     }
@@ -766,13 +781,16 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
     double tu[m];
 #pragma unroll
     for (int i = 0; i < m; i++) tu[i] = 0.0;
-    for (int z = 0; z < nu; z++) {
-      const RowInfo& ri = rows[ur[z]];
-      const int id = ri.idx[0];
+    static_for<0, PU>([&](auto zc) {
+      constexpr int z = decltype(zc)::value;
+      const double v = quad_bcast<z % TQ>(rv[z / TQ]), g = quad_bcast<z % TQ>(rg[z / TQ]);
+      const int id = idx_of(zc);
+      if (z < nu) {
 #pragma unroll
-      for (int i = 0; i < m; i++)
-        if (id == n + i) tu[i] = fma(ri.v[0], ri.g, tu[i]);
-    }
+        for (int i = 0; i < m; i++)
+          if (id == n + i) tu[i] = fma(v, g, tu[i]);
+      }
+    });
 #pragma unroll
     for (int i = 0; i < m; i++) Qu[i] += tu[i];
     {  // Q.x .+= 0 (team_expand adds the empty sum: tx = 0.0)
@@ -796,8 +814,7 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
 }
 
 template <class M, int ALI>
-__global__ void __launch_bounds__(64) k_expand_u(const DevProblem* P, DevBuffers Bf) {
-  extern __shared__ double expand_lds[];
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) k_expand_u(const DevProblem* P, DevBuffers Bf) {
   const int team = threadIdx.x / 4, tl = threadIdx.x % 4;
   const int N = P->N;
   const long long idx = (long long)blockIdx.x * 16 + team;
@@ -807,7 +824,7 @@ __global__ void __launch_bounds__(64) k_expand_u(const DevProblem* P, DevBuffers
   if (b < 0) return;  // whole teams return together (DPP broadcasts stay within a quad)
   if (!Bf.st[b].active || Bf.st[b].ls_pend) return;
   if (ALI && P->knot_nx[k] > 0) return;  // a dense knot: k_expand_team
-  quad_expand<M, ALI != 0>(P, Bf, b, k, expand_lds + (size_t)team * expand_u_stride<M>(Bf.expand_u_pmax), tl, team);
+  quad_expand<M, ALI != 0>(P, Bf, b, k, tl);
 }
 
 #ifndef TOG_BWD_WAVES

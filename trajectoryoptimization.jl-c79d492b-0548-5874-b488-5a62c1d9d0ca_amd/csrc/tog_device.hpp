@@ -174,7 +174,6 @@ struct DevBuffers {
                       // dual-staged A/B form: 2n duals per lane), or null
   int jac_chain;      // Kuka RK3 Jacobian in stage-chain form (tog_kuka_jac.hpp; 0: TOG_KUKA_JAC=dual A/B)
   int dense_stage_knots;  // some stage knot has a state-gradient row (k_expand_u / k_expand_team split)
-  int expand_u_pmax;      // most rows at a stage knot without state rows (k_expand_u's LDS row table)
   // compacted tail launches (tog_solve_step, k_list_active): the step's active trajectories and their
   // count; null outside a tail step (launch slot = trajectory index)
   int* act_list;

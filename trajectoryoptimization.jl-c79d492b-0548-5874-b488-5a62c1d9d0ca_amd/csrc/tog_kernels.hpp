@@ -3302,9 +3302,8 @@ struct ModelLaunch {
         const char* eq = getenv("TOG_EXPAND_QUAD");
         if (sq && !(eq && eq[0] == '0')) {
           const long long qteams = B * (long long)(N - 1);
-          const unsigned smq = al ? (unsigned)(sizeof(double) * 16 * expand_u_stride<M>(Bf.expand_u_pmax)) : 0u;
-          if (al) hipLaunchKernelGGL((k_expand_u<M, 1>), dim3((unsigned)((qteams + 15) / 16)), dim3(64), smq, st, P, Bf);
-          else hipLaunchKernelGGL((k_expand_u<M, 0>), dim3((unsigned)((qteams + 15) / 16)), dim3(64), smq, st, P, Bf);
+          if (al) hipLaunchKernelGGL((k_expand_u<M, 1>), dim3((unsigned)((qteams + 15) / 16)), dim3(64), 0, st, P, Bf);
+          else hipLaunchKernelGGL((k_expand_u<M, 0>), dim3((unsigned)((qteams + 15) / 16)), dim3(64), 0, st, P, Bf);
           mode = (al && Bf.dense_stage_knots) ? 1 : 2;
         }
       }

@@ -735,11 +735,8 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
 
   DevBuffers& b = h->buf;
   b.dense_stage_knots = 0;  // a stage knot with a state row (its square-root expansion changes Q.xx)
-  b.expand_u_pmax = 0;
-  for (int k = 0; k + 1 < N; k++) {
+  for (int k = 0; k + 1 < N; k++)
     if (nxk[k] > 0) b.dense_stage_knots = 1;
-    else b.expand_u_pmax = std::max(b.expand_u_pmax, cnt[k]);
-  }
   if ((rc = dalloc(h, &b.x0, B * n)) || (rc = dalloc(h, &b.X, B * N * n)) || (rc = dalloc(h, &b.U, B * (N - 1) * m)) ||
       (rc = dalloc(h, &b.Xb, B * N * n)) || (rc = dalloc(h, &b.Ub, B * (N - 1) * m)) ||
       (rc = dalloc(h, &b.AB, B * (N - 1) * n * (n + m))) || (rc = dalloc(h, &b.K, B * (N - 1) * m * n)) ||
