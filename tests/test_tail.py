@@ -67,3 +67,16 @@ def test_tail_backward_kernels_agree(tog, gpu, kind):
     assert np.array_equal(a._U, b._U)
     assert np.array_equal(Sa, Sb)
     assert Sa[:, tog.abi.STAT_BP_RESTARTS].max() >= 0
+
+
+@pytest.mark.gpu
+def test_expansion_kernels_agree(tog, gpu):
+    """The stage knots' square-root expansion on 4-lane teams (k_expand_u, the default) performs
+    k_expand_team's operations in its order: a config-3 batch solved with TOG_EXPAND_QUAD=0 (every knot
+    on k_expand_team) equals the default bit for bit (X, U, every per-trajectory statistic)."""
+    B = 64
+    _, _, a, Sa = _solve(tog, B, {"TOG_EXPAND_QUAD": None})
+    _, _, b, Sb = _solve(tog, B, {"TOG_EXPAND_QUAD": "0"})
+    assert np.array_equal(a._X, b._X)
+    assert np.array_equal(a._U, b._U)
+    assert np.array_equal(Sa, Sb)
