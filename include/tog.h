@@ -30,7 +30,9 @@ extern "C" {
 
 /* 3: tog_solve_altro / tog_altro_options, TOG_PROB_TF_MIN, TOG_NKERNELS = 4 (tog_profile_read fills 4
       entries), tog_solve's max_steps <= 0 = the tog_solve_budget default */
-#define TOG_ABI_VERSION 3
+/* 4: iteration histories (tog_history_enable, TOG_FIELD_HIST_*), tog_solve_altro_ex / tog_altro_result,
+      tog_altro_options.max_steps (was reserved), tog_get_pn_history */
+#define TOG_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status */
 enum tog_status_code {
@@ -250,10 +252,20 @@ enum tog_field {
   TOG_FIELD_X0 = 14,    /* (n,B)                                               */
   TOG_FIELD_STATS = 15, /* (TOG_NSTATS,B) see tog_stat                         */
   TOG_FIELD_RHO = 16,   /* (2,B)          [ρ, dρ]                              */
-  TOG_FIELD_Q = 17      /* (nq,N,B)       cost expansion Q[k] from tog_cost_expansion, per knot
+  TOG_FIELD_Q = 17,     /* (nq,N,B)       cost expansion Q[k] from tog_cost_expansion, per knot
                            [Q.x (n); Q.u (m); Q.xx (n,n); Q.uu (m,m); Q.ux (m,n)], nq = n+m+n²+m²+mn;
                            the terminal knot has Q.u = Q.uu = Q.ux = 0. Valid until the next
                            backward pass (the buffer doubles as its restart-replay scratch). */
+  /* iteration histories (tog_history_enable; read-only). Records are written in solve order since
+     tog_solve_init; a record past the capacity is counted but not stored. */
+  TOG_FIELD_HIST_INNER = 18, /* (3,cap,B) the iLQR solver's record_iteration! (ilqr_methods.jl:77-89):
+                                per record [stats[:cost], stats[:dJ], stats[:gradient]]. In an AL solve the
+                                inner solves follow each other (each opens with its (J_prev, Inf) record);
+                                TOG_FIELD_HIST_OUTER's iterations_inner splits them (stats_uncon). */
+  TOG_FIELD_HIST_OUTER = 19, /* (4,al_iterations+1,B) the AL solver's record_iteration!
+                                (augmented_lagrangian_methods.jl:79-97): per outer record
+                                [iterations_inner, cost, c_max, penalty_max]; record 0 is the initial one */
+  TOG_FIELD_HIST_COUNT = 20  /* (2,B) records written: [inner, outer] */
 };
 
 /* per-trajectory statistics row (TOG_FIELD_STATS), all stored as double */
@@ -351,6 +363,11 @@ int32_t tog_get(tog_handle* h, int32_t field, double* out);
 /* same, device pointers (no host staging) — for torch / RCCL interop */
 int32_t tog_get_device_ptr(tog_handle* h, int32_t field, void** dptr);
 int32_t tog_dims(tog_handle* h, int64_t* out6); /* [n, m, N, B, pmax, mode] */
+/* Per-trajectory iteration histories: the reference's solver.stats vectors (ilqr_methods.jl:77-89,
+   augmented_lagrangian_methods.jl:79-97), recorded on the device as the solve runs (one store per
+   iteration) and read with tog_get(TOG_FIELD_HIST_*). capacity = inner records kept per trajectory
+   (an AL solve records at most al_iterations x (iterations + 1)); 0 turns recording off (the default). */
+int32_t tog_history_enable(tog_handle* h, int32_t capacity);
 
 /* ---- step level (exported because tests and callers use them:
         src/TrajectoryOptimization.jl:82-95, test/sqrt_bp_tests.jl:27-37) ---- */
@@ -447,6 +464,10 @@ enum tog_pn_stat {
    of S + 1e-2 I, chord-method line searches with reg_solve refinement to |r| < 1e-8).
    out: (TOG_PN_NSTATS, B) host pointer or NULL. */
 int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out);
+/* solver_pn.stats[:cost] and [:c_max] (record_iteration!, projected_newton.jl:23-29) of the last tog_solve_pn:
+   out (2, n_steps, B), per newton step [cost, c_max] (NaN after a trajectory's last step); steps_out (B) the
+   records each trajectory made (stats[:iterations]) or NULL. */
+int32_t tog_get_pn_history(tog_handle* h, double* out, int32_t* steps_out);
 
 /* ---- ALTRO (src/solvers/altro/altro_methods.jl:2-124) ---- */
 /* ALTROSolverOptions (src/solvers/altro/altro_solver.jl:6-65), its live fields; tog_default_altro_options
@@ -461,7 +482,8 @@ typedef struct tog_altro_options {
   int32_t dynamically_feasible_projection; /* 1 */
   int32_t resolve_feasible_problem;     /* 1 */
   int32_t projected_newton;             /* 0 */
-  int32_t reserved;
+  int32_t max_steps;                    /* batch-step budget of each AL solve (tog_solve's max_steps;
+                                           0 = the tog_solve_budget default)                         */
   tog_pn_options opts_pn;
 } tog_altro_options;
 void tog_default_altro_options(tog_altro_options* opts);
@@ -482,6 +504,32 @@ void tog_default_altro_options(tog_altro_options* opts);
 int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
                         const double* x0, double* X, double* U, double* h, double* stats, double* stats_resolve,
                         double* stats_pn);
+
+/* What solve!(prob, ALTROSolverOptions) returns (altro_methods.jl:40-52, ALTROSolver altro_solver.jl:70-94):
+   solver.stats[:time], [:time_al], [:time_pn]; solver.solver_al.stats (the AL phase: the infeasible or
+   minimum-time problem's solve) as summary rows and iteration histories; solver.solver_pn.stats. Inputs
+   are the capacities and output buffers (each pointer may be NULL); the times and the handle are outputs. */
+typedef struct tog_altro_result {
+  int32_t inner_capacity;  /* in: inner records per trajectory in hist_inner (0: no histories)            */
+  int32_t keep_handle;     /* in: 1 = hand the AL phase's handle (solver_al's buffers: K, d, λ, μ, ...) back
+                              in `handle` instead of destroying it; the caller tog_destroys it            */
+  double* stats;           /* (TOG_NSTATS, B) AL phase                                                   */
+  double* stats_resolve;   /* (TOG_NSTATS, B) the feasible resolve of an infeasible start                */
+  double* stats_pn;        /* (TOG_PN_NSTATS, B) projected Newton                                        */
+  double* hist_inner;      /* (3, inner_capacity, B) AL phase, TOG_FIELD_HIST_INNER                       */
+  double* hist_outer;      /* (4, al_iterations + 1, B) AL phase, TOG_FIELD_HIST_OUTER (AL solves)        */
+  double* hist_count;      /* (2, B) TOG_FIELD_HIST_COUNT                                                 */
+  double* hist_pn;         /* (2, opts_pn.n_steps, B) solver_pn.stats [:cost, :c_max] per newton step     */
+  double time, time_al, time_pn; /* out: seconds (wall clock of the whole call, the AL phase, projected Newton) */
+  tog_handle* handle;      /* out: see keep_handle (NULL otherwise)                                       */
+} tog_altro_result;
+/* tog_solve_altro with the solver's statistics (tog_solve_altro = this with only the three stats rows).
+   A trajectory whose AL phase ends with the reference's exceptions (TOG_TRAJ_COST_INCREASED,
+   TOG_TRAJ_SQRT_PD_FAIL) is not resolved and not projected: its X, U are what the exception would leave
+   (the AL phase's for a feasible start; the caller's inputs for an infeasible or minimum-time start,
+   whose AL phase ran on a copy of the problem). */
+int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
+                           const double* x0, double* X, double* U, double* h, tog_altro_result* res);
 
 /* per-kernel timing with HIP events recorded on the handle's stream around every launch issued by
    tog_solve_step (used by bench.py for the live roofline). */

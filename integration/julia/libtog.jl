@@ -20,7 +20,7 @@ using LinearAlgebra: PosDefException
 const libtog = get(ENV, "TOG_LIB", "libtog.so")
 
 # ------------------------------------------------------------------------ include/tog.h mirrors
-const TOG_ABI_VERSION = Int32(3)    # include/tog.h; checked against tog_version() at first use
+const TOG_ABI_VERSION = Int32(4)    # include/tog.h; checked against tog_version() at first use
 const TOG_OK = Int32(0)
 const TOG_RK3, TOG_RK4, TOG_MIDPOINT, TOG_RK3_IMPLICIT, TOG_MIDPOINT_IMPLICIT = Int32.(0:4)
 const TOG_CON_BOUND, TOG_CON_GOAL, TOG_CON_CIRCLES, TOG_CON_SPHERES, TOG_CON_INFEASIBLE, TOG_CON_USER,
@@ -34,6 +34,9 @@ const TOG_STAT_J, TOG_STAT_ITERATIONS, TOG_STAT_C_MAX, TOG_STAT_AL_ITER, TOG_STA
       TOG_STAT_FLAGS = 0, 3, 7, 8, 9, 12
 const TOG_TRAJ_COST_INCREASED = Int32(1 << 3)
 const TOG_TRAJ_SQRT_PD_FAIL = Int32(1 << 6)     # lowrankdowndate! PosDefException (the trajectory stopped)
+const TOG_TRAJ_PN_ERROR = Int32(1 << 11)        # _projection_linesearch!'s MethodError (projected_newton.jl:273-277)
+const TOG_FIELD_HIST_INNER, TOG_FIELD_HIST_OUTER, TOG_FIELD_HIST_COUNT = Int32(18), Int32(19), Int32(20)
+const TOG_PN_C_MAX, TOG_PN_J, TOG_PN_STEPS = 1, 2, 6
 const TOG_MODEL_USER = Int32(100)
 
 struct TogConstraint
@@ -59,7 +62,7 @@ end
 # include/tog.h compiled by gcc): sizeof and field offsets of the mirrored structs. tog_check_layout()
 # asserts them in Julia at first use.
 const TOG_LAYOUT = (tog_constraint = 16, tog_constraint_set = 16, tog_problem_desc = 152, tog_options = 200,
-                    tog_pn_options = 24, tog_altro_options = 280)
+                    tog_pn_options = 24, tog_altro_options = 280, tog_altro_result = 96)
 const TOG_DESC_OFFSETS = (0, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64, 72, 80, 88, 96, 104, 112, 116, 120,
                           128, 136, 144)
 
@@ -103,13 +106,21 @@ mutable struct TogAltroOptions     # = tog_altro_options
     R_inf::Float64; R_minimum_time::Float64; dt_max::Float64; dt_min::Float64
     projected_newton_tolerance::Float64
     dynamically_feasible_projection::Int32; resolve_feasible_problem::Int32; projected_newton::Int32
-    reserved::Int32
+    max_steps::Int32
     opts_pn::TogPNOptions
     function TogAltroOptions()
         a = new()
         ccall((:tog_default_altro_options, libtog), Cvoid, (Ref{TogAltroOptions},), a)
         return a
     end
+end
+
+mutable struct TogAltroResult      # = tog_altro_result
+    inner_capacity::Int32; keep_handle::Int32
+    stats::Ptr{Float64}; stats_resolve::Ptr{Float64}; stats_pn::Ptr{Float64}
+    hist_inner::Ptr{Float64}; hist_outer::Ptr{Float64}; hist_count::Ptr{Float64}; hist_pn::Ptr{Float64}
+    time::Float64; time_al::Float64; time_pn::Float64
+    handle::Ptr{Cvoid}
 end
 
 const TOG_CHECKED = Ref(false)
@@ -126,6 +137,7 @@ function tog_check_layout()
     sizeof(TogOptionsI) == TOG_LAYOUT.tog_options || error("tog_options layout")
     sizeof(TogPNOptions) == TOG_LAYOUT.tog_pn_options || error("tog_pn_options layout")
     sizeof(TogAltroOptions) == TOG_LAYOUT.tog_altro_options || error("tog_altro_options layout")
+    sizeof(TogAltroResult) == TOG_LAYOUT.tog_altro_result || error("tog_altro_result layout")
     TOG_CHECKED[] = true
     return nothing
 end
@@ -471,19 +483,49 @@ end
 const TOG_ALTRO = Ref(true)
 
 """
+The solver `solve!(prob, ::ALTROSolverOptions)` returns (altro_solver.jl:70-75, altro_methods.jl:40-52):
+`stats` (:time, :time_al, :time_pn), `solver_al.stats` (the AL phase's :iterations, :iterations_total,
+:iterations_inner, :cost, :c_max, :penalty_max vectors; its inner solves' stats in `solver_al.stats_uncon`)
+and `solver_pn.stats` (:iterations, :cost, :c_max per newton step), so callers such as
+examples/IROS_2019/quadrotor_maze.jl:75-79 read them unchanged.
+"""
+struct TogStatsSolver{T} <: AbstractSolver{T}
+    opts::AbstractSolverOptions{T}
+    stats::Dict{Symbol,Any}
+    stats_uncon::Vector{Dict{Symbol,Any}}
+end
+struct TogALTROSolver{T} <: AbstractSolver{T}
+    opts::ALTROSolverOptions{T}
+    stats::Dict{Symbol,Any}
+    solver_al::TogStatsSolver{T}
+    solver_pn::TogStatsSolver{T}
+end
+
+"record_iteration!'s vectors of one inner solve (ilqr_methods.jl:77-89) from history records r (3 x k)."
+function _tog_ilqr_stats(r::AbstractMatrix{Float64})
+    k = size(r, 2)
+    zc = 0
+    for j = 1:k; zc = r[2, j] == 0.0 ? zc + 1 : 0; end
+    return Dict{Symbol,Any}(:iterations => k, :cost => r[1, :], :dJ => r[2, :], :gradient => r[3, :],
+                            :dJ_zero_counter => zc)
+end
+
+"""
     solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float64})
 
 The reference's ALTRO entry (src/solvers/altro/altro_methods.jl:2-53; README.md:32-67's quick start),
 more specific than its `solve!(::Problem{T,Discrete}, ::ALTROSolverOptions)`, so a Float64 problem on a
-libtog model reaches tog_solve_altro: altro_problem (an initial state trajectory -> infeasible_problem; tf = 0
--> minimum_time_problem), the AL solve on the GPU, projected Newton, process_results! and the feasible
+libtog model reaches tog_solve_altro_ex: altro_problem (an initial state trajectory -> infeasible_problem;
+tf = 0 -> minimum_time_problem), the AL solve on the GPU, projected Newton, process_results! and the feasible
 resolve run in libtog (csrc/tog_altro.cpp). prob.X, prob.U are written in place; a minimum-time solve leaves
-prob.U[k] = [u; u; h] as the reference's process_results! does. Returns solver stats in a Dict.
+prob.U[k] = [u; u; h] as the reference's process_results! does. Returns a TogALTROSolver (the reference's
+ALTROSolver fields: opts, stats, solver_al, solver_pn).
 """
 function solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float64})
     if !TOG_ALTRO[]
         return invoke(solve!, Tuple{Problem{Float64,Discrete},ALTROSolverOptions}, prob, opts)
     end
+    tog_check_layout()
     if opts.projected_newton   # altro_methods.jl:5-13 (mutates opts_al, as the reference does)
         if opts.projected_newton_tolerance >= 0
             opts.opts_al.constraint_tolerance = opts.projected_newton_tolerance
@@ -504,10 +546,20 @@ function solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float6
     h = Vector{Float64}(undef, N - 1)
     St, Sr = zeros(TOG_NSTATS), zeros(TOG_NSTATS)
     Spn = zeros(TOG_PN_NSTATS)
-    togcheck(ccall((:tog_solve_altro, libtog), Int32,
-                   (Ref{TogProblemDesc}, Ref{TogAltroOptions}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
-                   desc.desc, a, Int32(0), x0, X, U, h, St, Sr, Spn))
+    al_it, it = opts.opts_al.iterations, opts.opts_al.opts_uncon.iterations
+    cap = al_it * (it + 1) + 1
+    Hin, Hout, Hcnt = zeros(3, cap), zeros(4, al_it + 1), zeros(2)
+    npn = opts.projected_newton ? max(opts.opts_pn.n_steps, 0) : 0
+    Hpn = fill(NaN, 2, max(npn, 1))
+    GC.@preserve St Sr Spn Hin Hout Hcnt Hpn begin
+        r = TogAltroResult(Int32(cap), Int32(0), pointer(St), pointer(Sr), pointer(Spn), pointer(Hin),
+                           pointer(Hout), pointer(Hcnt), npn > 0 ? pointer(Hpn) : Ptr{Float64}(C_NULL),
+                           0.0, 0.0, 0.0, C_NULL)
+        togcheck(ccall((:tog_solve_altro_ex, libtog), Int32,
+                       (Ref{TogProblemDesc}, Ref{TogAltroOptions}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                        Ptr{Float64}, Ref{TogAltroResult}),
+                       desc.desc, a, Int32(0), x0, X, U, h, r))
+    end
     copyto!(prob.X, [X[:, k] for k = 1:N])
     if tf_min   # process_results! (altro_methods.jl:81-85): U[k] = [u; u; h]
         for k = 1:N-1; prob.U[k] = [U[:, k]; U[:, k]; h[k]]; end
@@ -517,8 +569,27 @@ function solve!(prob::Problem{Float64,Discrete}, opts::ALTROSolverOptions{Float6
     flags = Int32(St[TOG_STAT_FLAGS+1]) | Int32(Sr[TOG_STAT_FLAGS+1])
     flags & TOG_TRAJ_SQRT_PD_FAIL != 0 && throw(PosDefException(0))   # backward_pass.jl:186-192
     flags & TOG_TRAJ_COST_INCREASED != 0 && error("Cost increased during Forward Pass")  # forward_pass.jl:80-82
-    return Dict{Symbol,Any}(:iterations => Int(St[TOG_STAT_TOTAL_STEPS+1]), :cost => St[TOG_STAT_J+1],
-                            :c_max => St[TOG_STAT_C_MAX+1], :iterations_outer => Int(St[TOG_STAT_AL_ITER+1]),
-                            :flags => flags, :iterations_resolve => Int(Sr[TOG_STAT_TOTAL_STEPS+1]),
-                            :projected_newton => Spn)
+    # solver_al.stats (augmented_lagrangian_methods.jl:79-97); an unconstrained problem's AL phase keeps
+    # only its inner records (the AL solver's own records need constraints)
+    n_in, n_out = Int(Hcnt[1]), Int(Hcnt[2])
+    it_in = Int.(Hout[1, 1:n_out])
+    uncon = Dict{Symbol,Any}[]
+    o = 0
+    for k in it_in
+        push!(uncon, _tog_ilqr_stats(Hin[:, o+1:o+k]))
+        o += k
+    end
+    sal = Dict{Symbol,Any}(:iterations => n_out, :iterations_total => sum(it_in), :iterations_inner => it_in,
+                           :cost => Hout[2, 1:n_out], :c_max => Hout[3, 1:n_out], :penalty_max => Hout[4, 1:n_out],
+                           :flags => flags)
+    spn = Dict{Symbol,Any}(:iterations => 0, :cost => Float64[], :c_max => Float64[])
+    if opts.projected_newton
+        k = Int(Spn[TOG_PN_STEPS+1])
+        spn = Dict{Symbol,Any}(:iterations => k, :cost => Hpn[1, 1:k], :c_max => Hpn[2, 1:k])
+        Int32(St[TOG_STAT_FLAGS+1]) & TOG_TRAJ_PN_ERROR != 0 &&   # projected_newton.jl:273-277
+            error("projected Newton: line search did not reduce the violation")
+    end
+    stats = Dict{Symbol,Any}(:time => r.time, :time_al => r.time_al, :time_pn => r.time_pn)
+    return TogALTROSolver{Float64}(opts, stats, TogStatsSolver{Float64}(opts.opts_al, sal, uncon),
+                                   TogStatsSolver{Float64}(opts.opts_pn, spn, Dict{Symbol,Any}[]))
 end

@@ -75,6 +75,7 @@ def _load(path):
     L.oc_max_violation.argtypes = [vp]
     L.oc_max_violation.restype = C.c_double
     L.oc_get_trace.argtypes = [vp, dp]
+    L.oc_get_history.argtypes = [vp, C.c_int, dp]
     L.oc_discrete_f.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
     L.oc_continuous_f.argtypes = [C.c_int, dp, dp, dp]
     L.oc_discrete_jacobian.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_double]
@@ -227,6 +228,19 @@ class OracleSolver:
         if rc != 0:
             raise NotImplementedError("projected Newton solve_type :optimal is not built")
         return out
+
+    def history(self):
+        """The solver.stats vectors of the last solve: inner records (n, 3) [cost, dJ, gradient] (iLQR
+        record_iteration!, ilqr_methods.jl:77-89), outer records (n, 4) [iterations_inner, cost, c_max,
+        penalty_max] (augmented_lagrangian_methods.jl:79-97), projected Newton records (n, 2) [cost, c_max]."""
+        out = []
+        for which, w in ((0, 3), (1, 4), (2, 2)):
+            k = self.L.oc_get_history(self.s, which, C.cast(None, C.POINTER(C.c_double)))
+            a = np.empty((k, w))
+            if k:
+                self.L.oc_get_history(self.s, which, _dp(a))
+            out.append(a)
+        return tuple(out)
 
     def trace(self):
         out = np.empty((4096, 6))

@@ -1319,9 +1319,29 @@ typedef struct oc_solver {
   int trace_len;
   double* trace; /* [J, alpha, rho, restarts, trials, z] per step */
   int al_mode;   /* the current inner solve's objective is the AL one (compute_gradient's prob.obj) */
+  /* the solver.stats vectors: iLQR record_iteration! (ilqr_methods.jl:77-89) [cost, dJ, gradient] per inner
+     record, AL record_iteration! (augmented_lagrangian_methods.jl:79-97) [iterations_inner, cost, c_max,
+     penalty_max] per outer record (tog.h TOG_FIELD_HIST_*) */
+  double* hin;
+  int hin_n, hin_cap;
+  double* hout;
+  int hout_n, hout_cap;
+  double* hpn; /* projected Newton record_iteration! (projected_newton.jl:23-29): [cost, c_max] per step */
+  int hpn_n, hpn_cap;
 } oc_solver;
 
-static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
+static void hist_push(double** buf, int* n, int* cap, int w, const double* rec) {
+  if (*n == *cap) {
+    *cap = *cap ? 2 * *cap : 256;
+    *buf = realloc(*buf, sizeof(double) * w * (size_t)*cap);
+  }
+  memcpy(*buf + (size_t)w * *n, rec, sizeof(double) * w);
+  (*n)++;
+}
+
+/* mb: the controls a bound row may constrain (m less the slack controls of an infeasible-start problem:
+   its BoundConstraint keeps the model's m, update_constraint_set_jacobians constraint_sets.jl:135-150) */
+static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb) {
   memset(oc, 0, sizeof(*oc));
   oc->type = tc->type;
   switch (tc->type) {
@@ -1342,8 +1362,8 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m) {
       for (int i = 0; i < m; i++) {
         oc->u_max[i] = D[2 * n + i];
         oc->u_min[i] = D[2 * n + m + i];
-        oc->au_max[i] = keep || isfinite(D[2 * n + i]);
-        oc->au_min[i] = keep || isfinite(D[2 * n + m + i]);
+        oc->au_max[i] = i < mb && (keep || isfinite(D[2 * n + i]));
+        oc->au_min[i] = i < mb && (keep || isfinite(D[2 * n + m + i]));
         cu += oc->au_max[i];
         cun += oc->au_min[i];
       }
@@ -1555,7 +1575,7 @@ static void desc_load(oc_solver* s, const tog_problem_desc* d) {
     oc_cset* os = &s->sets[i];
     os->ncon = d->sets[i].n_con;
     for (int j = 0; j < os->ncon; j++) {
-      con_init(&os->con[j], &d->sets[i].con[j], n, m);
+      con_init(&os->con[j], &d->sets[i].con[j], n, m, s->mb);
       os->p_stage += os->con[j].p_stage;
       os->p_term += os->con[j].p_term;
     }
@@ -1616,6 +1636,7 @@ OC_EXPORT void oc_destroy(oc_solver* s) {
   free(s->x0); free(s->X); free(s->U); free(s->Xb); free(s->Ub); free(s->K); free(s->d); free(s->F);
   free(s->Sxx); free(s->Sx); free(s->Qx); free(s->Qu); free(s->Qxx); free(s->Quu); free(s->Qux);
   free(s->C); free(s->lam); free(s->mu); free(s->active); free(s->ineq); free(s->trace);
+  free(s->hin); free(s->hout); free(s->hpn);
   free(s);
 }
 
@@ -2406,6 +2427,13 @@ static void record_iteration(oc_solver* s, double J, double dJ) {
     s->zero_count++;
   else
     s->zero_count = 0;
+  const double rec[3] = {J, dJ, s->gradient};
+  hist_push(&s->hin, &s->hin_n, &s->hin_cap, 3, rec);
+}
+
+static void record_outer(oc_solver* s, double J, double mumax) { /* augmented_lagrangian_methods.jl:79-97 */
+  const double rec[4] = {(double)s->iterations, J, s->c_max, mumax};
+  hist_push(&s->hout, &s->hout_n, &s->hout_cap, 4, rec);
 }
 
 static int evaluate_convergence(oc_solver* s, double cost_tol, double grad_tol) {
@@ -2424,6 +2452,9 @@ static int ilqr_iterate(oc_solver* s, int al, double cost_tol, double grad_tol) 
   oc_backward(s, s->opts.square_root, NULL);
   if (s->flags & TOG_TRAJ_BP_ABORTED) return 1; /* restart cap hit: the trajectory stops here */
   double J = oc_forward(s, al, s->J);
+  /* error("Cost increased during Forward Pass") (forward_pass.jl:80-82): the solve ends there, with no
+     bookkeeping of the step */
+  if (s->flags & TOG_TRAJ_COST_INCREASED) return 1;
   s->total_steps++;
   if (s->trace_len < 4096) {
     double* t = s->trace + 6 * s->trace_len++;
@@ -2467,6 +2498,7 @@ OC_EXPORT int oc_solve_ilqr(oc_solver* s) {
   s->flags = 0;
   s->total_steps = 0;
   s->trace_len = 0;
+  s->hin_n = s->hout_n = 0;
   ilqr_solve(s, 0, s->opts.cost_tolerance, s->opts.gradient_norm_tolerance);
   s->flags |= TOG_TRAJ_CONVERGED;
   return s->total_steps;
@@ -2507,8 +2539,14 @@ OC_EXPORT int oc_solve_al(oc_solver* s) {
     s->mu[i] = o->penalty_initial;
   }
   oc_rollout_open_loop(s);
-  (void)al_cost(s, s->X, s->U); /* record_iteration!(prob_al, solver, cost(prob_al)) */
+  s->hin_n = s->hout_n = 0;
+  s->iterations = 0; /* the reset inner solver's stats[:iterations] */
+  const double J0 = al_cost(s, s->X, s->U); /* record_iteration!(prob_al, solver, cost(prob_al)) */
   s->c_max = max_violation(s);
+  double mu0 = 0.0; /* max_penalty(solver) */
+  for (int k = 0; k < N; k++)
+    for (int j = 0; j < s->p[k]; j++) mu0 = fmax(mu0, s->mu[(size_t)k * P + j]);
+  record_outer(s, J0, mu0);
   for (int i = 1; i <= o->al_iterations; i++) {
     s->al_iter = i;
     /* set_tolerances! (:39-50) */
@@ -2516,7 +2554,8 @@ OC_EXPORT int oc_solve_al(oc_solver* s) {
     double gt = (i != o->al_iterations) ? o->al_gradient_norm_tolerance_intermediate : o->al_gradient_norm_tolerance;
     ilqr_solve(s, 1, ct, gt);
     if (s->flags & TOG_TRAJ_BP_ABORTED) break; /* stopped by the restart cap (tog.h) */
-    (void)al_cost(s, s->X, s->U); /* J = cost(prob) */
+    if (s->flags & TOG_TRAJ_COST_INCREASED) break; /* the inner solve raised */
+    const double Jal = al_cost(s, s->X, s->U); /* J = cost(prob) */
     /* dual_update! (:107-118) */
     for (int k = 0; k < N; k++)
       for (int j = 0; j < s->p[k]; j++) {
@@ -2536,6 +2575,7 @@ OC_EXPORT int oc_solve_al(oc_solver* s) {
         if (s->mu[q] > mumax) mumax = s->mu[q];
       }
     s->c_max = max_violation(s);
+    record_outer(s, Jal, mumax);
     int conv = 0;
     if (o->kickout_max_penalty && mumax == o->penalty_max) conv = 1;
     if (s->c_max < o->constraint_tolerance) conv = 1;
@@ -2635,6 +2675,17 @@ OC_EXPORT int oc_get_trace(oc_solver* s, double* out) {
 }
 
 OC_EXPORT double oc_max_violation(oc_solver* s) { return max_violation(s); }
+
+/* the solver.stats vectors of the last solve: which 0 = inner records (3 doubles each), 1 = outer records
+   (4 doubles each), 2 = projected Newton records (2 doubles each); out may be NULL (count only). Returns
+   the record count. */
+OC_EXPORT int oc_get_history(oc_solver* s, int which, double* out) {
+  const int n = which == 2 ? s->hpn_n : (which ? s->hout_n : s->hin_n);
+  const int w = which == 2 ? 2 : (which ? 4 : 3);
+  const double* src = which == 2 ? s->hpn : (which ? s->hout : s->hin);
+  if (out && n) memcpy(out, src, sizeof(double) * w * (size_t)n);
+  return n;
+}
 
 /* =====================================================================
  * Batched CPU baseline: B independent solves over `nthreads` OpenMP threads.

@@ -367,6 +367,7 @@ OC_EXPORT int oc_solve_pn(oc_solver* s, const tog_pn_options* o, double* out) {
   for (int i = 0; i < m; i++) ws->wu[i] = 1.0 / (s->R[IDX(i, i, m)] * s->dt);
   double viol = 0.0, c_max = 0.0, J = 0.0;
   int steps = 0;
+  s->hpn_n = 0;
   for (int it = 0; it < o->n_steps; it++) {
     /* newton_step!: update! (active set at V), then projection_solve! */
     pn_eval(s, ws, s->X, s->U);
@@ -379,6 +380,8 @@ OC_EXPORT int oc_solve_pn(oc_solver* s, const tog_pn_options* o, double* out) {
     update_constraints(s, s->X, s->U);
     c_max = max_violation(s);
     J = obj_cost(s, s->X, s->U);
+    const double rec[2] = {J, c_max};
+    hist_push(&s->hpn, &s->hpn_n, &s->hpn_cap, 2, rec);
     if (ws->error || c_max <= o->feasibility_tolerance) break;
   }
   if (ws->error) s->flags |= TOG_TRAJ_PN_ERROR;

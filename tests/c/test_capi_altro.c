@@ -13,8 +13,10 @@
  * The state guess comes from the caller (initial_states!, src/problem.jl:153-154), as the Julia user would
  * pass it.
  *   test_capi_altro <in.bin> <out.bin>  in: int64 B, x0 (13, B), U0 (4, 100, B), X0 (13, 101, B);
- *                                       out: X (13, 101, B), U (4, 100, B), stats (TOG_NSTATS, B)
- * tests/test_c_caller.py compares out.bin with the Python path (solve_b with ALTROSolverOptions) bit for bit.
+ *                                       out: X (13, 101, B), U (4, 100, B), stats (TOG_NSTATS, B),
+ *                                       hist_count (2, B), hist_outer (4, 41, B), hist_inner (3, 12041, B)
+ * tests/test_c_caller.py compares out.bin with the Python path (solve_b with ALTROSolverOptions) bit for bit,
+ * the iteration histories of tog_solve_altro_ex included.
  */
 #include <math.h>
 #include <stdio.h>
@@ -151,16 +153,34 @@ int main(int argc, char** argv) {
   a.resolve_feasible_problem = 0;
   a.R_inf = 0.001;
 
+  /* the solver the reference returns (altro_methods.jl:40-52): solver_al.stats with its per-iteration
+     vectors (every inner record of the AL phase: al_iterations x (iterations + 1) at most) */
+  const int cap = a.opts_al.al_iterations * (a.opts_al.iterations + 1) + 1, ocap = a.opts_al.al_iterations + 1;
   double* St = malloc(sizeof(double) * TOG_NSTATS * B);
-  int rc = tog_solve_altro(&d, &a, 0, x0, X, U, NULL, St, NULL, NULL);
-  if (rc) return fail_rc("tog_solve_altro", rc);
+  double* Hin = malloc(sizeof(double) * 3 * (size_t)cap * B);
+  double* Hout = malloc(sizeof(double) * 4 * (size_t)ocap * B);
+  double* Hcnt = malloc(sizeof(double) * 2 * B);
+  tog_altro_result res;
+  memset(&res, 0, sizeof(res));
+  res.inner_capacity = cap;
+  res.stats = St;
+  res.hist_inner = Hin;
+  res.hist_outer = Hout;
+  res.hist_count = Hcnt;
+  int rc = tog_solve_altro_ex(&d, &a, 0, x0, X, U, NULL, &res);
+  if (rc) return fail_rc("tog_solve_altro_ex", rc);
+  if (!(res.time >= res.time_al && res.time_al > 0.0 && res.time_pn == 0.0 && res.handle == NULL))
+    return fail_rc("tog_altro_result times / handle", -1);
   f = fopen(argv[2], "wb");
   if (!f) return fail_rc("open output", -1);
   fwrite(X, sizeof(double), nX, f);
   fwrite(U, sizeof(double), nU, f);
   fwrite(St, sizeof(double), (size_t)TOG_NSTATS * B, f);
+  fwrite(Hcnt, sizeof(double), 2 * (size_t)B, f);
+  fwrite(Hout, sizeof(double), 4 * (size_t)ocap * B, f);
+  fwrite(Hin, sizeof(double), 3 * (size_t)cap * B, f);
   fclose(f);
   printf("ok B=%lld\n", (long long)B);
-  free(x0), free(U), free(X), free(St);
+  free(x0), free(U), free(X), free(St), free(Hin), free(Hout), free(Hcnt);
   return 0;
 }

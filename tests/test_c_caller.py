@@ -73,10 +73,28 @@ def test_c_caller_altro_equals_python_path(tog, gpu, tmp_path):
     out = np.fromfile(tmp_path / "out.bin", dtype=np.float64)
     X_c = out[:B * N * n].reshape(B, N, n)
     U_c = out[B * N * n:B * N * n + B * (N - 1) * m].reshape(B, N - 1, m)
-    St_c = out[B * N * n + B * (N - 1) * m:].reshape(B, tog.abi.NSTATS)
+    o = B * N * n + B * (N - 1) * m
+    St_c = out[o:o + B * tog.abi.NSTATS].reshape(B, tog.abi.NSTATS)
+    o += B * tog.abi.NSTATS
+    opts = tog.Problems.maze_altro_options()
+    ocap = opts.opts_al.iterations + 1
+    cap = opts.opts_al.iterations * (opts.opts_al.opts_uncon.iterations + 1) + 1
+    cnt_c = out[o:o + 2 * B].reshape(B, 2).astype(np.int64)
+    o += 2 * B
+    Hout_c = out[o:o + 4 * ocap * B].reshape(B, ocap, 4)
+    o += 4 * ocap * B
+    Hin_c = out[o:].reshape(B, cap, 3)
     gp = prob.copy()
-    solver = tog.solve_b(gp, tog.Problems.maze_altro_options())
+    solver = tog.solve_b(gp, opts, history=cap)
     assert np.array_equal(X_c, gp._X), np.max(np.abs(X_c - gp._X))
     assert np.array_equal(U_c, gp._U), np.max(np.abs(U_c - gp._U))
     assert np.array_equal(St_c[:, tog.abi.STAT_TOTAL_STEPS], solver.stats["iterations_total"])
     assert np.array_equal(St_c[:, tog.abi.STAT_FLAGS].astype(np.int64), solver.stats["flags"])
+    # the C caller reads the same solver_al.stats histories
+    Hin, Hout, cnt = solver.solver_al.history
+    assert np.array_equal(cnt_c, cnt)
+    for b in range(B):
+        assert np.array_equal(Hin_c[b, :cnt[b, 0]], Hin[b, :cnt[b, 0]], equal_nan=True)
+        assert np.array_equal(Hout_c[b, :cnt[b, 1]], Hout[b, :cnt[b, 1]], equal_nan=True)
+        st = solver.solver_al.traj_stats(b)
+        assert st["iterations_total"] == int(St_c[b, tog.abi.STAT_TOTAL_STEPS]) + st["iterations"] - 1

@@ -17,6 +17,7 @@ JL = (ROOT / "integration" / "julia" / "libtog.jl").read_text()
 STRUCTS = {  # Julia mirror -> C struct
     "TogConstraint": "tog_constraint", "TogConstraintSet": "tog_constraint_set", "TogProblemDesc": "tog_problem_desc",
     "TogOptionsI": "tog_options", "TogPNOptions": "tog_pn_options", "TogAltroOptions": "tog_altro_options",
+    "TogAltroResult": "tog_altro_result",
 }
 PRIM = {"Int32": (4, 4), "Int64": (8, 8), "Float64": (8, 8), "Cvoid": None}
 

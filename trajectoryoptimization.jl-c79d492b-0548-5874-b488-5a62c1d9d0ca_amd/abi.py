@@ -16,7 +16,7 @@ import numpy as np
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "csrc" / "libtog.so"
 
-TOG_ABI_VERSION = 3
+TOG_ABI_VERSION = 4
 
 # models (include/tog.h tog_model_id)
 MODEL_DOUBLE_INTEGRATOR, MODEL_CARTPOLE, MODEL_QUADROTOR, MODEL_CAR, MODEL_PENDULUM, MODEL_KUKA = range(6)
@@ -34,6 +34,8 @@ MODE_ILQR, MODE_AL = 0, 1
 
 (FIELD_X, FIELD_U, FIELD_XBAR, FIELD_UBAR, FIELD_K, FIELD_D, FIELD_A, FIELD_B, FIELD_S, FIELD_SX,
  FIELD_DV, FIELD_LAMBDA, FIELD_MU, FIELD_C, FIELD_X0, FIELD_STATS, FIELD_RHO, FIELD_Q) = range(18)
+# iteration histories (tog_history_enable): (3,cap,B) inner records, (4,al_iterations+1,B) outer, (2,B) counts
+FIELD_HIST_INNER, FIELD_HIST_OUTER, FIELD_HIST_COUNT = 18, 19, 20
 
 (STAT_J, STAT_DJ, STAT_GRADIENT, STAT_ITERATIONS, STAT_ZERO_COUNT, STAT_ALPHA, STAT_Z, STAT_C_MAX,
  STAT_AL_ITER, STAT_TOTAL_STEPS, STAT_LS_TRIALS, STAT_BP_RESTARTS, STAT_FLAGS, STAT_PENALTY_MAX) = range(14)
@@ -111,7 +113,16 @@ class tog_altro_options(C.Structure):
     _fields_ = [("opts_al", tog_options), ("R_inf", C.c_double), ("R_minimum_time", C.c_double),
                 ("dt_max", C.c_double), ("dt_min", C.c_double), ("projected_newton_tolerance", C.c_double),
                 ("dynamically_feasible_projection", C.c_int32), ("resolve_feasible_problem", C.c_int32),
-                ("projected_newton", C.c_int32), ("reserved", C.c_int32), ("opts_pn", tog_pn_options)]
+                ("projected_newton", C.c_int32), ("max_steps", C.c_int32), ("opts_pn", tog_pn_options)]
+
+
+class tog_altro_result(C.Structure):
+    """What solve!(prob, ALTROSolverOptions) returns (include/tog.h tog_altro_result)."""
+    _fields_ = [("inner_capacity", C.c_int32), ("keep_handle", C.c_int32),
+                ("stats", _dp), ("stats_resolve", _dp), ("stats_pn", _dp),
+                ("hist_inner", _dp), ("hist_outer", _dp), ("hist_count", _dp), ("hist_pn", _dp),
+                ("time", C.c_double), ("time_al", C.c_double), ("time_pn", C.c_double),
+                ("handle", C.c_void_p)]
 
 
 def default_options() -> tog_options:
@@ -284,6 +295,10 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_default_altro_options.argtypes = [C.POINTER(tog_altro_options)]
     lib.tog_solve_altro.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_altro_options), C.c_int32, _dp, _dp,
                                     _dp, _dp, _dp, _dp, _dp]
+    lib.tog_solve_altro_ex.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_altro_options), C.c_int32, _dp,
+                                       _dp, _dp, _dp, C.POINTER(tog_altro_result)]
+    lib.tog_history_enable.argtypes = [vp, C.c_int32]
+    lib.tog_get_pn_history.argtypes = [vp, _dp, _ip]
     lib.tog_model_load.argtypes = [C.c_char_p, C.POINTER(vp)]
     lib.tog_model_dims.argtypes = [vp, _ip, _ip]
     lib.tog_model_free.argtypes = [vp]
@@ -300,7 +315,8 @@ def load_library(path: os.PathLike | None = None):
                  "tog_profile", "tog_profile_read", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion",
                  "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn", "tog_model_load", "tog_model_dims",
                  "tog_model_free", "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device",
-                 "tog_generic_cost_free", "tog_solve_altro"):
+                 "tog_generic_cost_free", "tog_solve_altro", "tog_solve_altro_ex", "tog_history_enable",
+                 "tog_get_pn_history"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -319,7 +335,7 @@ EXPORTED_SYMBOLS = (
     "tog_profile_read", "tog_last_error", "tog_dynamics_bias", "tog_slack_controls", "tog_cost_expansion", "tog_solve_ilqr",
     "tog_solve_al", "tog_default_pn_options", "tog_solve_pn", "tog_model_load", "tog_model_dims", "tog_model_free",
     "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device", "tog_generic_cost_free",
-    "tog_default_altro_options", "tog_solve_altro",
+    "tog_default_altro_options", "tog_solve_altro", "tog_solve_altro_ex", "tog_history_enable", "tog_get_pn_history",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD, KERNEL_EXPANSION = 0, 1, 2, 3
 NKERNELS = 4

@@ -16,6 +16,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -136,18 +137,19 @@ int infeasible_desc(const tog_problem_desc* s, double R_inf, Desc& o) {
             const tog_constraint& con = set.con[c];
             if ((con.type == TOG_CON_BOUND) != (pass == 1)) continue;
             if (con.type == TOG_CON_BOUND) {
-              if (con.count == 1) return tog__fail(TOG_ERR_UNSUPPORTED, "trim=false bounds on an infeasible-start problem");
               // [x_max; x_min; u_max; u_min] over the augmented controls: the slack entries are unbounded
+              // (and never get rows, trim=false included: the bound keeps the model's m, build_rows)
               std::vector<double> b(2 * n + 2 * mi);
               for (int i = 0; i < 2 * n; i++) b[i] = con.data[i];
               for (int i = 0; i < mi; i++) {
                 b[2 * n + i] = i < m ? con.data[2 * n + i] : INFINITY;
                 b[2 * n + mi + i] = i < m ? con.data[2 * n + m + i] : -INFINITY;
               }
-              cs.push_back({TOG_CON_BOUND, 0, nullptr});
+              cs.push_back({TOG_CON_BOUND, con.count, nullptr});
               ds.push_back(std::move(b));
             } else {
-              if (con.type == TOG_CON_USER) return tog__fail(TOG_ERR_UNSUPPORTED, "user constraint rows in tog_solve_altro");
+              // circles, spheres, user functions c(x, u[1:m]): the plugin evaluates them on the model's
+              // controls, their Jacobian columns over the slack controls are zero (_∇c's view, :137-143)
               cs.push_back(con);
               ds.push_back(copy_data(con, n, m));
             }
@@ -188,6 +190,14 @@ int min_time_desc(const tog_problem_desc* s, double R_min_time, double dt_max, d
   o.r = pad(s->r, m, 1, mt, 1);
   o.Qf = pad(s->Qf, n, n, nt, nt);
   o.qf = pad(s->qf, n, 1, nt, 1);
+  // @assert has_bounds(prob.constraints) (minimum_time.jl:6)
+  bool has_bounds = false;
+  for (int k = 0; k < N && !has_bounds; k++) {
+    const int si = s->knot_set ? s->knot_set[k] : -1;
+    if (si < 0 || si >= s->n_sets) continue;
+    for (int c = 0; c < s->sets[si].n_con; c++) has_bounds = has_bounds || s->sets[si].con[c].type == TOG_CON_BOUND;
+  }
+  if (!has_bounds) return tog__fail(TOG_ERR_ARG, "minimum time: the problem has no BoundConstraint (minimum_time.jl:6)");
   o.knot_set.assign(N, -1);
   std::vector<int> memo(3 * (s->n_sets + 1), -1);
   for (int k = 0; k < N; k++) {
@@ -246,16 +256,49 @@ struct Handle {
   ~Handle() {
     if (h) tog_destroy(h);
   }
+  tog_handle* release() {
+    tog_handle* r = h;
+    h = nullptr;
+    return r;
+  }
 };
 
-// create, set the state, (slack controls), solve to completion with the default step budget
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// create, set the state, (slack controls), (histories), solve to completion within max_steps batch steps
+// (0: the tog_solve_budget default)
 int run(const tog_problem_desc* d, const tog_options* o, int32_t device, const double* x0, const double* U,
-        const double* X, bool slack, int mode, Handle& H) {
+        const double* X, bool slack, int mode, Handle& H, int max_steps, int hcap) {
   int rc = tog_create(d, o, device, &H.h);
   if (rc) return rc;
   if ((rc = tog_set_state(H.h, x0, U, X))) return rc;
   if (slack && (rc = tog_slack_controls(H.h))) return rc;
-  return tog_solve(H.h, mode, 0);
+  if (hcap > 0 && (rc = tog_history_enable(H.h, hcap))) return rc;
+  return tog_solve(H.h, mode, max_steps);
+}
+
+// solver_al.stats of the AL phase: the summary rows and the iteration histories
+int read_al(tog_handle* h, tog_altro_result* r) {
+  int rc;
+  if (r->stats && (rc = tog_get(h, TOG_FIELD_STATS, r->stats))) return rc;
+  if (r->inner_capacity > 0) {
+    if (r->hist_inner && (rc = tog_get(h, TOG_FIELD_HIST_INNER, r->hist_inner))) return rc;
+    if (r->hist_outer && (rc = tog_get(h, TOG_FIELD_HIST_OUTER, r->hist_outer))) return rc;
+    if (r->hist_count && (rc = tog_get(h, TOG_FIELD_HIST_COUNT, r->hist_count))) return rc;
+  }
+  return TOG_OK;
+}
+
+// trajectories whose AL phase ended with one of the reference's exceptions: forward_pass.jl:80-82's
+// error("Cost increased") and lowrankdowndate!'s PosDefException (backward_pass.jl:186-192)
+std::vector<char> raised(tog_handle* h, long long B, int& rc) {
+  std::vector<int32_t> f(B);
+  std::vector<char> out(B, 0);
+  rc = tog_status(h, f.data());
+  for (long long b = 0; b < B && !rc; b++) out[b] = (f[b] & (TOG_TRAJ_COST_INCREASED | TOG_TRAJ_SQRT_PD_FAIL)) != 0;
+  return out;
 }
 
 }  // namespace
@@ -273,15 +316,34 @@ void tog_default_altro_options(tog_altro_options* a) {
   a->dynamically_feasible_projection = 1;
   a->resolve_feasible_problem = 1;
   a->projected_newton = 0;
+  a->max_steps = 0;
   tog_default_pn_options(&a->opts_pn);
 }
 
 int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
                         const double* x0, double* X, double* U, double* h_out, double* stats,
                         double* stats_resolve, double* stats_pn) {
+  tog_altro_result r;
+  memset(&r, 0, sizeof(r));
+  r.stats = stats;
+  r.stats_resolve = stats_resolve;
+  r.stats_pn = stats_pn;
+  return tog_solve_altro_ex(desc, opts, device, x0, X, U, h_out, &r);
+}
+
+int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
+                           const double* x0, double* X, double* U, double* h_out, tog_altro_result* res) {
+  const double t0 = now_s();
   if (!desc || !opts || !x0 || !U) return tog__fail(TOG_ERR_ARG, "tog_solve_altro: null argument");
   if (desc->flags & (TOG_PROB_INFEASIBLE | TOG_PROB_MIN_TIME))
     return tog__fail(TOG_ERR_ARG, "tog_solve_altro takes the original problem (altro_problem transforms it)");
+  tog_altro_result local;
+  memset(&local, 0, sizeof(local));
+  tog_altro_result* R = res ? res : &local;
+  R->handle = nullptr;
+  R->time = R->time_al = R->time_pn = 0.0;
+  if (R->inner_capacity < 0) return tog__fail(TOG_ERR_ARG, "inner_capacity must be >= 0");
+  const int hcap = R->inner_capacity;
   const int n = desc->n, m = desc->m, N = desc->N;
   const long long B = desc->batch;
   // altro_problem (altro_methods.jl:101): an initial state trajectory that is not all NaN
@@ -299,6 +361,7 @@ int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* o
   if (infeasible && min_time) return tog__fail(TOG_ERR_UNSUPPORTED, "infeasible start + minimum time");
   if (opts->projected_newton && (infeasible || min_time))
     return tog__fail(TOG_ERR_UNSUPPORTED, "projected Newton on the infeasible-start or minimum-time problem");
+  if (opts->max_steps < 0) return tog__fail(TOG_ERR_ARG, "max_steps must be >= 0");
   tog_options oal = opts->opts_al;
   if (opts->projected_newton) {  // altro_methods.jl:5-13
     if (opts->projected_newton_tolerance >= 0) {
@@ -309,7 +372,12 @@ int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* o
     }
   }
   int rc;
-  const size_t nU = (size_t)m * (N - 1), nX = (size_t)n * N;
+  const size_t nX = (size_t)n * N;
+  auto finish = [&](Handle& H) {
+    if (R->keep_handle) R->handle = H.release();
+    R->time = now_s() - t0;
+    return TOG_OK;
+  };
   if (infeasible) {
     Desc di;
     if ((rc = infeasible_desc(desc, opts->R_inf, di))) return rc;
@@ -318,31 +386,41 @@ int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* o
     for (long long b = 0; b < B; b++)
       for (int k = 0; k < N - 1; k++)
         for (int i = 0; i < m; i++) Ui[i + mi * (k + (size_t)(N - 1) * b)] = U[i + m * (k + (size_t)(N - 1) * b)];
-    {
-      Handle H;
-      if ((rc = run(&di.d, &oal, device, x0, Ui.data(), X, true, TOG_MODE_AL, H))) return rc;
-      std::vector<double> Xi(nX * B);
-      if ((rc = tog_get(H.h, TOG_FIELD_X, Xi.data())) || (rc = tog_get(H.h, TOG_FIELD_U, Ui.data()))) return rc;
-      if (stats && (rc = tog_get(H.h, TOG_FIELD_STATS, stats))) return rc;
-      // process_results!: X and the model controls U[1:m]
-      memcpy(X, Xi.data(), sizeof(double) * nX * B);
-      for (long long b = 0; b < B; b++)
-        for (int k = 0; k < N - 1; k++)
-          for (int i = 0; i < m; i++) U[i + m * (k + (size_t)(N - 1) * b)] = Ui[i + mi * (k + (size_t)(N - 1) * b)];
-    }
+    // the caller's X, U: what a raised trajectory keeps (its solve ran on infeasible_problem's copy)
+    const std::vector<double> X_in(X, X + nX * B), U_in(U, U + (size_t)m * (N - 1) * B);
+    Handle H1;
+    const double ta = now_s();
+    if ((rc = run(&di.d, &oal, device, x0, Ui.data(), X, true, TOG_MODE_AL, H1, opts->max_steps, hcap))) return rc;
+    R->time_al = now_s() - ta;
+    std::vector<double> Xi(nX * B);
+    if ((rc = tog_get(H1.h, TOG_FIELD_X, Xi.data())) || (rc = tog_get(H1.h, TOG_FIELD_U, Ui.data()))) return rc;
+    if ((rc = read_al(H1.h, R))) return rc;
+    const std::vector<char> err = raised(H1.h, B, rc);
+    if (rc) return rc;
+    // process_results!: X and the model controls U[1:m]
+    memcpy(X, Xi.data(), sizeof(double) * nX * B);
+    for (long long b = 0; b < B; b++)
+      for (int k = 0; k < N - 1; k++)
+        for (int i = 0; i < m; i++) U[i + m * (k + (size_t)(N - 1) * b)] = Ui[i + mi * (k + (size_t)(N - 1) * b)];
     if (opts->resolve_feasible_problem) {
       // the feasible problem from the infeasible solve's controls; projection! (ilqr_methods.jl:179-190)
       // leaves the open-loop rollout of U from x0: X = NaN
       const bool con = is_constrained(desc);
       tog_options ores = oal;
-      Handle H;
+      Handle H2;
       if ((rc = run(desc, &ores, device, x0, U, opts->dynamically_feasible_projection ? nullptr : X, false,
-                    con ? TOG_MODE_AL : TOG_MODE_ILQR, H)))
+                    con ? TOG_MODE_AL : TOG_MODE_ILQR, H2, opts->max_steps, 0)))
         return rc;
-      if ((rc = tog_get(H.h, TOG_FIELD_X, X)) || (rc = tog_get(H.h, TOG_FIELD_U, U))) return rc;
-      if (stats_resolve && (rc = tog_get(H.h, TOG_FIELD_STATS, stats_resolve))) return rc;
+      if ((rc = tog_get(H2.h, TOG_FIELD_X, X)) || (rc = tog_get(H2.h, TOG_FIELD_U, U))) return rc;
+      if (R->stats_resolve && (rc = tog_get(H2.h, TOG_FIELD_STATS, R->stats_resolve))) return rc;
     }
-    return TOG_OK;
+    for (long long b = 0; b < B; b++) {
+      if (!err[b]) continue;  // the exception left prob untouched: no process_results!, no resolve
+      memcpy(X + nX * b, X_in.data() + nX * b, sizeof(double) * nX);
+      memcpy(U + (size_t)m * (N - 1) * b, U_in.data() + (size_t)m * (N - 1) * b, sizeof(double) * m * (N - 1));
+      if (R->stats_resolve) memset(R->stats_resolve + (size_t)TOG_NSTATS * b, 0, sizeof(double) * TOG_NSTATS);
+    }
+    return finish(H1);
   }
   if (min_time) {
     Desc dm;
@@ -359,10 +437,16 @@ int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* o
       }
     }
     Handle H;
-    if ((rc = run(&dm.d, &oal, device, x0t.data(), Ut.data(), nullptr, false, TOG_MODE_AL, H))) return rc;
+    const double ta = now_s();
+    if ((rc = run(&dm.d, &oal, device, x0t.data(), Ut.data(), nullptr, false, TOG_MODE_AL, H, opts->max_steps, hcap)))
+      return rc;
+    R->time_al = now_s() - ta;
     if ((rc = tog_get(H.h, TOG_FIELD_X, Xt.data())) || (rc = tog_get(H.h, TOG_FIELD_U, Ut.data()))) return rc;
-    if (stats && (rc = tog_get(H.h, TOG_FIELD_STATS, stats))) return rc;
+    if ((rc = read_al(H.h, R))) return rc;
+    const std::vector<char> err = raised(H.h, B, rc);
+    if (rc) return rc;
     for (long long b = 0; b < B; b++) {  // process_results!: X[1:n], U[1:m]; h separately
+      if (err[b]) continue;  // minimum_time_problem's copy raised: prob untouched
       if (X)
         for (int k = 0; k < N; k++)
           for (int i = 0; i < n; i++) X[i + n * (k + (size_t)N * b)] = Xt[i + nt * (k + (size_t)N * b)];
@@ -371,24 +455,51 @@ int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* o
         if (h_out) h_out[k + (size_t)(N - 1) * b] = Ut[m + mt * (k + (size_t)(N - 1) * b)];
       }
     }
-    return TOG_OK;
+    return finish(H);
   }
   // feasible start, fixed time: solve!(prob_altro, solver.solver_al), the AL solver itself (an unconstrained
   // problem too: the solver-level solve! has no iLQR fallback), then projected Newton
   tog_options o = oal;
   Handle H;
-  if ((rc = run(desc, &o, device, x0, U, nullptr, false, TOG_MODE_AL, H))) return rc;
+  const double ta = now_s();
+  if ((rc = run(desc, &o, device, x0, U, nullptr, false, TOG_MODE_AL, H, opts->max_steps, hcap))) return rc;
+  R->time_al = now_s() - ta;
+  const std::vector<char> err = raised(H.h, B, rc);
+  if (rc) return rc;
   if (opts->projected_newton) {
+    // a raised trajectory never reaches projected Newton: its X, U (the AL phase's, prob_altro = prob) are
+    // put back after the batched projection
+    std::vector<double> Xs(nX * B), Us((size_t)m * (N - 1) * B);
+    if ((rc = tog_get(H.h, TOG_FIELD_X, Xs.data())) || (rc = tog_get(H.h, TOG_FIELD_U, Us.data()))) return rc;
     std::vector<double> pn((size_t)TOG_PN_NSTATS * B);
+    const double tp = now_s();
     if ((rc = tog_solve_pn(H.h, &opts->opts_pn, pn.data()))) return rc;
-    if (stats_pn) memcpy(stats_pn, pn.data(), sizeof(double) * pn.size());
+    R->time_pn = now_s() - tp;
+    if (R->hist_pn && (rc = tog_get_pn_history(H.h, R->hist_pn, nullptr))) return rc;
+    bool any = false;
+    for (long long b = 0; b < B; b++) any = any || err[b];
+    if (any) {
+      std::vector<double> Xp(nX * B), Up((size_t)m * (N - 1) * B);
+      if ((rc = tog_get(H.h, TOG_FIELD_X, Xp.data())) || (rc = tog_get(H.h, TOG_FIELD_U, Up.data()))) return rc;
+      const size_t nu = (size_t)m * (N - 1), np = 2 * (size_t)opts->opts_pn.n_steps;
+      for (long long b = 0; b < B; b++) {
+        if (!err[b]) continue;
+        memcpy(Xp.data() + nX * b, Xs.data() + nX * b, sizeof(double) * nX);
+        memcpy(Up.data() + nu * b, Us.data() + nu * b, sizeof(double) * nu);
+        memset(pn.data() + (size_t)TOG_PN_NSTATS * b, 0, sizeof(double) * TOG_PN_NSTATS);
+        if (R->hist_pn)
+          for (size_t i = 0; i < np; i++) R->hist_pn[np * b + i] = NAN;
+      }
+      if ((rc = tog_set(H.h, TOG_FIELD_X, Xp.data())) || (rc = tog_set(H.h, TOG_FIELD_U, Up.data()))) return rc;
+    }
+    if (R->stats_pn) memcpy(R->stats_pn, pn.data(), sizeof(double) * pn.size());
   }
+  // (the statistics rows after projected Newton: its TOG_TRAJ_PN_ERROR lands in the flags)
+  if ((rc = read_al(H.h, R))) return rc;
   std::vector<double> Xs(nX * B);
   if ((rc = tog_get(H.h, TOG_FIELD_X, Xs.data())) || (rc = tog_get(H.h, TOG_FIELD_U, U))) return rc;
   if (X) memcpy(X, Xs.data(), sizeof(double) * nX * B);
-  if (stats && (rc = tog_get(H.h, TOG_FIELD_STATS, stats))) return rc;
-  (void)nU;
-  return TOG_OK;
+  return finish(H);
 }
 
 }  // extern "C"

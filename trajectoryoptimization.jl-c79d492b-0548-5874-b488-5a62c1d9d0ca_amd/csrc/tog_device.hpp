@@ -123,6 +123,9 @@ struct TrajState {
   // line search carried over to the next batch step (k_ls_decide, pending mode): the trials [0, ls_pend)
   // are evaluated and stored; the trajectory skips that step's Jacobians and backward pass
   int ls_pend, pad_;
+  // records written to the iteration histories (DevBuffers::hist_in / hist_out; counted past the
+  // capacity, so a truncated history is visible)
+  int hn_in, hn_out;
 };
 
 // the regularisation scalars the backward pass mutates (kept in registers)
@@ -152,7 +155,8 @@ struct DevBuffers {
   int nc;       // candidates evaluated per trajectory per launch (<= 64)
   int* ls_list;   // (2, B) ping-pong lists of trajectories still undecided after a speculative round
   int* ls_done;   // = ls_list + B: the trajectories whose inner solve finished this step (k_ls_book -> k_al_outer)
-  int* ls_count;  // [LS_MAX_ROUNDS] list lengths, zeroed at the start of every forward pass
+  int* ls_count;  // [LS_COUNT_SLOTS] list lengths, zeroed at the start of every forward pass
+  int* ls_fb;     // (B) trajectories whose line search ran out of trials (k_ls_fallback), or null
   int bwd_stride;     // k_bwd_team: per-team LDS stride (doubles) of the launch
   int bwd_shmem;      // k_bwd_team: dynamic LDS bytes per block of the launch
   int bwd_stride2[2]; // [std, sqrt] strides
@@ -179,7 +183,40 @@ struct DevBuffers {
   int* act_list;
   int* act_count;
   TrajState* st;
+  // per-trajectory iteration histories (tog_history_enable; null = off): the iLQR solver's
+  // stats[:cost], [:dJ], [:gradient] (record_iteration!, ilqr_methods.jl:77-89) as hist_in (3, hcap, B),
+  // and the AL solver's stats[:iterations_inner], [:cost], [:c_max], [:penalty_max]
+  // (augmented_lagrangian_methods.jl:79-97) as hist_out (4, ocap, B)
+  double* hist_in;
+  double* hist_out;
+  int hcap, ocap;
 };
+
+// iLQR record_iteration! (ilqr_methods.jl:77-89): one (J, dJ, gradient) record
+__device__ __forceinline__ void hist_inner(const DevBuffers& Bf, long long b, TrajState& s, double J, double dJ,
+                                           double g) {
+  if (!Bf.hist_in) return;
+  if (s.hn_in < Bf.hcap) {
+    double* h = Bf.hist_in + ((size_t)b * Bf.hcap + s.hn_in) * 3;
+    h[0] = J;
+    h[1] = dJ;
+    h[2] = g;
+  }
+  s.hn_in++;
+}
+// AL record_iteration! (augmented_lagrangian_methods.jl:79-97): (iterations_inner, cost, c_max, penalty_max)
+__device__ __forceinline__ void hist_outer(const DevBuffers& Bf, long long b, TrajState& s, int inner, double J,
+                                           double c_max, double mu_max) {
+  if (!Bf.hist_out) return;
+  if (s.hn_out < Bf.ocap) {
+    double* h = Bf.hist_out + ((size_t)b * Bf.ocap + s.hn_out) * 4;
+    h[0] = (double)inner;
+    h[1] = J;
+    h[2] = c_max;
+    h[3] = mu_max;
+  }
+  s.hn_out++;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Scalar helpers (double and Dual share names)

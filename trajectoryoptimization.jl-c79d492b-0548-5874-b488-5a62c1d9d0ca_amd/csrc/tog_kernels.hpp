@@ -421,6 +421,13 @@ __global__ void __launch_bounds__(64) k_init(const DevProblem* __restrict__ P, D
   s.dJ = INFINITY;
   s.zero_cnt = 0;
   s.grad = INFINITY;
+  if (Bf.hist_in) {
+    // the AL solver's initial record (augmented_lagrangian_methods.jl:13, iterations_inner 0 of a reset
+    // solver), then the inner solver's (ilqr_methods.jl:20): its gradient is calculate_gradient at the
+    // initial trajectory with the solver's current d (zero for a new handle)
+    if (mode == TOG_MODE_AL) hist_outer(Bf, b, s, 0, s.J, s.c_max, s.mu_max);
+    hist_inner(Bf, b, s, s.J, INFINITY, traj_gradient<M>(P, Bf, b, mode == TOG_MODE_AL));
+  }
   Bf.st[b] = s;
 }
 
@@ -1615,6 +1622,9 @@ static __device__ unsigned long long tog_bwd_prof[BPROF_N];
 
 constexpr int FTEAM = 32;
 constexpr int LS_MAX_ROUNDS = 2;  // speculative line-search rounds per forward pass
+// ls_count slots: [0] undecided after the first round, [1] inner solves finished (k_al_outer),
+// [2] line searches that ran out of trials (k_ls_fallback)
+constexpr int LS_COUNT_SLOTS = 4;
 #ifndef TOG_LS_FIRST
 #define TOG_LS_FIRST 8
 #endif
@@ -1841,8 +1851,8 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
 // solve! bookkeeping after an accepted forward pass (ilqr_methods.jl:21-42) and the AL outer update
 // when the inner solve finished (augmented_lagrangian_methods.jl:53-126). One lane per trajectory.
 // Inner part: returns true when the AL outer update is due (inner solve finished in AL mode).
-__device__ inline bool inner_bookkeeping(const DevProblem* __restrict__ P, TrajState& s, double J, double grad,
-                                         int mode) {
+__device__ inline bool inner_bookkeeping(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b,
+                                         TrajState& s, double J, double grad, int mode) {
   const tog_options& o = P->o;
   const bool al = (mode == TOG_MODE_AL);
   s.total_steps++;
@@ -1856,6 +1866,7 @@ __device__ inline bool inner_bookkeeping(const DevProblem* __restrict__ P, TrajS
     s.iters++;
     s.grad = grad;
     s.zero_cnt = (s.dJ == 0.0) ? s.zero_cnt + 1 : 0;
+    hist_inner(Bf, b, s, s.J, s.dJ, s.grad);
     // evaluate_convergence (ilqr_methods.jl:139-162)
     if ((0.0 < s.dJ && s.dJ < s.cost_tol) || s.grad < s.grad_tol || s.iters >= o.iterations ||
         s.zero_cnt > o.dJ_counter_limit) {
@@ -1874,11 +1885,15 @@ __device__ inline bool inner_bookkeeping(const DevProblem* __restrict__ P, TrajS
 
 // AL outer update after the inner solve (augmented_lagrangian_methods.jl:53-126): cost(prob) to refresh
 // C, dual_update!, penalty_update!, max_violation, convergence, and the next outer iteration's reset.
-__device__ inline void al_outer_finish(const DevProblem* __restrict__ P, TrajState& s, double mumax, double c_max,
-                                       double Jnext, int mode) {
+// Jal: cost(prob) at the inner solve's X, U before the multiplier update (:59, the AL record's cost);
+// grad_next: calculate_gradient for the next inner solve's initial record (used with histories only).
+__device__ inline void al_outer_finish(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b, TrajState& s,
+                                       double mumax, double c_max, double Jal, double Jnext, double grad_next,
+                                       int mode) {
   const tog_options& o = P->o;
   s.mu_max = mumax;
   s.c_max = c_max;
+  hist_outer(Bf, b, s, s.iters, Jal, c_max, mumax);
   const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (s.c_max < o.constraint_tolerance);
   if (conv) {
     s.flags |= TOG_TRAJ_AL_CONVERGED;
@@ -1896,6 +1911,7 @@ __device__ inline void al_outer_finish(const DevProblem* __restrict__ P, TrajSta
     s.iters = 1;
     s.dJ = INFINITY;
     s.zero_cnt = 0;
+    hist_inner(Bf, b, s, Jnext, INFINITY, grad_next);
   }
 }
 
@@ -1906,13 +1922,13 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
   const tog_options& o = P->o;
-  if (!inner_bookkeeping(P, s, J, grad, mode)) return;
+  if (!inner_bookkeeping(P, Bf, b, s, J, grad, mode)) return;
   const double* X = Bf.X + (size_t)b * N * n;
   const double* U = Bf.U + (size_t)b * (N - 1) * m;
   double* C = Bf.C + (size_t)b * N * pmax;
   double* lam = Bf.lam + (size_t)b * N * pmax;
   double* mu = Bf.mu + (size_t)b * N * pmax;
-  (void)traj_cost<M>(P, Bf, b, X, U, true, C);  // J = cost(prob): updates C
+  const double Jal = traj_cost<M>(P, Bf, b, X, U, true, C);  // J = cost(prob): updates C
   double mumax = 0.0;
   for (int k = 0; k < N; k++) {
     const int cnt = knot_count(P, k);
@@ -1929,8 +1945,10 @@ __device__ void step_bookkeeping(const DevProblem* __restrict__ P, const DevBuff
   }
   const double c_max = traj_max_violation(P, Bf, b);
   const bool conv = (o.kickout_max_penalty && mumax == o.penalty_max) || (c_max < o.constraint_tolerance);
-  const double Jnext = (conv || s.al_iter >= o.al_iterations) ? 0.0 : traj_cost<M>(P, Bf, b, X, U, true, C);
-  al_outer_finish(P, s, mumax, c_max, Jnext, mode);
+  const bool next = !(conv || s.al_iter >= o.al_iterations);
+  const double Jnext = next ? traj_cost<M>(P, Bf, b, X, U, true, C) : 0.0;
+  const double gnext = (next && Bf.hist_in) ? traj_gradient<M>(P, Bf, b, true) : 0.0;
+  al_outer_finish(P, Bf, b, s, mumax, c_max, Jal, Jnext, gnext, mode);
 }
 
 // Does the sequential acceptance logic of forwardpass! (forward_pass.jl:19-65) settle within the
@@ -2670,11 +2688,12 @@ __global__ void __launch_bounds__(256) k_ls_decide(const DevProblem* __restrict_
         }
       } else {
         st->ls_pend = 0;
-        if (state == 2) {  // forward_pass.jl:22-37: z = expected = α = 0, J from cost(X) in k_ls_book
+        if (state == 2) {  // forward_pass.jl:22-37: z = expected = α = 0, J from cost(X) (k_ls_fallback)
           win = -2;
           z = 0.0;
           expected = 0.0;
           alpha_last = 0.0;
+          if (Bf.ls_fb) Bf.ls_fb[atomicAdd(Bf.ls_count + 2, 1)] = (int)b;
         } else if (win < 0) {
           win = -3;
         }
@@ -2744,6 +2763,85 @@ __global__ void __launch_bounds__(256) k_ls_apply(const DevProblem* __restrict__
   }
 }
 
+// k_ls_book's replay of an accepted trajectory without an evaluated trial (win -3, J_prev NaN): a serial
+// rollout, kept out of line so that the bookkeeping kernel's common path does not carry its registers
+template <class M, int INTEG>
+__device__ __noinline__ void replay_cost(const DevProblem* __restrict__ P, const DevBuffers& Bf, long long b,
+                                         double alpha, bool al, int bookkeeping, double max_cost, double J,
+                                         double& grad, bool& copied, const RowTables& RT) {
+  double Jw;
+  if (!bookkeeping) {
+    rollout_cost<M, INTEG, 1>(P, Bf, b, alpha, al, Jw, nullptr, RT);
+  } else if (!(J > max_cost)) {
+    rollout_cost<M, INTEG, 2>(P, Bf, b, alpha, al, Jw, &grad, RT);
+    copied = true;
+  }
+}
+
+// forwardpass! when every trial failed (forward_pass.jl:22-37): X̄ = X and J = cost(prob.obj, X̄, Ū), which
+// also refreshes C (A.10). One wave per trajectory k_ls_decide listed, lanes over knots: per knot the
+// constraint values, the stage (terminal) cost, the AL terms λ'c + ½c'Iμc (al_knot_terms' operations) and
+// the todorov term max_i |d_i| / (|u_i| + 1) into gk; lane 0 sums the knots in traj_cost's order (stage
+// costs, terminal cost, then the AL terms), so J is traj_cost's bit for bit. (On one lane per trajectory
+// this was a serial 101-knot chain of scattered loads: 50 µs at one trajectory, 0.5 ms at 16-128.)
+template <class M>
+__global__ void __launch_bounds__(64) k_ls_fallback(const DevProblem* __restrict__ P, DevBuffers Bf, int al,
+                                                    const int* __restrict__ list, const int* __restrict__ count) {
+  if ((int)blockIdx.x >= *count) return;
+  extern __shared__ double fb_lds[];
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pmax = P->pmax;
+  const long long b = list[blockIdx.x];
+  const int lane = threadIdx.x;
+  double* sk = fb_lds;       // [N] stage / terminal cost of knot k
+  double* ak = fb_lds + N;   // [N] AL terms of knot k
+  int* hk = reinterpret_cast<int*>(fb_lds + 2 * N);  // [N] knot has rows
+  const double* X = Bf.X + (size_t)b * N * n;
+  const double* U = Bf.U + (size_t)b * (N - 1) * m;
+  const double* d = Bf.d + (size_t)b * (N - 1) * m;
+  double* C = Bf.C + (size_t)b * N * pmax;
+  const double* lam = Bf.lam + (size_t)b * N * pmax;
+  const double* mu = Bf.mu + (size_t)b * N * pmax;
+  for (int k = lane; k < N; k += WAVE) {
+    const double* x = X + (size_t)k * n;
+    const double* u = (k < N - 1) ? U + (size_t)k * m : nullptr;
+    sk[k] = (k < N - 1) ? stage_cost_m<M>(P, x, u) : terminal_cost_m<M>(P, x);
+    const int cnt = al ? knot_count(P, k) : 0;
+    const cptr<ConRow> rows = knot_rows(P, k);
+    double lc = 0.0, cIc = 0.0;
+    for (int i = 0; i < cnt; i++) {  // al_knot_terms' operations (rows differ across lanes: no uniform_row)
+      const size_t q = (size_t)k * pmax + i;
+      const ConRow r = load_row(rows + i);
+      const double c = row_value_m<M>(r, x, u);
+      const double l = lam[q];
+      const bool a = row_inequality<(ModelTraits<M>::slack > 0)>(r) ? ((c >= 0.0) || (l > 0.0)) : true;
+      const double w = a ? mu[q] : 0.0;
+      lc = fma(l, c, lc);
+      cIc = fma(c * w, c, cIc);
+      C[q] = c;
+    }
+    ak[k] = lc + 0.5 * cIc;
+    hk[k] = cnt;
+    if (k < N - 1) {
+      double mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        const double v = fabs(d[(size_t)k * m + i]) / (fabs(u[i]) + 1.0);
+        if (v > mx || isnan(v)) mx = v;
+      }
+      Bf.gk[(size_t)b * N + k] = mx;
+    }
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  double J = 0.0, Jc = 0.0;
+  for (int k = 0; k < N - 1; k++) J += sk[k];
+  J += sk[N - 1];
+  for (int k = 0; k < N; k++)
+    if (hk[k]) Jc += ak[k];
+  Bf.ls_Jw[b] = al ? J + Jc : J;
+}
+
 template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P, DevBuffers Bf, int mode,
                                                 int bookkeeping, const double* Jprev_in, double* Jout) {
@@ -2766,27 +2864,28 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
   double grad = 0.0;
   bool copied = false;
   if (win == -2) {  // max line-search iterations (forward_pass.jl:22-37), as k_ls_commit
-    const double* X = Bf.X + (size_t)b * N * n;
-    const double* U = Bf.U + (size_t)b * (N - 1) * m;
     if (!bookkeeping) {
+      const double* X = Bf.X + (size_t)b * N * n;
+      const double* U = Bf.U + (size_t)b * (N - 1) * m;
       double* Xb = Bf.Xb + (size_t)b * N * n;
       double* Ub = Bf.Ub + (size_t)b * (N - 1) * m;
       for (int i = 0; i < N * n; i++) Xb[i] = X[i];
       for (int i = 0; i < (N - 1) * m; i++) Ub[i] = U[i];
     }
-    J = traj_cost<M>(P, Bf, b, X, U, al, al ? Bf.C + (size_t)b * N * P->pmax : nullptr);
+    // J = cost(X̄ = X) and C(X) from k_ls_fallback (ls_Jw), its todorov terms in gk
     reg_increase(P, s);
     s.rho += o.bp_reg_fp;
-    grad = traj_gradient<M>(P, Bf, b, al);
+    if (o.gradient_type == 0) {
+      const double* g = Bf.gk + (size_t)b * N;
+      double gsum = 0.0;
+      for (int k = 0; k < N - 1; k++) gsum += g[k];
+      grad = gsum / N;
+    } else {
+      grad = traj_gradient<M>(P, Bf, b, al);
+    }
     copied = true;
   } else if (win == -3) {
-    double Jw;
-    if (!bookkeeping) {
-      rollout_cost<M, INTEG, 1>(P, Bf, b, s.alpha, al, Jw, nullptr, RT);
-    } else if (!(J > o.max_cost_value)) {
-      rollout_cost<M, INTEG, 2>(P, Bf, b, s.alpha, al, Jw, &grad, RT);
-      copied = true;
-    }
+    replay_cost<M, INTEG>(P, Bf, b, s.alpha, al, bookkeeping, o.max_cost_value, J, grad, copied, RT);
   } else if (bookkeeping && !(J > o.max_cost_value)) {
     const double* g = Bf.gk + (size_t)b * N;
     double gsum = 0.0;
@@ -2802,7 +2901,7 @@ __global__ void __launch_bounds__(64) k_ls_book(const DevProblem* __restrict__ P
   if (bookkeeping) {
     if (s.flags & TOG_TRAJ_COST_INCREASED) {
       s.active = 0;  // reference: error("Cost increased during Forward Pass")
-    } else if (inner_bookkeeping(P, s, J, grad, mode)) {
+    } else if (inner_bookkeeping(P, Bf, b, s, J, grad, mode)) {
       // the AL outer update runs wave-parallel over the knots in k_al_outer
       Bf.ls_done[atomicAdd(Bf.ls_count + 1, 1)] = (int)b;
     }
@@ -2893,7 +2992,10 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
       if (hk[k]) Jc += ak[k];
     Jnext = J + Jc;
   }
-  al_outer_finish(P, s, mumax, cmax, Jnext, mode);
+  // the AL record's cost(prob) is the inner solve's last J: the same objective at the same X, U and
+  // multipliers, summed in the same order (rollout_cost / traj_cost)
+  const double gnext = (Bf.hist_in && !conv && s.al_iter < o.al_iterations) ? traj_gradient<M>(P, Bf, b, true) : 0.0;
+  al_outer_finish(P, Bf, b, s, mumax, cmax, s.J, Jnext, gnext, mode);
   Bf.st[b] = s;
 }
 
@@ -3368,7 +3470,7 @@ struct ModelLaunch {
   static void forward_cand(const DevProblem* P, const DevBuffers& Bf, long long B, int mode, int bk, const double* Jp,
                            double* Jo, hipStream_t st) {
     const int F = Bf.ls_first;
-    (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_MAX_ROUNDS, st);
+    (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_COUNT_SLOTS, st);
     if (F >= Bf.nc) {
       spec<INTEG>(P, Bf, B, mode, 0, Bf.nc, nullptr, nullptr, st);
       hipLaunchKernelGGL((k_ls_decide<M>), dim3(grid(B, 256)), dim3(256), 0, st, P, Bf, Bf.nc, bk, Jp, nullptr,
@@ -3389,6 +3491,9 @@ struct ModelLaunch {
     }
     const long long tot = B * (long long)Bf.nknots * cand_q<M>();
     hipLaunchKernelGGL((k_ls_apply<M>), dim3(grid(tot, 256)), dim3(256), 0, st, P, Bf, bk);
+    hipLaunchKernelGGL((k_ls_fallback<M>), dim3((unsigned)B), dim3(64),
+                       (unsigned)(Bf.nknots * (2 * sizeof(double) + sizeof(int))), st, P, Bf,
+                       (int)(mode == TOG_MODE_AL), Bf.ls_fb, Bf.ls_count + 2);
     hipLaunchKernelGGL((k_ls_book<M, INTEG>), dim3(grid(B, 64)), dim3(64), (unsigned)Bf.rows_lds, st, P, Bf, mode,
                        bk, Jp, Jo);
     if (bk && mode == TOG_MODE_AL) {
@@ -3415,7 +3520,7 @@ struct ModelLaunch {
     // (k_ls_compact lists them, so the second round's waves are dense). Narrower first rounds were
     // measured slower: 8 lanes sharing one trajectory's K/X/U per load is what keeps the rollouts
     // coalesced, and the Kuka's heavy lanes need the width to fill the SIMDs.
-    (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_MAX_ROUNDS, st);
+    (void)hipMemsetAsync(Bf.ls_count, 0, sizeof(int) * LS_COUNT_SLOTS, st);
     if (sp && LS_MAX_ROUNDS == 2 && Bf.nc > LS_FIRST) {
       // the decided trajectories' commit (phase 1) overlaps the second round on a second stream;
       // both kernels are latency bound at low occupancy

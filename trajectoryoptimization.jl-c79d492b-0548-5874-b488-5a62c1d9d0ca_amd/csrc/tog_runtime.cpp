@@ -98,6 +98,10 @@ struct tog_handle {
   // projected Newton workspace, allocated by the first tog_solve_pn (tog_pn.hpp)
   PNBuffers pn = {};
   bool pn_alloc = false;
+  // solver_pn.stats histories of the last tog_solve_pn: (2, n_steps, B) [cost, c_max], records per trajectory
+  std::vector<double> pn_hist;
+  std::vector<int32_t> pn_hist_rec;
+  int pn_hist_steps = -1;
 };
 
 static hipEvent_t next_event(tog_handle* h) {
@@ -212,17 +216,20 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
       switch (con.type) {
         case TOG_CON_BOUND: {
           // data = [x_max(n), x_min(n), u_max(m), u_min(m)]; order [x_max; u_max; x_min; u_min].
-          // count 0: trim = true (infinite bounds dropped); 1: trim = false (every row kept)
+          // count 0: trim = true (infinite bounds dropped); 1: trim = false (every row kept). The slack
+          // controls of an infeasible-start problem are never bounded: its BoundConstraint keeps the model's
+          // m (update_constraint_set_jacobians, constraint_sets.jl:135-150)
           const bool keep = (con.count == 1);
+          const int mb = m - slack;
           for (int i = 0; i < n; i++)
             if (keep || isfinite(D[i])) rows.push_back({ROW_XMAX, i, D[i], 0, 0, 0});
           if (!term)
-            for (int i = 0; i < m; i++)
+            for (int i = 0; i < mb; i++)
               if (keep || isfinite(D[2 * n + i])) rows.push_back({ROW_UMAX, i, D[2 * n + i], 0, 0, 0});
           for (int i = 0; i < n; i++)
             if (keep || isfinite(D[n + i])) rows.push_back({ROW_XMIN, i, D[n + i], 0, 0, 0});
           if (!term)
-            for (int i = 0; i < m; i++)
+            for (int i = 0; i < mb; i++)
               if (keep || isfinite(D[2 * n + m + i])) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
           break;
         }
@@ -564,6 +571,9 @@ static size_t per_traj(const tog_handle* h, int field) {
     case TOG_FIELD_X0: return n;
     case TOG_FIELD_STATS: return TOG_NSTATS;
     case TOG_FIELD_Q: return N * (size_t)h->nq;
+    case TOG_FIELD_HIST_INNER: return 3 * (size_t)h->buf.hcap;
+    case TOG_FIELD_HIST_OUTER: return 4 * (size_t)h->buf.ocap;
+    case TOG_FIELD_HIST_COUNT: return 2;
   }
   return 0;
 }
@@ -747,7 +757,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
       (rc = dalloc(h, &h->d_iscratch, B)) || (rc = dalloc(h, &h->d_stats, 4)) ||
       (rc = dalloc(h, &h->d_act_list, B)) || (rc = dalloc(h, &h->d_act_count, 1)) ||
       (rc = dalloc(h, &b.lsJ, B * 64)) || (rc = dalloc(h, &b.lsok, B * 64)) ||
-      (rc = dalloc(h, &b.ls_list, 2 * B)) || (rc = dalloc(h, &b.ls_count, LS_MAX_ROUNDS)))
+      (rc = dalloc(h, &b.ls_list, 2 * B)) || (rc = dalloc(h, &b.ls_count, LS_COUNT_SLOTS)))
     return rc;
   b.Sdbg = nullptr;
   b.sdbg = nullptr;
@@ -756,6 +766,10 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
                               //  compacted launch's slot count)
   b.act_list = nullptr;  // set only in the launch view of a compacted tail step
   b.act_count = nullptr;
+  b.hist_in = nullptr;  // tog_history_enable
+  b.hist_out = nullptr;
+  b.hcap = 0;
+  b.ocap = 0;
   if (h->bwd_team) {  // expansion records of the team backward pass (k_expand_team)
     const size_t ne = (size_t)n + m + (size_t)m * m + (size_t)n * n;
     if ((rc = dalloc(h, &b.E, B * N * ne))) return rc;
@@ -775,6 +789,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   b.ls_pend_ok = getenv("TOG_LS_NOPEND") ? 0 : 1;
   b.ls_first = LS_FIRST;
   b.cand = nullptr;
+  b.ls_fb = nullptr;
   // candidate-copy line search when every trial fits the speculative window (TOG_LS=replay: the
   // replaying k_ls_commit path, for A/B checks)
   {
@@ -782,7 +797,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     const bool replay = ev && strcmp(ev, "replay") == 0;
     if (!replay && opts->iterations_linesearch + 1 <= 64) {
       if ((rc = dalloc(h, &b.cand, B * (size_t)b.ncp * N * 4 * ((n + m + 3) / 4))) || (rc = dalloc(h, &b.ls_win, B)) ||
-          (rc = dalloc(h, &b.ls_Jw, B)) || (rc = dalloc(h, &b.gk, B * N)))
+          (rc = dalloc(h, &b.ls_Jw, B)) || (rc = dalloc(h, &b.gk, B * N)) || (rc = dalloc(h, &b.ls_fb, B)))
         return rc;
     }
   }
@@ -911,6 +926,35 @@ int32_t tog_dims(tog_handle* h, int64_t* o) {
   return TOG_OK;
 }
 
+int32_t tog_history_enable(tog_handle* h, int32_t capacity) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (capacity < 0) return fail(TOG_ERR_ARG, "capacity must be >= 0");
+  const int ocap = h->opts.al_iterations + 1 > 1 ? h->opts.al_iterations + 1 : 1;
+  if (is_multi(h)) {
+    int32_t rc = each_part(h, [&](tog_handle* p, size_t) { return tog_history_enable(p, capacity); });
+    h->buf.hcap = capacity;
+    h->buf.ocap = capacity > 0 ? ocap : 0;
+    return rc;
+  }
+  HIPCHECK(hipSetDevice(h->device));
+  HIPCHECK(hipStreamSynchronize(h->stream));
+  DevBuffers& b = h->buf;
+  if (capacity == 0) {  // off (the buffers stay allocated until the handle is destroyed)
+    b.hist_in = nullptr;
+    b.hist_out = nullptr;
+    b.hcap = b.ocap = 0;
+    return TOG_OK;
+  }
+  if (capacity != b.hcap || !b.hist_in) {
+    int rc;
+    if ((rc = dalloc(h, &b.hist_in, (size_t)h->B * 3 * capacity)) || (rc = dalloc(h, &b.hist_out, (size_t)h->B * 4 * ocap)))
+      return rc;
+    b.hcap = capacity;
+    b.ocap = ocap;
+  }
+  return TOG_OK;
+}
+
 static size_t field_count(tog_handle* h, int field, double** dptr) {
   const size_t B = h->B, n = h->n, m = h->m, N = h->N, P1 = h->pmax > 0 ? h->pmax : 1;
   DevBuffers& b = h->buf;
@@ -928,6 +972,8 @@ static size_t field_count(tog_handle* h, int field, double** dptr) {
     case TOG_FIELD_S: *dptr = b.Sdbg; return B * N * n * n;
     case TOG_FIELD_SX: *dptr = b.sdbg; return B * N * n;
     case TOG_FIELD_Q: *dptr = b.Qscr; return B * N * (size_t)h->nq;
+    case TOG_FIELD_HIST_INNER: *dptr = b.hist_in; return B * 3 * (size_t)b.hcap;
+    case TOG_FIELD_HIST_OUTER: *dptr = b.hist_out; return B * 4 * (size_t)b.ocap;
   }
   *dptr = nullptr;
   return 0;
@@ -977,6 +1023,18 @@ int32_t tog_get(tog_handle* h, int32_t field, double* out) {
     HIPCHECK(hipStreamSynchronize(h->stream));
     return TOG_OK;
   }
+  if (field == TOG_FIELD_HIST_COUNT) {
+    std::vector<TrajState> st;
+    int rc = get_states(h, st);
+    if (rc) return rc;
+    for (size_t i = 0; i < B; i++) {
+      out[2 * i] = st[i].hn_in;
+      out[2 * i + 1] = st[i].hn_out;
+    }
+    return TOG_OK;
+  }
+  if ((field == TOG_FIELD_HIST_INNER || field == TOG_FIELD_HIST_OUTER) && !b.hist_in)
+    return fail(TOG_ERR_ARG, "iteration histories are off (tog_history_enable)");
   if (field == TOG_FIELD_STATS || field == TOG_FIELD_DV || field == TOG_FIELD_RHO) {
     std::vector<TrajState> st;
     int rc = get_states(h, st);
@@ -1041,7 +1099,8 @@ int32_t tog_set(tog_handle* h, int32_t field, const double* in) {
     }
     return put_states(h, st);
   }
-  if (field == TOG_FIELD_A || field == TOG_FIELD_B || field == TOG_FIELD_STATS)
+  if (field == TOG_FIELD_A || field == TOG_FIELD_B || field == TOG_FIELD_STATS || field == TOG_FIELD_HIST_INNER ||
+      field == TOG_FIELD_HIST_OUTER || field == TOG_FIELD_HIST_COUNT)
     return fail(TOG_ERR_ARG, "field is read-only");
   double* p = nullptr;
   size_t count = field_count(h, field, &p);
@@ -1464,6 +1523,11 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
   W.atol = opts->active_set_tolerance;
   W.eps = opts->feasibility_tolerance;
   HIPCHECK(hipMemsetAsync(W.st, 0, sizeof(PNState) * B, h->stream));
+  // solver_pn.stats[:cost] / [:c_max] per newton step (tog_get_pn_history): read after each step's
+  // record_iteration! (k_pn_finish); a trajectory records in a step iff its step counter moved
+  h->pn_hist.assign((size_t)2 * std::max(opts->n_steps, 0) * B, NAN);
+  h->pn_hist_steps = opts->n_steps;
+  std::vector<PNState> stp(B);
   for (int step = 0; step < opts->n_steps; step++) {
     h->ops->pn(h->dP, h->buf, W, B, h->integ, 0, h->stream);
     for (int it = 0; it < 10; it++) {
@@ -1472,7 +1536,16 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     }
     h->ops->pn(h->dP, h->buf, W, B, h->integ, 2, h->stream);
     HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(stp.data(), W.st, sizeof(PNState) * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    for (long long b = 0; b < B; b++)
+      if (stp[b].steps == step + 1) {
+        h->pn_hist[2 * ((size_t)b * opts->n_steps + step)] = stp[b].J;
+        h->pn_hist[2 * ((size_t)b * opts->n_steps + step) + 1] = stp[b].c_max;
+      }
   }
+  h->pn_hist_rec.assign(B, 0);
+  for (long long b = 0; b < B && opts->n_steps > 0; b++) h->pn_hist_rec[b] = stp[b].steps;
   if (out) {
     std::vector<PNState> st(B);
     HIPCHECK(hipMemcpyAsync(st.data(), W.st, sizeof(PNState) * B, hipMemcpyDeviceToHost, h->stream));
@@ -1488,6 +1561,21 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
       o[TOG_PN_STEPS] = st[b].steps;
     }
   }
+  return TOG_OK;
+}
+
+int32_t tog_get_pn_history(tog_handle* h, double* out, int32_t* steps_out) {
+  if (!h || !out) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    const size_t w = 2 * (size_t)std::max(h->parts[0]->pn_hist_steps, 0);
+    return each_part(h, [&](tog_handle* p, size_t o) {
+      return tog_get_pn_history(p, out + o * w, steps_out ? steps_out + o : nullptr);
+    });
+  }
+  if (h->pn_hist_steps < 0) return fail(TOG_ERR_ARG, "no projected Newton solve on this handle");
+  std::copy(h->pn_hist.begin(), h->pn_hist.end(), out);
+  if (steps_out)
+    for (long long b = 0; b < h->B; b++) steps_out[b] = h->pn_hist_rec.empty() ? 0 : h->pn_hist_rec[b];
   return TOG_OK;
 }
 

@@ -15,6 +15,7 @@ class BatchHandle:
         """``devices``: a list of HIP device ids for one handle over several GPUs
         (tog_create_multi: the batch is split into contiguous slices, one per entry)."""
         self.lib = abi.load_library()
+        self.hcap = 0
         self.desc_builder = prob.build_desc()
         self.opts = opts
         h = C.c_void_p()
@@ -33,6 +34,18 @@ class BatchHandle:
         if stream is not None:
             abi.check(self.lib, self.lib.tog_set_stream(self.h, C.c_void_p(int(stream))))
         self.upload_state(prob)
+
+    @classmethod
+    def adopt(cls, lib, handle: int, opts: abi.tog_options):
+        """Wrap a ``tog_handle`` created inside libtog (tog_solve_altro_ex's keep_handle): this object
+        owns it from now on and destroys it."""
+        self = cls.__new__(cls)
+        self.lib, self.opts, self.desc_builder, self.hcap = lib, opts, None, 0
+        self.h = C.c_void_p(handle)
+        dims = (C.c_int64 * 6)()
+        abi.check(self.lib, self.lib.tog_dims(self.h, dims))
+        self.n, self.m, self.N, self.B, self.pmax, _ = [int(v) for v in dims]
+        return self
 
     def __del__(self):
         try:
@@ -187,6 +200,34 @@ class BatchHandle:
     def stats_dict(self):
         return stats_dict(self.get(abi.FIELD_STATS))
 
+    # ------------------------------------------------------------------ iteration histories
+    def enable_history(self, capacity: int):
+        """tog_history_enable: keep `capacity` inner records per trajectory (0: off)."""
+        abi.check(self.lib, self.lib.tog_history_enable(self.h, int(capacity)))
+        self.hcap = int(capacity)
+
+    def history(self):
+        """(inner (B, cap, 3) [cost, dJ, gradient], outer (B, al_iterations + 1, 4) [iterations_inner, cost,
+        c_max, penalty_max], counts (B, 2) records written [inner, outer]) of the solve since
+        tog_solve_init; None when recording is off."""
+        if not self.hcap:
+            return None
+        inner = np.empty((self.B, self.hcap, 3))
+        abi.check(self.lib, self.lib.tog_get(self.h, abi.FIELD_HIST_INNER, abi.as_dp(inner)))
+        ocap = self.opts.al_iterations + 1
+        outer = np.empty((self.B, ocap, 4))
+        abi.check(self.lib, self.lib.tog_get(self.h, abi.FIELD_HIST_OUTER, abi.as_dp(outer)))
+        cnt = np.empty((self.B, 2))
+        abi.check(self.lib, self.lib.tog_get(self.h, abi.FIELD_HIST_COUNT, abi.as_dp(cnt)))
+        return inner, outer, cnt.astype(np.int64)
+
+    def pn_history(self, n_steps: int):
+        """solver_pn.stats [:cost, :c_max] per newton step (B, n_steps, 2) and records per trajectory (B,)."""
+        out = np.empty((self.B, max(int(n_steps), 0), 2))
+        rec = np.zeros(self.B, dtype=np.int32)
+        abi.check(self.lib, self.lib.tog_get_pn_history(self.h, abi.as_dp(out), rec.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out, rec
+
 
 def stats_dict(S):
     """solver.stats from the (B, TOG_NSTATS) statistics rows (TOG_FIELD_STATS)."""
@@ -200,3 +241,38 @@ def stats_dict(S):
         "penalty_max": S[:, abi.STAT_PENALTY_MAX],
         "flags": S[:, abi.STAT_FLAGS].astype(np.int64),
     }
+
+
+def ilqr_traj_stats(inner, n_rec, zero_counter=None):
+    """One inner solve's ``solver.stats`` as iLQRSolver's record_iteration! builds it (ilqr_methods.jl:77-89):
+    :iterations, and the :cost, :dJ, :gradient vectors; `inner` holds its records."""
+    d = {"iterations": int(n_rec), "cost": inner[:n_rec, 0].copy(), "dJ": inner[:n_rec, 1].copy(),
+         "gradient": inner[:n_rec, 2].copy()}
+    if zero_counter is None:  # dJ == 0 counts consecutive records (the counter's value after the last one)
+        z = 0
+        for v in d["dJ"]:
+            z = z + 1 if v == 0.0 else 0
+        zero_counter = z
+    d["dJ_zero_counter"] = int(zero_counter)
+    return d
+
+
+def al_traj_stats(inner, n_in, outer, n_out):
+    """AugmentedLagrangianSolver.stats of one trajectory (augmented_lagrangian_methods.jl:79-97):
+    :iterations, :iterations_total, the :iterations_inner, :cost, :c_max, :penalty_max vectors, and
+    stats_uncon (the inner solver's stats at every outer record; the first is the reset solver's). The
+    inner records are split by :iterations_inner; records past the history's capacity are absent, so a
+    truncated history leaves the later inner solves short."""
+    it_in = outer[:n_out, 0].astype(np.int64)
+    d = {"iterations": int(n_out), "iterations_total": int(it_in.sum()), "iterations_inner": it_in,
+         "cost": outer[:n_out, 1].copy(), "c_max": outer[:n_out, 2].copy(), "penalty_max": outer[:n_out, 3].copy()}
+    inner = inner[:min(int(n_in), inner.shape[0])]
+    uncon, o = [], 0
+    for k in it_in:
+        sl = inner[o:o + int(k)]
+        uncon.append(ilqr_traj_stats(sl, len(sl)))
+        o += int(k)
+    d["stats_uncon"] = uncon
+    d["truncated"] = bool(n_in > inner.shape[0])
+    return d
+

@@ -24,7 +24,7 @@ import numpy as np
 from . import abi
 import ctypes as C
 
-from .device import BatchHandle, stats_dict
+from .device import BatchHandle, al_traj_stats, ilqr_traj_stats, stats_dict
 
 
 class PosDefException(np.linalg.LinAlgError):
@@ -261,6 +261,7 @@ class AbstractSolver:
     def __init__(self, prob, opts, device: int = 0, stream=None, devices=None):
         self.opts = opts
         self.stats: dict = {}
+        self.history = None
         self.handle = BatchHandle(prob, to_tog_options(opts), device=device, stream=stream, devices=devices)
         self.n, self.m, self.N = prob.model.n, prob.model.m, prob.N
 
@@ -269,6 +270,24 @@ class AbstractSolver:
 
     def reset_b(self):
         self.stats = {}
+        self.history = None
+
+    def traj_stats(self, b: int) -> dict:
+        """Trajectory b's ``solver.stats`` as the reference builds it, with its per-iteration vectors:
+        iLQR :iterations, :cost, :dJ, :gradient, :dJ_zero_counter (ilqr_methods.jl:77-89); AL
+        :iterations, :iterations_total, :iterations_inner, :cost, :c_max, :penalty_max and stats_uncon
+        (augmented_lagrangian_methods.jl:79-97). ``solver.stats`` itself is the batch summary (final
+        values, one entry per trajectory). Needs the histories the solve recorded (solve_b's `history`)."""
+        if self.history is None:
+            raise RuntimeError("no iteration histories: solve with history enabled (solve_b(..., history=True))")
+        inner, outer, cnt = self.history
+        n_in, n_out = int(cnt[b, 0]), int(cnt[b, 1])
+        if self.mode == abi.MODE_AL:
+            return al_traj_stats(inner[b], n_in, outer[b], n_out)
+        zc = self.stats["dJ_zero_counter"][b] if "dJ_zero_counter" in self.stats else None
+        d = ilqr_traj_stats(inner[b], min(n_in, inner.shape[1]), zc)
+        d["truncated"] = bool(n_in > inner.shape[1])
+        return d
 
     # ---- device views (copies to host), reference field names
     @property
@@ -324,8 +343,22 @@ class AugmentedLagrangianSolver(AbstractSolver):
 
 
 class ALTROSolver(AugmentedLagrangianSolver):
-    """``ALTROSolver`` (altro_solver.jl:70-94): the AL phase, and with ``projected_newton`` the
-    projected Newton phase on the same device buffers (``solver_pn``)."""
+    """``ALTROSolver`` (altro_solver.jl:70-94). After ``solve_b(prob, ALTROSolverOptions)``: ``stats`` holds
+    the reference's :time, :time_al, :time_pn (seconds, altro_methods.jl:44-48) next to the AL phase's
+    batch summary; ``solver_al`` is the AL phase's solver (its device buffers: K, d, λ, μ, ... of the
+    infeasible / minimum-time problem when the start was one; ``solver_al.traj_stats(b)`` its per-iteration
+    statistics); ``solver_pn`` the projected Newton phase (``solver_pn.traj_stats(b)``: :iterations,
+    :cost, :c_max per newton step). The solver's own device views are solver_al's."""
+
+
+def history_capacity(opts, B: int, budget_bytes: float = 256e6) -> int:
+    """Inner records per trajectory solve_b keeps by default: a whole solve's worth (an AL solve records at
+    most al_iterations x (iterations + 1)), capped so that the batch's histories stay within `budget_bytes`
+    of HBM (24 B a record; a longer history is counted, not stored)."""
+    o = to_tog_options(opts)
+    full = (o.iterations + 1) * (o.al_iterations if isinstance(opts, (AugmentedLagrangianSolverOptions,
+                                                                       ALTROSolverOptions)) else 1) + 1
+    return int(max(1, min(full, budget_bytes // (24 * max(1, B)))))
 
 
 class ProjectedNewtonSolver(AbstractSolver):
@@ -351,6 +384,17 @@ def _pn_stats(out, flags):
             "refinements": out[:, abi.PN_REFINEMENTS].astype(int), "flags": flags}
 
 
+class _PNStatsView(ProjectedNewtonSolver):
+    """ALTROSolver.solver_pn after an ALTRO solve: the projected Newton statistics on the AL phase's buffers."""
+
+    def traj_stats(self, b: int) -> dict:
+        """solver_pn.stats of trajectory b (projected_newton.jl:23-29): :iterations and the :cost, :c_max
+        vectors, one entry per newton step."""
+        hist, rec = self.pn_history
+        k = int(rec[b])
+        return {"iterations": k, "cost": hist[b, :k, 0].copy(), "c_max": hist[b, :k, 1].copy()}
+
+
 def _solve_pn(prob, solver: ProjectedNewtonSolver):
     """``solve!(prob, ::ProjectedNewtonSolver)`` (projected_newton.jl:6-20). The reference raises
     (a MethodError in ``_projection_linesearch!``, projected_newton.jl:273-277) when a line search's
@@ -361,6 +405,7 @@ def _solve_pn(prob, solver: ProjectedNewtonSolver):
     h.download_state(prob)
     flags = h.status()
     solver.stats = _pn_stats(out, flags)
+    solver.pn_history = h.pn_history(solver.opts.n_steps)
     if np.any(flags & abi.TRAJ_PN_ERROR):
         raise RuntimeError("projected Newton: line search did not reduce the violation "
                            "(the reference's _projection_linesearch! raises here)")
@@ -427,21 +472,25 @@ def to_tog_altro_options(opts: ALTROSolverOptions) -> abi.tog_altro_options:
     return a
 
 
-def _solve_altro(prob, opts: ALTROSolverOptions, device: int):
-    """``solve!(prob, ::ALTROSolverOptions)`` (altro_methods.jl:2-124) through ``tog_solve_altro``: the C
+def _solve_altro(prob, opts: ALTROSolverOptions, device: int, max_steps=None, history=None):
+    """``solve!(prob, ::ALTROSolverOptions)`` (altro_methods.jl:2-124) through ``tog_solve_altro_ex``: the C
     ABI runs altro_problem (an initial state trajectory -> infeasible_problem, infeasible.jl:2-33; tf = 0 ->
     minimum_time_problem, minimum_time.jl:2-34), the AL solve, projected Newton, process_results! and the
     feasible resolve (csrc/tog_altro.cpp), so the Julia binding and C callers reach the same flow.
 
-    The returned solver carries ``stats`` (the AL phase: the infeasible / minimum-time problem's solve),
-    ``stats_feasible`` (the resolve of an infeasible start), ``stats_pn`` (projected Newton); a
-    minimum-time solve's time steps go to ``prob.h`` (the reference stores [u; u; h] in prob.U) and
-    ``total_time(prob)`` reads them."""
+    Returns the ``ALTROSolver`` as the reference does (altro_methods.jl:52): ``stats`` (:time, :time_al,
+    :time_pn and the AL phase's batch summary), ``solver_al`` (the AL phase's solver on its live device
+    buffers, with per-iteration ``traj_stats``), ``solver_pn`` (projected Newton), plus ``stats_feasible``
+    (the resolve of an infeasible start, which the reference does not keep). A minimum-time solve's time
+    steps go to ``prob.h`` (the reference stores [u; u; h] in prob.U) and ``total_time(prob)`` reads them."""
     lib = abi.load_library()
     infeasible = _altro_infeasible(prob)
     desc = prob.build_desc(tf_min=prob.tf == 0.0)
     a = to_tog_altro_options(opts)
+    if max_steps is not None:
+        a.max_steps = int(max_steps)
     B, N, n, m = prob.B, prob.N, prob.model.n, prob.model.m
+    hcap = 0 if history is False else (int(history) if history not in (None, True) else history_capacity(opts, B))
     x0 = np.ascontiguousarray(prob.x0, dtype=np.float64)
     X = np.ascontiguousarray(prob._X, dtype=np.float64) if infeasible else np.full((B, N, n), np.nan)
     U = np.ascontiguousarray(prob._U, dtype=np.float64)
@@ -449,14 +498,43 @@ def _solve_altro(prob, opts: ALTROSolverOptions, device: int):
     St = np.zeros((B, abi.NSTATS))
     St_res = np.zeros((B, abi.NSTATS))
     pn = np.zeros((B, abi.PN_NSTATS))
-    abi.check(lib, lib.tog_solve_altro(C.byref(desc.desc), C.byref(a), int(device), abi.as_dp(x0), abi.as_dp(X),
-                                       abi.as_dp(U), abi.as_dp(h), abi.as_dp(St), abi.as_dp(St_res), abi.as_dp(pn)))
+    ocap = a.opts_al.al_iterations + 1
+    Hin = np.zeros((B, max(hcap, 1), 3))
+    Hout = np.zeros((B, ocap, 4))
+    Hcnt = np.zeros((B, 2))
+    npn = max(int(a.opts_pn.n_steps), 0) if opts.projected_newton else 0
+    Hpn = np.full((B, max(npn, 1), 2), np.nan)
+    r = abi.tog_altro_result()
+    r.inner_capacity = hcap
+    r.keep_handle = 1
+    r.stats, r.stats_resolve, r.stats_pn = abi.as_dp(St), abi.as_dp(St_res), abi.as_dp(pn)
+    r.hist_inner, r.hist_outer, r.hist_count = abi.as_dp(Hin), abi.as_dp(Hout), abi.as_dp(Hcnt)
+    r.hist_pn = abi.as_dp(Hpn) if npn else C.cast(None, C.POINTER(C.c_double))
+    abi.check(lib, lib.tog_solve_altro_ex(C.byref(desc.desc), C.byref(a), int(device), abi.as_dp(x0), abi.as_dp(X),
+                                          abi.as_dp(U), abi.as_dp(h), C.byref(r)))
     prob._X[...] = X
     prob._U[...] = U
-    solver = ALTROSolver.__new__(ALTROSolver)
-    solver.opts, solver.handle = opts, None
-    solver.n, solver.m, solver.N = n, m, N
-    solver.stats = stats_dict(St)
+    handle = BatchHandle.adopt(lib, r.handle, a.opts_al)
+    handle.hcap = hcap
+
+    def view(cls, o):  # a solver object on the AL phase's handle
+        sv = cls.__new__(cls)
+        sv.opts, sv.handle, sv.history = o, handle, None
+        sv.n, sv.m, sv.N = handle.n, handle.m, handle.N
+        return sv
+
+    hist = (Hin[:, :hcap], Hout, Hcnt.astype(np.int64)) if hcap else None
+    solver = view(ALTROSolver, opts)
+    al = view(AugmentedLagrangianSolver, opts.opts_al)
+    al.stats, al.history = stats_dict(St), hist
+    solver.solver_al = al
+    solver.stats = dict(stats_dict(St))
+    solver.stats.update({"time": r.time, "time_al": r.time_al, "time_pn": r.time_pn})
+    solver.history = hist
+    pnv = view(_PNStatsView, opts.opts_pn)
+    pnv.stats = _pn_stats(pn, solver.stats["flags"]) if opts.projected_newton else {}
+    pnv.pn_history = (Hpn[:, :npn], pn[:, abi.PN_STEPS].astype(np.int32)) if npn else (np.zeros((B, 0, 2)), np.zeros(B, np.int32))
+    solver.solver_pn = pnv
     if prob.tf == 0.0:
         prob.h = h
     if infeasible and opts.resolve_feasible_problem:
@@ -464,16 +542,19 @@ def _solve_altro(prob, opts: ALTROSolverOptions, device: int):
     flags = solver.stats["flags"] | (solver.stats_feasible["flags"] if hasattr(solver, "stats_feasible") else 0)
     _raise_trajectory_errors(flags)
     if opts.projected_newton:
-        solver.stats_pn = _pn_stats(pn, solver.stats["flags"])
+        solver.stats_pn = pnv.stats
         if np.any(solver.stats["flags"] & abi.TRAJ_PN_ERROR):
             raise RuntimeError("projected Newton: line search did not reduce the violation "
                                "(the reference's _projection_linesearch! raises here)")
     return solver
 
 
-def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int = 0):
+def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int = 0, history=None):
     """``solve!(prob, opts)`` / ``solve!(prob, solver)`` (src/solvers.jl:91-94). Mutates
-    ``prob.X``/``prob.U`` in place and returns the solver."""
+    ``prob.X``/``prob.U`` in place and returns the solver.
+
+    ``history``: record the per-iteration statistics (``solver.traj_stats(b)``): None = on with
+    ``history_capacity`` records per trajectory, False = off, an int = that capacity."""
     if isinstance(solver_or_opts, ProjectedNewtonSolver):
         solver_or_opts.handle.upload_state(prob)
         return _solve_pn(prob, solver_or_opts)
@@ -489,7 +570,7 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
             if prob.tf == 0.0 and _altro_infeasible(prob):
                 raise NotImplementedError("infeasible start + minimum time is not built")
             _altro_pn_tolerances(opts)  # (mutates opts.opts_al, as the reference does)
-            return _solve_altro(prob, opts, device)
+            return _solve_altro(prob, opts, device, max_steps=max_steps, history=history)
         if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
             # solve!(prob, ::AugmentedLagrangianSolverOptions) on an unconstrained problem
             # falls back to the unconstrained solver (augmented_lagrangian_methods.jl:33-36)
@@ -497,9 +578,14 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
         solver = AbstractSolverFor(prob, opts, device=device)
     mode = solver.mode
     h = solver.handle
+    hcap = 0 if history is False else (int(history) if history not in (None, True) else
+                                       history_capacity(solver.opts, h.B))
+    if hcap != h.hcap:
+        h.enable_history(hcap)
     h.solve(mode, max_steps=max_steps if max_steps is not None else _default_max_steps(solver))
     h.download_state(prob)
     solver.stats = h.stats_dict()
+    solver.history = h.history()
     _raise_trajectory_errors(solver.stats["flags"])
     return solver
 
