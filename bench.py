@@ -379,26 +379,56 @@ def main():
 def time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_rank, pkg, chunk=4, max_steps=10000):
     """The whole solve, SURVEY.md §8(d): from tog_solve_init (initial rollout + cost) until no
     trajectory of the job is active, including the batch-level stopping check every `chunk` steps
-    (a host readback of [n_active, Σ J, max c_max]; over RCCL for several ranks). Same trajectories
-    as the window leg (re-initialised from the same U0). Returns Σ steps ÷ max-over-ranks wall time."""
+    (the job-wide [n_active, Σ J, max c_max]; over RCCL for several ranks). Same trajectories as the
+    window leg (re-initialised from the same U0). Returns Σ steps ÷ max-over-ranks wall time.
+
+    The check is pipelined as tog_solve does it: the next chunk is enqueued before the host waits for
+    the previous chunk's statistics (tog_batch_stats_begin / _end; for RCCL a copy into pinned host
+    memory behind an event), so the device does not idle during the host round trip. The solve stops one
+    chunk after the check that saw no active trajectory (that chunk's kernels return at once)."""
+    torch = None
+    if dist is not None:
+        import torch
     h.upload_state(prob)
     if prob.model.slack:
         h.slack_controls()
     barrier_sync()
     t0 = time.perf_counter()
     h.solve_init(mode)
-    done = 0
     B_job = float(prob.B) * (dist.get_world_size() if dist is not None else 1)
     timeline = [(0.0, B_job)]  # (seconds since init, job-wide n_active) at every stopping check
-    while done < max_steps:
-        h.solve_step(chunk)
-        done += chunk
+
+    def begin():
+        h.batch_stats_begin()  # local check: also the handle's tail-mode hint
+        if dist is None:
+            return None
         red = allreduce_stats()
-        n_local = float(h.batch_stats()[0])  # host readback: also sets the handle's tail-mode hint
-        n_active = float(red[0].item()) if red is not None else n_local
+        host = torch.empty(3, dtype=torch.float64, pin_memory=True)
+        host.copy_(red, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
+
+    def end(tok):
+        loc = h.batch_stats_end()
+        if tok is None:
+            return float(loc[0])
+        tok[1].synchronize()
+        return float(tok[0][0].item())
+
+    done = chunk
+    h.solve_step(chunk)
+    tok = begin()
+    while True:
+        nxt = min(chunk, max_steps - done)
+        if nxt > 0:
+            h.solve_step(nxt)
+        done += nxt
+        n_active = end(tok)  # the chunk before `nxt`
         timeline.append((time.perf_counter() - t0, n_active))
-        if n_active == 0.0:
+        if n_active == 0.0 or nxt == 0:
             break
+        tok = begin()
     barrier_sync()
     wall = time.perf_counter() - t0
     # tail share: the fraction of the solve's wall time spent with fewer than 1 % of the job's
@@ -422,7 +452,8 @@ def time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_ra
                      "seconds": round(tail, 4)},
             "traj_iterations": {"min": int(it.min()), "mean": round(float(it.mean()), 2), "max": int(it.max())},
             "converged": conv, "batch": int(prob.B),
-            "note": "tog_solve_init .. last trajectory finished, stopping check every 4 steps included"}
+            "note": "tog_solve_init .. last trajectory finished; stopping check every 4 steps, pipelined "
+                    "(the next chunk is enqueued before the host reads the previous one's statistics)"}
 
 
 if __name__ == "__main__":

@@ -31,7 +31,7 @@ extern "C" {
 /* 3: tog_solve_altro / tog_altro_options, TOG_PROB_TF_MIN, TOG_NKERNELS = 4 (tog_profile_read fills 4
       entries), tog_solve's max_steps <= 0 = the tog_solve_budget default */
 /* 4: iteration histories (tog_history_enable, TOG_FIELD_HIST_*), tog_solve_altro_ex / tog_altro_result,
-      tog_altro_options.max_steps (was reserved), tog_get_pn_history */
+      tog_altro_options.max_steps (was reserved), tog_get_pn_history, tog_batch_stats_begin / _end */
 #define TOG_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status */
@@ -417,6 +417,12 @@ int32_t tog_solve_step(tog_handle* h, int32_t nsteps);
 int32_t tog_batch_stats(tog_handle* h, double* out3);
 /* batch stats into a device buffer of 3 doubles (stream-ordered, no host sync) */
 int32_t tog_batch_stats_device(tog_handle* h, void* dptr3);
+/* the stopping check without a device bubble: _begin enqueues the batch statistics and their copy into
+   a pinned host buffer on the handle's stream (no wait); _end waits for that copy only, so steps enqueued
+   in between keep the device busy while the host waits. One check may be outstanding per handle. Same
+   out3 as tog_batch_stats, which also updates the handle's tail-mode hint. */
+int32_t tog_batch_stats_begin(tog_handle* h);
+int32_t tog_batch_stats_end(tog_handle* h, double* out3);
 /* counter of step!s executed since tog_solve_init (device side, read blocking) */
 int32_t tog_total_steps(tog_handle* h, int64_t* out);
 /* full solves: run until no trajectory is active (or max_steps batch steps; max_steps <= 0: the

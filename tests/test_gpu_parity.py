@@ -270,3 +270,25 @@ def test_solve_pendulum_altro(tog, oracle, gpu, integ):
     gp = prob.copy()
     tog.solve_b(gp, opts)
     assert tog.max_violation(gp) < al.constraint_tolerance
+
+
+@pytest.mark.gpu
+def test_batch_stats_begin_end(tog, gpu):
+    """tog_batch_stats_begin / _end (the pipelined stopping check) return what the blocking
+    tog_batch_stats returns at the same point of the stream; one check may be outstanding."""
+    prob, opts = tog.Problems.config_quadrotor(B=16)
+    h = tog.AbstractSolverFor(prob, opts).handle
+    h.solve_init(tog.abi.MODE_AL)
+    h.solve_step(3)
+    h.batch_stats_begin()
+    with pytest.raises(RuntimeError):
+        h.batch_stats_begin()
+    a = h.batch_stats_end()
+    with pytest.raises(RuntimeError):
+        h.batch_stats_end()
+    b = h.batch_stats()
+    assert np.array_equal(a, b)
+    h.batch_stats_begin()
+    h.solve_step(2)  # enqueued behind the check: the check sees the state after 3 steps
+    c = h.batch_stats_end()
+    assert np.array_equal(c, a)

@@ -298,6 +298,8 @@ def load_library(path: os.PathLike | None = None):
     lib.tog_solve_altro_ex.argtypes = [C.POINTER(tog_problem_desc), C.POINTER(tog_altro_options), C.c_int32, _dp,
                                        _dp, _dp, _dp, C.POINTER(tog_altro_result)]
     lib.tog_history_enable.argtypes = [vp, C.c_int32]
+    lib.tog_batch_stats_begin.argtypes = [vp]
+    lib.tog_batch_stats_end.argtypes = [vp, _dp]
     lib.tog_get_pn_history.argtypes = [vp, _dp, _ip]
     lib.tog_model_load.argtypes = [C.c_char_p, C.POINTER(vp)]
     lib.tog_model_dims.argtypes = [vp, _ip, _ip]
@@ -316,7 +318,7 @@ def load_library(path: os.PathLike | None = None):
                  "tog_solve_ilqr", "tog_solve_al", "tog_solve_pn", "tog_model_load", "tog_model_dims",
                  "tog_model_free", "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device",
                  "tog_generic_cost_free", "tog_solve_altro", "tog_solve_altro_ex", "tog_history_enable",
-                 "tog_get_pn_history"):
+                 "tog_get_pn_history", "tog_batch_stats_begin", "tog_batch_stats_end"):
         getattr(lib, name).restype = C.c_int32
     if lib.tog_version() != TOG_ABI_VERSION:
         raise RuntimeError("libtog ABI version mismatch")
@@ -336,6 +338,7 @@ EXPORTED_SYMBOLS = (
     "tog_solve_al", "tog_default_pn_options", "tog_solve_pn", "tog_model_load", "tog_model_dims", "tog_model_free",
     "tog_generic_cost_load", "tog_generic_cost_dims", "tog_generic_cost_expand", "tog_generic_cost_expand_device", "tog_generic_cost_free",
     "tog_default_altro_options", "tog_solve_altro", "tog_solve_altro_ex", "tog_history_enable", "tog_get_pn_history",
+    "tog_batch_stats_begin", "tog_batch_stats_end",
 )
 KERNEL_JACOBIAN, KERNEL_BACKWARD, KERNEL_FORWARD, KERNEL_EXPANSION = 0, 1, 2, 3
 NKERNELS = 4

@@ -175,6 +175,16 @@ class BatchHandle:
         abi.check(self.lib, self.lib.tog_batch_stats(self.h, abi.as_dp(out)))
         return out
 
+    def batch_stats_begin(self):
+        """tog_batch_stats_begin: enqueue the stopping check (no host wait)."""
+        abi.check(self.lib, self.lib.tog_batch_stats_begin(self.h))
+
+    def batch_stats_end(self):
+        """tog_batch_stats_end: wait for the enqueued check only; [n_active, Σ J, max c_max]."""
+        out = np.empty(3)
+        abi.check(self.lib, self.lib.tog_batch_stats_end(self.h, abi.as_dp(out)))
+        return out
+
     def total_steps(self):
         v = C.c_int64()
         abi.check(self.lib, self.lib.tog_total_steps(self.h, C.byref(v)))
