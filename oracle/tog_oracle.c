@@ -1328,7 +1328,29 @@ typedef struct oc_solver {
   int hout_n, hout_cap;
   double* hpn; /* projected Newton record_iteration! (projected_newton.jl:23-29): [cost, c_max] per step */
   int hpn_n, hpn_cap;
+  /* a time-varying Objective (src/objective.jl:15-29): per stage knot [Q; R; H; q; r; c] (tog.h
+     stage_costs), or NULL (the stage cost Q, R, H, q, r, c at every stage knot) */
+  double* kc;
+  int kc_stride;
 } oc_solver;
+
+/* stage knot k's QuadraticCost (src/cost.jl:112-157): the shared one, or row k of the per-knot table */
+static inline const double* kQ(const oc_solver* s, int k) { return s->kc ? s->kc + (size_t)k * s->kc_stride : s->Q; }
+static inline const double* kR(const oc_solver* s, int k) {
+  return s->kc ? s->kc + (size_t)k * s->kc_stride + s->n * s->n : s->R;
+}
+static inline const double* kH(const oc_solver* s, int k) {
+  return s->kc ? s->kc + (size_t)k * s->kc_stride + s->n * s->n + s->m * s->m : s->H;
+}
+static inline const double* kq(const oc_solver* s, int k) {
+  return s->kc ? s->kc + (size_t)k * s->kc_stride + s->n * s->n + s->m * s->m + s->m * s->n : s->q;
+}
+static inline const double* kr(const oc_solver* s, int k) {
+  return s->kc ? s->kc + (size_t)k * s->kc_stride + s->n * s->n + s->m * s->m + s->m * s->n + s->n : s->r;
+}
+static inline double kc0(const oc_solver* s, int k) {
+  return s->kc ? s->kc[(size_t)k * s->kc_stride + s->n * s->n + s->m * s->m + s->m * s->n + s->n + s->m] : s->c;
+}
 
 static void hist_push(double** buf, int* n, int* cap, int w, const double* rec) {
   if (*n == *cap) {
@@ -1564,6 +1586,12 @@ static void desc_load(oc_solver* s, const tog_problem_desc* d) {
   s->r = malloc(sizeof(double) * m);
   memcpy(s->r, d->r, sizeof(double) * m);
   s->c = d->c;
+  s->kc_stride = n * n + m * m + m * n + n + m + 1;
+  s->kc = NULL;
+  if (d->stage_costs) {
+    s->kc = malloc(sizeof(double) * (size_t)s->kc_stride * (d->N - 1));
+    memcpy(s->kc, d->stage_costs, sizeof(double) * (size_t)s->kc_stride * (d->N - 1));
+  }
   s->Qf = malloc(sizeof(double) * n * n);
   memcpy(s->Qf, d->Qf, sizeof(double) * n * n);
   s->qf = malloc(sizeof(double) * n);
@@ -1636,7 +1664,7 @@ OC_EXPORT void oc_destroy(oc_solver* s) {
   free(s->x0); free(s->X); free(s->U); free(s->Xb); free(s->Ub); free(s->K); free(s->d); free(s->F);
   free(s->Sxx); free(s->Sx); free(s->Qx); free(s->Qu); free(s->Qxx); free(s->Quu); free(s->Qux);
   free(s->C); free(s->lam); free(s->mu); free(s->active); free(s->ineq); free(s->trace);
-  free(s->hin); free(s->hout); free(s->hpn);
+  free(s->hin); free(s->hout); free(s->hpn); free(s->kc);
   free(s);
 }
 
@@ -1655,28 +1683,29 @@ OC_EXPORT void oc_set_state(oc_solver* s, const double* x0, const double* U, con
 /* =====================================================================
  * Cost (src/cost.jl:171-181, src/objective.jl:40-48)
  * ===================================================================== */
-static double stage_cost(const oc_solver* s, const double* x, const double* u, double dt) {
+static double stage_cost(const oc_solver* s, int k, const double* x, const double* u, double dt) {
   int n = s->n, m = s->m;
+  const double *Q = kQ(s, k), *R = kR(s, k), *H = kH(s, k), *q = kq(s, k), *r = kr(s, k);
   /* 0.5*x'Q*x + 0.5*u'*R*u + q'x + r'u + c + u'*H*x, then *dt */
   double xQx = 0, uRu = 0, qx = 0, ru = 0, uHx = 0;
   for (int j = 0; j < n; j++) {
     double t = 0;
-    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], s->Q[IDX(i, j, n)], t);
+    for (int i = 0; i < n; i++) t = fma(0.5 * x[i], Q[IDX(i, j, n)], t);
     xQx = fma(t, x[j], xQx);
   }
   for (int j = 0; j < m; j++) {
     double t = 0;
-    for (int i = 0; i < m; i++) t = fma(0.5 * u[i], s->R[IDX(i, j, m)], t);
+    for (int i = 0; i < m; i++) t = fma(0.5 * u[i], R[IDX(i, j, m)], t);
     uRu = fma(t, u[j], uRu);
   }
-  for (int i = 0; i < n; i++) qx = fma(s->q[i], x[i], qx);
-  for (int i = 0; i < m; i++) ru = fma(s->r[i], u[i], ru);
+  for (int i = 0; i < n; i++) qx = fma(q[i], x[i], qx);
+  for (int i = 0; i < m; i++) ru = fma(r[i], u[i], ru);
   for (int j = 0; j < n; j++) {
     double t = 0;
-    for (int i = 0; i < m; i++) t = fma(u[i], s->H[IDX(i, j, m)], t);
+    for (int i = 0; i < m; i++) t = fma(u[i], H[IDX(i, j, m)], t);
     uHx = fma(t, x[j], uHx);
   }
-  return ((((xQx + uRu) + qx) + ru) + s->c + uHx) * dt;
+  return ((((xQx + uRu) + qx) + ru) + kc0(s, k) + uHx) * dt;
 }
 static double terminal_cost(const oc_solver* s, const double* x) {
   int n = s->n;
@@ -1697,9 +1726,9 @@ static double obj_cost(const oc_solver* s, const double* X, const double* U) {
     const double* u = U + (size_t)k * m;
     if (s->mt) { /* MinTimeCost (minimum_time.jl:148): stage_cost(cost, x, u, h) + R_min_time u[end]^2, h = get_dt */
       const double h = u[m - 1];
-      J += stage_cost(s, X + (size_t)k * n, u, h * h) + s->R_mt * (h * h);
+      J += stage_cost(s, k, X + (size_t)k * n, u, h * h) + s->R_mt * (h * h);
     } else {
-      J += stage_cost(s, X + (size_t)k * n, u, s->dt);
+      J += stage_cost(s, k, X + (size_t)k * n, u, s->dt);
     }
   }
   J += terminal_cost(s, X + (size_t)(N - 1) * n);
@@ -1890,29 +1919,30 @@ static void expansion_stage(oc_solver* s, int k) {
   double* Qx = s->Qx + (size_t)k * n;
   double* Qu = s->Qu + (size_t)k * m;
   double gx[16], gu[OM]; /* unscaled Qx, Qu (MinTimeCost's tmp and Q.ux rows) */
+  const double *cQ = kQ(s, k), *cR = kR(s, k), *cH = kH(s, k), *cq = kq(s, k), *cr = kr(s, k);
   /* Q.x .= cost.Q*x + cost.q + cost.H'*u ; Q.u .= cost.R*u + cost.r + cost.H*x ; then Q*dt */
   for (int i = 0; i < n; i++) {
     double a = 0, b = 0;
-    for (int j = 0; j < n; j++) a = fma(s->Q[IDX(i, j, n)], x[j], a);
-    for (int j = 0; j < m; j++) b = fma(s->H[IDX(j, i, m)], u[j], b);
-    gx[i] = (a + s->q[i]) + b;
+    for (int j = 0; j < n; j++) a = fma(cQ[IDX(i, j, n)], x[j], a);
+    for (int j = 0; j < m; j++) b = fma(cH[IDX(j, i, m)], u[j], b);
+    gx[i] = (a + cq[i]) + b;
     Qx[i] = gx[i] * dt;
   }
   for (int i = 0; i < m; i++) {
     double a = 0, b = 0;
-    for (int j = 0; j < m; j++) a = fma(s->R[IDX(i, j, m)], u[j], a);
-    for (int j = 0; j < n; j++) b = fma(s->H[IDX(i, j, m)], x[j], b);
-    gu[i] = (a + s->r[i]) + b;
+    for (int j = 0; j < m; j++) a = fma(cR[IDX(i, j, m)], u[j], a);
+    for (int j = 0; j < n; j++) b = fma(cH[IDX(i, j, m)], x[j], b);
+    gu[i] = (a + cr[i]) + b;
     Qu[i] = gu[i] * dt;
   }
-  for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = s->Q[i] * dt;
-  for (int i = 0; i < m * m; i++) s->Quu[(size_t)k * m * m + i] = s->R[i] * dt;
-  for (int i = 0; i < m * n; i++) s->Qux[(size_t)k * m * n + i] = s->H[i] * dt;
+  for (int i = 0; i < n * n; i++) s->Qxx[(size_t)k * n * n + i] = cQ[i] * dt;
+  for (int i = 0; i < m * m; i++) s->Quu[(size_t)k * m * m + i] = cR[i] * dt;
+  for (int i = 0; i < m * n; i++) s->Qux[(size_t)k * m * n + i] = cH[i] * dt;
   if (s->mt) {
     /* ℓ1 = stage_cost(cost.cost, x, u); tmp = 2τ Qu; Q.u[end] = τ(2ℓ1 + R); Q.uu[u, end] = tmp;
        Q.uu[end, end] = 2ℓ1 + R; Q.ux[end, x] = 2τ Qx'; Q.x[end] = R x[end]; Q.xx[end, end] = R */
     const double R = s->R_mt, tau = u[m - 1];
-    const double l1 = stage_cost(s, x, u, 1.0);
+    const double l1 = stage_cost(s, k, x, u, 1.0);
     const double w = 2.0 * l1 + R, t2 = 2.0 * tau;
     double* Quu = s->Quu + (size_t)k * m * m;
     double* Qux = s->Qux + (size_t)k * m * n;

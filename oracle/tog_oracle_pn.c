@@ -33,7 +33,7 @@ typedef struct {
   double *Cv;                 /* constraint values (N, pmax) */
   double *Xt, *Ut;            /* trial point */
   double *Xs, *Us;            /* the point S and HinvY were formed at (fixed through the line searches) */
-  double *wx, *wu;            /* H⁻¹ diagonal: wx (N, n), wu (m) */
+  double *wx, *wu;            /* H⁻¹ diagonal: wx (N, n), wu (N-1, m) */
   int refinements, linesearches, projections, error;
 } pn_ws;
 
@@ -124,7 +124,7 @@ static void pn_build_S(oc_solver* s, pn_ws* ws, const double* X, const double* U
       for (int i = 0; i < sb; i++) {
         double acc = 0.0;
         for (int v = 0; v < nv; v++) {
-          double w = v < n ? wxj[v] : ws->wu[v - n];
+          double w = v < n ? wxj[v] : ws->wu[(size_t)j * m + (v - n)];
           acc = fma(Yz[i + SM * v], w * Yz[l + SM * v], acc);
         }
         if (b < N && i < n && i == l) acc = acc + ws->wx[(size_t)(j + 1) * n + i];
@@ -265,7 +265,7 @@ static void pn_trial(oc_solver* s, pn_ws* ws, double alpha) {
       else
         t = 0.0;
       for (int i = 0; i < ws->sz[b]; i++) t = fma(Yz[i + SM * v], PNV(ws->xv, b, i), t);
-      double w = v < n ? ws->wx[(size_t)j * n + v] : ws->wu[v - n];
+      double w = v < n ? ws->wx[(size_t)j * n + v] : ws->wu[(size_t)j * m + (v - n)];
       double dz = -(w * t);
       if (v < n)
         ws->Xt[(size_t)j * n + v] = s->X[(size_t)j * n + v] + alpha * dz;
@@ -359,12 +359,14 @@ OC_EXPORT int oc_solve_pn(oc_solver* s, const tog_pn_options* o, double* out) {
   ws->Xs = calloc((size_t)N * n, sizeof(double));
   ws->Us = calloc((size_t)(N - 1) * m, sizeof(double));
   ws->wx = calloc((size_t)N * n, sizeof(double));
-  ws->wu = calloc(m, sizeof(double));
-  /* H = Diagonal(solver.H): stage Q·dt, R·dt (cost.jl:214-223), terminal Qf (:225-228) */
+  ws->wu = calloc((size_t)(N - 1) * m, sizeof(double));
+  /* H = Diagonal(solver.H): stage Q·dt, R·dt (cost.jl:214-223), terminal Qf (:225-228); per knot (a
+     time-varying Objective) */
   for (int k = 0; k < N; k++)
     for (int i = 0; i < n; i++)
-      ws->wx[(size_t)k * n + i] = 1.0 / (k < N - 1 ? s->Q[IDX(i, i, n)] * s->dt : s->Qf[IDX(i, i, n)]);
-  for (int i = 0; i < m; i++) ws->wu[i] = 1.0 / (s->R[IDX(i, i, m)] * s->dt);
+      ws->wx[(size_t)k * n + i] = 1.0 / (k < N - 1 ? kQ(s, k)[IDX(i, i, n)] * s->dt : s->Qf[IDX(i, i, n)]);
+  for (int k = 0; k < N - 1; k++)
+    for (int i = 0; i < m; i++) ws->wu[(size_t)k * m + i] = 1.0 / (kR(s, k)[IDX(i, i, m)] * s->dt);
   double viol = 0.0, c_max = 0.0, J = 0.0;
   int steps = 0;
   s->hpn_n = 0;

@@ -1,7 +1,7 @@
 """Config 3 at its full benchmark size (BASELINE.json configs[1]): the quadrotor
 AL-iLQR batch of B = 8192 trajectories solved to completion on the device, exactly as bench.py's
 solve leg runs it (tog_solve with the default budget, every tail mode: pending line searches,
-compacted launches, k_bwd_duo).
+compacted launches, k_bwd_quad).
 
 Properties over the whole batch: no trajectory left active, finite X/U, x0 kept, every AL-converged
 trajectory within the constraint tolerance. Against the CPU oracle (oracle/tog_oracle.c, the

@@ -55,10 +55,9 @@ def test_discretize_model_schemes(tog):
     assert tog.rk3_implicit(tog.Dynamics.cartpole).integration == tog.abi.RK3_IMPLICIT
     with pytest.raises(ValueError):
         tog.discretize_model(tog.Dynamics.pendulum, "bogus")
-    # the device instantiates the Newton step for n <= 4 and the quadrotor (not the Kuka arm)
+    # the device instantiates the Newton step for n <= 4, the quadrotor and the Kuka arm (KukaImplicit)
     assert tog.discretize_model(tog.Dynamics.quadrotor, "midpoint_implicit").integration == tog.abi.MIDPOINT_IMPLICIT
-    with pytest.raises(NotImplementedError):
-        tog.discretize_model(tog.Dynamics.kuka, "midpoint_implicit")
+    assert tog.discretize_model(tog.Dynamics.kuka, "rk3_implicit").integration == tog.abi.RK3_IMPLICIT
 
 
 @pytest.mark.parametrize("scheme", SCHEMES)
@@ -149,7 +148,7 @@ def test_oracle_reference_pendulum_schemes(tog, oracle, scheme):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scheme", SCHEMES)
-@pytest.mark.parametrize("name", ["pendulum", "cartpole", "car", "doubleintegrator", "quadrotor"])
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "car", "doubleintegrator", "quadrotor", "kuka"])
 def test_gpu_implicit_jacobian_parity(tog, oracle, gpu, scheme, name):
     """k_jacobian through the device Newton step vs the oracle's dual restatement, bit for bit."""
     model = getattr(tog.Dynamics, name)
@@ -225,8 +224,33 @@ def test_gpu_implicit_quadrotor_solve(tog, oracle, gpu, scheme):
 
 @pytest.mark.gpu
 def test_gpu_implicit_unsupported_model(tog, gpu):
-    """tog_create rejects an implicit scheme on a model it is not instantiated for."""
+    """tog_create rejects an implicit scheme on a model it is not instantiated for (the minimum-time
+    augmentation, whose dt is a control)."""
     prob = tog.Problems.kuka(N=5)
-    prob.model = tog.Model(tog.abi.MODEL_KUKA, 14, 7, "kuka", tog.abi.MIDPOINT_IMPLICIT)
+    prob.model = tog.Model(tog.abi.MODEL_KUKA, 15, 8, "kuka_mt", tog.abi.MIDPOINT_IMPLICIT, min_time=True)
     with pytest.raises(Exception):
         tog.iLQRSolver(prob, tog.iLQRSolverOptions())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scheme", ["midpoint_implicit", "rk3_implicit"])
+def test_gpu_implicit_kuka_solve(tog, oracle, gpu, scheme):
+    """The Kuka arm (n = 14, RigidBodyDynamics restated) under the implicit schemes
+    (src/integration.jl:44-73, :171-205): Newton solves inside every rollout step and the Jacobian through
+    the Newton loop; a short AL-iLQR solve on the device equals the oracle's, iterations included."""
+    base = tog.Problems.kuka(N=11, tf=0.5)
+    model = tog.discretize_model(tog.Dynamics.kuka, scheme)
+    rng = np.random.default_rng(21)
+    U0 = base._U[0] + 0.1 * rng.standard_normal((2, base.N - 1, 7))
+    prob = tog.Problem(model, base.obj, U0, constraints=base.constraints, x0=np.tile(base.x0[0], (2, 1)),
+                       xf=base.xf, N=base.N, dt=base.dt)
+    opts = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(iterations=15), iterations=3,
+                                                constraint_tolerance=1e-3, penalty_initial=0.01,
+                                                penalty_scaling=50.0)
+    gp = prob.copy()
+    solver = tog.solve_b(gp, opts)
+    for b in range(prob.B):
+        o = oracle.OracleSolver(prob, opts, b=b)
+        steps = o.solve()
+        assert rel(gp._X[b], o.get("X")) < TOL_STEP and rel(gp._U[b], o.get("U")) < TOL_STEP, b
+        assert steps == solver.stats["iterations_total"][b]

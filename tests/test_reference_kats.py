@@ -294,11 +294,11 @@ def test_undefined_integration_raises(tog):
     prob = tog.Problems.pendulum()
     with pytest.raises(ValueError):
         tog.Problem(tog.Dynamics.pendulum, prob.obj, integration="bogus", N=prob.N, dt=prob.dt)
-    # the implicit Newton step is instantiated for models with n <= 4 and the quadrotor
-    # (csrc/tog_device.hpp implicit_step), not the Kuka arm
+    # the implicit Newton step is instantiated for models with n <= 4, the quadrotor and the Kuka arm
+    # (csrc/tog_device.hpp implicit_step, KukaImplicit), not for user plugin models with n > 4
     assert tog.discretize_model(tog.Dynamics.pendulum, "midpoint_implicit").integration == tog.abi.MIDPOINT_IMPLICIT
     with pytest.raises(NotImplementedError):
-        tog.discretize_model(tog.Dynamics.kuka, "midpoint_implicit")
+        tog.discretize_model(tog.Model(tog.abi.MODEL_USER, 5, 2, "user5"), "midpoint_implicit")
 
 
 def test_midpoint_jacobian_matches_central_differences(tog, oracle):

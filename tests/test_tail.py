@@ -54,12 +54,13 @@ def test_compacted_tail_equals_full_launches(tog, gpu, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["trio", "duo", "team"])
+@pytest.mark.parametrize("kind", ["team"])
 def test_tail_backward_kernels_agree(tog, gpu, kind):
-    """The tail backward kernels (k_bwd_quad, the default; k_bwd_trio; k_bwd_duo; the one-wave
+    """The tail backward kernels (k_bwd_quad, the default, four waves per trajectory; the one-wave
     k_bwd_team; TOG_BWD_TAIL) perform the same operations in the same order: a batch solved with each equals the
-    others bit for bit (X, U, every per-trajectory statistic). B = 24 keeps every step in the tail
-    mode, and the restarts of the config-3 solves exercise the faithful replays."""
+    other bit for bit (X, U, every per-trajectory statistic). B = 24 keeps every step in the tail
+    mode, and the restarts of the config-3 solves exercise the faithful replays. (Round 4's two- and
+    three-wave variants are retired.)"""
     B = 24
     _, _, a, Sa = _solve(tog, B, {"TOG_BWD_TAIL": None})
     _, _, b, Sb = _solve(tog, B, {"TOG_BWD_TAIL": kind})

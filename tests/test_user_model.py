@@ -171,3 +171,38 @@ def test_user_constraints_unicycle_solve(tog, gpu):
     cmax = tog.max_violation(prob)
     assert np.all(cmax < opts.constraint_tolerance)
     assert np.all(np.abs(prob._X[:, -1] - np.array([2.0, 1.0, 0, 0, 0])) < 1e-2)
+
+
+@pytest.mark.gpu
+def test_user_pendulum_min_time_equals_builtin(tog, gpu):
+    """minimum_time_problem on a user model (the plugin's MinTime<M>, add_min_time_controls
+    minimum_time.jl:83-104): ALTRO with tf = :min on the user pendulum equals the same solve on the built-in
+    pendulum bit for bit (X, U, the time steps h, every statistic); the built-in one is held to the oracle
+    by tests/test_minimum_time.py."""
+    import math
+
+    user = tog.Model.from_plugin(PLUG / "user_pendulum.so")
+    n, m, N = 2, 1, 31
+    Q, R = 1e-3 * np.eye(n), 1e-3 * np.eye(m)
+    xf, x0 = np.array([math.pi, 0.0]), np.zeros(n)
+
+    def make(model):
+        cons = tog.Constraints(N)
+        bnd = tog.BoundConstraint(n, m, u_min=-5.0, u_max=5.0)
+        for k in range(N - 1):
+            cons[k] += bnd
+        cons[N - 1] += tog.goal_constraint(xf)
+        U0 = np.ones((N - 1, m)) + 0.1 * np.sin(np.arange(N - 1))[:, None]
+        return tog.Problem(tog.rk3(model), tog.LQRObjective(Q, R, Q, xf, N), U0, constraints=cons, dt=0.075,
+                           x0=x0, N=N, tf="min")
+
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(), iterations=50, penalty_scaling=10.0)
+    opts = tog.ALTROSolverOptions(opts_al=al, R_minimum_time=15.0, dt_max=0.15, dt_min=1.0e-3)
+    pu, pb = make(user), make(tog.Dynamics.pendulum)
+    su = tog.solve_b(pu, opts.copy())
+    sb = tog.solve_b(pb, opts.copy())
+    assert np.array_equal(pu._X, pb._X) and np.array_equal(pu._U, pb._U)
+    assert np.array_equal(pu.h, pb.h)
+    for key in ("iterations_total", "flags", "cost", "c_max"):
+        assert np.array_equal(su.stats[key], sb.stats[key]), key
+    assert 0.0 < tog.total_time(pu) < math.inf

@@ -2,10 +2,10 @@
 //
 // Reference: src/solvers/ilqr/backward_pass.jl:87-192 (_backwardpass_sqrt!, chol_plus, chol_minus).
 //
-// k_bwd_trio (tog_bwd_trio.hpp) with its downdate wave split in two. In the trio kernel wave C ran
-// Q.ux, then per released row of the new Q.xx factor one substitution step and one systolic
-// chol_minus step (≈ 820 cycles a row against the QR's ≈ 650), so the chain waited on C
-// (profiles/r4o_trio_sections_b1.txt). Here
+// Round 4's three-wave variant ran Q.ux, then per released row of the new Q.xx factor one substitution
+// step and one systolic chol_minus step on one wave (≈ 820 cycles a row against the QR's ≈ 650), so the
+// chain waited on it (profiles/r4o_trio_sections_b1.txt); the two- and three-wave variants are retired
+// (round 5). Here
 //   wave A (QRs):   qr([Q.xx; S A]) releasing the factor's rows; as soon as K (B) and tmp1 (C) are out,
 //                   the top rows Q.xx + tmp1 K of the S-update operand; after B2b its bottom rows
 //                   tmp2 K and qr([Q.xx + tmp1 K; tmp2 K]) = S_k releasing S_k's rows
@@ -17,8 +17,8 @@
 //   wave D (chol):  chol_minus(Q.uu, tmp1), systolic step t as row t of tmp1 is released
 // Two workgroup barriers per knot: B2b (tmp2, the verdict, the downdate's failure flag; all four waves
 // restart or stop together) and B3 (S_k whole, S_k A_{k-1} and S_k B_{k-1} on the bus). Everything else
-// passes through LDS tagged with the knot's sequence number (tog_bwd_trio.hpp: a wave's LDS operations
-// are performed in issue order, so a tag stored after its data is never visible before the data). Every
+// passes through LDS tagged with the knot's sequence number (a release store after the data, an acquire
+// load before the reads; see tag_store for why wavefront scope suffices and what the alternatives cost). Every
 // value is computed by the same operations in the same order as the other backward kernels (and the
 // oracle): the results are bit-identical.
 #pragma once
@@ -143,11 +143,17 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   bool done = false;
   auto dense = [&](int k) { return knot_dense<SQRT, AL>(k, N, AL ? kcnt[k] : 0, AL ? knx[k] : 0); };
   int seq = 0;  // knot sequence number (every wave counts alike): the tags' value for this knot
-  // A release store orders the tagged data's stores before the tag in the compiled code; wavefront
-  // scope, because the hardware needs no wait for the order (a wave's LDS operations are performed in
-  // issue order) -- and unlike a compiler barrier it leaves the scheduler free to move arithmetic
-  // across the release.
-  // (every lane stores the same tag: no exec-mask change splits the scheduling region)
+  // The tag is a release store at wavefront scope, read with a workgroup-scope acquire. The release keeps
+  // the compiler from moving the tagged data's stores after the tag; the cross-wave order then rests on
+  // the hardware: the data and the tag are DS stores (no FLAT store in the kernel: every LDS access is a
+  // DS instruction), and the LDS unit performs one wave's DS operations in issue order, so a consumer
+  // that has read the tag and then reads the data sees the data. Measured alternatives
+  // (profiles/r5_quad_tag_isa.txt, tools/quad_tag_isa.py): a workgroup-scope release adds an
+  // s_waitcnt lgkmcnt(0) before each of the 33 tag stores; a bounded wait (a poll counter that flags an
+  // error word or traps) grows the kernel from 10.6 k to 13-16 k instructions and the tail backward from
+  // 0.886 to 0.96 ms per step (B = 1; whole solve 88.3 k -> 83.4 k it/s). The waits stay unbounded; a hang
+  // is reported by the host watchdog of the blocking readbacks (tog_runtime.cpp wait_event) instead.
+  // (Every lane stores the same tag: no exec-mask change splits the scheduling region.)
   auto tag_store = [&](int* t) { __hip_atomic_store(t, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WAVEFRONT); };
   auto tag_wait = [&](int* t) {
     while (__hip_atomic_load(t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq) {

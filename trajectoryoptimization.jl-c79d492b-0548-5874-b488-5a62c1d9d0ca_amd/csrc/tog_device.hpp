@@ -931,7 +931,10 @@ template <class M>
 struct ModelTraits {
   using Base = M;
   static constexpr int slack = 0;
-  static constexpr bool implicit_ok = M::n <= 4 || M::id == TOG_MODEL_QUADROTOR;  // implicit integrators instantiated
+  // implicit integrators instantiated: the small models and the quadrotor (the Kuka arm's are in a unit of
+  // their own, KukaImplicit); explicit_ok: the explicit integrators instantiated
+  static constexpr bool implicit_ok = M::n <= 4 || M::id == TOG_MODEL_QUADROTOR;
+  static constexpr bool explicit_ok = true;
   static constexpr bool min_time = false;
 };
 template <class Mb>
@@ -939,6 +942,7 @@ struct ModelTraits<MinTime<Mb>> {
   using Base = Mb;
   static constexpr int slack = 0;
   static constexpr bool implicit_ok = false;
+  static constexpr bool explicit_ok = true;
   static constexpr bool min_time = true;
 };
 template <class Mb>
@@ -946,6 +950,19 @@ struct ModelTraits<Infeasible<Mb>> {
   using Base = Mb;
   static constexpr int slack = Mb::n;
   static constexpr bool implicit_ok = false;
+  static constexpr bool explicit_ok = true;
+  static constexpr bool min_time = false;
+};
+// The Kuka arm under the implicit schemes (midpoint_implicit / rk3_implicit): the same model, its kernels
+// instantiated for those two integrators only, in their own translation unit (k_kuka_implicit.hip), so the
+// 14-state Newton steps do not double the Kuka unit's build time
+struct KukaImplicit : Kuka {};
+template <>
+struct ModelTraits<KukaImplicit> {
+  using Base = KukaImplicit;
+  static constexpr int slack = 0;
+  static constexpr bool implicit_ok = true;
+  static constexpr bool explicit_ok = false;
   static constexpr bool min_time = false;
 };
 
@@ -956,9 +973,9 @@ struct ModelTraits<Infeasible<Mb>> {
 // when T is a Dual, ∇g is formed at the values (∂f/∂x one Dual<1> column at a time), and
 // δy = (-∇g)\g by partial-pivoting LU. rk3_implicit reproduces the reference's aliasing of
 // fc1 = fc2 = fc3 (one array), so its residual is y - x - dt/6 F - 4/6 dt F - dt/6 F, F = f(Xm).
-// Built for models with n <= 4 and the quadrotor (ModelTraits::implicit_ok; at n = 13 the real ∇g
-// and its LU live in scratch, several KB per lane); the reference's 1000-iteration error
-// becomes a NaN state (the rollout then fails as diverged).
+// Built for models with n <= 4, the quadrotor and the Kuka arm (ModelTraits::implicit_ok, KukaImplicit; at
+// n = 13-14 the real ∇g and its LU live in scratch, several KB per lane: parity, not speed); the reference's
+// 1000-iteration error becomes a NaN state (the rollout then fails as diverged).
 template <int n>
 __host__ __device__ __forceinline__ double jl_norm2(const double* g) {
   double mx = 0.0;
@@ -1133,6 +1150,13 @@ __host__ __device__ __forceinline__ void implicit_step(T* y, const T* x, const T
   }
 }
 
+// The 13-14 state Newton steps out of line: one copy per (model, scheme, scalar type) instead of one per
+// calling kernel (the Kuka unit's build time; the arithmetic is the same call for call)
+template <class M, int INTEG, class T>
+__host__ __device__ __attribute__((noinline)) void implicit_step_outlined(T* y, const T* x, const T* u, double dt) {
+  implicit_step<M, INTEG, T>(y, x, u, dt);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Explicit Runge-Kutta discretisation with runtime dt (src/integration.jl:115-158). Running-sum
 // form keeps the reference's left-to-right association: RK4 ((k1 + 2k2) + 2k3) + k4,
@@ -1153,7 +1177,10 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
   } else {
   constexpr int n = M::n;
   if constexpr (INTEG == TOG_MIDPOINT_IMPLICIT || INTEG == TOG_RK3_IMPLICIT) {
-    implicit_step<M, INTEG, T>(xn, x, u, dt);
+    if constexpr (M::n > 4)
+      implicit_step_outlined<M, INTEG, T>(xn, x, u, dt);
+    else
+      implicit_step<M, INTEG, T>(xn, x, u, dt);
     return;
   } else if constexpr (INTEG == TOG_MIDPOINT) {
     // midpoint (src/integration.jl:26-33): ẋ = f(x,u); ẋ .*= dt/2; ẋ = f(x + ẋ, u); x+ = x + ẋ*dt

@@ -3004,8 +3004,6 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
 // =============================================================================================
 }  // namespace tog
 #include "tog_bwd_team.hpp"
-#include "tog_bwd_duo.hpp"
-#include "tog_bwd_trio.hpp"
 #include "tog_bwd_quad.hpp"
 #include "tog_pn.hpp"
 namespace tog {
@@ -3270,6 +3268,13 @@ struct ModelLaunch {
   // rejects them elsewhere)
   template <class F>
   static void with_integ(int integ, F&& f) {
+    if constexpr (!ModelTraits<M>::explicit_ok) {  // KukaImplicit: the implicit schemes only
+      if (integ == TOG_RK3_IMPLICIT)
+        f(std::integral_constant<int, TOG_RK3_IMPLICIT>{});
+      else
+        f(std::integral_constant<int, TOG_MIDPOINT_IMPLICIT>{});
+      return;
+    }
     if (integ == TOG_RK4) {
       f(std::integral_constant<int, TOG_RK4>{});
     } else if (integ == TOG_MIDPOINT) {
@@ -3306,7 +3311,7 @@ struct ModelLaunch {
         hipLaunchKernelGGL((k_jacobian_mt<M, I, JW>), dim3(grid(total, 256)), dim3(256), 0, st, P, Bf, total);
       });
     } else if (Mb::id == TOG_MODEL_KUKA && integ == TOG_RK3 && Bf.jws && Bf.jac_chain) {
-      if constexpr (Mb::id == TOG_MODEL_KUKA) {  // stage-chain form (tog_kuka_jac.hpp)
+      if constexpr (Mb::id == TOG_MODEL_KUKA && ModelTraits<M>::explicit_ok) {  // stage-chain form (tog_kuka_jac.hpp)
         const long long total = B * (long long)(N - 1);
         hipLaunchKernelGGL((k_kuka_points<M>), dim3(grid(total, 64)), dim3(64), 0, st, P, Bf, total);
         hipLaunchKernelGGL((k_kuka_sjac<M, 0>), dim3(grid(total * 21, 256)), dim3(256), 0, st, P, Bf, total);
@@ -3314,7 +3319,7 @@ struct ModelLaunch {
         hipLaunchKernelGGL((k_kuka_chain<M>), dim3((unsigned)total), dim3(64), 0, st, P, Bf, total);
       }
     } else if (Mb::id == TOG_MODEL_KUKA && integ == TOG_RK3 && Bf.jws) {
-      if constexpr (Mb::id == TOG_MODEL_KUKA) {  // duals through the step, one launch per RK3 stage (A/B)
+      if constexpr (Mb::id == TOG_MODEL_KUKA && ModelTraits<M>::explicit_ok) {  // duals through the step, one launch per RK3 stage (A/B)
         constexpr int SW = TOG_JAC_STAGE_W, NCHS = (Mb::n + Mb::m + SW - 1) / SW;
         const long long total = B * (long long)(N - 1) * NCHS;
         const dim3 g(grid(total, 256)), blk(256);
@@ -3351,28 +3356,17 @@ struct ModelLaunch {
           else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
         }
       };
-      // TOG_BWD_TAIL: "quad" (default), "trio", "duo", or "team" (the one-wave team kernel), for A/B
-      // checks (read per launch: tests switch it within one process)
+      // TOG_BWD_TAIL: "quad" (default) or "team" (the one-wave team kernel), for A/B checks (read per
+      // launch: tests switch it within one process)
       const char* tk = getenv("TOG_BWD_TAIL");
-      const int tail_kind = (getenv("TOG_NO_DUO") || (tk && !strcmp(tk, "team")))
-                                ? 0
-                                : (tk && !strcmp(tk, "duo")) ? 2 : (tk && !strcmp(tk, "trio")) ? 3 : 4;
-      if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && tail_kind) {
+      const bool quad = !(getenv("TOG_NO_DUO") || (tk && !strcmp(tk, "team")));
+      if (Bf.tail && sq && TeamCfg<M>::TEAM == 16 && quad) {
         // convergence tail, square-root pass, one trajectory per workgroup: the QRs, the side work, tmp1
-        // and the downdate on four waves (tog_bwd_quad.hpp), the last two on one (tog_bwd_trio.hpp), or
-        // the chain and the side work on two (tog_bwd_duo.hpp)
+        // and the downdate on four waves (tog_bwd_quad.hpp)
         if constexpr (TeamCfg<M>::TEAM == 16) {
           const dim3 gd((unsigned)B);
-          if (tail_kind == 4) {
-            if (al) hipLaunchKernelGGL((k_bwd_quad<M, 1>), gd, dim3(256), 0, st, P, Bf, flags);
-            else hipLaunchKernelGGL((k_bwd_quad<M, 0>), gd, dim3(256), 0, st, P, Bf, flags);
-          } else if (tail_kind == 3) {
-            if (al) hipLaunchKernelGGL((k_bwd_trio<M, 1>), gd, dim3(192), 0, st, P, Bf, flags);
-            else hipLaunchKernelGGL((k_bwd_trio<M, 0>), gd, dim3(192), 0, st, P, Bf, flags);
-          } else {
-            if (al) hipLaunchKernelGGL((k_bwd_duo<M, 1>), gd, dim3(128), 0, st, P, Bf, flags);
-            else hipLaunchKernelGGL((k_bwd_duo<M, 0>), gd, dim3(128), 0, st, P, Bf, flags);
-          }
+          if (al) hipLaunchKernelGGL((k_bwd_quad<M, 1>), gd, dim3(256), 0, st, P, Bf, flags);
+          else hipLaunchKernelGGL((k_bwd_quad<M, 0>), gd, dim3(256), 0, st, P, Bf, flags);
         }
       } else if (Bf.tail) {
         launch(std::integral_constant<int, 1>{});

@@ -14,8 +14,9 @@
 // it with double, the Jacobian kernel with Dual<W> (ForwardDiff's forward mode, src/model.jl:491-522).
 // Use +, -, *, / and the helpers sin_, cos_, sqrt_, inv_ and cst_(value, like) (a constant of T's
 // type) from tog_device.hpp. The plugin instantiates every kernel of the path (rollouts, Jacobians,
-// backward passes, line search, AL updates, projected Newton) for the model and for its
-// infeasible-start variant add_slack_controls(model) (src/model.jl:761-779); libtog dispatches to
+// backward passes, line search, AL updates, projected Newton) for the model, for its
+// infeasible-start variant add_slack_controls(model) (src/model.jl:761-779) and for its minimum-time
+// variant add_min_time_controls(model) (src/solvers/altro/minimum_time.jl:83-104); libtog dispatches to
 // them through the same ModelOps table its built-in models use. tog_model_load checks the plugin's
 // layout fingerprint, so a plugin built against other headers is refused instead of misread.
 #pragma once
@@ -36,6 +37,7 @@ constexpr long long plugin_fingerprint() {
 #define TOG_PLUGIN(MODEL)                                                                         \
   static_assert(MODEL::n >= 1 && MODEL::n <= tog::NMAX, "plugin model: 1 <= n <= NMAX");          \
   static_assert(MODEL::m >= 1 && MODEL::m + MODEL::n <= tog::MMAX, "plugin model: m + n <= MMAX"); \
+  static_assert(MODEL::n + 1 <= tog::NMAX, "plugin model: n + 1 <= NMAX (minimum-time state)");   \
   extern "C" long long tog_plugin_fingerprint() { return tog::plugin_fingerprint(); }             \
   extern "C" const tog::ModelOps* tog_plugin_ops() {                                              \
     static const tog::ModelOps o = tog::ModelLaunch<MODEL>::ops();                                \
@@ -43,5 +45,9 @@ constexpr long long plugin_fingerprint() {
   }                                                                                               \
   extern "C" const tog::ModelOps* tog_plugin_ops_infeasible() {                                   \
     static const tog::ModelOps o = tog::ModelLaunch<tog::Infeasible<MODEL>>::ops();              \
+    return &o;                                                                                    \
+  }                                                                                               \
+  extern "C" const tog::ModelOps* tog_plugin_ops_min_time() {                                     \
+    static const tog::ModelOps o = tog::ModelLaunch<tog::MinTime<MODEL>>::ops();                 \
     return &o;                                                                                    \
   }

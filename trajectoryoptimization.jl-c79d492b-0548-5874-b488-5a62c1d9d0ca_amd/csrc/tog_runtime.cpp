@@ -9,6 +9,8 @@
 #include <string.h>
 
 #include <string>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include <dlfcn.h>
@@ -25,6 +27,7 @@ const ModelOps* ops_quadrotor();
 const ModelOps* ops_car();
 const ModelOps* ops_pendulum();
 const ModelOps* ops_kuka();
+const ModelOps* ops_kuka_implicit();
 // add_slack_controls(model) variants (infeasible start, src/model.jl:761-779)
 const ModelOps* ops_inf_double_integrator();
 const ModelOps* ops_inf_cartpole();
@@ -50,6 +53,27 @@ static constexpr double TAIL_ACTIVE = 2048.0;
 static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+// Host watchdog of the blocking readbacks: wait for `ev` polling, and give up after TOG_WATCHDOG_S seconds
+// (default 600) with TOG_ERR_DEVICE, so that a kernel that never finishes (e.g. a lost LDS hand-off in the
+// tail backward kernel, whose waits are unbounded for speed, tog_bwd_quad.hpp) is reported instead of
+// blocking the caller forever. The device queue itself stays hung: the process should exit.
+static int wait_event(hipEvent_t ev, const char* what) {
+  static const double limit = getenv("TOG_WATCHDOG_S") ? atof(getenv("TOG_WATCHDOG_S")) : 600.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  unsigned polls = 0;
+  while (true) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return TOG_OK;
+    if (e != hipErrorNotReady) return fail(TOG_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    if (++polls > 64) {  // (first a short spin: a check usually completes within microseconds)
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit)
+        return fail(TOG_ERR_DEVICE, std::string(what) + ": the device did not finish within TOG_WATCHDOG_S = " +
+                                        std::to_string(limit) + " s (a hung kernel?)");
+      std::this_thread::sleep_for(std::chrono::microseconds(polls < 1000 ? 2 : 200));
+    }
+  }
 }
 
 #define HIPCHECK(expr)                                                                   \
@@ -102,6 +126,11 @@ struct tog_handle {
   std::vector<double> pn_hist;
   std::vector<int32_t> pn_hist_rec;
   int pn_hist_steps = -1;
+  // asynchronous stopping check (tog_batch_stats_begin / _end): pinned landing buffer + completion event
+  double* h_stats = nullptr;
+  hipEvent_t stats_ev = nullptr;
+  bool stats_pending = false;
+  hipEvent_t sync_ev = nullptr;  // tog_synchronize's watchdog wait
 };
 
 static hipEvent_t next_event(tog_handle* h) {
@@ -141,11 +170,15 @@ struct tog_model {
   void* so;
   const tog::ModelOps* ops;
   const tog::ModelOps* ops_inf;
+  const tog::ModelOps* ops_mt;  // MinTime<M> (add_min_time_controls)
 };
 
-static const ModelOps* ops_for(int model, bool infeasible, bool min_time, const tog_model* user) {
+static const ModelOps* ops_for(int model, bool infeasible, bool min_time, const tog_model* user, int integ) {
+  if (model == TOG_MODEL_KUKA && !infeasible && !min_time && (integ == TOG_RK3_IMPLICIT || integ == TOG_MIDPOINT_IMPLICIT))
+    return ops_kuka_implicit();
   if (min_time) {
     if (infeasible) return nullptr;
+    if (model == TOG_MODEL_USER) return user ? user->ops_mt : nullptr;
     switch (model) {
       case TOG_MODEL_PENDULUM: return ops_mt_pendulum();
       case TOG_MODEL_CAR: return ops_mt_car();
@@ -379,7 +412,8 @@ int32_t tog_model_load(const char* path, tog_model** out) {
   auto fp = reinterpret_cast<long long (*)()>(dlsym(so, "tog_plugin_fingerprint"));
   auto ops = reinterpret_cast<const ModelOps* (*)()>(dlsym(so, "tog_plugin_ops"));
   auto opi = reinterpret_cast<const ModelOps* (*)()>(dlsym(so, "tog_plugin_ops_infeasible"));
-  if (!fp || !ops || !opi) {
+  auto opm = reinterpret_cast<const ModelOps* (*)()>(dlsym(so, "tog_plugin_ops_min_time"));
+  if (!fp || !ops || !opi || !opm) {
     dlclose(so);
     return fail(TOG_ERR_ARG, "not a libtog model plugin (TOG_PLUGIN symbols missing)");
   }
@@ -387,7 +421,7 @@ int32_t tog_model_load(const char* path, tog_model** out) {
     dlclose(so);
     return fail(TOG_ERR_ARG, "model plugin was built against different libtog headers");
   }
-  tog_model* m = new tog_model{so, ops(), opi()};
+  tog_model* m = new tog_model{so, ops(), opi(), opm()};
   *out = m;
   return TOG_OK;
 }
@@ -604,6 +638,9 @@ int32_t tog_destroy(tog_handle* h) {
   if (h->sp.fork) (void)hipEventDestroy(h->sp.fork);
   if (h->sp.join) (void)hipEventDestroy(h->sp.join);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->stats_ev) (void)hipEventDestroy(h->stats_ev);
+  if (h->sync_ev) (void)hipEventDestroy(h->sync_ev);
+  if (h->h_stats) (void)hipHostFree(h->h_stats);
   delete h;
   return TOG_OK;
 }
@@ -829,7 +866,7 @@ int32_t tog_create(const tog_problem_desc* d, const tog_options* opts, int32_t d
   if ((d->flags & TOG_PROB_MIN_TIME) && opts->square_root)
     return fail(TOG_ERR_UNSUPPORTED, "minimum time: MinTimeCost has no square-root expansion (std backward pass)");
   const ModelOps* ops = ops_for(d->model, (d->flags & TOG_PROB_INFEASIBLE) != 0, (d->flags & TOG_PROB_MIN_TIME) != 0,
-                                d->user_model);
+                                d->user_model, d->integrator);
   if (!ops) return fail(TOG_ERR_UNSUPPORTED, "model not built");
   if (d->n != ops->n || d->m != ops->m) return fail(TOG_ERR_ARG, "n, m do not match the model");
   if (d->N < 2) return fail(TOG_ERR_ARG, "N must be >= 2");
@@ -911,8 +948,9 @@ int32_t tog_synchronize(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
   if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_synchronize(p); });
   HIPCHECK(hipSetDevice(h->device));
-  HIPCHECK(hipStreamSynchronize(h->stream));
-  return TOG_OK;
+  if (!h->sync_ev) HIPCHECK(hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming));
+  HIPCHECK(hipEventRecord(h->sync_ev, h->stream));
+  return wait_event(h->sync_ev, "tog_synchronize");
 }
 
 int32_t tog_dims(tog_handle* h, int64_t* o) {
@@ -1354,29 +1392,47 @@ int32_t tog_batch_stats_device(tog_handle* h, void* dptr3) {
 
 int32_t tog_batch_stats(tog_handle* h, double* out3) {
   if (!h || !out3) return fail(TOG_ERR_ARG, "null argument");
-  if (is_multi(h)) {
-    // queue every device's reduction first, then gather: [Σ n_active, Σ J, max c_max]
-    for (tog_handle* p : h->parts) {
-      int32_t rc = tog_batch_stats_device(p, p->d_stats);
-      if (rc) return rc;
-    }
-    out3[0] = 0.0, out3[1] = 0.0, out3[2] = 0.0;
-    for (tog_handle* p : h->parts) {
-      double v[3];
-      HIPCHECK(hipSetDevice(p->device));
-      HIPCHECK(hipMemcpyAsync(v, p->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, p->stream));
-      HIPCHECK(hipStreamSynchronize(p->stream));
-      p->last_active = v[0];
-      out3[0] += v[0];
-      out3[1] += v[1];
-      out3[2] = tog_jlmax(out3[2], v[2]);
-    }
-    return TOG_OK;
-  }
+  // (a multi-device handle queues every device's reduction before it gathers: _begin / _end fan out)
+  int32_t rc = tog_batch_stats_begin(h);
+  return rc ? rc : tog_batch_stats_end(h, out3);
+}
+
+int32_t tog_batch_stats_begin(tog_handle* h) {
+  if (!h) return fail(TOG_ERR_ARG, "null handle");
+  if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_batch_stats_begin(p); });
+  HIPCHECK(hipSetDevice(h->device));
+  if (h->stats_pending) return fail(TOG_ERR_ARG, "tog_batch_stats_begin: the previous check was not ended");
+  if (!h->h_stats) HIPCHECK(hipHostMalloc((void**)&h->h_stats, sizeof(double) * 4, hipHostMallocDefault));
+  if (!h->stats_ev) HIPCHECK(hipEventCreateWithFlags(&h->stats_ev, hipEventDisableTiming));
   int rc = tog_batch_stats_device(h, h->d_stats);
   if (rc) return rc;
-  HIPCHECK(hipMemcpyAsync(out3, h->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, h->stream));
-  HIPCHECK(hipStreamSynchronize(h->stream));
+  HIPCHECK(hipMemcpyAsync(h->h_stats, h->d_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, h->stream));
+  HIPCHECK(hipEventRecord(h->stats_ev, h->stream));
+  h->stats_pending = true;
+  return TOG_OK;
+}
+
+int32_t tog_batch_stats_end(tog_handle* h, double* out3) {
+  if (!h || !out3) return fail(TOG_ERR_ARG, "null argument");
+  if (is_multi(h)) {
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (tog_handle* p : h->parts) {
+      double v[3];
+      int32_t rc = tog_batch_stats_end(p, v);
+      if (rc) return rc;
+      acc[0] += v[0];
+      acc[1] += v[1];
+      acc[2] = tog_jlmax(acc[2], v[2]);
+    }
+    out3[0] = acc[0], out3[1] = acc[1], out3[2] = acc[2];
+    return TOG_OK;
+  }
+  if (!h->stats_pending) return fail(TOG_ERR_ARG, "tog_batch_stats_end without tog_batch_stats_begin");
+  HIPCHECK(hipSetDevice(h->device));
+  h->stats_pending = false;
+  const int rc = wait_event(h->stats_ev, "tog_batch_stats");
+  if (rc) return rc;
+  out3[0] = h->h_stats[0], out3[1] = h->h_stats[1], out3[2] = h->h_stats[2];
   h->last_active = out3[0];
   return TOG_OK;
 }
@@ -1403,18 +1459,25 @@ int32_t tog_total_steps(tog_handle* h, int64_t* out) {
   return TOG_OK;
 }
 
+// The stopping check is pipelined: chunk i+1's steps are enqueued before the host waits for chunk i's
+// statistics, so the device never idles on the host round trip. The last chunk after the batch finished
+// runs on inactive trajectories only (every kernel returns at once for them); the arithmetic of the
+// solve does not depend on when the host learns the active count (it only picks launch widths).
 int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps) {
   int rc = tog_solve_init(h, mode);
   if (rc) return rc;
   if (max_steps <= 0) max_steps = tog_solve_budget(h, mode);
   const int chunk = 4;
   double stats[3];
-  for (int done = 0; done < max_steps; done += chunk) {
-    rc = tog_solve_step(h, chunk < max_steps - done ? chunk : max_steps - done);
-    if (rc) return rc;
-    rc = tog_batch_stats(h, stats);
-    if (rc) return rc;
-    if (stats[0] == 0.0) break;
+  int done = chunk < max_steps ? chunk : max_steps;
+  if ((rc = tog_solve_step(h, done)) || (rc = tog_batch_stats_begin(h))) return rc;
+  while (true) {
+    const int next = chunk < max_steps - done ? chunk : max_steps - done;
+    if (next > 0 && (rc = tog_solve_step(h, next))) return rc;
+    done += next;
+    if ((rc = tog_batch_stats_end(h, stats))) return rc;  // the chunk before `next`
+    if (stats[0] == 0.0 || next == 0) break;
+    if ((rc = tog_batch_stats_begin(h))) return rc;
   }
   return TOG_OK;
 }

@@ -67,12 +67,12 @@ def discretize_model(model: Model, discretizer: str = "rk3", dt: float = 1.0) ->
               "midpoint_implicit": abi.MIDPOINT_IMPLICIT}
     if key not in integs:
         raise ValueError(f"Integration not defined: {discretizer!r}")  # src/model.jl:659
-    builtin_implicit = model.plugin is None and model.model_id == abi.MODEL_QUADROTOR
+    builtin_implicit = model.plugin is None and model.model_id in (abi.MODEL_QUADROTOR, abi.MODEL_KUKA)
     if integs[key] in (abi.RK3_IMPLICIT, abi.MIDPOINT_IMPLICIT) and model.n > 4 and not builtin_implicit:
-        # the device instantiates the implicit Newton step for n <= 4 and the built-in quadrotor
-        # (ModelTraits::implicit_ok, csrc/tog_device.hpp), decided by model id as the runtime does
-        raise NotImplementedError(f"implicit integration {discretizer!r} is built for models with n <= 4 "
-                                  "and the quadrotor")
+        # the device instantiates the implicit Newton step for n <= 4, the built-in quadrotor and the Kuka
+        # arm (ModelTraits::implicit_ok, csrc/tog_device.hpp), decided by model id as the runtime does
+        raise NotImplementedError(f"implicit integration {discretizer!r} is built for models with n <= 4, "
+                                  "the quadrotor and the Kuka arm")
     return Model(model.model_id, model.n, model.m, model.name, integs[key], plugin=model.plugin)
 
 
@@ -1022,9 +1022,11 @@ def add_min_time_controls(model: Model) -> Model:
     control [u; h], x+ = f_d(x, u, h²), τ+ = h (the device's MinTime<M>)."""
     if not model.discrete:
         raise ValueError("add_min_time_controls needs a discrete model")
-    if model.slack or model.min_time or model.plugin:
-        raise NotImplementedError("minimum time is built for the plain built-in models")
-    return Model(model.model_id, model.n + 1, model.m + 1, model.name + "_mt", model.integration, min_time=True)
+    if model.slack or model.min_time:
+        raise NotImplementedError("minimum time of an infeasible-start or minimum-time model is not built")
+    # (user plugin models too: each plugin instantiates MinTime<M>, csrc/tog_plugin.hpp)
+    return Model(model.model_id, model.n + 1, model.m + 1, model.name + "_mt", model.integration, min_time=True,
+                 plugin=model.plugin)
 
 
 class MinTimeEquality(_Constraint):
