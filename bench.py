@@ -91,16 +91,21 @@ def bwd_flops(n, m, N, p_x, p_u, sqrt=True):
     return per_knot * (N - 1)
 
 
-def measured_traffic(kernel):
+def measured_traffic(kernel, workload="quadrotor"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_traffic.json,
     written by tools/rocpd_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
     this same bench command, FETCH_SIZE x2 per the gfx950 correction). None if absent."""
     import glob
 
     # the headline workload's summaries are <round>_traffic.json; <round>_<workload>_traffic.json
-    # (e.g. r2e_kuka_traffic.json) belong to the other configs
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))
-                   if os.path.basename(f).count("_") == 1)
+    # (e.g. r4z_quad_maze_traffic.json) belong to the other configs
+    def ours(f):
+        b = os.path.basename(f)
+        if workload == "quadrotor":
+            return b.count("_") == 1
+        return b.endswith(f"_{workload}_traffic.json") and b.split("_", 1)[1] == f"{workload}_traffic.json"
+
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")) if ours(f))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -310,7 +315,7 @@ def main():
     per_launch_traj = steps_done / max(1, launches[dom])
     alg_bytes = kb[names[dom]] * per_launch_traj
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-    traffic, tsrc = measured_traffic(names[dom]) if args.workload == "quadrotor" else (None, None)
+    traffic, tsrc = measured_traffic(names[dom], args.workload)
     # whole step: Σ per-kernel algorithmic bytes of every trajectory-step of the job ÷ the window's wall
     # time, against the job's aggregate HBM peak (world x 8 TB/s)
     step_gbs = sum(kb.values()) * steps_all / elapsed / 1e9 / world
@@ -344,6 +349,10 @@ def main():
     # value: SURVEY.md §8(d)'s metric, the whole solve (tog_solve_init until no trajectory is active);
     # the full-batch step window is reported beside it as window_rate
     value = solve_leg["value"] if solve_leg is not None else window_rate
+    # the whole solve against the HBM roofline: its rate x the per-iteration algorithmic bytes of the
+    # staged step ÷ the job's aggregate peak (the tail runs few trajectories per launch, so this is far
+    # below step_frac)
+    roofline["solve_frac"] = round(value * sum(kb.values()) / 1e9 / world / HBM_PEAK_GBS, 5)
 
     if rank == 0:
         cpu = None

@@ -31,7 +31,8 @@ extern "C" {
 /* 3: tog_solve_altro / tog_altro_options, TOG_PROB_TF_MIN, TOG_NKERNELS = 4 (tog_profile_read fills 4
       entries), tog_solve's max_steps <= 0 = the tog_solve_budget default */
 /* 4: iteration histories (tog_history_enable, TOG_FIELD_HIST_*), tog_solve_altro_ex / tog_altro_result,
-      tog_altro_options.max_steps (was reserved), tog_get_pn_history, tog_batch_stats_begin / _end */
+      tog_altro_options.max_steps (was reserved), tog_get_pn_history, tog_batch_stats_begin / _end,
+      tog_problem_desc.stage_costs (time-varying objectives) */
 #define TOG_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status */
@@ -188,6 +189,11 @@ typedef struct tog_problem_desc {
   const struct tog_model* user_model;
   /* TOG_PROB_MIN_TIME: MinTimeCost's R_min_time (ALTROSolverOptions.R_minimum_time) */
   double R_min_time;
+  /* a time-varying Objective (Objective(costs::Vector{<:CostFunction}), src/objective.jl:12-29): NULL = the
+     stage cost Q, R, H, q, r, c above at every stage knot; else (nc, N-1) column-major, per stage knot k
+     [Q (n*n); R (m*m); H (m*n); q (n); r (m); c], nc = n*n + m*m + m*n + n + m + 1 (the fields above are
+     then unused; the terminal cost stays Qf, qf, cf) */
+  const double* stage_costs;
 } tog_problem_desc;
 
 /* ---------------------------------------------------------------- options */

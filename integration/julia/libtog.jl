@@ -57,14 +57,15 @@ struct TogProblemDesc
     sets::Ptr{TogConstraintSet}; knot_set::Ptr{Int32}
     user_model::Ptr{Cvoid}
     R_min_time::Float64
+    stage_costs::Ptr{Float64}   # NULL, or the (nc, N-1) per-knot [Q; R; H; q; r; c] of a time-varying Objective
 end
 # Layout pins (tests/test_julia_layout.py checks these numbers, and the field lists below, against
 # include/tog.h compiled by gcc): sizeof and field offsets of the mirrored structs. tog_check_layout()
 # asserts them in Julia at first use.
-const TOG_LAYOUT = (tog_constraint = 16, tog_constraint_set = 16, tog_problem_desc = 152, tog_options = 200,
+const TOG_LAYOUT = (tog_constraint = 16, tog_constraint_set = 16, tog_problem_desc = 160, tog_options = 200,
                     tog_pn_options = 24, tog_altro_options = 280, tog_altro_result = 96)
 const TOG_DESC_OFFSETS = (0, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64, 72, 80, 88, 96, 104, 112, 116, 120,
-                          128, 136, 144)
+                          128, 136, 144, 152)
 
 mutable struct TogOptions          # field order = tog_options
     cost_tolerance::Float64; gradient_norm_tolerance::Float64
@@ -252,19 +253,26 @@ mutable struct TogDesc
     keep::Vector{Any}
 end
 
+# knot 1's stage cost, the terminal cost, and whether knots 2..N-1 carry costs of their own (a
+# time-varying Objective, src/objective.jl:15-29: marshalled as tog_problem_desc.stage_costs)
 function stage_and_terminal_costs(obj::Objective, N::Int)
     ℓ = obj.cost[1]
     ℓ isa QuadraticCost || throw(ArgumentError("libtog evaluates QuadraticCost / LQRCost objectives"))
+    varying = false
     for k = 2:N-1
         c = obj.cost[k]
-        (c === ℓ || (c isa QuadraticCost && c.Q == ℓ.Q && c.R == ℓ.R && c.H == ℓ.H && c.q == ℓ.q &&
-                     c.r == ℓ.r && c.c == ℓ.c)) ||
-            throw(ArgumentError("libtog evaluates one stage cost shared by knots 1..N-1 (LQRObjective form)"))
+        c isa QuadraticCost || throw(ArgumentError("libtog evaluates QuadraticCost stage costs"))
+        varying |= !(c === ℓ || (c.Q == ℓ.Q && c.R == ℓ.R && c.H == ℓ.H && c.q == ℓ.q && c.r == ℓ.r && c.c == ℓ.c))
     end
     ℓN = obj.cost[N]
     ℓN isa QuadraticCost || throw(ArgumentError("terminal cost must be a QuadraticCost"))
-    return ℓ, ℓN
+    return ℓ, ℓN, varying
 end
+
+# the (nc, N-1) column-major table of tog_problem_desc.stage_costs: per knot [vec(Q); vec(R); vec(H); q; r; c]
+stage_cost_table(obj::Objective, N::Int) =
+    reduce(hcat, [vcat(vec(Matrix{Float64}(c.Q)), vec(Matrix{Float64}(c.R)), vec(Matrix{Float64}(c.H)),
+                       Vector{Float64}(c.q), Vector{Float64}(c.r), Float64(c.c)) for c in obj.cost[1:N-1]])
 
 """
     tog_desc(prob::Problem; batch=1, R_min_time=0.0) -> TogDesc
@@ -282,7 +290,9 @@ function tog_desc(prob::Problem; batch::Integer=1, R_min_time::Real=0.0, tf_min:
     keep = Any[]
     mat(A, r, c) = (a = Matrix{Float64}(reshape(collect(A), r, c)); push!(keep, a); a)
     vec_(v) = (a = Vector{Float64}(collect(v)); push!(keep, a); a)
-    ℓ, ℓN = stage_and_terminal_costs(prob.obj, N)
+    ℓ, ℓN, varying = stage_and_terminal_costs(prob.obj, N)
+    table = varying ? stage_cost_table(prob.obj, N) : Matrix{Float64}(undef, 0, 0)
+    push!(keep, table)
     Q = mat(ℓ.Q, n, n); R = mat(ℓ.R, m, m); H = mat(ℓ.H, m, n); q = vec_(ℓ.q); r = vec_(ℓ.r)
     Qf = mat(ℓN.Q, n, n); qf = vec_(ℓN.q)
     # constraint sets: one entry per distinct ConstraintSet object
@@ -311,7 +321,7 @@ function tog_desc(prob::Problem; batch::Integer=1, R_min_time::Real=0.0, tf_min:
                        Float64(prob.dt), pointer(Q), pointer(R), pointer(H), pointer(q), pointer(r),
                        Float64(ℓ.c), pointer(Qf), pointer(qf), Float64(ℓN.c), Int32(length(sets)), Int32(0),
                        isempty(sets) ? Ptr{TogConstraintSet}(C_NULL) : pointer(sets), pointer(knot_set),
-                       user, Float64(R_min_time))
+                       user, Float64(R_min_time), varying ? pointer(table) : Ptr{Float64}(C_NULL))
     return TogDesc(Ref(d), keep)
 end
 

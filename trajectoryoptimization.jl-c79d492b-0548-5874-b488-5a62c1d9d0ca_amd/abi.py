@@ -81,7 +81,7 @@ class tog_problem_desc(C.Structure):
         ("Qf", _dp), ("qf", _dp), ("cf", C.c_double),
         ("n_sets", C.c_int32), ("reserved1", C.c_int32),
         ("sets", C.POINTER(tog_constraint_set)), ("knot_set", _ip),
-        ("user_model", C.c_void_p), ("R_min_time", C.c_double),
+        ("user_model", C.c_void_p), ("R_min_time", C.c_double), ("stage_costs", _dp),
     ]
 
 
@@ -175,7 +175,9 @@ class DescBuilder:
     """
 
     def __init__(self, model, integrator, n, m, N, dt, Q, R, H, q, r, c, Qf, qf, cf, sets, knot_set,
-                 batch=1, flags=0, user_model=None, R_min_time=0.0):
+                 batch=1, flags=0, user_model=None, R_min_time=0.0, stage_costs=None):
+        """``stage_costs``: None, or the per-stage-knot table (N-1, nc) of a time-varying objective, each
+        row [Q; R; H; q; r; c] with the matrices column-major (tog_problem_desc.stage_costs)."""
         self._keep = []
 
         def arr(x, shape):
@@ -218,6 +220,12 @@ class DescBuilder:
         d.knot_set = ks.ctypes.data_as(_ip)
         d.user_model = user_model
         d.R_min_time = float(R_min_time)
+        if stage_costs is not None:
+            sc = np.ascontiguousarray(np.asarray(stage_costs, dtype=np.float64))
+            if sc.shape != (N - 1, n * n + m * m + m * n + n + m + 1):
+                raise ValueError("stage_costs must be (N-1, n*n + m*m + m*n + n + m + 1)")
+            self._keep.append(sc)
+            d.stage_costs = sc.ctypes.data_as(_dp)
         self.desc = d
 
 

@@ -170,8 +170,9 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
 #pragma unroll
       for (int i = 0; i < n; i++) Qx[i] = ek[n + m + m * m + i + n * c];
     } else {
+      const double* cQ = cost_at<n, m>(P, kk).cQ;
 #pragma unroll
-      for (int i = 0; i < n; i++) Qx[i] = P->cQ[i + n * c];
+      for (int i = 0; i < n; i++) Qx[i] = cQ[i + n * c];
     }
   };
   // wave B: knot kk's Q.x entry, Q.u and Q.uu column (the replayed ones in faithful mode), a knot ahead
@@ -526,7 +527,8 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         // ---------------------------------------------------------------- C: Q.ux, tmp1
         double Quxc[m];
 #pragma unroll
-        for (int i = 0; i < m; i++) Quxc[i] = replay ? Cqr[i] : Hdt[i];  // sqrt AL adds no Q.ux term (A.5)
+        for (int i = 0; i < m; i++)  // sqrt AL adds no Q.ux term (A.5); H dt per knot for a time-varying cost
+          Quxc[i] = replay ? Cqr[i] : (P->kc ? cost_at<n, m>(P, k).H[i + m * c] * dt : Hdt[i]);
         // Q.ux += tmp_u' tmp_x (backward_pass.jl:118), the sum wave B formed from S_{k+1}'s rows
 #pragma unroll
         for (int i = 0; i < m; i++) Quxc[i] += QXT[i + m * c];

@@ -441,15 +441,16 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   double Qxc[n], Quuc[m], Qu[m], Qxs;
   const double xc = xg[c];
   const int diag_mode = P->diag_cost;
+  const CostView C_ = cost_at<n, m>(P, TERM ? 0 : k);  // stage knot k's cost (a time-varying Objective)
   if (!TERM && diag_mode == 2) {
     // diagonal cost with +0.0 off-diagonals (host-checked): the per-lane constants are one
     // diagonal entry each, the rest literal zeros -- the same values the general path loads
-    const double Qcc = P->Q[c + n * c], qc = P->q[c];
-    const double qd = SQRT ? P->cQ[c + n * c] : Qcc * dt;
-    const double rd = SQRT ? P->cR[cu + m * cu] : P->R[cu + m * cu] * dt;
+    const double Qcc = C_.Q[c + n * c], qc = C_.q[c];
+    const double qd = SQRT ? C_.cQ[c + n * c] : Qcc * dt;
+    const double rd = SQRT ? C_.cR[cu + m * cu] : C_.R[cu + m * cu] * dt;
     Qxs = ((fma(Qcc, xc, 0.0) + qc) + 0.0) * dt;
 #pragma unroll
-    for (int i = 0; i < m; i++) Qu[i] = ((fma(P->R[i + m * i], ug[i], 0.0) + P->r[i]) + 0.0) * dt;
+    for (int i = 0; i < m; i++) Qu[i] = ((fma(C_.R[i + m * i], ug[i], 0.0) + C_.r[i]) + 0.0) * dt;
 #pragma unroll
     for (int i = 0; i < n; i++) Qxc[i] = (i == c) ? qd : 0.0;
 #pragma unroll
@@ -457,31 +458,31 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   } else if (!TERM) {
     double a = 0.0, bq = 0.0;
     if (diag_mode) {
-      a = fma(P->Q[c + n * c], xc, 0.0);
+      a = fma(C_.Q[c + n * c], xc, 0.0);
     } else {
 #pragma unroll
-      for (int j = 0; j < n; j++) a = fma(P->Q[c + n * j], xg[j], a);
+      for (int j = 0; j < n; j++) a = fma(C_.Q[c + n * j], xg[j], a);
 #pragma unroll
-      for (int j = 0; j < m; j++) bq = fma(P->H[j + m * c], ug[j], bq);
+      for (int j = 0; j < m; j++) bq = fma(C_.H[j + m * c], ug[j], bq);
     }
-    Qxs = ((a + P->q[c]) + bq) * dt;
+    Qxs = ((a + C_.q[c]) + bq) * dt;
 #pragma unroll
     for (int i = 0; i < m; i++) {
       double a2 = 0.0, b2 = 0.0;
       if (diag_mode) {
-        a2 = fma(P->R[i + m * i], ug[i], 0.0);
+        a2 = fma(C_.R[i + m * i], ug[i], 0.0);
       } else {
 #pragma unroll
-        for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
+        for (int j = 0; j < m; j++) a2 = fma(C_.R[i + m * j], ug[j], a2);
 #pragma unroll
-        for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
+        for (int j = 0; j < n; j++) b2 = fma(C_.H[i + m * j], xg[j], b2);
       }
-      Qu[i] = ((a2 + P->r[i]) + b2) * dt;
+      Qu[i] = ((a2 + C_.r[i]) + b2) * dt;
     }
 #pragma unroll
-    for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
+    for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;
 #pragma unroll
-    for (int i = 0; i < m; i++) Quuc[i] = SQRT ? P->cR[i + m * cu] : P->R[i + m * cu] * dt;
+    for (int i = 0; i < m; i++) Quuc[i] = SQRT ? C_.cR[i + m * cu] : C_.R[i + m * cu] * dt;
   } else {
     double a = 0.0;
     if (diag_mode) {
@@ -679,15 +680,16 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
   constexpr int NXL = (n + TQ - 1) / TQ;  // Q.x entries of this lane: tl + TQ j
   double Qxs[NXL], Quuc[m], Qu[m];
   const int diag_mode = P->diag_cost;
+  const CostView C_ = cost_at<n, m>(P, k);
   if (diag_mode == 2) {
 #pragma unroll
     for (int j = 0; j < NXL; j++) {
       const int cc = tl + TQ * j < n ? tl + TQ * j : 0;
-      Qxs[j] = ((fma(P->Q[cc + n * cc], xg[cc], 0.0) + P->q[cc]) + 0.0) * dt;
+      Qxs[j] = ((fma(C_.Q[cc + n * cc], xg[cc], 0.0) + C_.q[cc]) + 0.0) * dt;
     }
 #pragma unroll
-    for (int i = 0; i < m; i++) Qu[i] = ((fma(P->R[i + m * i], ug[i], 0.0) + P->r[i]) + 0.0) * dt;
-    const double rd = P->cR[cu + m * cu];
+    for (int i = 0; i < m; i++) Qu[i] = ((fma(C_.R[i + m * i], ug[i], 0.0) + C_.r[i]) + 0.0) * dt;
+    const double rd = C_.cR[cu + m * cu];
 #pragma unroll
     for (int i = 0; i < m; i++) Quuc[i] = (i == cu) ? rd : 0.0;
   } else {
@@ -696,30 +698,30 @@ __device__ __forceinline__ void quad_expand(const DevProblem* P, const DevBuffer
       const int cc = tl + TQ * j < n ? tl + TQ * j : 0;
       double a = 0.0, bq = 0.0;
       if (diag_mode) {
-        a = fma(P->Q[cc + n * cc], xg[cc], 0.0);
+        a = fma(C_.Q[cc + n * cc], xg[cc], 0.0);
       } else {
 #pragma unroll
-        for (int jj = 0; jj < n; jj++) a = fma(P->Q[cc + n * jj], xg[jj], a);
+        for (int jj = 0; jj < n; jj++) a = fma(C_.Q[cc + n * jj], xg[jj], a);
 #pragma unroll
-        for (int jj = 0; jj < m; jj++) bq = fma(P->H[jj + m * cc], ug[jj], bq);
+        for (int jj = 0; jj < m; jj++) bq = fma(C_.H[jj + m * cc], ug[jj], bq);
       }
-      Qxs[j] = ((a + P->q[cc]) + bq) * dt;
+      Qxs[j] = ((a + C_.q[cc]) + bq) * dt;
     }
 #pragma unroll
     for (int i = 0; i < m; i++) {
       double a2 = 0.0, b2 = 0.0;
       if (diag_mode) {
-        a2 = fma(P->R[i + m * i], ug[i], 0.0);
+        a2 = fma(C_.R[i + m * i], ug[i], 0.0);
       } else {
 #pragma unroll
-        for (int j = 0; j < m; j++) a2 = fma(P->R[i + m * j], ug[j], a2);
+        for (int j = 0; j < m; j++) a2 = fma(C_.R[i + m * j], ug[j], a2);
 #pragma unroll
-        for (int j = 0; j < n; j++) b2 = fma(P->H[i + m * j], xg[j], b2);
+        for (int j = 0; j < n; j++) b2 = fma(C_.H[i + m * j], xg[j], b2);
       }
-      Qu[i] = ((a2 + P->r[i]) + b2) * dt;
+      Qu[i] = ((a2 + C_.r[i]) + b2) * dt;
     }
 #pragma unroll
-    for (int i = 0; i < m; i++) Quuc[i] = P->cR[i + m * cu];
+    for (int i = 0; i < m; i++) Quuc[i] = C_.cR[i + m * cu];
   }
   const int p = AL ? P->knot_cnt[k] : 0;
   if (AL && p > 0) {
@@ -914,13 +916,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const int c = tlk < n ? tlk : 0, cu = tlk < m ? tlk : 0;
     const double* e = Eg + (size_t)k * NE;
     const int cnt = AL ? kcnt[k] : 0;
+    const CostView C_ = cost_at<n, m>(P, term ? 0 : k);
     Qxs = e[c];
     if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
 #pragma unroll
       for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
     } else {
 #pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
+      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;
     }
     if (!term) {
 #pragma unroll
@@ -930,7 +933,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const bool zterm = !SQRT && AL && cnt > 0;  // the std AL expansion's "+= cu'Iμcx" (an exact zero)
 #pragma unroll
       for (int i = 0; i < m; i++) {
-        const double h = P->H[i + m * c] * dt;
+        const double h = C_.H[i + m * c] * dt;
         Quxc[i] = zterm ? h + 0.0 : h;
       }
     } else {

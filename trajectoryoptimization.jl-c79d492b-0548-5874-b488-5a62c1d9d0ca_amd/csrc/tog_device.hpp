@@ -74,6 +74,10 @@ struct DevProblem {
   int pad1;
   double R_min_time;  // MinTimeCost weight (minimum-time problems; Q, R, H, q, r, Qf, qf are the base
                       // cost's, zero-padded to the augmented sizes)
+  // a time-varying Objective (tog_problem_desc.stage_costs): per stage knot [Q; R; H; q; r; c; cQ; cR]
+  // (compact n, m; cQ, cR the square-root expansion's factors), or null (the fields above at every knot)
+  const double* kc;
+  int kc_stride, kc_pad;
   const int* knot_off;  // [N] first row of knot k
   const int* knot_cnt;  // [N] rows at knot k (p_k)
   const ConRow* rows;
@@ -1251,43 +1255,63 @@ __host__ __device__ __forceinline__ void discrete_step(T* xn, const T* x, const 
 // DC: 0 = the cost's structure from P->diag_cost at run time; 1 = diagonal (the caller knows
 // P->diag_cost != 0); 2 = dense. A kernel that inlines only the diagonal form keeps x and u in registers
 // (the dense loops index them at run time).
+// Stage knot k's QuadraticCost (src/cost.jl:112-157): the problem's, or row k of a time-varying Objective's
+// table (DevProblem::kc). Matrices column-major with the compact n, m; cQ, cR the upper Cholesky factors of
+// Q dt and R dt (the square-root expansion, src/objective.jl:70-94).
+struct CostView {
+  const double *Q, *R, *H, *q, *r, *cQ, *cR;
+  double c;
+};
+template <int n, int m>
+__host__ __device__ constexpr int kc_stride_of() {
+  return 2 * n * n + 2 * m * m + m * n + n + m + 1;
+}
+template <int n, int m>
+__device__ __forceinline__ CostView cost_at(const DevProblem* P, int k) {
+  if (!P->kc) return CostView{P->Q, P->R, P->H, P->q, P->r, P->cQ, P->cR, P->c};
+  const double* b = P->kc + (size_t)k * kc_stride_of<n, m>();
+  constexpr int oR = n * n, oH = oR + m * m, oq = oH + m * n, orr = oq + n, oc = orr + m, ocQ = oc + 1, ocR = ocQ + n * n;
+  return CostView{b, b + oR, b + oH, b + oq, b + orr, b + ocQ, b + ocR, b[oc]};
+}
+
 template <int n, int m, int DC = 0>
-__device__ __forceinline__ double stage_cost_dt(const DevProblem* P, const double* x, const double* u, double dt) {
+__device__ __forceinline__ double stage_cost_dt(const DevProblem* P, int k, const double* x, const double* u, double dt) {
+  const CostView C = cost_at<n, m>(P, k);
   double xQx = 0.0, uRu = 0.0, qx = 0.0, ru = 0.0, uHx = 0.0;
   if (DC == 1 || (DC == 0 && P->diag_cost)) {
 #pragma unroll
-    for (int j = 0; j < n; j++) xQx = fma((0.5 * x[j]) * P->Q[j + n * j], x[j], xQx);
+    for (int j = 0; j < n; j++) xQx = fma((0.5 * x[j]) * C.Q[j + n * j], x[j], xQx);
 #pragma unroll
-    for (int j = 0; j < m; j++) uRu = fma((0.5 * u[j]) * P->R[j + m * j], u[j], uRu);
+    for (int j = 0; j < m; j++) uRu = fma((0.5 * u[j]) * C.R[j + m * j], u[j], uRu);
   } else {
 #pragma unroll 1
     for (int j = 0; j < n; j++) {
       double t = 0.0;
-      for (int i = 0; i < n; i++) t = fma(0.5 * x[i], P->Q[i + n * j], t);
+      for (int i = 0; i < n; i++) t = fma(0.5 * x[i], C.Q[i + n * j], t);
       xQx = fma(t, x[j], xQx);
     }
 #pragma unroll 1
     for (int j = 0; j < m; j++) {
       double t = 0.0;
-      for (int i = 0; i < m; i++) t = fma(0.5 * u[i], P->R[i + m * j], t);
+      for (int i = 0; i < m; i++) t = fma(0.5 * u[i], C.R[i + m * j], t);
       uRu = fma(t, u[j], uRu);
     }
 #pragma unroll 1
     for (int j = 0; j < n; j++) {
       double t = 0.0;
-      for (int i = 0; i < m; i++) t = fma(u[i], P->H[i + m * j], t);
+      for (int i = 0; i < m; i++) t = fma(u[i], C.H[i + m * j], t);
       uHx = fma(t, x[j], uHx);
     }
   }
 #pragma unroll
-  for (int i = 0; i < n; i++) qx = fma(P->q[i], x[i], qx);
+  for (int i = 0; i < n; i++) qx = fma(C.q[i], x[i], qx);
 #pragma unroll
-  for (int i = 0; i < m; i++) ru = fma(P->r[i], u[i], ru);
-  return ((((xQx + uRu) + qx) + ru) + P->c + uHx) * dt;
+  for (int i = 0; i < m; i++) ru = fma(C.r[i], u[i], ru);
+  return ((((xQx + uRu) + qx) + ru) + C.c + uHx) * dt;
 }
 template <int n, int m, int DC = 0>
-__device__ __forceinline__ double stage_cost(const DevProblem* P, const double* x, const double* u) {
-  return stage_cost_dt<n, m, DC>(P, x, u, P->dt);
+__device__ __forceinline__ double stage_cost(const DevProblem* P, int k, const double* x, const double* u) {
+  return stage_cost_dt<n, m, DC>(P, k, x, u, P->dt);
 }
 
 template <int n, int DC = 0>
@@ -1313,12 +1337,12 @@ __device__ __forceinline__ double terminal_cost(const DevProblem* P, const doubl
 // stage_cost(cost, x[1:n], u[1:m], h) + R_min_time u[end]^2 with dt = h = u[end]^2, terminal unchanged;
 // the zero-padded base matrices give the base cost of the leading parts bit for bit)
 template <class M, int DC = 0>
-__device__ __forceinline__ double stage_cost_m(const DevProblem* P, const double* x, const double* u) {
+__device__ __forceinline__ double stage_cost_m(const DevProblem* P, int k, const double* x, const double* u) {
   if constexpr (ModelTraits<M>::min_time) {
     const double h = u[M::m - 1];
-    return stage_cost_dt<M::n, M::m, DC>(P, x, u, h * h) + P->R_min_time * (h * h);
+    return stage_cost_dt<M::n, M::m, DC>(P, k, x, u, h * h) + P->R_min_time * (h * h);
   } else {
-    return stage_cost<M::n, M::m, DC>(P, x, u);
+    return stage_cost<M::n, M::m, DC>(P, k, x, u);
   }
 }
 template <class M, int DC = 0>

@@ -106,7 +106,7 @@ __device__ double traj_cost(const DevProblem* __restrict__ P, const DevBuffers& 
   constexpr int n = M::n, m = M::m;
   const int N = P->N, pmax = P->pmax;
   double J = 0.0, Jc = 0.0;
-  for (int k = 0; k < N - 1; k++) J += stage_cost_m<M>(P, Xs + (size_t)k * n, Us + (size_t)k * m);
+  for (int k = 0; k < N - 1; k++) J += stage_cost_m<M>(P, k, Xs + (size_t)k * n, Us + (size_t)k * m);
   J += terminal_cost_m<M>(P, Xs + (size_t)(N - 1) * n);
   if (!al) return J;
   const double* lam = Bf.lam + (size_t)b * N * pmax;
@@ -222,25 +222,26 @@ __device__ void expansion_gradient_entries(const DevProblem* __restrict__ P, con
     const double* u = term ? nullptr : U + (size_t)k * m;
     double q[W];
     if (!term) {
+      const CostView C_ = cost_at<n, m>(P, k);
       const double dt = MT ? u[m - 1] * u[m - 1] : P->dt;
       double gx[n], gu[m];
       for (int i = 0; i < n; i++) {
         double a = 0.0, c = 0.0;
-        for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], x[j], a);
-        for (int j = 0; j < m; j++) c = fma(P->H[j + m * i], u[j], c);
-        gx[i] = (a + P->q[i]) + c;
+        for (int j = 0; j < n; j++) a = fma(C_.Q[i + n * j], x[j], a);
+        for (int j = 0; j < m; j++) c = fma(C_.H[j + m * i], u[j], c);
+        gx[i] = (a + C_.q[i]) + c;
         q[i] = gx[i] * dt;
       }
       for (int i = 0; i < m; i++) {
         double a = 0.0, c = 0.0;
-        for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], u[j], a);
-        for (int j = 0; j < n; j++) c = fma(P->H[i + m * j], x[j], c);
-        gu[i] = (a + P->r[i]) + c;
+        for (int j = 0; j < m; j++) a = fma(C_.R[i + m * j], u[j], a);
+        for (int j = 0; j < n; j++) c = fma(C_.H[i + m * j], x[j], c);
+        gu[i] = (a + C_.r[i]) + c;
         q[n + i] = gu[i] * dt;
       }
       if constexpr (MT) {  // MinTimeCost (minimum_time.jl:155-188): Q.u[end] = τ(2ℓ1 + R), Q.x[end] = R x[end]
         const double R = P->R_min_time, tau = u[m - 1];
-        const double l1 = stage_cost_dt<n, m>(P, x, u, 1.0);
+        const double l1 = stage_cost_dt<n, m>(P, k, x, u, 1.0);
         q[n + m - 1] = tau * (2.0 * l1 + R);
         q[n - 1] = R * x[n - 1];
       }
@@ -828,35 +829,36 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
   // minimum time: dt = τ² with τ = u[end] (MinTimeCost cost_expansion!, minimum_time.jl:155-188)
   const double dt = (MT && !term) ? sh.uk[m - 1] * sh.uk[m - 1] : P->dt;
   if (!term) {
+    const CostView C_ = cost_at<n, m>(P, k);
     if (lane < n) {
       const int i = lane;
       double a = 0.0, bb = 0.0;
 #pragma unroll
-      for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], sh.xk[j], a);
+      for (int j = 0; j < n; j++) a = fma(C_.Q[i + n * j], sh.xk[j], a);
 #pragma unroll
-      for (int j = 0; j < m; j++) bb = fma(P->H[j + m * i], sh.uk[j], bb);
-      const double g = (a + P->q[i]) + bb;
+      for (int j = 0; j < m; j++) bb = fma(C_.H[j + m * i], sh.uk[j], bb);
+      const double g = (a + C_.q[i]) + bb;
       sh.Qx[i] = g * dt;
       if (MT) sh.mtx[i] = g;
     } else if (lane < n + m) {
       const int i = lane - n;
       double a = 0.0, bb = 0.0;
 #pragma unroll
-      for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], sh.uk[j], a);
+      for (int j = 0; j < m; j++) a = fma(C_.R[i + m * j], sh.uk[j], a);
 #pragma unroll
-      for (int j = 0; j < n; j++) bb = fma(P->H[i + m * j], sh.xk[j], bb);
-      const double g = (a + P->r[i]) + bb;
+      for (int j = 0; j < n; j++) bb = fma(C_.H[i + m * j], sh.xk[j], bb);
+      const double g = (a + C_.r[i]) + bb;
       sh.Qu[i] = g * dt;
       if (MT) sh.mtu[i] = g;
     }
-    for (int e = lane; e < n * n; e += WAVE) sh.Qxx[e] = SQRT ? P->cQ[e] : P->Q[e] * dt;
-    for (int e = lane; e < m * m; e += WAVE) sh.Quu[e] = SQRT ? P->cR[e] : P->R[e] * dt;
-    for (int e = lane; e < m * n; e += WAVE) sh.Qux[e] = P->H[e] * dt;
+    for (int e = lane; e < n * n; e += WAVE) sh.Qxx[e] = SQRT ? C_.cQ[e] : C_.Q[e] * dt;
+    for (int e = lane; e < m * m; e += WAVE) sh.Quu[e] = SQRT ? C_.cR[e] : C_.R[e] * dt;
+    for (int e = lane; e < m * n; e += WAVE) sh.Qux[e] = C_.H[e] * dt;
     if constexpr (MT) {
       // the τ / h entries: ℓ1 = stage_cost(cost, x, u) (no dt), tmp = 2τ Qu
       wsync();
       const double R = P->R_min_time, tau = sh.uk[m - 1];
-      const double l1 = stage_cost_dt<n, m>(P, sh.xk, sh.uk, 1.0);
+      const double l1 = stage_cost_dt<n, m>(P, k, sh.xk, sh.uk, 1.0);
       const double w = 2.0 * l1 + R, t2 = 2.0 * tau;
       if (lane < m - 1) {
         const double tmp = t2 * sh.mtu[lane];
@@ -1782,7 +1784,7 @@ __device__ bool rollout_cost(const DevProblem* __restrict__ P, const DevBuffers&
       gsum += mx;
     }
     // stage cost and AL terms of knot k-1 (x̄_{k-1}, ū_{k-1})
-    J += stage_cost_m<M, DC>(P, xb, ub);
+    J += stage_cost_m<M, DC>(P, k - 1, xb, ub);
     if (al) {
       const int cnt = RT.kcnt[k - 1];
       if (cnt) {
@@ -2139,7 +2141,7 @@ __global__ void __launch_bounds__(64) k_ls_spec_tail(const DevProblem* __restric
         }
 #pragma unroll
         for (int i = 0; i < m; i++) __builtin_nontemporal_store(ub[i], cw + cand_at(k - 1, i, cand_q<M>(), ncp));
-        J += stage_cost_m<M, DC>(P, xb, ub);
+        J += stage_cost_m<M, DC>(P, k - 1, xb, ub);
         if (al) {
           const int pc = RT.kcnt[k - 1];
           if (pc) {
@@ -2397,7 +2399,7 @@ __global__ void __launch_bounds__(192) k_ls_spec_tail2(const DevProblem* __restr
 #pragma unroll
             for (int i = 0; i < n; i++) __builtin_nontemporal_store(x[i], cw + cand_at(s, m + i, cand_q<M>(), ncp));
           }
-          J += stage_cost_m<M, DC>(P, x, u);
+          J += stage_cost_m<M, DC>(P, s, x, u);
         }
       }
       DPROF(22);
@@ -2805,7 +2807,7 @@ __global__ void __launch_bounds__(64) k_ls_fallback(const DevProblem* __restrict
   for (int k = lane; k < N; k += WAVE) {
     const double* x = X + (size_t)k * n;
     const double* u = (k < N - 1) ? U + (size_t)k * m : nullptr;
-    sk[k] = (k < N - 1) ? stage_cost_m<M>(P, x, u) : terminal_cost_m<M>(P, x);
+    sk[k] = (k < N - 1) ? stage_cost_m<M>(P, k, x, u) : terminal_cost_m<M>(P, x);
     const int cnt = al ? knot_count(P, k) : 0;
     const cptr<ConRow> rows = knot_rows(P, k);
     double lc = 0.0, cIc = 0.0;
@@ -2938,7 +2940,7 @@ __global__ void __launch_bounds__(64) k_al_outer(const DevProblem* __restrict__ 
   for (int k = lane; k < N; k += WAVE) {
     const double* x = X + (size_t)k * n;
     const double* u = (k < N - 1) ? U + (size_t)k * m : nullptr;
-    sk[k] = (k < N - 1) ? stage_cost_m<M>(P, x, u) : terminal_cost_m<M>(P, x);
+    sk[k] = (k < N - 1) ? stage_cost_m<M>(P, k, x, u) : terminal_cost_m<M>(P, x);
     const int cnt = knot_count(P, k);
     const cptr<ConRow> rows = knot_rows(P, k);
     double lc = 0.0, cIc = 0.0, e = 0.0, im = -INFINITY;
@@ -3105,21 +3107,22 @@ __global__ void __launch_bounds__(64) k_cost_expansion(const DevProblem* __restr
   const double* u = term ? nullptr : Bf.U + ((size_t)b * (N - 1) + k) * m;
   const double dt = P->dt;
   if (!term) {  // cost.jl:183-198
+    const CostView C_ = cost_at<n, m>(P, k);
     for (int i = 0; i < n; i++) {
       double a = 0.0, c = 0.0;
-      for (int j = 0; j < n; j++) a = fma(P->Q[i + n * j], x[j], a);
-      for (int j = 0; j < m; j++) c = fma(P->H[j + m * i], u[j], c);
-      Qx[i] = ((a + P->q[i]) + c) * dt;
+      for (int j = 0; j < n; j++) a = fma(C_.Q[i + n * j], x[j], a);
+      for (int j = 0; j < m; j++) c = fma(C_.H[j + m * i], u[j], c);
+      Qx[i] = ((a + C_.q[i]) + c) * dt;
     }
     for (int i = 0; i < m; i++) {
       double a = 0.0, c = 0.0;
-      for (int j = 0; j < m; j++) a = fma(P->R[i + m * j], u[j], a);
-      for (int j = 0; j < n; j++) c = fma(P->H[i + m * j], x[j], c);
-      Qu[i] = ((a + P->r[i]) + c) * dt;
+      for (int j = 0; j < m; j++) a = fma(C_.R[i + m * j], u[j], a);
+      for (int j = 0; j < n; j++) c = fma(C_.H[i + m * j], x[j], c);
+      Qu[i] = ((a + C_.r[i]) + c) * dt;
     }
-    for (int i = 0; i < n * n; i++) Qxx[i] = P->Q[i] * dt;
-    for (int i = 0; i < m * m; i++) Quu[i] = P->R[i] * dt;
-    for (int i = 0; i < m * n; i++) Qux[i] = P->H[i] * dt;
+    for (int i = 0; i < n * n; i++) Qxx[i] = C_.Q[i] * dt;
+    for (int i = 0; i < m * m; i++) Quu[i] = C_.R[i] * dt;
+    for (int i = 0; i < m * n; i++) Qux[i] = C_.H[i] * dt;
   } else {
     for (int i = 0; i < n * n; i++) Qxx[i] = P->Qf[i];
     for (int i = 0; i < n; i++) {

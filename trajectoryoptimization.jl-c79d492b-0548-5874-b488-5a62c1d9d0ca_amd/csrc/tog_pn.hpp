@@ -75,9 +75,14 @@ __device__ __forceinline__ void pn_sync() { __syncthreads(); }  // one-wave bloc
 // H⁻¹ diagonal (Diagonal(solver.H): Q·dt, R·dt, terminal Qf; cost.jl:214-228)
 __device__ __forceinline__ double pn_wx(const DevProblem* P, int k, int i) {
   const int n = P->n;
-  return 1.0 / (k < P->N - 1 ? P->Q[i + n * i] * P->dt : P->Qf[i + n * i]);
+  if (k == P->N - 1) return 1.0 / P->Qf[i + n * i];
+  const double* Q = P->kc ? P->kc + (size_t)k * P->kc_stride : P->Q;  // a time-varying Objective's knot k
+  return 1.0 / (Q[i + n * i] * P->dt);
 }
-__device__ __forceinline__ double pn_wu(const DevProblem* P, int i) { return 1.0 / (P->R[i + P->m * i] * P->dt); }
+__device__ __forceinline__ double pn_wu(const DevProblem* P, int k, int i) {
+  const double* R = P->kc ? P->kc + (size_t)k * P->kc_stride + P->n * P->n : P->R;
+  return 1.0 / (R[i + P->m * i] * P->dt);
+}
 
 // dynamics_constraints! + update_constraints! at (X, U): dynamics rows into yd, constraint values
 // into C (projected_newton.jl:36-44,67-73). A lane per knot.
@@ -185,7 +190,7 @@ __device__ void pn_build_S(const DevProblem* P, const DevBuffers& Bf, long long 
       const int i = e % sb, l = e / sb;
       double acc = 0.0;
       for (int v = 0; v < nv; v++) {
-        const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, v - n);
+        const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, j, v - n);
         acc = fma(Yz[i + SM * v], wv * Yz[l + SM * v], acc);
       }
       if (bb < N && i < n && i == l) acc = acc + pn_wx(P, j + 1, i);
@@ -383,7 +388,7 @@ __device__ void pn_trial(const DevProblem* P, const DevBuffers& Bf, long long b,
       if (v < n) t = (j == 0) ? w.V(w.xv, 0)[v] : -w.V(w.xv, j)[v];
       const double* lb = w.V(w.xv, bb);
       for (int i = 0; i < w.sz[bb]; i++) t = fma(Yz[i + SM * v], lb[i], t);
-      const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, v - n);
+      const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, j, v - n);
       const double dz = -(wv * t);
       if (v < n)
         Xt[(size_t)j * n + v] = X[(size_t)j * n + v] + alpha * dz;

@@ -686,48 +686,94 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   P.nrows = h->nrows;
   P.B = h->B;
   P.dt = d->dt;
-  memcpy(P.Q, d->Q, sizeof(double) * n * n);
-  memcpy(P.R, d->R, sizeof(double) * m * m);
-  memcpy(P.H, d->H, sizeof(double) * m * n);
-  memcpy(P.q, d->q, sizeof(double) * n);
-  memcpy(P.r, d->r, sizeof(double) * m);
-  P.c = d->c;
+  // the stage cost(s): one for every knot, or a time-varying Objective's table (desc->stage_costs, rows
+  // [Q; R; H; q; r; c]); the device table adds each knot's square-root factors cQ, cR (DevProblem::kc)
+  const int nc_in = n * n + m * m + m * n + n + m + 1, kst = 2 * n * n + 2 * m * m + m * n + n + m + 1;
+  const int nk = d->stage_costs ? N - 1 : 1;
+  std::vector<double> kc((size_t)nk * kst, 0.0);
+  for (int k = 0; k < nk; k++) {
+    double* o = kc.data() + (size_t)k * kst;
+    if (d->stage_costs) {
+      memcpy(o, d->stage_costs + (size_t)k * nc_in, sizeof(double) * nc_in);
+    } else {
+      memcpy(o, d->Q, sizeof(double) * n * n);
+      memcpy(o + n * n, d->R, sizeof(double) * m * m);
+      memcpy(o + n * n + m * m, d->H, sizeof(double) * m * n);
+      memcpy(o + n * n + m * m + m * n, d->q, sizeof(double) * n);
+      memcpy(o + n * n + m * m + m * n + n, d->r, sizeof(double) * m);
+      o[nc_in - 1] = d->c;
+    }
+  }
+  auto kQ = [&](int k) { return kc.data() + (size_t)k * kst; };
+  auto kR = [&](int k) { return kQ(k) + n * n; };
+  auto kH = [&](int k) { return kR(k) + m * m; };
+  auto kcQ = [&](int k) { return kQ(k) + nc_in; };
+  auto kcR = [&](int k) { return kcQ(k) + n * n; };
+  // P's own cost fields hold knot 0's (the shared one without a table)
+  memcpy(P.Q, kQ(0), sizeof(double) * n * n);
+  memcpy(P.R, kR(0), sizeof(double) * m * m);
+  memcpy(P.H, kH(0), sizeof(double) * m * n);
+  memcpy(P.q, kH(0) + m * n, sizeof(double) * n);
+  memcpy(P.r, kH(0) + m * n + n, sizeof(double) * m);
+  P.c = kQ(0)[nc_in - 1];
   memcpy(P.Qf, d->Qf, sizeof(double) * n * n);
   memcpy(P.qf, d->qf, sizeof(double) * n);
   P.cf = d->cf;
   {
-    double Qdt[NMAX * NMAX], Rdt[MMAX * MMAX];
-    for (int i = 0; i < n * n; i++) Qdt[i] = P.Q[i] * P.dt;
-    for (int i = 0; i < m * m; i++) Rdt[i] = P.R[i] * P.dt;
-    bool ok = host_chol_upper(Qdt, n, P.cQ) && host_chol_upper(Rdt, m, P.cR) && host_chol_upper(P.Qf, n, P.cQf);
+    bool ok = host_chol_upper(P.Qf, n, P.cQf);
+    for (int k = 0; k < nk; k++) {
+      double Qdt[NMAX * NMAX], Rdt[MMAX * MMAX];
+      for (int i = 0; i < n * n; i++) Qdt[i] = kQ(k)[i] * P.dt;
+      for (int i = 0; i < m * m; i++) Rdt[i] = kR(k)[i] * P.dt;
+      ok = host_chol_upper(Qdt, n, kcQ(k)) && host_chol_upper(Rdt, m, kcR(k)) && ok;
+    }
+    memcpy(P.cQ, kcQ(0), sizeof(double) * n * n);
+    memcpy(P.cR, kcR(0), sizeof(double) * m * m);
     P.sqrt_ok = ok ? 1 : 0;
     bool diag = true;
     for (int j = 0; j < n; j++)
       for (int i = 0; i < n; i++)
-        if (i != j && (P.Q[i + n * j] != 0.0 || P.Qf[i + n * j] != 0.0)) diag = false;
-    for (int j = 0; j < m; j++)
-      for (int i = 0; i < m; i++)
-        if (i != j && P.R[i + m * j] != 0.0) diag = false;
-    for (int i = 0; i < m * n; i++)
-      if (P.H[i] != 0.0) diag = false;
+        if (i != j && P.Qf[i + n * j] != 0.0) diag = false;
+    for (int k = 0; k < nk; k++) {
+      for (int j = 0; j < n; j++)
+        for (int i = 0; i < n; i++)
+          if (i != j && kQ(k)[i + n * j] != 0.0) diag = false;
+      for (int j = 0; j < m; j++)
+        for (int i = 0; i < m; i++)
+          if (i != j && kR(k)[i + m * j] != 0.0) diag = false;
+      for (int i = 0; i < m * n; i++)
+        if (kH(k)[i] != 0.0) diag = false;
+    }
     // 2: diagonal with every off-diagonal entry (and H, and the factors' off-diagonals) +0.0 and
     // dt > 0, so the kernels may use literal zeros for them and stay bit-identical
     bool pz = diag && P.dt > 0.0;
-    auto offdiag_pz = [&](const double* A, int k) {
-      for (int j = 0; j < k; j++)
-        for (int i = 0; i < k; i++)
-          if (i != j && (A[i + k * j] != 0.0 || std::signbit(A[i + k * j]))) return false;
+    auto offdiag_pz = [&](const double* A, int kk) {
+      for (int j = 0; j < kk; j++)
+        for (int i = 0; i < kk; i++)
+          if (i != j && (A[i + kk * j] != 0.0 || std::signbit(A[i + kk * j]))) return false;
       return true;
     };
-    if (pz) pz = offdiag_pz(P.Q, n) && offdiag_pz(P.Qf, n) && offdiag_pz(P.R, m);
-    if (pz && ok) pz = offdiag_pz(P.cQ, n) && offdiag_pz(P.cQf, n) && offdiag_pz(P.cR, m);
-    for (int i = 0; pz && i < m * n; i++)
-      if (std::signbit(P.H[i])) pz = false;
+    if (pz) pz = offdiag_pz(P.Qf, n) && (!ok || offdiag_pz(P.cQf, n));
+    for (int k = 0; pz && k < nk; k++) {
+      pz = offdiag_pz(kQ(k), n) && offdiag_pz(kR(k), m);
+      if (pz && ok) pz = offdiag_pz(kcQ(k), n) && offdiag_pz(kcR(k), m);
+      for (int i = 0; pz && i < m * n; i++)
+        if (std::signbit(kH(k)[i])) pz = false;
+    }
     P.diag_cost = diag ? (pz ? 2 : 1) : 0;
     h->buf.cost_diag = P.diag_cost;
     if (opts->square_root && !ok) {
       return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
     }
+  }
+  P.kc = nullptr;
+  P.kc_stride = kst;
+  P.kc_pad = 0;
+  if (d->stage_costs) {
+    double* dkc = nullptr;
+    if ((rc = dalloc(h, &dkc, kc.size()))) return rc;
+    HIPCHECK(hipMemcpy(dkc, kc.data(), sizeof(double) * kc.size(), hipMemcpyHostToDevice));
+    P.kc = dkc;
   }
   P.o = *opts;
   P.R_min_time = (d->flags & TOG_PROB_MIN_TIME) ? d->R_min_time : 0.0;

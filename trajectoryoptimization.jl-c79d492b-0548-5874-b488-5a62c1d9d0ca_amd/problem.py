@@ -444,8 +444,10 @@ def generic_cost(stage_body: str, terminal_body: str, n: int, m: int, name: str 
 
 
 class Objective:
-    """``Objective(costs)`` (src/objective.jl:15-29). The HIP path requires one stage cost
-    shared by knots 1..N-1 and one terminal cost (the form every config uses)."""
+    """``Objective(costs)`` (src/objective.jl:15-29): one cost per knot, the last the terminal cost.
+    Knots 1..N-1 may share one QuadraticCost (the form every config uses) or carry their own
+    (a time-varying objective: ``stage_table`` goes to the device as tog_problem_desc.stage_costs,
+    DevProblem::kc); ``stage`` is knot 1's cost."""
 
     def __init__(self, cost, cost_terminal=None, N=None):
         if isinstance(cost, list):
@@ -457,9 +459,11 @@ class Objective:
             costs = [cost] * (N - 1) + [term]
         self.cost = costs
         stage = costs[0]
-        for c in costs[:-1]:
-            if c is not stage and not _same_cost(c, stage):
-                raise NotImplementedError("time-varying stage costs are not built (one stage cost per problem)")
+        self.varying = any(c is not stage and not _same_cost(c, stage) for c in costs[:-1])
+        if self.varying:
+            sz = stage.sizes()
+            if not all(isinstance(c, QuadraticCost) and c.sizes() == sz for c in costs[:-1]):
+                raise ValueError("a time-varying objective's stage costs must be QuadraticCosts of one size")
         self.stage = stage
         self.terminal = costs[-1]
 
@@ -468,6 +472,32 @@ class Objective:
 
     def __getitem__(self, k):
         return self.cost[k]
+
+    def stage_table(self, m=None):
+        """The (N-1, nc) per-knot rows [Q; R; H; q; r; c] (matrices column-major) of a time-varying
+        objective, None when every stage knot shares one cost."""
+        if not self.varying:
+            return None
+        rows = []
+        for c in self.cost[:-1]:
+            n = c.Q.shape[0]
+            R = c.R if c.R.size else np.zeros((m, m))
+            mm = R.shape[0]
+            H = c.H if c.H.size else np.zeros((mm, n))
+            r = c.r if c.r.size else np.zeros(mm)
+            rows.append(np.concatenate([c.Q.ravel(order="F"), R.ravel(order="F"), H.ravel(order="F"), c.q, r,
+                                        [c.c]]))
+        return np.stack(rows)
+
+    def map_stage(self, f):
+        """A new Objective with f applied to each stage cost (knots sharing a cost keep sharing one)."""
+        memo = {}
+        out = []
+        for c in self.cost[:-1]:
+            if id(c) not in memo:
+                memo[id(c)] = f(c)
+            out.append(memo[id(c)])
+        return out
 
 
 def _same_cost(a, b):
@@ -883,7 +913,7 @@ class Problem:
         return abi.DescBuilder(self.model.model_id, self.model.integration, n, m, N, self.dt, stage.Q, R, stage.H,
                                stage.q, stage.r, stage.c, term.Q, term.q, term.c, sets, knot_set, batch=self.B,
                                flags=flags, user_model=self.model.plugin.ptr if self.model.plugin else None,
-                               R_min_time=getattr(self, "R_min_time", 0.0))
+                               R_min_time=getattr(self, "R_min_time", 0.0), stage_costs=self.obj.stage_table(m))
 
 
 def _validate_time(N, tf, dt):
@@ -985,14 +1015,17 @@ def infeasible_problem(prob: Problem, R_inf: float = 1.0) -> Problem:
     the device by ``slack_controls`` (infeasible.jl:63-80) when the solver is set up.
     """
     n, m, N = prob.model.n, prob.model.m, prob.N
-    stage, term = prob.obj.stage, prob.obj.terminal
-    R = np.zeros((m + n, m + n))
-    R[:m, :m] = stage.R
-    R[m:, m:] = R_inf * np.eye(n) / prob.dt
-    H = np.vstack([stage.H, np.zeros((n, n))])
-    r = np.concatenate([stage.r, np.zeros(n)])
-    cost_inf = QuadraticCost(stage.Q, R, H, stage.q, r, stage.c)
-    obj = Objective(cost_inf, term.copy(), N=N)
+    term = prob.obj.terminal
+
+    def cost_inf(stage):
+        R = np.zeros((m + n, m + n))
+        R[:m, :m] = stage.R
+        R[m:, m:] = R_inf * np.eye(n) / prob.dt
+        H = np.vstack([stage.H, np.zeros((n, n))])
+        r = np.concatenate([stage.r, np.zeros(n)])
+        return QuadraticCost(stage.Q, R, H, stage.q, r, stage.c)
+
+    obj = Objective(prob.obj.map_stage(cost_inf), term.copy())
     con_inf = infeasible_constraints(n, m)
     cons = Constraints(N)
     constrained = prob.is_constrained()
@@ -1074,7 +1107,7 @@ def minimum_time_problem(prob: Problem, R_min_time: float = 1.0, dt_max: float =
     augmented sizes plus R_min_time h², on the device), ``mintime_constraints``,
     U = [U; √dt], X = [X; √dt], x0 = [x0; 0]."""
     n, m, N = prob.model.n, prob.model.m, prob.N
-    stage, term = prob.obj.stage, prob.obj.terminal
+    term = prob.obj.terminal
 
     def pad(A, r, c):
         out = np.zeros((r, c))
@@ -1083,13 +1116,16 @@ def minimum_time_problem(prob: Problem, R_min_time: float = 1.0, dt_max: float =
             out[:A.shape[0], :A.shape[1]] = A
         return out
 
-    R = stage.R if stage.R.size else np.zeros((m, m))
-    st = QuadraticCost.__new__(QuadraticCost)
-    st._padded = True  # MinTimeCost's base cost on [x; τ], [u; h]: R is singular by construction
-    st.__init__(pad(stage.Q, n + 1, n + 1), pad(R, m + 1, m + 1), pad(stage.H, m + 1, n + 1),
-                np.append(stage.q, 0.0), np.append(stage.r if stage.r.size else np.zeros(m), 0.0), stage.c)
+    def cost_mt(stage):
+        R = stage.R if stage.R.size else np.zeros((m, m))
+        st = QuadraticCost.__new__(QuadraticCost)
+        st._padded = True  # MinTimeCost's base cost on [x; τ], [u; h]: R is singular by construction
+        st.__init__(pad(stage.Q, n + 1, n + 1), pad(R, m + 1, m + 1), pad(stage.H, m + 1, n + 1),
+                    np.append(stage.q, 0.0), np.append(stage.r if stage.r.size else np.zeros(m), 0.0), stage.c)
+        return st
+
     tm = QuadraticCost(pad(term.Q, n + 1, n + 1), None, None, np.append(term.q, 0.0), None, term.c)
-    obj = Objective(st, tm, N=N)
+    obj = Objective(prob.obj.map_stage(cost_mt), tm)
     x0 = np.hstack([prob.x0, np.zeros((prob.B, 1))])
     p = Problem(add_min_time_controls(prob.model), obj, constraints=mintime_constraints(prob, dt_max, dt_min),
                 x0=x0 if prob.batched else x0[0], xf=np.append(prob.xf, 0.0), N=N, dt=prob.dt)
