@@ -113,3 +113,21 @@ def test_full_size_shard_properties(tog, gpu, gold):
     for b in range(4):
         assert np.array_equal(gp._X[b], gold["X"][b]) and np.array_equal(gp._U[b], gold["U"][b]), b
         assert st["iterations_total"][b] == int(gold["stats"][b, A.STAT_TOTAL_STEPS]), b
+
+
+@pytest.mark.gpu
+def test_packed_records_equal_dense(tog, gpu, monkeypatch):
+    """The std AL expansion records carry only the Q.xx entries a stage row can change (DevProblem::qpat:
+    for config 4, the x-y-z block of the cylinders and spheres and the bounded states' diagonal); the backward
+    pass rebuilds the others as Q dt + 0.0, which is what the expansion computed for them. A solve with packed
+    records equals one with dense records (TOG_DENSE_RECORDS=1) bit for bit."""
+    prob, opts = tog.Problems.config_quad_maze(B=24, N=201)
+    out = []
+    for dense in (False, True):
+        if dense:
+            monkeypatch.setenv("TOG_DENSE_RECORDS", "1")
+        gp = prob.copy()
+        s = tog.solve_b(gp, opts)
+        out.append((gp._X, gp._U, s.handle.get(tog.abi.FIELD_STATS)))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)

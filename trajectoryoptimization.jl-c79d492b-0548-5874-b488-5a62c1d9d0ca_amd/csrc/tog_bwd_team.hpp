@@ -632,8 +632,17 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   int nxk = 0;
   if (AL && SQRT) nxk = P->knot_nx[k];
   if (colx && knot_dense<SQRT, AL>(k, N, p, nxk)) {
+    if (!SQRT && !TERM && P->qpat_on) {
+      // packed record: column tl's pattern entries only (DevProblem::qpat); the others are Q dt + 0.0
+      const unsigned int pc = P->qpat[tl];
+      double* eq = e + n + m + m * m + P->qoff[tl];
 #pragma unroll
-    for (int i = 0; i < n; i++) e[n + m + m * m + i + n * tl] = Qxc[i];
+      for (int i = 0; i < n; i++)
+        if (pc >> i & 1u) eq[__builtin_popcount(pc & ((1u << i) - 1u))] = Qxc[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < n; i++) e[n + m + m * m + i + n * tl] = Qxc[i];
+    }
   }
 }
 
@@ -919,8 +928,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const CostView C_ = cost_at<n, m>(P, term ? 0 : k);
     Qxs = e[c];
     if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
+      if (!SQRT && !term && P->qpat_on) {
+        // packed record (k_expand_team): the pattern entries; every other entry went through the
+        // expansion as Q dt + (an exact zero row sum)
+        const unsigned int pc = P->qpat[c];
+        const double* eq = e + n + m + m * m + P->qoff[c];
 #pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+        for (int i = 0; i < n; i++)
+          Qxc[i] = (pc >> i & 1u) ? eq[__builtin_popcount(pc & ((1u << i) - 1u))] : C_.Q[i + n * c] * dt + 0.0;
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;

@@ -766,6 +766,30 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
       return fail(TOG_ERR_ARG, "cost Hessians must be PD for the sqrt backward pass (objective.jl:70-94)");
     }
   }
+  // packed std AL expansion records: the Q.xx entries a stage row can change (row_grad's state indices)
+  {
+    unsigned int pat[NMAX] = {0};
+    for (const ConRow& r : rows) {
+      unsigned int sx = 0;
+      switch (r.type) {
+        case ROW_XMAX: case ROW_XMIN: case ROW_GOAL: case ROW_MT_EQ: sx = 1u << r.idx; break;
+        case ROW_UMAX: case ROW_UMIN: case ROW_USLACK: break;
+        case ROW_CIRCLE: sx = 3u; break;
+        case ROW_SPHERE: sx = 7u; break;
+        default: sx = (1u << n) - 1u;  // user rows: dense
+      }
+      for (int c = 0; c < n; c++)
+        if (sx >> c & 1u) pat[c] |= sx;
+    }
+    int off = 0;
+    for (int c = 0; c < n; c++) {
+      P.qpat[c] = pat[c];
+      P.qoff[c] = off;
+      off += __builtin_popcount(pat[c]);
+    }
+    P.qpat_n = off;
+    P.qpat_on = (off < n * n && getenv("TOG_DENSE_RECORDS") == nullptr) ? 1 : 0;
+  }
   P.kc = nullptr;
   P.kc_stride = kst;
   P.kc_pad = 0;
