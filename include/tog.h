@@ -511,8 +511,8 @@ void tog_default_altro_options(tog_altro_options* opts);
    (the infeasible / minimum-time problem's solve); stats_resolve (TOG_NSTATS, B): the feasible resolve;
    stats_pn (TOG_PN_NSTATS, B): projected Newton; each may be NULL. Host pointers, blocking. A trajectory
    whose forward pass reported TOG_TRAJ_COST_INCREASED (the reference's error) carries the flag in its
-   stats row. Not built: infeasible start + minimum time, projected Newton on those problems
-   (TOG_ERR_UNSUPPORTED). */
+   stats row. Projected Newton runs on the infeasible-start problem too (models with n + m + n <= 24). Not
+   built: infeasible start + minimum time, projected Newton on the minimum-time problem (TOG_ERR_UNSUPPORTED). */
 int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
                         const double* x0, double* X, double* U, double* h, double* stats, double* stats_resolve,
                         double* stats_pn);

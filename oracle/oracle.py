@@ -273,6 +273,8 @@ def solve_altro_infeasible(prob, opts, b=0):
     si = OracleSolver(pinf, opts, b)
     si.slack_controls()
     si.solve()
+    if opts.projected_newton:  # altro_methods.jl:31-39: phase 2 on the infeasible problem
+        si.solve_pn(opts.opts_pn)
     X = si.get("X")
     U = si.get("U")[:, :m].copy()
     sf = None

@@ -365,3 +365,47 @@ def test_gpu_infeasible_kuka(tog, oracle, gpu):
         assert rel(pk._X[b], Xo) < TOL_SOLVE, b
         assert rel(pk._U[b], Uo) < TOL_SOLVE, b
         assert int(solver.stats["iterations_total"][b]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS]), b
+
+
+def _pn_opts(tog, resolve):
+    opts = pendulum_opts(tog, resolve)
+    opts.projected_newton = True
+    opts.projected_newton_tolerance = 1e-2
+    opts.opts_pn.n_steps = 4
+    opts.opts_pn.feasibility_tolerance = 1e-8
+    return opts
+
+
+def test_oracle_infeasible_projected_newton(tog, oracle):
+    """ALTRO phase 2 on the infeasible-start problem (altro_methods.jl:31-39 runs solve!(prob_altro,
+    solver_pn) on the infeasible problem): after the AL phase stopped at projected_newton_tolerance, the
+    projection drives the infeasible problem's violation (the slack rows included) below the AL phase's."""
+    prob = pendulum_line(tog, True)
+    opts = _pn_opts(tog, False)
+    tog.solvers._altro_pn_tolerances(opts)
+    pinf = tog.infeasible_problem(prob, opts.R_inf)
+    si = oracle.OracleSolver(pinf, opts)
+    si.slack_controls()
+    si.solve()
+    c_al = si.max_violation()
+    st = si.solve_pn(opts.opts_pn)
+    assert st[tog.abi.PN_STEPS] >= 1
+    assert si.max_violation() < c_al
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("resolve", [False, True])
+def test_gpu_infeasible_projected_newton(tog, oracle, gpu, resolve):
+    """solve_b(prob, ALTROSolverOptions(projected_newton=true)) from an initial state trajectory: the
+    device's AL phase, projected Newton on Infeasible<Pendulum> (k_pn_*), process_results! and the resolve
+    against the oracle's same flow: X, U to the projected Newton tolerance of test_projected_newton.py
+    (1e-13) without the resolve, 1e-6 with it."""
+    prob = pendulum_line(tog, True)
+    opts = _pn_opts(tog, resolve)
+    ref = prob.copy()
+    solver = tog.solve_b(prob, opts)
+    assert solver.stats["time_pn"] > 0.0
+    Xo, Uo, si, sf = oracle.solve_altro_infeasible(ref, opts)
+    tol = TOL_SOLVE if resolve else TOL_STEP
+    assert rel(prob.X, Xo) < tol and rel(prob.U, Uo) < tol
+    assert int(solver.stats_pn["iterations"][0]) >= 1

@@ -79,11 +79,12 @@ def test_altro_pn_tolerances(tog):
     assert opts.opts_al.constraint_tolerance == tol0
 
 
-def test_pn_rejects_infeasible_start(tog):
+def test_pn_accepts_infeasible_start(tog):
+    """Round 5: phase 2 on the infeasible-start problem is built (tests/test_infeasible.py
+    test_gpu_infeasible_projected_newton); the host check lets it through."""
     prob = tog.Problems.pendulum()
     prob.X = tog.line_trajectory(prob.x0[0], prob.xf, prob.N)
-    with pytest.raises(NotImplementedError):
-        tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
+    tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
 
 
 def test_pn_rejects_min_time(tog):

@@ -53,7 +53,8 @@ def main(d):
 
 
 GROUPS = {"backward": ("k_bwd_team", "k_backward"), "forward": ("k_ls_spec", "k_ls_compact", "k_ls_commit", "k_ls_decide", "k_ls_apply", "k_ls_book"),
-          "jacobian": ("k_jacobian",)}
+          "jacobian": ("k_jacobian", "k_kuka_points", "k_kuka_sjac", "k_kuka_chain"),
+          "expansion": ("k_expand_team", "k_expand_u")}
 
 
 def traffic(d):

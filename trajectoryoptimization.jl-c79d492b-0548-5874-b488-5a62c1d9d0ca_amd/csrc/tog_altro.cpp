@@ -134,8 +134,8 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
   const bool infeasible = given == B && B > 0;
   const bool min_time = (desc->flags & TOG_PROB_TF_MIN) != 0;
   if (infeasible && min_time) return tog__fail(TOG_ERR_UNSUPPORTED, "infeasible start + minimum time");
-  if (opts->projected_newton && (infeasible || min_time))
-    return tog__fail(TOG_ERR_UNSUPPORTED, "projected Newton on the infeasible-start or minimum-time problem");
+  if (opts->projected_newton && min_time)
+    return tog__fail(TOG_ERR_UNSUPPORTED, "projected Newton on the minimum-time problem");
   if (opts->max_steps < 0) return tog__fail(TOG_ERR_ARG, "max_steps must be >= 0");
   tog_options oal = opts->opts_al;
   if (opts->projected_newton) {  // altro_methods.jl:5-13
@@ -167,11 +167,29 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     const double ta = now_s();
     if ((rc = run(&di.d, &oal, device, x0, Ui.data(), X, true, TOG_MODE_AL, H1, opts->max_steps, hcap))) return rc;
     R->time_al = now_s() - ta;
-    std::vector<double> Xi(nX * B);
-    if ((rc = tog_get(H1.h, TOG_FIELD_X, Xi.data())) || (rc = tog_get(H1.h, TOG_FIELD_U, Ui.data()))) return rc;
-    if ((rc = read_al(H1.h, R))) return rc;
     const std::vector<char> err = raised(H1.h, B, rc);
     if (rc) return rc;
+    if (opts->projected_newton) {
+      // solve!(prob_altro, solver.solver_pn) on the infeasible problem (altro_methods.jl:31-39); a raised
+      // trajectory never gets there (its X, U go back to the caller's below)
+      std::vector<double> pn((size_t)TOG_PN_NSTATS * B);
+      const double tp = now_s();
+      if ((rc = tog_solve_pn(H1.h, &opts->opts_pn, pn.data()))) return rc;
+      R->time_pn = now_s() - tp;
+      if (R->hist_pn && (rc = tog_get_pn_history(H1.h, R->hist_pn, nullptr))) return rc;
+      const size_t np = 2 * (size_t)opts->opts_pn.n_steps;
+      for (long long b = 0; b < B; b++) {
+        if (!err[b]) continue;
+        memset(pn.data() + (size_t)TOG_PN_NSTATS * b, 0, sizeof(double) * TOG_PN_NSTATS);
+        if (R->hist_pn)
+          for (size_t i = 0; i < np; i++) R->hist_pn[np * b + i] = NAN;
+      }
+      if (R->stats_pn) memcpy(R->stats_pn, pn.data(), sizeof(double) * pn.size());
+    }
+    std::vector<double> Xi(nX * B);
+    if ((rc = tog_get(H1.h, TOG_FIELD_X, Xi.data())) || (rc = tog_get(H1.h, TOG_FIELD_U, Ui.data()))) return rc;
+    // (the statistics rows after projected Newton: its TOG_TRAJ_PN_ERROR lands in the flags)
+    if ((rc = read_al(H1.h, R))) return rc;
     // process_results!: X and the model controls U[1:m]
     memcpy(X, Xi.data(), sizeof(double) * nX * B);
     for (long long b = 0; b < B; b++)

@@ -97,6 +97,7 @@ template <class M>
 __host__ __device__ constexpr int ne_of() {
   return M::n + M::m + M::m * M::m + M::n * M::n;
 }
+constexpr int QPK = 4;  // packed-pattern rows per column the std expansion's row loop specialises for
 template <bool SQRT, bool AL>
 __device__ __forceinline__ bool knot_dense(int k, int N, int cnt, int nx) {
   return k == N - 1 || (AL && (SQRT ? nx > 0 : cnt > 0));
@@ -501,6 +502,7 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
     }
   }
   const int p = AL ? P->knot_cnt[k] : 0;
+  bool packed = false;  // the packed Q.xx record is written (std AL, DevProblem::qpat)
   if (AL && p > 0) {
     // rows area after the 8-lane QR bus
     RowInfo* rows = reinterpret_cast<RowInfo*>(tlds + 48);
@@ -515,7 +517,53 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
     team_rows<M>(Bf, b, k, N, pmax, p, P->rows + P->knot_off[k], xs, TERM ? nullptr : us, rows, xr, ur, nx, nu,
                  team, tl, TEAM);
     team_sync();
-    if (!SQRT) {
+    if (!SQRT && !TERM && P->qpat_on && P->qpat_max <= QPK) {
+      // the same sums over the packed pattern (DevProblem::qpat): tX[i] can only change at column c's
+      // pattern rows, so the row loop tests an entry's index against those (at most QPK) instead of all n;
+      // every (row, entry) pair adds to the same sum in the same order. The record takes Q dt + the sum at
+      // the pattern rows (the other rows are Q dt + 0.0, rebuilt by the backward pass)
+      const unsigned int pc = colx ? as_const(P->qpat)[c] : 0u;
+      int pidx[QPK];
+      {
+        unsigned int r_ = pc;
+#pragma unroll
+        for (int j = 0; j < QPK; j++) {
+          pidx[j] = r_ ? __builtin_ctz(r_) : -1;
+          r_ &= r_ - 1u;
+        }
+      }
+      double tP[QPK], tUu[m];
+#pragma unroll
+      for (int j = 0; j < QPK; j++) tP[j] = 0.0;
+#pragma unroll
+      for (int i = 0; i < m; i++) tUu[i] = 0.0;
+      for (int r = 0; r < p; r++) {
+        const RowInfo& ri = rows[r];
+        const double vxc = colx ? row_at(ri, c) : 0.0;
+        const double vuc = colu ? row_at(ri, n + cu) : 0.0;
+        if (vxc == 0.0 && vuc == 0.0) continue;
+        for (int z = 0; z < ri.nnz; z++) {
+          const int id = ri.idx[z];
+          const double vw = ri.v[z] * ri.w;
+#pragma unroll
+          for (int j = 0; j < QPK; j++)
+            if (id == pidx[j] && vxc != 0.0) tP[j] = fma(vw, vxc, tP[j]);
+#pragma unroll
+          for (int i = 0; i < m; i++)
+            if (id == n + i && vuc != 0.0) tUu[i] = fma(vw, vuc, tUu[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < m; i++) Quuc[i] += tUu[i];
+      if (colx) {
+        const cptr<double> cQd = as_const(C_.Q);
+        double* eq = Bf.E + ((size_t)b * N + k) * NE + n + m + m * m + as_const(P->qoff)[c];
+#pragma unroll
+        for (int j = 0; j < QPK; j++)
+          if (pidx[j] >= 0) eq[j] = cQd[pidx[j] + n * c] * dt + tP[j];
+      }
+      packed = true;
+    } else if (!SQRT) {
       // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order; the
       // team kernel's rows never couple x and u, so the Q.ux term is an exact zero: ne_of)
       double tX[n], tUu[m];
@@ -631,7 +679,7 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   }
   int nxk = 0;
   if (AL && SQRT) nxk = P->knot_nx[k];
-  if (colx && knot_dense<SQRT, AL>(k, N, p, nxk)) {
+  if (colx && knot_dense<SQRT, AL>(k, N, p, nxk) && !packed) {
     if (!SQRT && !TERM && P->qpat_on) {
       // packed record: column tl's pattern entries only (DevProblem::qpat); the others are Q dt + 0.0
       const unsigned int pc = P->qpat[tl];
@@ -918,6 +966,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
   // Q blocks of knot k (terminal when TERM) from its expansion record (k_expand_team, ne_of):
   // this lane's columns of Q.xx, Q.uu, Q.ux, its Q.x entry and the whole Q.u
+  // (the problem's cost is read through the constant address space: a lane-indexed read through the generic
+  // DevProblem pointer is a flat load, whose wait also drains the wave's LDS operations)
+  const bool tvc = P->kc != nullptr;  // a time-varying Objective (cost_at)
+  const bool qpat = !SQRT && AL && P->qpat_on;
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
                     double(&Quxc)[m]) {
     constexpr bool term = decltype(term_c)::value;
@@ -925,24 +977,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const int c = tlk < n ? tlk : 0, cu = tlk < m ? tlk : 0;
     const double* e = Eg + (size_t)k * NE;
     const int cnt = AL ? kcnt[k] : 0;
-    const CostView C_ = cost_at<n, m>(P, term ? 0 : k);
+    // knot k's stage cost: the shared one (fixed offsets of P) or row k of the time-varying table
+    const CostView C_ = tvc ? cost_at<n, m>(P, term ? 0 : k)
+                            : CostView{P->Q, P->R, P->H, P->q, P->r, P->cQ, P->cR, 0.0};
+    const cptr<double> cQ = as_const(C_.cQ), cQd = as_const(C_.Q), cH = as_const(C_.H);
     Qxs = e[c];
     if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
-      if (!SQRT && !term && P->qpat_on) {
+      if (!term && qpat) {
         // packed record (k_expand_team): the pattern entries; every other entry went through the
         // expansion as Q dt + (an exact zero row sum)
-        const unsigned int pc = P->qpat[c];
-        const double* eq = e + n + m + m * m + P->qoff[c];
+        const unsigned int pc = as_const(P->qpat)[c];
+        const double* eq = e + n + m + m * m + as_const(P->qoff)[c];
 #pragma unroll
         for (int i = 0; i < n; i++)
-          Qxc[i] = (pc >> i & 1u) ? eq[__builtin_popcount(pc & ((1u << i) - 1u))] : C_.Q[i + n * c] * dt + 0.0;
+          Qxc[i] = (pc >> i & 1u) ? eq[__builtin_popcount(pc & ((1u << i) - 1u))] : cQd[i + n * c] * dt + 0.0;
       } else {
 #pragma unroll
         for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;
+      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? cQ[i + n * c] : cQd[i + n * c] * dt;
     }
     if (!term) {
 #pragma unroll
@@ -952,7 +1007,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const bool zterm = !SQRT && AL && cnt > 0;  // the std AL expansion's "+= cu'Iμcx" (an exact zero)
 #pragma unroll
       for (int i = 0; i < m; i++) {
-        const double h = C_.H[i + m * c] * dt;
+        const double h = cH[i + m * c] * dt;
         Quxc[i] = zterm ? h + 0.0 : h;
       }
     } else {

@@ -84,6 +84,7 @@ struct DevProblem {
   int qpat_on, qpat_n;
   unsigned int qpat[NMAX];
   int qoff[NMAX];
+  int qpat_max, qpat_pad;  // the most pattern entries in one column
   const int* knot_off;  // [N] first row of knot k
   const int* knot_cnt;  // [N] rows at knot k (p_k)
   const ConRow* rows;
@@ -184,7 +185,7 @@ struct DevBuffers {
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū
-  double* jws;        // Kuka RK3 Jacobian workspace (stage-chain form: KJ_WSK doubles per knot slot; the
+  double* jws;        // Kuka RK3 Jacobian workspace (stage-chain form: SoA stage points + KJ_JW per slot; the
                       // dual-staged A/B form: 2n duals per lane), or null
   int jac_chain;      // Kuka RK3 Jacobian in stage-chain form (tog_kuka_jac.hpp; 0: TOG_KUKA_JAC=dual A/B)
   int dense_stage_knots;  // some stage knot has a state-gradient row (k_expand_u / k_expand_team split)

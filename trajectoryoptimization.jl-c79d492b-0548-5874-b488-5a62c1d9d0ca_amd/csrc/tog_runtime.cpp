@@ -782,10 +782,12 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
         if (sx >> c & 1u) pat[c] |= sx;
     }
     int off = 0;
+    P.qpat_max = 0;
     for (int c = 0; c < n; c++) {
       P.qpat[c] = pat[c];
       P.qoff[c] = off;
       off += __builtin_popcount(pat[c]);
+      P.qpat_max = std::max(P.qpat_max, __builtin_popcount(pat[c]));
     }
     P.qpat_n = off;
     P.qpat_on = (off < n * n && getenv("TOG_DENSE_RECORDS") == nullptr) ? 1 : 0;
@@ -1614,7 +1616,9 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     });
   if (opts->solve_type != 0) return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal is not built");
   if (opts->n_steps < 0) return fail(TOG_ERR_ARG, "n_steps must be >= 0");
-  if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton on an infeasible (slack) problem is not built");
+  if (!h->ops->pn)
+    return fail(TOG_ERR_UNSUPPORTED, h->ops->min_time ? "projected Newton on a minimum-time problem is not built"
+                                                      : "projected Newton blocks larger than n + m = 24 are not built");
   const int SM = h->n + h->pmax;
   if (SM > PN_SM_MAX || h->n + h->m > 24)
     return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than 32 rows (n + pmax) are not built");
