@@ -16,6 +16,12 @@ if [ -n "$MICRO" ]; then
   timeout -k 10 60 tools/microbench/team_mfma_ab > $OUT/team_mfma_ab.txt 2>&1 || { cat $OUT/team_mfma_ab.txt; exit 1; }
   cat $OUT/team_mfma_ab.txt
 fi
+if [ -n "$SQW" ]; then  # one SQ counter pass over a short bench window of workload $SQW
+  TAG=${TAG}sq STEPS=3 BENCH_ARGS="--workload $SQW --no-solve-leg" bash tools/profile_sq.sh > $OUT/sq.log 2>&1 || { tail -20 $OUT/sq.log; exit 1; }
+  python3 -c "import sys; sys.path.insert(0, 'tools'); import rocpd_summary as r; r.sq_summary('gpurun_out/prof_${TAG}sq')" > $OUT/sq_$SQW.txt || exit 1
+  rm -rf gpurun_out/prof_${TAG}sq
+  head -8 $OUT/sq_$SQW.txt
+fi
 for w in ${WLS:-quad_maze kuka quadrotor}; do
   timeout -k 10 400 python bench.py --workload $w --cpu-seconds 4 > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { tail $OUT/bench_$w.err; exit 1; }
   python3 -c "

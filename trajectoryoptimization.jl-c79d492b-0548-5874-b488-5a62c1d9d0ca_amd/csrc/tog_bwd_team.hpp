@@ -517,7 +517,7 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
     team_rows<M>(Bf, b, k, N, pmax, p, P->rows + P->knot_off[k], xs, TERM ? nullptr : us, rows, xr, ur, nx, nu,
                  team, tl, TEAM);
     team_sync();
-    if (!SQRT && !TERM && P->qpat_on && P->qpat_max <= QPK) {
+    if (!SQRT && !TERM && P->qpat_on) {  // (qpat_on implies at most QPK pattern rows per column)
       // the same sums over the packed pattern (DevProblem::qpat): tX[i] can only change at column c's
       // pattern rows, so the row loop tests an entry's index against those (at most QPK) instead of all n;
       // every (row, entry) pair adds to the same sum in the same order. The record takes Q dt + the sum at
@@ -680,17 +680,8 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   int nxk = 0;
   if (AL && SQRT) nxk = P->knot_nx[k];
   if (colx && knot_dense<SQRT, AL>(k, N, p, nxk) && !packed) {
-    if (!SQRT && !TERM && P->qpat_on) {
-      // packed record: column tl's pattern entries only (DevProblem::qpat); the others are Q dt + 0.0
-      const unsigned int pc = P->qpat[tl];
-      double* eq = e + n + m + m * m + P->qoff[tl];
 #pragma unroll
-      for (int i = 0; i < n; i++)
-        if (pc >> i & 1u) eq[__builtin_popcount(pc & ((1u << i) - 1u))] = Qxc[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < n; i++) e[n + m + m * m + i + n * tl] = Qxc[i];
-    }
+    for (int i = 0; i < n; i++) e[n + m + m * m + i + n * tl] = Qxc[i];
   }
 }
 
@@ -966,10 +957,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
   // Q blocks of knot k (terminal when TERM) from its expansion record (k_expand_team, ne_of):
   // this lane's columns of Q.xx, Q.uu, Q.ux, its Q.x entry and the whole Q.u
-  // (the problem's cost is read through the constant address space: a lane-indexed read through the generic
-  // DevProblem pointer is a flat load, whose wait also drains the wave's LDS operations)
-  const bool tvc = P->kc != nullptr;  // a time-varying Objective (cost_at)
+  // Packed std AL records (k_expand_team, DevProblem::qpat): this lane's column pattern and its packed offset,
+  // loaded once (they do not change along the knots, and loading them per knot put a second memory round trip
+  // on the serial chain). A diagonal cost's Q dt + 0.0 needs only the diagonal entry: the other entries of a
+  // diagonal Q are zeros, and any zero times dt plus +0.0 is +0.0.
+  const bool tvc = P->kc != nullptr;  // a time-varying Objective (cost_at; its records stay dense)
   const bool qpat = !SQRT && AL && P->qpat_on;
+  const bool qdiag = P->diag_cost != 0;
+  unsigned int pc_l = 0u;
+  int oc_l = 0;
+  if (qpat) {
+    pc_l = as_global(P->qpat)[c];
+    oc_l = as_global(P->qoff)[c];
+  }
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
                     double(&Quxc)[m]) {
     constexpr bool term = decltype(term_c)::value;
@@ -977,27 +977,42 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const int c = tlk < n ? tlk : 0, cu = tlk < m ? tlk : 0;
     const double* e = Eg + (size_t)k * NE;
     const int cnt = AL ? kcnt[k] : 0;
-    // knot k's stage cost: the shared one (fixed offsets of P) or row k of the time-varying table
-    const CostView C_ = tvc ? cost_at<n, m>(P, term ? 0 : k)
-                            : CostView{P->Q, P->R, P->H, P->q, P->r, P->cQ, P->cR, 0.0};
-    const cptr<double> cQ = as_const(C_.cQ), cQd = as_const(C_.Q), cH = as_const(C_.H);
     Qxs = e[c];
-    if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
-      if (!term && qpat) {
-        // packed record (k_expand_team): the pattern entries; every other entry went through the
-        // expansion as Q dt + (an exact zero row sum)
-        const unsigned int pc = as_const(P->qpat)[c];
-        const double* eq = e + n + m + m * m + as_const(P->qoff)[c];
+    const bool dense = knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0);
+    if (!tvc) {
+      if (dense && !term && qpat) {
+        // packed record: the pattern entries (at most QPK, contiguous from oc_l); every other entry went
+        // through the expansion as Q dt + (an exact zero row sum)
+        const double* eq = e + n + m + m * m + oc_l;
+        double pv[QPK];
 #pragma unroll
-        for (int i = 0; i < n; i++)
-          Qxc[i] = (pc >> i & 1u) ? eq[__builtin_popcount(pc & ((1u << i) - 1u))] : cQd[i + n * c] * dt + 0.0;
-      } else {
+        for (int j = 0; j < QPK; j++) pv[j] = eq[j];  // (within the record: the packed area is < n*n)
+        const double qcc = qdiag ? P->Q[c + n * c] * dt + 0.0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+          const int rk = __builtin_popcount(pc_l & ((1u << i) - 1u));
+          double v = pv[0];
+#pragma unroll
+          for (int j = 1; j < QPK; j++) v = (rk == j) ? pv[j] : v;
+          const double base = qdiag ? ((i == c) ? qcc : 0.0) : P->Q[i + n * c] * dt + 0.0;
+          Qxc[i] = (pc_l >> i & 1u) ? v : base;
+        }
+      } else if (dense) {
 #pragma unroll
         for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
-      }
-    } else {
+      } else {
 #pragma unroll
-      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? cQ[i + n * c] : cQd[i + n * c] * dt;
+        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
+      }
+    } else {  // knot k's row of the time-varying table (dense records)
+      const CostView C_ = cost_at<n, m>(P, term ? 0 : k);
+      if (dense) {
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;
+      }
     }
     if (!term) {
 #pragma unroll
@@ -1005,9 +1020,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
       const bool zterm = !SQRT && AL && cnt > 0;  // the std AL expansion's "+= cu'Iμcx" (an exact zero)
+      const double* Hk = tvc ? cost_at<n, m>(P, k).H : P->H;
 #pragma unroll
       for (int i = 0; i < m; i++) {
-        const double h = cH[i + m * c] * dt;
+        const double h = Hk[i + m * c] * dt;
         Quxc[i] = zterm ? h + 0.0 : h;
       }
     } else {

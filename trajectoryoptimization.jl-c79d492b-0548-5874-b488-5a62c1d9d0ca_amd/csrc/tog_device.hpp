@@ -103,6 +103,15 @@ template <class T>
 __device__ __forceinline__ cptr<T> as_const(const T* p) {
   return (cptr<T>)p;
 }
+// The same data through the global address space: a lane-indexed read is a global load (vmcnt only, not the
+// flat load of a generic pointer), and, unlike the constant address space, the loads are not marked
+// invariant, so they are not hoisted out of a knot loop into long-lived registers.
+template <class T>
+using gptr = const T __attribute__((address_space(1)))*;
+template <class T>
+__device__ __forceinline__ gptr<T> as_global(const T* p) {
+  return (gptr<T>)p;
+}
 __device__ __forceinline__ cptr<ConRow> knot_rows(const DevProblem* P, int k) {
   return as_const(P->rows) + as_const(P->knot_off)[k];
 }
@@ -185,7 +194,7 @@ struct DevBuffers {
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū
-  double* jws;        // Kuka RK3 Jacobian workspace (stage-chain form: SoA stage points + KJ_JW per slot; the
+  double* jws;        // Kuka RK3 Jacobian workspace (stage-chain form: KJ_WSK doubles per knot slot; the
                       // dual-staged A/B form: 2n duals per lane), or null
   int jac_chain;      // Kuka RK3 Jacobian in stage-chain form (tog_kuka_jac.hpp; 0: TOG_KUKA_JAC=dual A/B)
   int dense_stage_knots;  // some stage knot has a state-gradient row (k_expand_u / k_expand_team split)

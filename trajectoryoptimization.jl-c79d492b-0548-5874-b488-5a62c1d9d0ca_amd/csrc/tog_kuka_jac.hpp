@@ -24,17 +24,10 @@
 namespace tog {
 
 constexpr int KJ_N = 14, KJ_M = 7, KJ_L = 21;
-constexpr int KJ_OFF_T2 = 0, KJ_OFF_T3 = 14;  // stage points s_2, s_3: 28 components per knot slot
-constexpr int KJ_JW = 448;                     // J[3][7][21] per knot slot (441, padded to 128-byte lines)
+constexpr int KJ_OFF_T2 = 0, KJ_OFF_T3 = 14, KJ_OFF_J = 28;  // per knot: s_2, s_3, J[3][7][21]
+constexpr int KJ_WSK = 472;                                   // doubles per knot slot (469, padded)
 
-// The workspace of one launch over `total` knot slots: the stage points structure-of-arrays (component i
-// of slot t at i * total + t: k_kuka_points' stores are whole lines), then the stage Jacobians slot by slot
-__device__ __forceinline__ double* kj_pt(const DevBuffers& Bf, long long total, long long t, int i) {
-  return Bf.jws + (size_t)i * total + t;
-}
-__device__ __forceinline__ double* kj_J(const DevBuffers& Bf, long long total, long long t) {
-  return Bf.jws + 28 * (size_t)total + (size_t)t * KJ_JW;
-}
+__device__ __forceinline__ double* kj_slot(const DevBuffers& Bf, long long t) { return Bf.jws + t * KJ_WSK; }
 
 // (traj, knot) of knot slot t (t < slots * (N - 1)); -1 when the trajectory takes no Jacobian this step
 __device__ __forceinline__ long long kj_traj(const DevBuffers& Bf, const DevProblem* P, long long t, int* k) {
@@ -93,13 +86,14 @@ __global__ void __launch_bounds__(64) k_kuka_points(const DevProblem* __restrict
   for (int i = 0; i < n; i++) x[i] = xg[i];
 #pragma unroll
   for (int i = 0; i < 7; i++) u[i] = ug[i];
+  double* w = kj_slot(Bf, t);
   // stage 1 at x: k1 = f dt, s_2 = x + k1/2 (discrete_step's rk3)
   kj_primal(vd, L, x, u);
 #pragma unroll
   for (int i = 0; i < n; i++) {
     k1[i] = (i < 7 ? x[7 + i] : vd[i - 7]) * dt;
     s[i] = x[i] + k1[i] / 2.0;
-    *kj_pt(Bf, total, t, KJ_OFF_T2 + i) = s[i];
+    w[KJ_OFF_T2 + i] = s[i];
   }
   // stage 2 at s_2: k2 = f dt, s_3 = (x - k1) + 2 k2
   kj_primal(vd, L, s, u);
@@ -109,7 +103,7 @@ __global__ void __launch_bounds__(64) k_kuka_points(const DevProblem* __restrict
     s[i] = (x[i] - k1[i]) + 2.0 * k2;
   }
 #pragma unroll
-  for (int i = 0; i < n; i++) *kj_pt(Bf, total, t, KJ_OFF_T3 + i) = s[i];
+  for (int i = 0; i < n; i++) w[KJ_OFF_T3 + i] = s[i];
 }
 
 // one lane per (knot, stage, direction p): TYPE 0 the q_p partial (full dual step), TYPE 1 the v_p partial
@@ -125,17 +119,15 @@ k_kuka_sjac(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
   const long long b = kj_traj(Bf, P, t, &k);
   if (b < 0) return;
   const int N = P->N;
-  // stage input component i: the knot's state (stage 1) or the SoA stage point
-  const double* xg = Bf.X + ((size_t)b * N + k) * n;
-  const int po = st == 1 ? KJ_OFF_T2 : KJ_OFF_T3;
-  auto sg = [&](int i) { return st == 0 ? xg[i] : *kj_pt(Bf, total, t, po + i); };
+  double* w = kj_slot(Bf, t);
+  const double* sg = st == 0 ? Bf.X + ((size_t)b * N + k) * n : w + (st == 1 ? KJ_OFF_T2 : KJ_OFF_T3);
   const double* ug = Bf.U + ((size_t)b * (N - 1) + k) * m;
-  double* J = kj_J(Bf, total, t) + st * 7 * KJ_L;
+  double* J = w + KJ_OFF_J + st * 7 * KJ_L;
   if constexpr (TYPE == 0) {
     Dual<1> xs[n], us[7], fd[n];
 #pragma unroll
     for (int i = 0; i < n; i++) {
-      xs[i].v = sg(i);
+      xs[i].v = sg[i];
       xs[i].g[0] = (i == p) ? 1.0 : 0.0;
     }
 #pragma unroll
@@ -151,8 +143,8 @@ k_kuka_sjac(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
     Dual<1> qd[7], tau[7], vd[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) {
-      q[i] = sg(i);
-      qd[i].v = sg(7 + i);
+      q[i] = sg[i];
+      qd[i].v = sg[7 + i];
       qd[i].g[0] = (i == p) ? 1.0 : 0.0;
       u[i] = ug[i];
     }
@@ -219,8 +211,8 @@ __global__ void __launch_bounds__(64) k_kuka_chain(const DevProblem* __restrict_
   double* Jl = lds;
   double* T = Jl + 441;
   double* stash = T + 16 * KJ_L;
-  const double* w = kj_J(Bf, total, t);
-  for (int e = lane; e < 441; e += WAVE) Jl[e] = w[e];
+  const double* w = kj_slot(Bf, t);
+  for (int e = lane; e < 441; e += WAVE) Jl[e] = w[KJ_OFF_J + e];
   for (int e = lane; e < 2 * KJ_L; e += WAVE) T[(e >> 1) * 16 + 14 + (e & 1)] = 0.0;
   double K1[KJ_ER], Ss[KJ_ER];
   // stage 1: K1 = J_1 dt (rows 0..6: ∂q̇/∂v = I), T2 = I + K1/2

@@ -790,7 +790,10 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
       P.qpat_max = std::max(P.qpat_max, __builtin_popcount(pat[c]));
     }
     P.qpat_n = off;
-    P.qpat_on = (off < n * n && getenv("TOG_DENSE_RECORDS") == nullptr) ? 1 : 0;
+    // (the backward pass reads QPK entries from a column's packed offset: every column within QPK, and the
+    // packed area QPK short of the record's end; a time-varying Objective keeps dense records)
+    P.qpat_on = (P.qpat_max <= QPK && off + QPK <= n * n && !d->stage_costs &&
+                 getenv("TOG_DENSE_RECORDS") == nullptr) ? 1 : 0;
   }
   P.kc = nullptr;
   P.kc_stride = kst;
