@@ -288,6 +288,41 @@ def solve_altro_infeasible(prob, opts, b=0):
     return X, U, si, sf
 
 
+def solve_altro_infeasible_min_time(prob, opts, b=0):
+    """Oracle restatement of ``solve!(prob, ::ALTROSolverOptions)`` with an initial state trajectory and
+    tf = 0 (altro_methods.jl:98-124): minimum_time_problem(infeasible_problem(prob)) -- the slacks from
+    slack_controls on the infeasible problem, the time-step bounds on the first slack control as
+    mintime_constraints combines them (minimum_time.jl:125-141) -- then process_results! (:56-95) with
+    infeasible_to_feasible_problem (infeasible.jl:37-58: the feasible minimum-time problem, h and τ from the
+    infeasible solve, projection! = the open-loop rollout) and the resolve. Returns (X[1:n], U[1:m], h,
+    solver_inf, solver_feasible or None). Mirrors ``tog_solve_altro`` (csrc/tog_altro.cpp)."""
+    n, m = prob.model.n, prob.model.m
+    pinf = _pkg.infeasible_problem(prob, opts.R_inf)
+    s0 = OracleSolver(pinf, opts, b)
+    s0.slack_controls()
+    pinf._U[b] = s0.get("U")
+    pmt = _pkg.minimum_time_problem(pinf, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    si = OracleSolver(pmt, opts.opts_al, b)
+    si.solve()
+    Xi, Ui = si.get("X"), si.get("U")
+    X, U, h = Xi[:, :n].copy(), Ui[:, :m].copy(), Ui[:, -1].copy()
+    p2 = prob.copy()
+    p2._X[b], p2._U[b] = X, U
+    pm2 = _pkg.minimum_time_problem(p2, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    pm2._U[b, :, m] = h
+    pm2._X[b, :, n] = Xi[:, -1]
+    pm2._X[b, 0, n] = 0.0
+    if opts.dynamically_feasible_projection:
+        pm2._X[b] = np.nan
+    sf = None
+    if opts.resolve_feasible_problem:
+        sf = OracleSolver(pm2, opts.opts_al, b)
+        sf.solve()
+        Xf, Uf = sf.get("X"), sf.get("U")
+        X, U, h = Xf[:, :n].copy(), Uf[:, :m].copy(), Uf[:, m].copy()
+    return X, U, h, si, sf
+
+
 def solve_altro_min_time(prob, opts, b=0):
     """Oracle restatement of ``solve!(prob, ::ALTROSolverOptions)`` for tf = 0 (altro_methods.jl:98-124,
     minimum_time.jl:2-34) for trajectory ``b``: returns (X[1:n], U[1:m], h, solver). Mirrors

@@ -1281,6 +1281,8 @@ typedef struct {
   /* obstacles */
   int count;
   double obs[64 * 4];
+  /* infeasible_constraints: the slack controls u[s0 : s0 + ns] */
+  int s0, ns;
 } oc_con;
 
 typedef struct {
@@ -1363,7 +1365,11 @@ static void hist_push(double** buf, int* n, int* cap, int w, const double* rec) 
 
 /* mb: the controls a bound row may constrain (m less the slack controls of an infeasible-start problem:
    its BoundConstraint keeps the model's m, update_constraint_set_jacobians constraint_sets.jl:135-150) */
-static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb) {
+/* mb: the controls of the model inside add_slack_controls / add_min_time_controls; slack: the slack count.
+   A trim=false bound keeps one row per model control (the slack and time-step controls get none); a trimmed
+   bound has rows for its finite entries over all m (an infeasible problem's slack entries are infinite;
+   the infeasible minimum-time problem's combined bound reaches u[1:m+1], minimum_time.jl:125-141) */
+static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb, int slack) {
   memset(oc, 0, sizeof(*oc));
   oc->type = tc->type;
   switch (tc->type) {
@@ -1384,8 +1390,8 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb)
       for (int i = 0; i < m; i++) {
         oc->u_max[i] = D[2 * n + i];
         oc->u_min[i] = D[2 * n + m + i];
-        oc->au_max[i] = i < mb && (keep || isfinite(D[2 * n + i]));
-        oc->au_min[i] = i < mb && (keep || isfinite(D[2 * n + m + i]));
+        oc->au_max[i] = (keep ? i < mb : 1) && (keep || isfinite(D[2 * n + i]));
+        oc->au_min[i] = (keep ? i < mb : 1) && (keep || isfinite(D[2 * n + m + i]));
         cu += oc->au_max[i];
         cun += oc->au_min[i];
       }
@@ -1418,7 +1424,9 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb)
       break;
     case TOG_CON_INFEASIBLE: /* infeasible_constraints(n, m) src/constraints.jl:306-314 */
       oc->inequality = 0;
-      oc->p_stage = n;
+      oc->s0 = mb;
+      oc->ns = slack;
+      oc->p_stage = slack;
       oc->p_term = 0; /* :stage only */
       break;
     case TOG_CON_MIN_TIME_EQ: /* mintime_equality(n, m) minimum_time.jl:106-124, :stage */
@@ -1504,10 +1512,9 @@ static int con_eval(const oc_con* oc, int n, int m, const double* x, const doubl
     case TOG_CON_INFEASIBLE:
       /* inf_con(v, x, u) = copyto!(v, u[m+1:m+n]); ∇inf = [0 0 I] (src/constraints.jl:306-314) */
       if (!term) {
-        int mb = m - n;
-        for (int i = 0; i < n; i++) {
-          v[r] = u[mb + i];
-          if (Ju) Ju[r + ldj * (mb + i)] = 1.0;
+        for (int i = 0; i < oc->ns; i++) {
+          v[r] = u[oc->s0 + i];
+          if (Ju) Ju[r + ldj * (oc->s0 + i)] = 1.0;
           r++;
         }
       }
@@ -1570,9 +1577,10 @@ static void desc_load(oc_solver* s, const tog_problem_desc* d) {
   s->m = d->m;
   s->N = d->N;
   s->dt = d->dt;
-  s->slack = (d->flags & TOG_PROB_INFEASIBLE) ? d->n : 0;
-  s->mb = d->m - s->slack;
+  /* add_min_time_controls(add_slack_controls(model)) (altro_methods.jl:98-124): x = [x; τ], u = [u; s; h] */
   s->mt = (d->flags & TOG_PROB_MIN_TIME) ? 1 : 0;
+  s->slack = (d->flags & TOG_PROB_INFEASIBLE) ? d->n - s->mt : 0;
+  s->mb = d->m - s->slack - s->mt;
   s->R_mt = s->mt ? d->R_min_time : 0.0;
   int n = s->n, m = s->m, N = s->N;
   s->Q = malloc(sizeof(double) * n * n);
@@ -1603,7 +1611,7 @@ static void desc_load(oc_solver* s, const tog_problem_desc* d) {
     oc_cset* os = &s->sets[i];
     os->ncon = d->sets[i].n_con;
     for (int j = 0; j < os->ncon; j++) {
-      con_init(&os->con[j], &d->sets[i].con[j], n, m, s->mb);
+      con_init(&os->con[j], &d->sets[i].con[j], n, m, s->mb, s->slack);
       os->p_stage += os->con[j].p_stage;
       os->p_term += os->con[j].p_term;
     }
@@ -1792,6 +1800,7 @@ static void traj_f(const oc_solver* s, double* xn, const double* x, const double
   if (s->mt) { /* add_min_time_controls f!: h = u[end]; model.f(x+, x, u, h^2); x+[n̄] = h (minimum_time.jl:91-95) */
     const double h = u[s->m - 1];
     oc_discrete_f(s->model, s->integ, xn, x, u, h * h);
+    for (int i = 0; i < s->slack; i++) xn[i] += u[s->mb + i]; /* an infeasible model inside: x+ .+= s */
     xn[s->n - 1] = h;
     return;
   }
@@ -1806,7 +1815,7 @@ static void traj_jacobian(const oc_solver* s, double* F, const double* x, const 
   if (s->mt) {
     /* ∇f! of add_min_time_controls (minimum_time.jl:97-101): model.∇f(view(Z, idx.x, idx2), x, u, h^2) with
        idx2 = [x columns; u columns + n̄; last], Z[idx.x, end] .*= 2h, Z[n̄, end] = 1 */
-    const int nb = n - 1, mbb = m - 1;
+    const int nb = n - 1, mbb = mb;
     const double h = u[m - 1];
     double Z[16 * (16 + OM + 1)];
     discrete_jacobian_fd(s->model, s->integ, Z, x, u, h * h); /* nb x (nb + mbb + 1) */
@@ -1815,8 +1824,10 @@ static void traj_jacobian(const oc_solver* s, double* F, const double* x, const 
       for (int i = 0; i < nb; i++) F[i + n * j] = Z[i + nb * j];
     for (int j = 0; j < mbb; j++)
       for (int i = 0; i < nb; i++) F[i + n * (n + j)] = Z[i + nb * (nb + j)];
-    for (int i = 0; i < nb; i++) F[i + n * (n + mbb)] = Z[i + nb * (nb + mbb)] * (2.0 * h);
-    F[nb + n * (n + mbb)] = 1.0;
+    /* an infeasible model inside: its ∇f! writes Diagonal(1.0I, n) in the slack columns (src/model.jl:771-774) */
+    for (int j = 0; j < s->slack; j++) F[j + n * (n + mbb + j)] = 1.0;
+    for (int i = 0; i < nb; i++) F[i + n * (n + m - 1)] = Z[i + nb * (nb + mbb)] * (2.0 * h);
+    F[nb + n * (n + m - 1)] = 1.0;
     return;
   }
   if (!s->slack) {
@@ -1835,7 +1846,7 @@ static void traj_jacobian(const oc_solver* s, double* F, const double* x, const 
    with x[k+1] = f(x[k], U[k]); s_k = X[k+1] - x[k+1]; x[k+1] += s_k. Writes U[m+1:m+n]. */
 OC_EXPORT void oc_slack_controls(oc_solver* s) {
   int n = s->n, m = s->m, N = s->N;
-  if (!s->slack) return;
+  if (!s->slack || s->mt) return; /* (the infeasible minimum-time problem takes its slacks from infeasible_problem) */
   double x[16], xn[16];
   memcpy(x, s->x0, sizeof(double) * n);
   for (int k = 0; k < N - 1; k++) {

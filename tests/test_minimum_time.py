@@ -165,3 +165,62 @@ def test_gpu_min_time_models_equal_oracle(tog, oracle, gpu, name):
     pmt, opts = _mt_model_case(tog, name)
     assert pmt.model.min_time and pmt.model.n == {"quadrotor": 14, "cartpole": 5, "kuka": 15}[name]
     _solve_and_compare(tog, oracle, pmt, opts)
+
+
+# ----------------------------------------------------------------------------- infeasible start + minimum time
+
+
+def _inf_mt_case(tog, resolve=True):
+    """test/minimum_time_tests.jl's pendulum from a straight-line state guess with tf = :min: altro_problem
+    makes it minimum_time_problem(infeasible_problem(prob)) (altro_methods.jl:98-124)."""
+    make, opts, xf, U0, dt, dt_mt, _ = pendulum_case(tog)
+    p = make(U0, dt_mt, tf="min")
+    p.X = tog.line_trajectory(p.x0[0], xf, p.N)
+    opts.resolve_feasible_problem = resolve
+    opts.opts_al.iterations = 15
+    return p, opts, xf
+
+
+def test_infeasible_min_time_bounds_quirk(tog):
+    """mintime_constraints on the infeasible problem (minimum_time.jl:125-141): combine(bnd, mt_bnd) sizes the
+    bound by the infeasible problem's BoundConstraint, which keeps the model's m, so √dt_min <= u[m+1] <=
+    √dt_max lands on the first slack control and h (the last control) is unbounded. Reproduced as written."""
+    p, opts, _ = _inf_mt_case(tog)
+    pinf = tog.infeasible_problem(p, opts.R_inf)
+    pmt = tog.minimum_time_problem(pinf, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    n, m = p.model.n, p.model.m
+    assert (pmt.model.n, pmt.model.m, pmt.model.slack, pmt.model.min_time) == (n + 1, m + n + 1, n, True)
+    bnd = [c for c in pmt.constraints[3] if isinstance(c, tog.BoundConstraint)][0]
+    _, _, data = bnd.to_abi(pmt.model.m)
+    u_max = data[2 * (n + 1): 2 * (n + 1) + pmt.model.m]
+    assert u_max[m] == math.sqrt(opts.dt_max) and np.isinf(u_max[-1])
+    labels = [type(c).__name__ for c in pmt.constraints[3]]
+    assert labels == ["InfeasibleConstraint", "BoundConstraint", "MinTimeEquality"]
+
+
+def test_oracle_infeasible_min_time_flow(tog, oracle):
+    """The whole flow on the oracle: the infeasible minimum-time AL phase, then the feasible minimum-time
+    resolve from its controls and time steps; the resolve meets test/minimum_time_tests.jl's goal threshold."""
+    p, opts, xf = _inf_mt_case(tog)
+    X, U, h, si, sf = oracle.solve_altro_infeasible_min_time(p, opts, 0)
+    assert np.all(np.isfinite(X)) and np.all(np.isfinite(U)) and np.all(h > 0)
+    assert sf is not None and np.max(np.abs(X[-1] - xf)) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("resolve", [False, True])
+def test_gpu_infeasible_min_time_equals_oracle(tog, oracle, gpu, resolve):
+    """solve_b(prob, ALTROSolverOptions) with an initial state trajectory and tf = :min on the device
+    (MinTime<Infeasible<Pendulum>>, tog_altro.cpp's transforms) against the oracle's flow: X, U, h within
+    1e-6 and equal iteration counts in both phases."""
+    p, opts, _ = _inf_mt_case(tog, resolve)
+    ref = p.copy()
+    solver = tog.solve_b(p, opts)
+    Xo, Uo, ho, si, sf = oracle.solve_altro_infeasible_min_time(ref, opts, 0)
+    scale = lambda a: max(1.0, float(np.max(np.abs(a))))  # noqa: E731
+    assert np.max(np.abs(p._X[0] - Xo)) <= 1e-6 * scale(Xo)
+    assert np.max(np.abs(p._U[0] - Uo)) <= 1e-6 * scale(Uo)
+    assert np.max(np.abs(p.h[0] - ho)) <= 1e-6
+    assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+    if resolve:
+        assert int(solver.stats_feasible["iterations_total"][0]) == int(sf.get("stats")[tog.abi.STAT_TOTAL_STEPS])

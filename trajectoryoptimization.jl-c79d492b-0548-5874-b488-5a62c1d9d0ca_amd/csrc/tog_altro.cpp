@@ -133,7 +133,6 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     return tog__fail(TOG_ERR_ARG, "infeasible start: X must be given for every trajectory of the batch or for none");
   const bool infeasible = given == B && B > 0;
   const bool min_time = (desc->flags & TOG_PROB_TF_MIN) != 0;
-  if (infeasible && min_time) return tog__fail(TOG_ERR_UNSUPPORTED, "infeasible start + minimum time");
   if (opts->projected_newton && min_time)
     return tog__fail(TOG_ERR_UNSUPPORTED, "projected Newton on the minimum-time problem");
   if (opts->max_steps < 0) return tog__fail(TOG_ERR_ARG, "max_steps must be >= 0");
@@ -153,6 +152,102 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     R->time = now_s() - t0;
     return TOG_OK;
   };
+  if (infeasible && min_time) {
+    // minimum_time_problem(infeasible_problem(prob)) (altro_methods.jl:98-124). The slacks come from
+    // slack_controls on the infeasible problem (infeasible.jl:63-80, the model at prob.dt), on a handle of
+    // its own, before the time step becomes a control
+    const int mi = m + n, nt = n + 1, mt = mi + 1;
+    const double h0 = sqrt(desc->dt);
+    std::vector<double> Ui((size_t)mi * (N - 1) * B, 0.0);
+    for (long long b = 0; b < B; b++)
+      for (int k = 0; k < N - 1; k++)
+        for (int i = 0; i < m; i++) Ui[i + mi * (k + (size_t)(N - 1) * b)] = U[i + m * (k + (size_t)(N - 1) * b)];
+    {
+      Desc di;
+      if ((rc = infeasible_desc(desc, opts->R_inf, di))) return rc;
+      Handle Hs;
+      if ((rc = tog_create(&di.d, &oal, device, &Hs.h)) || (rc = tog_set_state(Hs.h, x0, Ui.data(), X)) ||
+          (rc = tog_slack_controls(Hs.h)) || (rc = tog_get(Hs.h, TOG_FIELD_U, Ui.data())))
+        return rc;
+    }
+    Desc dmi;
+    if ((rc = infeasible_min_time_desc(desc, opts->R_inf, opts->R_minimum_time, opts->dt_max, opts->dt_min, dmi)))
+      return rc;
+    // U = [U; s; √dt], X = [X; √dt], x0 = [x0; 0] (minimum_time.jl:30-33)
+    std::vector<double> x0t((size_t)nt * B), Ut((size_t)mt * (N - 1) * B), Xt((size_t)nt * N * B);
+    for (long long b = 0; b < B; b++) {
+      for (int i = 0; i < n; i++) x0t[i + (size_t)nt * b] = x0[i + (size_t)n * b];
+      x0t[n + (size_t)nt * b] = 0.0;
+      for (int k = 0; k < N - 1; k++) {
+        for (int i = 0; i < mi; i++) Ut[i + mt * (k + (size_t)(N - 1) * b)] = Ui[i + mi * (k + (size_t)(N - 1) * b)];
+        Ut[mi + mt * (k + (size_t)(N - 1) * b)] = h0;
+      }
+      for (int k = 0; k < N; k++) {
+        for (int i = 0; i < n; i++) Xt[i + nt * (k + (size_t)N * b)] = X[i + n * (k + (size_t)N * b)];
+        Xt[n + nt * (k + (size_t)N * b)] = h0;
+      }
+    }
+    const std::vector<double> X_in(X, X + nX * B), U_in(U, U + (size_t)m * (N - 1) * B);
+    Handle H1;
+    const double ta = now_s();
+    if ((rc = run(&dmi.d, &oal, device, x0t.data(), Ut.data(), Xt.data(), false, TOG_MODE_AL, H1, opts->max_steps,
+                  hcap)))
+      return rc;
+    R->time_al = now_s() - ta;
+    const std::vector<char> err = raised(H1.h, B, rc);
+    if (rc) return rc;
+    if ((rc = tog_get(H1.h, TOG_FIELD_X, Xt.data())) || (rc = tog_get(H1.h, TOG_FIELD_U, Ut.data()))) return rc;
+    if ((rc = read_al(H1.h, R))) return rc;
+    // process_results!: X[1:n], U[1:m]; then infeasible_to_feasible_problem (infeasible.jl:37-58): the feasible
+    // minimum-time problem from them, h and τ from the infeasible solve (τ_1 = 0); projection! leaves the
+    // open-loop rollout (X = NaN)
+    std::vector<double> Uf((size_t)(m + 1) * (N - 1) * B), Xf((size_t)nt * N * B), hf((size_t)(N - 1) * B);
+    for (long long b = 0; b < B; b++) {
+      for (int k = 0; k < N; k++) {
+        for (int i = 0; i < n; i++) X[i + n * (k + (size_t)N * b)] = Xt[i + nt * (k + (size_t)N * b)];
+        for (int i = 0; i < n; i++) Xf[i + nt * (k + (size_t)N * b)] = Xt[i + nt * (k + (size_t)N * b)];
+        Xf[n + nt * (k + (size_t)N * b)] = k == 0 ? 0.0 : Xt[n + nt * (k + (size_t)N * b)];
+      }
+      for (int k = 0; k < N - 1; k++) {
+        for (int i = 0; i < m; i++) {
+          U[i + m * (k + (size_t)(N - 1) * b)] = Ut[i + mt * (k + (size_t)(N - 1) * b)];
+          Uf[i + (m + 1) * (k + (size_t)(N - 1) * b)] = Ut[i + mt * (k + (size_t)(N - 1) * b)];
+        }
+        const double hk = Ut[mi + mt * (k + (size_t)(N - 1) * b)];
+        Uf[m + (m + 1) * (k + (size_t)(N - 1) * b)] = hk;
+        hf[k + (size_t)(N - 1) * b] = hk;
+      }
+    }
+    if (opts->resolve_feasible_problem) {
+      Desc dm;
+      if ((rc = min_time_desc(desc, opts->R_minimum_time, opts->dt_max, opts->dt_min, dm))) return rc;
+      Handle H2;
+      if ((rc = run(&dm.d, &oal, device, x0t.data(), Uf.data(), opts->dynamically_feasible_projection ? nullptr : Xf.data(),
+                    false, TOG_MODE_AL, H2, opts->max_steps, 0)))
+        return rc;
+      std::vector<double> X2((size_t)nt * N * B);
+      if ((rc = tog_get(H2.h, TOG_FIELD_X, X2.data())) || (rc = tog_get(H2.h, TOG_FIELD_U, Uf.data()))) return rc;
+      if (R->stats_resolve && (rc = tog_get(H2.h, TOG_FIELD_STATS, R->stats_resolve))) return rc;
+      for (long long b = 0; b < B; b++) {
+        for (int k = 0; k < N; k++)
+          for (int i = 0; i < n; i++) X[i + n * (k + (size_t)N * b)] = X2[i + nt * (k + (size_t)N * b)];
+        for (int k = 0; k < N - 1; k++) {
+          for (int i = 0; i < m; i++) U[i + m * (k + (size_t)(N - 1) * b)] = Uf[i + (m + 1) * (k + (size_t)(N - 1) * b)];
+          hf[k + (size_t)(N - 1) * b] = Uf[m + (m + 1) * (k + (size_t)(N - 1) * b)];
+        }
+      }
+    }
+    for (long long b = 0; b < B; b++) {
+      if (err[b]) {  // the exception left prob untouched: no process_results!, no resolve
+        memcpy(X + nX * b, X_in.data() + nX * b, sizeof(double) * nX);
+        memcpy(U + (size_t)m * (N - 1) * b, U_in.data() + (size_t)m * (N - 1) * b, sizeof(double) * m * (N - 1));
+        if (R->stats_resolve) memset(R->stats_resolve + (size_t)TOG_NSTATS * b, 0, sizeof(double) * TOG_NSTATS);
+        continue;
+      }
+      if (h_out) memcpy(h_out + (size_t)(N - 1) * b, hf.data() + (size_t)(N - 1) * b, sizeof(double) * (N - 1));
+    }
+    return finish(H1);
+  }
   if (infeasible) {
     Desc di;
     if ((rc = infeasible_desc(desc, opts->R_inf, di))) return rc;

@@ -124,7 +124,7 @@ inline int infeasible_desc(const tog_problem_desc* s, double R_inf, Desc& o) {
   const int n = s->n, m = s->m, N = s->N, mi = m + n;
   o.d = *s;
   o.d.m = mi;
-  o.d.flags = s->flags | TOG_PROB_INFEASIBLE;
+  o.d.flags = (s->flags & ~TOG_PROB_TF_MIN) | TOG_PROB_INFEASIBLE;
   o.Qf.assign(s->Qf, s->Qf + n * n);
   o.qf.assign(s->qf, s->qf + n);
   map_stage_costs(s, n, mi, o, [&](const StageCost& c) {
@@ -268,6 +268,109 @@ inline int min_time_desc(const tog_problem_desc* s, double R_min_time, double dt
       }
       b[2 * nt + m] = sqrt(dt_max);
       b[2 * nt + mt + m] = sqrt(dt_min);
+      cs.push_back({TOG_CON_BOUND, 0, nullptr});
+      ds.push_back(std::move(b));
+      if (pos == 2) {
+        cs.push_back({TOG_CON_MIN_TIME_EQ, 0, nullptr});
+        ds.push_back({});
+      }
+      memo[key] = o.add_set(std::move(cs), std::move(ds));
+    }
+    o.knot_set[k] = memo[key];
+  }
+  o.finalize();
+  return TOG_OK;
+}
+
+// minimum_time_problem(infeasible_problem(prob)) (altro_methods.jl:98-124): x = [x; τ], u = [u; s; h]; the cost
+// is the infeasible problem's (R_inf I/dt on the slacks, infeasible.jl:2-33) zero-padded for [τ; h], and every
+// set is mintime_constraints' over the infeasible problem (minimum_time.jl:125-141): the non-bound constraints,
+// infeasible_constraints at the stage knots, the combined bound, h_k = τ_k at 1 < k < N. combine(bnd, mt_bnd)
+// sizes the bound by the infeasible problem's BoundConstraint, which keeps the model's (n, m): its √dt bounds
+// land on u[m+1], the first slack control, and h is unbounded; a knot without a bound gets
+// BoundConstraint(n, m + n) combined, whose √dt bounds are on h. Reproduced as written.
+inline int infeasible_min_time_desc(const tog_problem_desc* s, double R_inf, double R_min_time, double dt_max,
+                                    double dt_min, Desc& o) {
+  const int n = s->n, m = s->m, N = s->N, mi = m + n, nt = n + 1, mt = mi + 1;
+  o.d = *s;
+  o.d.n = nt;
+  o.d.m = mt;
+  o.d.flags = (s->flags & ~TOG_PROB_TF_MIN) | TOG_PROB_INFEASIBLE | TOG_PROB_MIN_TIME;
+  o.d.R_min_time = R_min_time;
+  auto pad = [](const double* A, int r, int c, int R, int Cc) {
+    std::vector<double> out((size_t)R * Cc, 0.0);
+    for (int j = 0; j < c; j++)
+      for (int i = 0; i < r; i++) out[i + (size_t)R * j] = A[i + (size_t)r * j];
+    return out;
+  };
+  map_stage_costs(s, nt, mt, o, [&](const StageCost& c) {
+    // infeasible_problem's cost (R = blockdiag(R, R_inf I/dt), H = [H; 0], r = [r; 0]), then the padding
+    std::vector<double> R((size_t)mi * mi, 0.0), H((size_t)mi * n, 0.0), r(mi, 0.0);
+    for (int j = 0; j < m; j++)
+      for (int i = 0; i < m; i++) R[i + mi * j] = c.R[i + m * j];
+    for (int i = 0; i < n; i++) R[(m + i) + mi * (m + i)] = R_inf * 1.0 / s->dt;
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < m; i++) H[i + mi * j] = c.H[i + m * j];
+    for (int i = 0; i < m; i++) r[i] = c.r[i];
+    std::vector<double> row;
+    for (auto v : {pad(c.Q, n, n, nt, nt), pad(R.data(), mi, mi, mt, mt), pad(H.data(), mi, n, mt, nt),
+                   pad(c.q, n, 1, nt, 1), pad(r.data(), mi, 1, mt, 1)})
+      row.insert(row.end(), v.begin(), v.end());
+    row.push_back(c.c);
+    return row;
+  });
+  o.Qf = pad(s->Qf, n, n, nt, nt);
+  o.qf = pad(s->qf, n, 1, nt, 1);
+  bool has_bounds = false;  // @assert has_bounds(prob.constraints) (minimum_time.jl:6)
+  for (int k = 0; k < N && !has_bounds; k++) {
+    const int si = s->knot_set ? s->knot_set[k] : -1;
+    if (si < 0 || si >= s->n_sets) continue;
+    for (int c = 0; c < s->sets[si].n_con; c++) has_bounds = has_bounds || s->sets[si].con[c].type == TOG_CON_BOUND;
+  }
+  if (!has_bounds) return tog__fail(TOG_ERR_ARG, "minimum time: the problem has no BoundConstraint (minimum_time.jl:6)");
+  o.knot_set.assign(N, -1);
+  std::vector<int> memo(3 * (s->n_sets + 1), -1);
+  for (int k = 0; k < N; k++) {
+    const int si = s->knot_set ? s->knot_set[k] : -1;
+    const int pos = (k == 0) ? 0 : (k == N - 1 ? 1 : 2);
+    const int key = 3 * (si < 0 ? s->n_sets : si) + pos;
+    if (memo[key] < 0) {
+      std::vector<tog_constraint> cs;
+      std::vector<std::vector<double>> ds;
+      const tog_constraint* bnd = nullptr;
+      if (si >= 0) {
+        const tog_constraint_set& set = s->sets[si];
+        for (int c = 0; c < set.n_con; c++) {
+          const tog_constraint& con = set.con[c];
+          if (con.type == TOG_CON_BOUND) {
+            if (!bnd) bnd = &con;
+            continue;
+          }
+          if (con.type == TOG_CON_USER || con.type == TOG_CON_INFEASIBLE || con.type == TOG_CON_MIN_TIME_EQ)
+            return tog__fail(TOG_ERR_UNSUPPORTED, "infeasible minimum time with user, slack or time-step rows");
+          tog_constraint cc = con;
+          if (cc.type == TOG_CON_GOAL && cc.count == 0) cc.count = n;  // the goal stays on x[1:n]
+          cs.push_back(cc);
+          ds.push_back(copy_data(con, n, m));
+        }
+      }
+      if (pos != 1) {  // infeasible_constraints, after the others (update_constraint_set_jacobians order)
+        cs.push_back({TOG_CON_INFEASIBLE, 0, nullptr});
+        ds.push_back({});
+      }
+      // the combined bound over [x; τ], [u; s; h]
+      std::vector<double> b(2 * nt + 2 * mt);
+      for (int i = 0; i < nt; i++) {
+        b[i] = (bnd && i < n) ? bnd->data[i] : INFINITY;
+        b[nt + i] = (bnd && i < n) ? bnd->data[n + i] : -INFINITY;
+      }
+      for (int i = 0; i < mt; i++) {
+        b[2 * nt + i] = (bnd && i < m) ? bnd->data[2 * n + i] : INFINITY;
+        b[2 * nt + mt + i] = (bnd && i < m) ? bnd->data[2 * n + m + i] : -INFINITY;
+      }
+      const int ih = bnd ? m : mi;  // u[m+1] (the first slack) when the knot had a bound, else h
+      b[2 * nt + ih] = sqrt(dt_max);
+      b[2 * nt + mt + ih] = sqrt(dt_min);
       cs.push_back({TOG_CON_BOUND, 0, nullptr});
       ds.push_back(std::move(b));
       if (pos == 2) {

@@ -950,6 +950,7 @@ struct MinTime {
 template <class M>
 struct ModelTraits {
   using Base = M;
+  using Core = M;  // the model inside every wrapper (the one whose dynamics are differentiated)
   static constexpr int slack = 0;
   // implicit integrators instantiated: the small models and the quadrotor (the Kuka arm's are in a unit of
   // their own, KukaImplicit); explicit_ok: the explicit integrators instantiated
@@ -960,6 +961,7 @@ struct ModelTraits {
 template <class Mb>
 struct ModelTraits<MinTime<Mb>> {
   using Base = Mb;
+  using Core = Mb;
   static constexpr int slack = 0;
   static constexpr bool implicit_ok = false;
   static constexpr bool explicit_ok = true;
@@ -968,10 +970,24 @@ struct ModelTraits<MinTime<Mb>> {
 template <class Mb>
 struct ModelTraits<Infeasible<Mb>> {
   using Base = Mb;
+  using Core = Mb;
   static constexpr int slack = Mb::n;
   static constexpr bool implicit_ok = false;
   static constexpr bool explicit_ok = true;
   static constexpr bool min_time = false;
+};
+// altro_problem's infeasible start with tf = :min (altro_methods.jl:98-124): minimum_time_problem of the
+// infeasible problem, add_min_time_controls(add_slack_controls(model)): x = [x; τ], u = [u; s; h],
+// x+ = f_d(x, u, h²) + s, τ+ = h. discrete_step unwraps MinTime to Infeasible<Mb> (Base); the Jacobian
+// differentiates Mb (Core) and writes the slack identity and the h column as the two wrappers' ∇f! do.
+template <class Mb>
+struct ModelTraits<MinTime<Infeasible<Mb>>> {
+  using Base = Infeasible<Mb>;
+  using Core = Mb;
+  static constexpr int slack = Mb::n;
+  static constexpr bool implicit_ok = false;
+  static constexpr bool explicit_ok = true;
+  static constexpr bool min_time = true;
 };
 // The Kuka arm under the implicit schemes (midpoint_implicit / rk3_implicit): the same model, its kernels
 // instantiated for those two integrators only, in their own translation unit (k_kuka_implicit.hip), so the
@@ -980,6 +996,7 @@ struct KukaImplicit : Kuka {};
 template <>
 struct ModelTraits<KukaImplicit> {
   using Base = KukaImplicit;
+  using Core = KukaImplicit;
   static constexpr int slack = 0;
   static constexpr bool implicit_ok = true;
   static constexpr bool explicit_ok = false;

@@ -617,11 +617,14 @@ k_jacobian_rk3_stage(const DevProblem* __restrict__ P, DevBuffers Bf, long long 
 // model's ForwardDiff Jacobian over [x; u; dt] at dt = h² (partial c of the chunk, dt the last one),
 // placed at the augmented columns; the dt column times 2h becomes the h column, and row τ+ = h has a 1
 // there. The τ column and the other entries of row τ are zero.
+// With an infeasible model inside (MinTime<Infeasible<Mb>>) the differentiated model is Mb (ModelTraits::Core):
+// its columns [x; u; dt], the slack columns the identity (src/model.jl:771-774), h the last control.
 template <class M, int INTEG, int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TOG_JAC_WAVES)))
 k_jacobian_mt(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) {
-  using Mb = typename ModelTraits<M>::Base;
+  using Mb = typename ModelTraits<M>::Core;
   constexpr int n = M::n, m = M::m, L = n + m, nb = Mb::n, mb = Mb::m, Lz = nb + mb + 1, NCH = (Lz + W - 1) / W;
+  constexpr int SL = ModelTraits<M>::slack;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int N = P->N;
@@ -632,7 +635,7 @@ k_jacobian_mt(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) 
   if (b < 0 || !Bf.st[b].active || Bf.st[b].ls_pend) return;
   const double* x = Bf.X + ((size_t)b * N + k) * n;
   const double* u = Bf.U + ((size_t)b * (N - 1) + k) * m;
-  const double h = u[mb];
+  const double h = u[m - 1];
   Dual<W> xd[nb], ud[mb], xn[nb + 1], dtd;
 #pragma unroll
   for (int i = 0; i < nb; i++) {
@@ -664,13 +667,19 @@ k_jacobian_mt(const DevProblem* __restrict__ P, DevBuffers Bf, long long total) 
       out[nb + n * (n + col - nb)] = 0.0;
     } else if (col == nb + mb) {  // h column: (∂f/∂dt) .* (2h); τ+ = h
 #pragma unroll
-      for (int i = 0; i < nb; i++) out[i + n * (n + mb)] = xn[i].g[w] * (2.0 * h);
-      out[nb + n * (n + mb)] = 1.0;
+      for (int i = 0; i < nb; i++) out[i + n * (n + m - 1)] = xn[i].g[w] * (2.0 * h);
+      out[nb + n * (n + m - 1)] = 1.0;
     }
   }
   if (c == 0) {
 #pragma unroll
     for (int i = 0; i < n; i++) out[i + n * nb] = 0.0;  // τ column
+    if constexpr (SL > 0) {  // slack columns: Diagonal(1.0I, n) (row τ zero)
+#pragma unroll
+      for (int j = 0; j < SL; j++)
+#pragma unroll
+        for (int i = 0; i < n; i++) out[i + n * (n + mb + j)] = (i == j) ? 1.0 : 0.0;
+    }
   }
 }
 
@@ -3307,7 +3316,8 @@ struct ModelLaunch {
   }
   static void jacobian(const DevProblem* P, const DevBuffers& Bf, long long B, int N, int integ, hipStream_t st) {
     if constexpr (ModelTraits<M>::min_time) {
-      constexpr int NCHT = (Mb::n + Mb::m + 1 + JW - 1) / JW;
+      using Mc = typename ModelTraits<M>::Core;
+      constexpr int NCHT = (Mc::n + Mc::m + 1 + JW - 1) / JW;
       const long long total = B * (long long)(N - 1) * NCHT;
       with_integ(integ, [&](auto ic) {
         constexpr int I = decltype(ic)::value;
@@ -3570,7 +3580,8 @@ struct ModelLaunch {
     });
   }
   static void slack_controls(const DevProblem* P, const DevBuffers& Bf, long long B, int integ, hipStream_t st) {
-    if constexpr (ModelTraits<M>::slack > 0) {
+    // (an infeasible minimum-time model takes its slacks from the infeasible problem: tog_slack_controls refuses)
+    if constexpr (ModelTraits<M>::slack > 0 && !ModelTraits<M>::min_time) {
       with_integ(integ, [&](auto ic) {
         constexpr int I = decltype(ic)::value;
         hipLaunchKernelGGL((k_slack_controls<M, I>), dim3(grid(B, 64)), dim3(64), 0, st, P, Bf);

@@ -37,6 +37,10 @@ const ModelOps* ops_inf_pendulum();
 const ModelOps* ops_inf_kuka();
 // add_min_time_controls(model) variants (minimum time, src/solvers/altro/minimum_time.jl:83-104)
 const ModelOps* ops_mt_pendulum();
+const ModelOps* ops_mtinf_pendulum();
+const ModelOps* ops_mtinf_car();
+const ModelOps* ops_mtinf_double_integrator();
+const ModelOps* ops_mtinf_cartpole();
 const ModelOps* ops_mt_car();
 const ModelOps* ops_mt_double_integrator();
 const ModelOps* ops_mt_quadrotor();
@@ -176,8 +180,16 @@ struct tog_model {
 static const ModelOps* ops_for(int model, bool infeasible, bool min_time, const tog_model* user, int integ) {
   if (model == TOG_MODEL_KUKA && !infeasible && !min_time && (integ == TOG_RK3_IMPLICIT || integ == TOG_MIDPOINT_IMPLICIT))
     return ops_kuka_implicit();
+  if (min_time && infeasible) {  // minimum_time_problem(infeasible_problem(prob)): the small models
+    switch (model) {
+      case TOG_MODEL_PENDULUM: return ops_mtinf_pendulum();
+      case TOG_MODEL_CAR: return ops_mtinf_car();
+      case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_mtinf_double_integrator();
+      case TOG_MODEL_CARTPOLE: return ops_mtinf_cartpole();
+    }
+    return nullptr;
+  }
   if (min_time) {
-    if (infeasible) return nullptr;
     if (model == TOG_MODEL_USER) return user ? user->ops_mt : nullptr;
     switch (model) {
       case TOG_MODEL_PENDULUM: return ops_mt_pendulum();
@@ -234,6 +246,7 @@ static bool host_chol_upper(const double* A, int n, double* U) {
 static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_con, std::vector<ConRow>& rows,
                       std::vector<int>& off, std::vector<int>& cnt) {
   const int n = d->n, m = d->m, N = d->N;
+  const int mt = (d->flags & TOG_PROB_MIN_TIME) ? 1 : 0;  // h, the last control
   off.assign(N, 0);
   cnt.assign(N, 0);
   for (int k = 0; k < N; k++) {
@@ -252,8 +265,10 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
           // count 0: trim = true (infinite bounds dropped); 1: trim = false (every row kept). The slack
           // controls of an infeasible-start problem are never bounded: its BoundConstraint keeps the model's
           // m (update_constraint_set_jacobians, constraint_sets.jl:135-150)
+          // (trimmed bounds: rows for the finite entries over all m; the infeasible minimum-time problem's
+          // combined bound reaches u[1:m+1], mintime_constraints, minimum_time.jl:125-141)
           const bool keep = (con.count == 1);
-          const int mb = m - slack;
+          const int mb = keep ? m - slack - mt : m;
           for (int i = 0; i < n; i++)
             if (keep || isfinite(D[i])) rows.push_back({ROW_XMAX, i, D[i], 0, 0, 0});
           if (!term)
@@ -287,7 +302,7 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
           // infeasible_constraints(n, m) (src/constraints.jl:306-314): c = u[m+1:m+n], stage only
           if (!slack) return fail(TOG_ERR_ARG, "TOG_CON_INFEASIBLE needs a TOG_PROB_INFEASIBLE problem");
           if (!term)
-            for (int i = 0; i < slack; i++) rows.push_back({ROW_USLACK, m - slack + i, 0.0, 0.0, 0.0, 0.0});
+            for (int i = 0; i < slack; i++) rows.push_back({ROW_USLACK, m - slack - mt + i, 0.0, 0.0, 0.0, 0.0});
           break;
         case TOG_CON_MIN_TIME_EQ:
           if (!(d->flags & TOG_PROB_MIN_TIME)) return fail(TOG_ERR_ARG, "TOG_CON_MIN_TIME_EQ needs a TOG_PROB_MIN_TIME problem");
@@ -1261,6 +1276,9 @@ int32_t tog_slack_controls(tog_handle* h) {
   if (!h) return fail(TOG_ERR_ARG, "null handle");
   if (is_multi(h)) return each_part(h, [](tog_handle* p, size_t) { return tog_slack_controls(p); });
   if (!h->ops->slack) return fail(TOG_ERR_ARG, "slack_controls needs a TOG_PROB_INFEASIBLE handle");
+  if (h->ops->min_time)
+    return fail(TOG_ERR_ARG, "slack_controls runs on the infeasible problem (infeasible.jl:63-80), before "
+                             "minimum_time_problem appends h");
   HIPCHECK(hipSetDevice(h->device));
   h->ops->slack_controls(h->dP, h->buf, h->B, h->integ, h->stream);
   HIPCHECK(hipGetLastError());

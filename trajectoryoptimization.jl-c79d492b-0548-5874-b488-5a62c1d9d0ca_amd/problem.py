@@ -1055,11 +1055,15 @@ def add_min_time_controls(model: Model) -> Model:
     control [u; h], x+ = f_d(x, u, h²), τ+ = h (the device's MinTime<M>)."""
     if not model.discrete:
         raise ValueError("add_min_time_controls needs a discrete model")
-    if model.slack or model.min_time:
-        raise NotImplementedError("minimum time of an infeasible-start or minimum-time model is not built")
-    # (user plugin models too: each plugin instantiates MinTime<M>, csrc/tog_plugin.hpp)
-    return Model(model.model_id, model.n + 1, model.m + 1, model.name + "_mt", model.integration, min_time=True,
-                 plugin=model.plugin)
+    if model.min_time:
+        raise ValueError("model already has a time-step control")
+    # (user plugin models too: each plugin instantiates MinTime<M>, csrc/tog_plugin.hpp). An infeasible-start
+    # model (altro_problem's infeasible + minimum-time case, altro_methods.jl:98-124) keeps its slacks:
+    # u = [u; s; h], the device's MinTime<Infeasible<M>>
+    if model.slack and model.plugin is not None:
+        raise NotImplementedError("minimum time of an infeasible-start user plugin model is not built")
+    return Model(model.model_id, model.n + 1, model.m + 1, model.name + "_mt", model.integration, model.slack,
+                 plugin=model.plugin, min_time=True)
 
 
 class MinTimeEquality(_Constraint):
@@ -1094,8 +1098,12 @@ def mintime_constraints(prob: Problem, dt_max: float = 1.0, dt_min: float = 1.0e
             others = [c for c in cs if not isinstance(c, BoundConstraint)]
             bnds = [c for c in cs if isinstance(c, BoundConstraint)]
             b = bnds[0] if bnds else BoundConstraint(n, m)
-            bnd2 = BoundConstraint(n + 1, m + 1, x_min=np.append(b.x_min, -math.inf), x_max=np.append(b.x_max, math.inf),
-                                   u_min=np.append(b.u_min, math.sqrt(dt_min)), u_max=np.append(b.u_max, math.sqrt(dt_max)))
+            # combine(bnd, mt_bnd) (constraints.jl:195-203) sizes the result by the bound's own (n, m): an
+            # infeasible problem's bound keeps the model's m, so its √dt bounds land on u[m+1], the first
+            # slack control, and h stays unbounded (the reference's behaviour, reproduced as written)
+            bnd2 = BoundConstraint(n + 1, len(b.u_max) + 1, x_min=np.append(b.x_min, -math.inf),
+                                   x_max=np.append(b.x_max, math.inf), u_min=np.append(b.u_min, math.sqrt(dt_min)),
+                                   u_max=np.append(b.u_max, math.sqrt(dt_max)))
             memo[key] = ConstraintSet(others + [bnd2] + ([eq] if 0 < k < N - 1 else []))
         cons.C[k] = memo[key]
     return cons

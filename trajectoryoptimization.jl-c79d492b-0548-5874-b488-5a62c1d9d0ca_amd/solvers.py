@@ -567,8 +567,6 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
             return _solve_pn(prob, ProjectedNewtonSolver(prob, opts, device=device))
         if isinstance(opts, ALTROSolverOptions):
             _altro_check(prob, opts)
-            if prob.tf == 0.0 and _altro_infeasible(prob):
-                raise NotImplementedError("infeasible start + minimum time is not built")
             _altro_pn_tolerances(opts)  # (mutates opts.opts_al, as the reference does)
             return _solve_altro(prob, opts, device, max_steps=max_steps, history=history)
         if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
