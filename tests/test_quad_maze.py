@@ -116,11 +116,11 @@ def test_full_size_shard_properties(tog, gpu, gold):
 
 
 @pytest.mark.gpu
-def test_packed_records_equal_dense(tog, gpu, monkeypatch):
-    """The std AL expansion records carry only the Q.xx entries a stage row can change (DevProblem::qpat:
-    for config 4, the x-y-z block of the cylinders and spheres and the bounded states' diagonal); the backward
-    pass rebuilds the others as Q dt + 0.0, which is what the expansion computed for them. A solve with packed
-    records equals one with dense records (TOG_DENSE_RECORDS=1) bit for bit."""
+def test_pattern_loop_equals_general_loop(tog, gpu, monkeypatch):
+    """The std AL expansion's row loop over the Q.xx entries a stage row can change (DevProblem::qpat: for
+    config 4, the x-y-z block of the cylinders and spheres and the bounded states' diagonal) adds the same
+    terms in the same order as the general loop over all n entries: a solve with it equals one with the
+    general loop (TOG_DENSE_RECORDS=1) bit for bit."""
     prob, opts = tog.Problems.config_quad_maze(B=24, N=201)
     out = []
     for dense in (False, True):

@@ -142,7 +142,6 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   double dV0 = 0.0, dV1 = 0.0;
   bool done = false;
   auto dense = [&](int k) { return knot_dense<SQRT, AL>(k, N, AL ? kcnt[k] : 0, AL ? knx[k] : 0); };
-  const bool tvc = P->kc != nullptr;  // a time-varying Objective (cost_at)
   int seq = 0;  // knot sequence number (every wave counts alike): the tags' value for this knot
   // The tag is a release store at wavefront scope, read with a workgroup-scope acquire. The release keeps
   // the compiler from moving the tagged data's stores after the tag; the cross-wave order then rests on
@@ -170,13 +169,9 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
       const double* ek = Eg + (size_t)kk * NE;
 #pragma unroll
       for (int i = 0; i < n; i++) Qx[i] = ek[n + m + m * m + i + n * c];
-    } else if (!tvc) {  // the shared cost: its factor at a fixed offset of P (scalar loads)
+    } else {  // (the shared cost: a time-varying Objective takes the LDS kernel)
 #pragma unroll
       for (int i = 0; i < n; i++) Qx[i] = P->cQ[i + n * c];
-    } else {
-      const double* cQ = cost_at<n, m>(P, kk).cQ;
-#pragma unroll
-      for (int i = 0; i < n; i++) Qx[i] = cQ[i + n * c];
     }
   };
   // wave B: knot kk's Q.x entry, Q.u and Q.uu column (the replayed ones in faithful mode), a knot ahead
@@ -531,8 +526,7 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
         // ---------------------------------------------------------------- C: Q.ux, tmp1
         double Quxc[m];
 #pragma unroll
-        for (int i = 0; i < m; i++)  // sqrt AL adds no Q.ux term (A.5); H dt per knot for a time-varying cost
-          Quxc[i] = replay ? Cqr[i] : (tvc ? cost_at<n, m>(P, k).H[i + m * c] * dt : Hdt[i]);
+        for (int i = 0; i < m; i++) Quxc[i] = replay ? Cqr[i] : Hdt[i];  // sqrt AL adds no Q.ux term (A.5)
         // Q.ux += tmp_u' tmp_x (backward_pass.jl:118), the sum wave B formed from S_{k+1}'s rows
 #pragma unroll
         for (int i = 0; i < m; i++) Quxc[i] += QXT[i + m * c];

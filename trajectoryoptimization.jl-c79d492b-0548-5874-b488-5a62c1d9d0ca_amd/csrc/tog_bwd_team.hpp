@@ -502,7 +502,6 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
     }
   }
   const int p = AL ? P->knot_cnt[k] : 0;
-  bool packed = false;  // the packed Q.xx record is written (std AL, DevProblem::qpat)
   if (AL && p > 0) {
     // rows area after the 8-lane QR bus
     RowInfo* rows = reinterpret_cast<RowInfo*>(tlds + 48);
@@ -518,10 +517,9 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
                  team, tl, TEAM);
     team_sync();
     if (!SQRT && !TERM && P->qpat_on) {  // (qpat_on implies at most QPK pattern rows per column)
-      // the same sums over the packed pattern (DevProblem::qpat): tX[i] can only change at column c's
-      // pattern rows, so the row loop tests an entry's index against those (at most QPK) instead of all n;
-      // every (row, entry) pair adds to the same sum in the same order. The record takes Q dt + the sum at
-      // the pattern rows (the other rows are Q dt + 0.0, rebuilt by the backward pass)
+      // the same sums over the pattern (DevProblem::qpat): tX[i] can only change at column c's pattern rows,
+      // so the row loop tests an entry's index against those (at most QPK) instead of all n; every (row,
+      // entry) pair adds to the same sum in the same order, and the other tX[i] stay +0.0
       const unsigned int pc = colx ? as_const(P->qpat)[c] : 0u;
       int pidx[QPK];
       {
@@ -554,15 +552,15 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
         }
       }
 #pragma unroll
-      for (int i = 0; i < m; i++) Quuc[i] += tUu[i];
-      if (colx) {
-        const cptr<double> cQd = as_const(C_.Q);
-        double* eq = Bf.E + ((size_t)b * N + k) * NE + n + m + m * m + as_const(P->qoff)[c];
+      for (int i = 0; i < n; i++) {
+        const int rk = __builtin_popcount(pc & ((1u << i) - 1u));
+        double t = 0.0;
 #pragma unroll
-        for (int j = 0; j < QPK; j++)
-          if (pidx[j] >= 0) eq[j] = cQd[pidx[j] + n * c] * dt + tP[j];
+        for (int j = 0; j < QPK; j++) t = (rk == j && (pc >> i & 1u)) ? tP[j] : t;
+        Qxc[i] += t;
       }
-      packed = true;
+#pragma unroll
+      for (int i = 0; i < m; i++) Quuc[i] += tUu[i];
     } else if (!SQRT) {
       // Q.xx .+= cx'Iμ cx ; Q.uu .+= cu'Iμ cu ; Q.ux .+= cu'Iμ cx  (per-entry sums in row order; the
       // team kernel's rows never couple x and u, so the Q.ux term is an exact zero: ne_of)
@@ -679,7 +677,7 @@ __device__ __forceinline__ void team_expand(const DevProblem* P, const DevBuffer
   }
   int nxk = 0;
   if (AL && SQRT) nxk = P->knot_nx[k];
-  if (colx && knot_dense<SQRT, AL>(k, N, p, nxk) && !packed) {
+  if (colx && knot_dense<SQRT, AL>(k, N, p, nxk)) {
 #pragma unroll
     for (int i = 0; i < n; i++) e[n + m + m * m + i + n * tl] = Qxc[i];
   }
@@ -955,21 +953,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   int pk = -1;  // knot whose inputs the p* registers hold
   BPROF_DECL
 
+  // (the team kernels run the shared stage cost only: a time-varying Objective takes the LDS kernel. Every
+  // alternative form of this lambda measured -- a branch on the per-knot table, strided cost pointers, packed
+  // Q.xx records read back here -- made the std AL backward 20-30 % slower on config 4, profiles/r5s_*)
   // Q blocks of knot k (terminal when TERM) from its expansion record (k_expand_team, ne_of):
   // this lane's columns of Q.xx, Q.uu, Q.ux, its Q.x entry and the whole Q.u
-  // Packed std AL records (k_expand_team, DevProblem::qpat): this lane's column pattern and its packed offset,
-  // loaded once (they do not change along the knots, and loading them per knot put a second memory round trip
-  // on the serial chain). A diagonal cost's Q dt + 0.0 needs only the diagonal entry: the other entries of a
-  // diagonal Q are zeros, and any zero times dt plus +0.0 is +0.0.
-  const bool tvc = P->kc != nullptr;  // a time-varying Objective (cost_at; its records stay dense)
-  const bool qpat = !SQRT && AL && P->qpat_on;
-  const bool qdiag = P->diag_cost != 0;
-  unsigned int pc_l = 0u;
-  int oc_l = 0;
-  if (qpat) {
-    pc_l = as_global(P->qpat)[c];
-    oc_l = as_global(P->qoff)[c];
-  }
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
                     double(&Quxc)[m]) {
     constexpr bool term = decltype(term_c)::value;
@@ -978,41 +966,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const double* e = Eg + (size_t)k * NE;
     const int cnt = AL ? kcnt[k] : 0;
     Qxs = e[c];
-    const bool dense = knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0);
-    if (!tvc) {
-      if (dense && !term && qpat) {
-        // packed record: the pattern entries (at most QPK, contiguous from oc_l); every other entry went
-        // through the expansion as Q dt + (an exact zero row sum)
-        const double* eq = e + n + m + m * m + oc_l;
-        double pv[QPK];
+    if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
 #pragma unroll
-        for (int j = 0; j < QPK; j++) pv[j] = eq[j];  // (within the record: the packed area is < n*n)
-        const double qcc = qdiag ? P->Q[c + n * c] * dt + 0.0 : 0.0;
+      for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+    } else {
 #pragma unroll
-        for (int i = 0; i < n; i++) {
-          const int rk = __builtin_popcount(pc_l & ((1u << i) - 1u));
-          double v = pv[0];
-#pragma unroll
-          for (int j = 1; j < QPK; j++) v = (rk == j) ? pv[j] : v;
-          const double base = qdiag ? ((i == c) ? qcc : 0.0) : P->Q[i + n * c] * dt + 0.0;
-          Qxc[i] = (pc_l >> i & 1u) ? v : base;
-        }
-      } else if (dense) {
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
-      } else {
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
-      }
-    } else {  // knot k's row of the time-varying table (dense records)
-      const CostView C_ = cost_at<n, m>(P, term ? 0 : k);
-      if (dense) {
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
-      } else {
-#pragma unroll
-        for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;
-      }
+      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
     }
     if (!term) {
 #pragma unroll
@@ -1020,10 +979,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
       const bool zterm = !SQRT && AL && cnt > 0;  // the std AL expansion's "+= cu'Iμcx" (an exact zero)
-      const double* Hk = tvc ? cost_at<n, m>(P, k).H : P->H;
 #pragma unroll
       for (int i = 0; i < m; i++) {
-        const double h = Hk[i + m * c] * dt;
+        const double h = P->H[i + m * c] * dt;
         Quxc[i] = zterm ? h + 0.0 : h;
       }
     } else {

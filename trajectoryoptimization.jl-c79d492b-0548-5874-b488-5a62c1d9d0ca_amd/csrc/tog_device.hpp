@@ -78,9 +78,9 @@ struct DevProblem {
   // (compact n, m; cQ, cR the square-root expansion's factors), or null (the fields above at every knot)
   const double* kc;
   int kc_stride, kc_pad;
-  // packed Q.xx records of the std AL expansion (tog_bwd_team.hpp ne_of): the entries any stage row can
-  // change, the union over rows of (state gradient indices)^2, by column: qpat[c] a bit per row i of column
-  // c, qoff[c] the packed offset of column c. qpat_on = 0: dense records.
+  // the Q.xx entries any stage row can change in the std AL expansion (k_expand_team's pattern loop): the
+  // union over rows of (state gradient indices)^2, by column: qpat[c] a bit per row i of column c, qoff[c]
+  // its running count. qpat_on = 0: the general loop.
   int qpat_on, qpat_n;
   unsigned int qpat[NMAX];
   int qoff[NMAX];

@@ -805,10 +805,9 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
       P.qpat_max = std::max(P.qpat_max, __builtin_popcount(pat[c]));
     }
     P.qpat_n = off;
-    // (the backward pass reads QPK entries from a column's packed offset: every column within QPK, and the
-    // packed area QPK short of the record's end; a time-varying Objective keeps dense records)
-    P.qpat_on = (P.qpat_max <= QPK && off + QPK <= n * n && !d->stage_costs &&
-                 getenv("TOG_DENSE_RECORDS") == nullptr) ? 1 : 0;
+    // (the expansion's pattern loop: every column within QPK pattern rows; TOG_DENSE_RECORDS=1 runs the
+    // general loop, for A/B checks)
+    P.qpat_on = (P.qpat_max <= QPK && getenv("TOG_DENSE_RECORDS") == nullptr) ? 1 : 0;
   }
   P.kc = nullptr;
   P.kc_stride = kst;
@@ -842,7 +841,9 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     // TOG_BWD=lds forces the one-wave-per-trajectory LDS backward kernel (A/B checks)
     const char* ev = getenv("TOG_BWD");
     const bool force_lds = ev && strcmp(ev, "lds") == 0;
-    h->bwd_team = (!force_lds && !ops->min_time &&
+    // (a time-varying Objective takes the LDS kernel too: the team kernels run the shared stage cost on
+    // their serial chain, where every per-knot cost read measured 20-30 % slower)
+    h->bwd_team = (!force_lds && !ops->min_time && !d->stage_costs &&
                    team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
                       ? 1 : 0;
     for (int sq = 0; sq < 2; sq++) {
