@@ -513,8 +513,9 @@ void tog_default_altro_options(tog_altro_options* opts);
    whose forward pass reported TOG_TRAJ_COST_INCREASED (the reference's error) carries the flag in its
    stats row. Projected Newton runs on the infeasible-start problem too (models with n + m + n <= 24). An
    initial state trajectory with TOG_PROB_TF_MIN solves minimum_time_problem(infeasible_problem(prob)) (the
-   pendulum, car, double integrator and cartpole), then the feasible minimum-time resolve. Not built: projected
-   Newton on a minimum-time problem (TOG_ERR_UNSUPPORTED). */
+   pendulum, car, double integrator and cartpole), then the feasible minimum-time resolve. Projected Newton
+   runs on minimum-time problems too (its H diagonal from MinTimeCost's hessian! at each newton step's X, U;
+   models with n + m <= 24 after the transforms, larger ones return TOG_ERR_UNSUPPORTED). */
 int32_t tog_solve_altro(const tog_problem_desc* desc, const tog_altro_options* opts, int32_t device,
                         const double* x0, double* X, double* U, double* h, double* stats, double* stats_resolve,
                         double* stats_pn);

@@ -304,6 +304,8 @@ def solve_altro_infeasible_min_time(prob, opts, b=0):
     pmt = _pkg.minimum_time_problem(pinf, opts.R_minimum_time, opts.dt_max, opts.dt_min)
     si = OracleSolver(pmt, opts.opts_al, b)
     si.solve()
+    if opts.projected_newton:  # altro_methods.jl:31-39: phase 2 on prob_altro
+        si.solve_pn(opts.opts_pn)
     Xi, Ui = si.get("X"), si.get("U")
     X, U, h = Xi[:, :n].copy(), Ui[:, :m].copy(), Ui[:, -1].copy()
     p2 = prob.copy()
@@ -331,6 +333,8 @@ def solve_altro_min_time(prob, opts, b=0):
     pmt = _pkg.minimum_time_problem(prob, opts.R_minimum_time, opts.dt_max, opts.dt_min)
     s = OracleSolver(pmt, opts.opts_al, b)
     s.solve()
+    if opts.projected_newton:  # altro_methods.jl:31-39: phase 2 on the minimum-time problem
+        s.solve_pn(opts.opts_pn)
     X, U = s.get("X"), s.get("U")
     return X[:, :n].copy(), U[:, :m].copy(), U[:, m].copy(), s
 

@@ -327,6 +327,26 @@ OC_EXPORT void oc_default_pn_options(tog_pn_options* o) {
   o->feasibility_tolerance = 1e-6;
 }
 
+/* H of a minimum-time problem (update!'s cost_expansion!, projected_newton.jl:122-148, at the newton step's
+   X, U): MinTimeCost's hessian! (minimum_time.jl:238-280) on the diagonal: Q·h² and R·h² for the model's
+   states and controls (dt = h² = u[end]²), R_min_time for τ, 2 ℓ(x, u) + R_min_time for h (ℓ the quadratic
+   stage cost without dt), terminal Qf and R_min_time. */
+static void pn_weights_min_time(const oc_solver* s, pn_ws* ws) {
+  const int n = s->n, m = s->m, N = s->N;
+  for (int k = 0; k < N - 1; k++) {
+    const double* x = s->X + (size_t)k * n;
+    const double* u = s->U + (size_t)k * m;
+    const double h = u[m - 1], dt = h * h;
+    for (int i = 0; i < n - 1; i++) ws->wx[(size_t)k * n + i] = 1.0 / (kQ(s, k)[IDX(i, i, n)] * dt);
+    ws->wx[(size_t)k * n + n - 1] = 1.0 / s->R_mt;
+    for (int i = 0; i < m - 1; i++) ws->wu[(size_t)k * m + i] = 1.0 / (kR(s, k)[IDX(i, i, m)] * dt);
+    const double l1 = stage_cost(s, k, x, u, 1.0);
+    ws->wu[(size_t)k * m + m - 1] = 1.0 / (2.0 * l1 + s->R_mt);
+  }
+  for (int i = 0; i < n - 1; i++) ws->wx[(size_t)(N - 1) * n + i] = 1.0 / s->Qf[IDX(i, i, n)];
+  ws->wx[(size_t)(N - 1) * n + n - 1] = 1.0 / s->R_mt;
+}
+
 /* solve!(prob, ProjectedNewtonSolver) (projected_newton.jl:6-20); out: TOG_PN_NSTATS doubles.
    Returns 0, or -4 for solve_type :optimal (not built). */
 OC_EXPORT int oc_solve_pn(oc_solver* s, const tog_pn_options* o, double* out) {
@@ -371,6 +391,7 @@ OC_EXPORT int oc_solve_pn(oc_solver* s, const tog_pn_options* o, double* out) {
   int steps = 0;
   s->hpn_n = 0;
   for (int it = 0; it < o->n_steps; it++) {
+    if (s->mt) pn_weights_min_time(s, ws);
     /* newton_step!: update! (active set at V), then projection_solve! */
     pn_eval(s, ws, s->X, s->U);
     pn_active_set(s, ws, o->active_set_tolerance);

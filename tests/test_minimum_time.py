@@ -224,3 +224,58 @@ def test_gpu_infeasible_min_time_equals_oracle(tog, oracle, gpu, resolve):
     assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])
     if resolve:
         assert int(solver.stats_feasible["iterations_total"][0]) == int(sf.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+
+
+def _pn_mt_opts(opts):
+    opts.projected_newton = True
+    # 1e-2 leaves the pendulum's projection short of 1e-8 in 3 steps: the line search fails and the oracle flags
+    # TOG_TRAJ_PN_ERROR (the reference raises), as the device does; from 1e-3 one newton step reaches 6.6e-9
+    opts.projected_newton_tolerance = 1e-3
+    opts.opts_pn.n_steps = 3
+    opts.opts_pn.feasibility_tolerance = 1e-8
+    return opts
+
+
+def test_oracle_min_time_projected_newton(tog, oracle):
+    """Projected Newton on the minimum-time problem (altro_methods.jl:31-39 with prob_altro =
+    minimum_time_problem): its H is MinTimeCost's hessian! diagonal at the newton step's X, U
+    (minimum_time.jl:238-280). After the AL phase stopped at projected_newton_tolerance the projection
+    reduces the violation."""
+    make, opts, xf, U0, dt, dt_mt, _ = pendulum_case(tog)
+    opts = _pn_mt_opts(opts)
+    tog.solvers._altro_pn_tolerances(opts)
+    p = make(U0, dt_mt, tf="min")
+    pmt = tog.minimum_time_problem(p, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    s = oracle.OracleSolver(pmt, opts.opts_al)
+    s.solve()
+    c_al = s.max_violation()
+    st = s.solve_pn(opts.opts_pn)
+    assert st[tog.abi.PN_STEPS] >= 1 and s.max_violation() < min(c_al, 1e-8)
+    assert not int(s.get("stats")[tog.abi.STAT_FLAGS]) & tog.abi.TRAJ_PN_ERROR
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("infeasible", [False, True])
+def test_gpu_min_time_projected_newton(tog, oracle, gpu, infeasible):
+    """solve_b with tf = :min and projected_newton (and an initial state trajectory): the device's projected
+    Newton on MinTime<Pendulum> / MinTime<Infeasible<Pendulum>> (per-knot H from the newton step's X, U)
+    against the oracle's same flow: X, U, h within 1e-6, as the minimum-time AL phase before it."""
+    if infeasible:
+        p, opts, _ = _inf_mt_case(tog, resolve=False)
+    else:
+        make, opts, xf, U0, dt, dt_mt, _ = pendulum_case(tog)
+        p = make(U0, dt_mt, tf="min")
+    opts = _pn_mt_opts(opts)
+    ref = p.copy()
+    solver = tog.solve_b(p, opts)
+    assert solver.stats["time_pn"] > 0.0
+    if infeasible:
+        Xo, Uo, ho, si, _ = oracle.solve_altro_infeasible_min_time(ref, opts, 0)
+    else:
+        Xo, Uo, ho, si = oracle.solve_altro_min_time(ref, opts, 0)
+    tol = 1e-6
+    scale = lambda a: max(1.0, float(np.max(np.abs(a))))  # noqa: E731
+    assert np.max(np.abs(p._X[0] - Xo)) <= tol * scale(Xo)
+    assert np.max(np.abs(p._U[0] - Uo)) <= tol * scale(Uo)
+    assert np.max(np.abs(p.h[0] - ho)) <= tol
+    assert int(solver.stats_pn["iterations"][0]) >= 1

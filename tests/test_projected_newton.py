@@ -87,13 +87,12 @@ def test_pn_accepts_infeasible_start(tog):
     tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
 
 
-def test_pn_rejects_min_time(tog):
-    """phase 2 on a minimum-time problem (altro_methods.jl:98-124) is refused, not
-    silently skipped."""
+def test_pn_accepts_min_time(tog):
+    """Round 5: phase 2 on a minimum-time problem (altro_methods.jl:98-124) is built (its H from MinTimeCost's
+    hessian!, tests/test_minimum_time.py test_gpu_min_time_projected_newton); the host check lets it through."""
     prob = tog.Problems.pendulum()
     prob.tf = 0.0
-    with pytest.raises(NotImplementedError):
-        tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
+    tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
     tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=False))
 
 

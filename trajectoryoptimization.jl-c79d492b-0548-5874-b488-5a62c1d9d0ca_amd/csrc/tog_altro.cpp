@@ -133,8 +133,6 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     return tog__fail(TOG_ERR_ARG, "infeasible start: X must be given for every trajectory of the batch or for none");
   const bool infeasible = given == B && B > 0;
   const bool min_time = (desc->flags & TOG_PROB_TF_MIN) != 0;
-  if (opts->projected_newton && min_time)
-    return tog__fail(TOG_ERR_UNSUPPORTED, "projected Newton on the minimum-time problem");
   if (opts->max_steps < 0) return tog__fail(TOG_ERR_ARG, "max_steps must be >= 0");
   tog_options oal = opts->opts_al;
   if (opts->projected_newton) {  // altro_methods.jl:5-13
@@ -151,6 +149,25 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     if (R->keep_handle) R->handle = H.release();
     R->time = now_s() - t0;
     return TOG_OK;
+  };
+  // solve!(prob_altro, solver.solver_pn) (altro_methods.jl:31-39) on the AL phase's handle, before
+  // process_results!; a trajectory whose AL phase raised never gets there (its statistics zero, its history NaN)
+  auto phase2 = [&](Handle& H, const std::vector<char>& err) {
+    std::vector<double> pn((size_t)TOG_PN_NSTATS * B);
+    const double tp = now_s();
+    int rc2;
+    if ((rc2 = tog_solve_pn(H.h, &opts->opts_pn, pn.data()))) return rc2;
+    R->time_pn = now_s() - tp;
+    if (R->hist_pn && (rc2 = tog_get_pn_history(H.h, R->hist_pn, nullptr))) return rc2;
+    const size_t np = 2 * (size_t)opts->opts_pn.n_steps;
+    for (long long b = 0; b < B; b++) {
+      if (!err[b]) continue;
+      memset(pn.data() + (size_t)TOG_PN_NSTATS * b, 0, sizeof(double) * TOG_PN_NSTATS);
+      if (R->hist_pn)
+        for (size_t i = 0; i < np; i++) R->hist_pn[np * b + i] = NAN;
+    }
+    if (R->stats_pn) memcpy(R->stats_pn, pn.data(), sizeof(double) * pn.size());
+    return (int)TOG_OK;
   };
   if (infeasible && min_time) {
     // minimum_time_problem(infeasible_problem(prob)) (altro_methods.jl:98-124). The slacks come from
@@ -196,6 +213,7 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     R->time_al = now_s() - ta;
     const std::vector<char> err = raised(H1.h, B, rc);
     if (rc) return rc;
+    if (opts->projected_newton && (rc = phase2(H1, err))) return rc;
     if ((rc = tog_get(H1.h, TOG_FIELD_X, Xt.data())) || (rc = tog_get(H1.h, TOG_FIELD_U, Ut.data()))) return rc;
     if ((rc = read_al(H1.h, R))) return rc;
     // process_results!: X[1:n], U[1:m]; then infeasible_to_feasible_problem (infeasible.jl:37-58): the feasible
@@ -264,23 +282,8 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     R->time_al = now_s() - ta;
     const std::vector<char> err = raised(H1.h, B, rc);
     if (rc) return rc;
-    if (opts->projected_newton) {
-      // solve!(prob_altro, solver.solver_pn) on the infeasible problem (altro_methods.jl:31-39); a raised
-      // trajectory never gets there (its X, U go back to the caller's below)
-      std::vector<double> pn((size_t)TOG_PN_NSTATS * B);
-      const double tp = now_s();
-      if ((rc = tog_solve_pn(H1.h, &opts->opts_pn, pn.data()))) return rc;
-      R->time_pn = now_s() - tp;
-      if (R->hist_pn && (rc = tog_get_pn_history(H1.h, R->hist_pn, nullptr))) return rc;
-      const size_t np = 2 * (size_t)opts->opts_pn.n_steps;
-      for (long long b = 0; b < B; b++) {
-        if (!err[b]) continue;
-        memset(pn.data() + (size_t)TOG_PN_NSTATS * b, 0, sizeof(double) * TOG_PN_NSTATS);
-        if (R->hist_pn)
-          for (size_t i = 0; i < np; i++) R->hist_pn[np * b + i] = NAN;
-      }
-      if (R->stats_pn) memcpy(R->stats_pn, pn.data(), sizeof(double) * pn.size());
-    }
+    // (on the infeasible problem; a raised trajectory's X, U go back to the caller's below)
+    if (opts->projected_newton && (rc = phase2(H1, err))) return rc;
     std::vector<double> Xi(nX * B);
     if ((rc = tog_get(H1.h, TOG_FIELD_X, Xi.data())) || (rc = tog_get(H1.h, TOG_FIELD_U, Ui.data()))) return rc;
     // (the statistics rows after projected Newton: its TOG_TRAJ_PN_ERROR lands in the flags)
@@ -329,10 +332,12 @@ int32_t tog_solve_altro_ex(const tog_problem_desc* desc, const tog_altro_options
     if ((rc = run(&dm.d, &oal, device, x0t.data(), Ut.data(), nullptr, false, TOG_MODE_AL, H, opts->max_steps, hcap)))
       return rc;
     R->time_al = now_s() - ta;
-    if ((rc = tog_get(H.h, TOG_FIELD_X, Xt.data())) || (rc = tog_get(H.h, TOG_FIELD_U, Ut.data()))) return rc;
-    if ((rc = read_al(H.h, R))) return rc;
     const std::vector<char> err = raised(H.h, B, rc);
     if (rc) return rc;
+    // projected Newton on the minimum-time problem (its H from MinTimeCost's hessian!, tog_pn.hpp)
+    if (opts->projected_newton && (rc = phase2(H, err))) return rc;
+    if ((rc = tog_get(H.h, TOG_FIELD_X, Xt.data())) || (rc = tog_get(H.h, TOG_FIELD_U, Ut.data()))) return rc;
+    if ((rc = read_al(H.h, R))) return rc;
     for (long long b = 0; b < B; b++) {  // process_results!: X[1:n], U[1:m]; h separately
       if (err[b]) continue;  // minimum_time_problem's copy raised: prob untouched
       if (X)

@@ -3631,9 +3631,9 @@ struct ModelLaunch {
     o.cost = cost;
     o.rollout = rollout;
     o.update_constraints = update_constraints;
-    // projected Newton: plain models, and the infeasible-start models whose [x; u; s] fits the PN
-    // kernels' blocks (n + m <= 24: the small models; tog_solve_pn refuses larger ones)
-    if constexpr (!ModelTraits<M>::min_time && (ModelTraits<M>::slack == 0 || M::n + M::m <= 24))
+    // projected Newton: plain models; the infeasible-start and minimum-time models whose [x; u] fits the PN
+    // kernels' blocks (n + m <= 24; tog_solve_pn refuses larger ones)
+    if constexpr ((ModelTraits<M>::slack == 0 && !ModelTraits<M>::min_time) || M::n + M::m <= 24)
       o.pn = pn;
     else
       o.pn = nullptr;

@@ -36,13 +36,14 @@ struct PNBuffers {
   double* Xs;                       // (B, N, n) the point S and H⁻¹Yᵀ were formed at (_projection_solve! start)
   int *act, *na, *sz;               // (B, N, pmax) active rows, (B, N) counts, (B, nb) block sizes
   PNState* st;                      // (B)
+  double* wt;                       // (B, N n + (N-1) m) H⁻¹ diagonal of a minimum-time problem, per newton step
   int SM, nb;
   double atol, eps;                 // active_set_tolerance, feasibility_tolerance
 };
 
 // per-trajectory views of the workspace
 struct PNView {
-  double *Sd, *So, *Ld, *Lo, *yv, *xv, *rv, *wv, *dv, *yd, *Xs;
+  double *Sd, *So, *Ld, *Lo, *yv, *xv, *rv, *wv, *dv, *yd, *Xs, *wt;
   int *act, *na, *sz;
   int SM;
   __device__ double* M(double* A, int b) const { return A + (size_t)b * SM * SM; }
@@ -63,6 +64,7 @@ __device__ __forceinline__ PNView pn_view(const PNBuffers& W, const DevProblem* 
   v.dv = W.dv + b * vec;
   v.yd = W.yd + (size_t)b * P->N * P->n;
   v.Xs = W.Xs + (size_t)b * P->N * P->n;
+  v.wt = W.wt ? W.wt + (size_t)b * (P->N * P->n + (P->N - 1) * P->m) : nullptr;
   v.act = W.act + (size_t)b * P->N * P->pmax;
   v.na = W.na + (size_t)b * P->N;
   v.sz = W.sz + (size_t)b * W.nb;
@@ -72,16 +74,55 @@ __device__ __forceinline__ PNView pn_view(const PNBuffers& W, const DevProblem* 
 
 __device__ __forceinline__ void pn_sync() { __syncthreads(); }  // one-wave blocks: orders LDS traffic
 
-// H⁻¹ diagonal (Diagonal(solver.H): Q·dt, R·dt, terminal Qf; cost.jl:214-228)
-__device__ __forceinline__ double pn_wx(const DevProblem* P, int k, int i) {
-  const int n = P->n;
-  if (k == P->N - 1) return 1.0 / P->Qf[i + n * i];
-  const double* Q = P->kc ? P->kc + (size_t)k * P->kc_stride : P->Q;  // a time-varying Objective's knot k
-  return 1.0 / (Q[i + n * i] * P->dt);
+// H⁻¹ diagonal (Diagonal(solver.H): Q·dt, R·dt, terminal Qf; cost.jl:214-228). A minimum-time problem's
+// depends on the newton step's X, U (MinTimeCost's hessian!, minimum_time.jl:238-280): k_pn_begin writes it
+// to the view's wt (pn_weights_min_time).
+template <class M>
+__device__ __forceinline__ double pn_wx(const DevProblem* P, const PNView& w, int k, int i) {
+  if constexpr (ModelTraits<M>::min_time) {
+    return w.wt[(size_t)k * M::n + i];
+  } else {
+    const int n = P->n;
+    if (k == P->N - 1) return 1.0 / P->Qf[i + n * i];
+    const double* Q = P->kc ? P->kc + (size_t)k * P->kc_stride : P->Q;  // a time-varying Objective's knot k
+    return 1.0 / (Q[i + n * i] * P->dt);
+  }
 }
-__device__ __forceinline__ double pn_wu(const DevProblem* P, int k, int i) {
-  const double* R = P->kc ? P->kc + (size_t)k * P->kc_stride + P->n * P->n : P->R;
-  return 1.0 / (R[i + P->m * i] * P->dt);
+template <class M>
+__device__ __forceinline__ double pn_wu(const DevProblem* P, const PNView& w, int k, int i) {
+  if constexpr (ModelTraits<M>::min_time) {
+    return w.wt[(size_t)P->N * M::n + (size_t)k * M::m + i];
+  } else {
+    const double* R = P->kc ? P->kc + (size_t)k * P->kc_stride + P->n * P->n : P->R;
+    return 1.0 / (R[i + P->m * i] * P->dt);
+  }
+}
+// update!'s cost_expansion! of a minimum-time problem (projected_newton.jl:122-148) at X, U, on the diagonal:
+// Q·h² and R·h² for the model's states and controls (dt = h² = u[end]²), R_min_time for τ, 2 ℓ(x, u) +
+// R_min_time for h (ℓ the quadratic stage cost without dt), terminal Qf and R_min_time. A lane per knot.
+template <class M>
+__device__ void pn_weights_min_time(const DevProblem* P, const PNView& w, const double* X, const double* U, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  for (int k = lane; k < N; k += WAVE) {
+    double* wx = w.wt + (size_t)k * n;
+    if (k < N - 1) {
+      double* wu = w.wt + (size_t)N * n + (size_t)k * m;
+      const double* x = X + (size_t)k * n;
+      const double* u = U + (size_t)k * m;
+      const CostView C_ = cost_at<n, m>(P, k);
+      const double h = u[m - 1], dt = h * h;
+      for (int i = 0; i < n - 1; i++) wx[i] = 1.0 / (C_.Q[i + n * i] * dt);
+      wx[n - 1] = 1.0 / P->R_min_time;
+      for (int i = 0; i < m - 1; i++) wu[i] = 1.0 / (C_.R[i + m * i] * dt);
+      const double l1 = stage_cost_dt<n, m>(P, k, x, u, 1.0);
+      wu[m - 1] = 1.0 / (2.0 * l1 + P->R_min_time);
+    } else {
+      for (int i = 0; i < n - 1; i++) wx[i] = 1.0 / P->Qf[i + n * i];
+      wx[n - 1] = 1.0 / P->R_min_time;
+    }
+  }
+  pn_sync();
 }
 
 // dynamics_constraints! + update_constraints! at (X, U): dynamics rows into yd, constraint values
@@ -180,7 +221,7 @@ __device__ void pn_build_S(const DevProblem* P, const DevBuffers& Bf, long long 
   const int N = P->N, SM = w.SM;
   {
     double* S0 = w.M(w.Sd, 0);
-    for (int e = lane; e < SM * SM; e += WAVE) S0[e] = ((e % SM) == (e / SM) && (e % SM) < n) ? pn_wx(P, 0, e % SM) : 0.0;
+    for (int e = lane; e < SM * SM; e += WAVE) S0[e] = ((e % SM) == (e / SM) && (e % SM) < n) ? pn_wx<M>(P, w, 0, e % SM) : 0.0;
   }
   for (int bb = 1; bb < nb; bb++) {
     const int j = bb - 1, sb = w.sz[bb], sp = w.sz[bb - 1], nv = (bb < N) ? n + m : n;
@@ -190,17 +231,17 @@ __device__ void pn_build_S(const DevProblem* P, const DevBuffers& Bf, long long 
       const int i = e % sb, l = e / sb;
       double acc = 0.0;
       for (int v = 0; v < nv; v++) {
-        const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, j, v - n);
+        const double wv = v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
         acc = fma(Yz[i + SM * v], wv * Yz[l + SM * v], acc);
       }
-      if (bb < N && i < n && i == l) acc = acc + pn_wx(P, j + 1, i);
+      if (bb < N && i < n && i == l) acc = acc + pn_wx<M>(P, w, j + 1, i);
       Sd[i + SM * l] = acc;
     }
     const double sg = (bb - 1 == 0) ? 1.0 : -1.0;
     double* So = w.M(w.So, bb);
     for (int e = lane; e < sb * sp; e += WAVE) {
       const int i = e % sb, c = e / sb;
-      So[i + SM * c] = (c < n) ? Yz[i + SM * c] * (sg * pn_wx(P, j, c)) : 0.0;
+      So[i + SM * c] = (c < n) ? Yz[i + SM * c] * (sg * pn_wx<M>(P, w, j, c)) : 0.0;
     }
     pn_sync();
   }
@@ -388,7 +429,7 @@ __device__ void pn_trial(const DevProblem* P, const DevBuffers& Bf, long long b,
       if (v < n) t = (j == 0) ? w.V(w.xv, 0)[v] : -w.V(w.xv, j)[v];
       const double* lb = w.V(w.xv, bb);
       for (int i = 0; i < w.sz[bb]; i++) t = fma(Yz[i + SM * v], lb[i], t);
-      const double wv = v < n ? pn_wx(P, j, v) : pn_wu(P, j, v - n);
+      const double wv = v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
       const double dz = -(wv * t);
       if (v < n)
         Xt[(size_t)j * n + v] = X[(size_t)j * n + v] + alpha * dz;
@@ -408,6 +449,8 @@ __global__ void __launch_bounds__(64) k_pn_begin(const DevProblem* __restrict__ 
   if (s.finished) return;
   const PNView w = pn_view(W, P, b);
   const int N = P->N;
+  if constexpr (ModelTraits<M>::min_time)
+    pn_weights_min_time<M>(P, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
   pn_eval<M, INTEG>(P, Bf, b, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
   pn_active_set(P, Bf, b, w, W.atol, W.nb, lane);
   const double viol = pn_gather_y(P, Bf, b, w, W.nb, lane);

@@ -1638,9 +1638,7 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     });
   if (opts->solve_type != 0) return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal is not built");
   if (opts->n_steps < 0) return fail(TOG_ERR_ARG, "n_steps must be >= 0");
-  if (!h->ops->pn)
-    return fail(TOG_ERR_UNSUPPORTED, h->ops->min_time ? "projected Newton on a minimum-time problem is not built"
-                                                      : "projected Newton blocks larger than n + m = 24 are not built");
+  if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than n + m = 24 are not built");
   const int SM = h->n + h->pmax;
   if (SM > PN_SM_MAX || h->n + h->m > 24)
     return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than 32 rows (n + pmax) are not built");
@@ -1670,7 +1668,8 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
         (rc = dalloc(h, &W.yd, (size_t)B * h->N * h->n)) || (rc = dalloc(h, &W.Xs, (size_t)B * h->N * h->n)) ||
         (rc = dalloc(h, &W.act, (size_t)B * h->N * (h->pmax > 0 ? h->pmax : 1))) ||
         (rc = dalloc(h, &W.na, (size_t)B * h->N)) || (rc = dalloc(h, &W.sz, (size_t)B * W.nb)) ||
-        (rc = dalloc(h, &W.st, (size_t)B))) {
+        (rc = dalloc(h, &W.st, (size_t)B)) ||
+        (h->ops->min_time && (rc = dalloc(h, &W.wt, (size_t)B * ((size_t)h->N * h->n + (size_t)(h->N - 1) * h->m))))) {
       // partial failure: release what this call allocated, so a retry does not leak it
       for (size_t i = mark; i < h->allocs.size(); i++) (void)hipFree(h->allocs[i]);
       h->allocs.resize(mark);

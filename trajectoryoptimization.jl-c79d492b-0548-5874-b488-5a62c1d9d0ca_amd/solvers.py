@@ -428,12 +428,9 @@ def AbstractSolverFor(prob, opts, **kw):
 
 
 def _altro_check(prob, opts):
-    # projected Newton on the infeasible-start problem: the device builds it for n + (m + n) <= 24
-    # (tog_solve_pn refuses larger blocks with TOG_ERR_UNSUPPORTED)
-    if opts.projected_newton and prob.tf == 0.0:
-        # altro_methods.jl:98-124 would run phase 2 on the minimum-time problem (the projection over
-        # [u; h]); the device projected Newton has no MinTime model, so refuse instead of skipping it
-        raise NotImplementedError("projected Newton on the minimum-time problem is not built")
+    # projected Newton on the infeasible-start and minimum-time problems: the device builds it for models whose
+    # [x; u] has n + m <= 24 (tog_solve_pn refuses larger blocks with TOG_ERR_UNSUPPORTED)
+    return None
 
 
 def _altro_pn_tolerances(opts):
