@@ -443,11 +443,12 @@ int32_t tog_status(tog_handle* h, int32_t* flags_out);
 
 /* ---- ALTRO phase 2: projected Newton (src/solvers/direct/projected_newton.jl) ---- */
 /* ProjectedNewtonSolverOptions (src/solvers/direct/direct_solvers.jl:14-30); tog_default_pn_options
-   fills the reference defaults. Only solve_type :feasible (the default) is built: newton_step!
-   returns after projection_solve! (projected_newton.jl:498-501). */
+   fills the reference defaults. solve_type :feasible (the default): newton_step! returns after
+   projection_solve! (projected_newton.jl:518-520); :optimal adds multiplier_projection!, solveKKT_Shur and
+   line_search (:522-546), not built on minimum-time problems (TOG_ERR_UNSUPPORTED). */
 typedef struct tog_pn_options {
   int32_t n_steps;              /* 1                                                          */
-  int32_t solve_type;           /* 0 = :feasible (1 = :optimal -> TOG_ERR_UNSUPPORTED)        */
+  int32_t solve_type;           /* 0 = :feasible, 1 = :optimal                                */
   double active_set_tolerance;  /* 1e-3: inequality rows with c >= -tol are projected         */
   double feasibility_tolerance; /* 1e-6                                                       */
 } tog_pn_options;

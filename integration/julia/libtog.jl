@@ -484,8 +484,9 @@ function tog_altro_options(opts::ALTROSolverOptions)
     a.resolve_feasible_problem = opts.resolve_feasible_problem
     a.projected_newton = opts.projected_newton
     pn = opts.opts_pn
-    pn.solve_type == :feasible || throw(ArgumentError("projected Newton solve_type $(pn.solve_type) is not built"))
-    a.opts_pn = TogPNOptions(Int32(pn.n_steps), Int32(0), pn.active_set_tolerance, pn.feasibility_tolerance)
+    pn.solve_type in (:feasible, :optimal) || throw(ArgumentError("solve_type must be :feasible or :optimal"))
+    a.opts_pn = TogPNOptions(Int32(pn.n_steps), Int32(pn.solve_type == :optimal ? 1 : 0), pn.active_set_tolerance,
+                             pn.feasibility_tolerance)
     return a
 end
 

@@ -59,8 +59,7 @@ def test_pn_options_defaults(tog):
     d = tog.abi.tog_pn_options()
     lib.tog_default_pn_options(d)
     assert (d.n_steps, d.solve_type, d.active_set_tolerance, d.feasibility_tolerance) == (1, 0, 1e-3, 1e-6)
-    with pytest.raises(NotImplementedError):
-        tog.to_tog_pn_options(tog.ProjectedNewtonSolverOptions(solve_type="optimal"))
+    assert tog.to_tog_pn_options(tog.ProjectedNewtonSolverOptions(solve_type="optimal")).solve_type == 1
     with pytest.raises(ValueError):
         tog.to_tog_pn_options(tog.ProjectedNewtonSolverOptions(solve_type="fast"))
 
@@ -128,6 +127,56 @@ def test_oracle_projection_noop_when_feasible(tog, oracle):
     out = o.solve_pn(tog.ProjectedNewtonSolverOptions(feasibility_tolerance=1e-2))
     assert out[tog.abi.PN_PROJECTIONS] == 0 and out[tog.abi.PN_STEPS] == 1
     assert np.array_equal(o.get("X"), X) and np.array_equal(o.get("U"), U)
+
+
+def _optimal_vs_feasible(tog, oracle, ft=1e-10, n_steps=1, prob=None):
+    prob = prob if prob is not None else tog.Problems.car_obstacles()
+    res = {}
+    for st in ("feasible", "optimal"):
+        o = oracle.OracleSolver(prob, car_al_opts(tog))
+        o.solve()
+        out = o.solve_pn(tog.ProjectedNewtonSolverOptions(feasibility_tolerance=ft, n_steps=n_steps, solve_type=st))
+        res[st] = (o, out, int(o.get("stats")[tog.abi.STAT_FLAGS]))
+    return res
+
+
+def test_oracle_optimal_newton_step(tog, oracle):
+    """solve_type :optimal (newton_step!, projected_newton.jl:501-547: the projection, multiplier_projection!,
+    solveKKT_Shur with stats[:S], line_search with projection! at each trial) on the reference's projected
+    Newton problem: test/projected_newton_test.jl:161-170's assertions for a newton step -- the result is
+    feasible to 1e-10 and costs less than the start -- and it costs less than the :feasible projection of the
+    same AL iterate (the KKT step moves along the constraint manifold towards the optimum)."""
+    r = _optimal_vs_feasible(tog, oracle)
+    (of, outf, ff), (oo, outo, fo) = r["feasible"], r["optimal"]
+    assert not fo & tog.abi.TRAJ_PN_ERROR and not ff & tog.abi.TRAJ_PN_ERROR
+    assert outo[tog.abi.PN_C_MAX] < 1e-10 and outo[tog.abi.PN_C_MAX] == oo.max_violation()
+    assert outo[tog.abi.PN_J] < outf[tog.abi.PN_J]
+    assert outo[tog.abi.PN_J] == oo.cost()
+    assert outo[tog.abi.PN_STEPS] == 1 and outo[tog.abi.PN_PROJECTIONS] >= 1
+
+
+def test_oracle_optimal_steps_restart_from_solver_v(tog, oracle):
+    """solve! copies each newton step's V_ into prob but never into solver.V (projected_newton.jl:8-17), so a
+    second :optimal step restarts from the projected solver.V: with a tolerance the first step cannot meet
+    (feasibility_tolerance = 0 never breaks), three steps return what one step returns, or flag the stale
+    stats[:S] (a step that did not project uses the previous factor)."""
+    one = _optimal_vs_feasible(tog, oracle, ft=0.0, n_steps=1)["optimal"]
+    three = _optimal_vs_feasible(tog, oracle, ft=0.0, n_steps=3)["optimal"]
+    if not three[2] & tog.abi.TRAJ_PN_ERROR:
+        assert np.array_equal(one[0].get("X"), three[0].get("X"))
+        assert np.array_equal(one[0].get("U"), three[0].get("U"))
+
+
+def test_oracle_optimal_refused_on_min_time(tog, oracle):
+    """The minimum-time problem's H moves with V inside the line search: :optimal there is not built, on the
+    oracle as on the device (TOG_ERR_UNSUPPORTED)."""
+    import test_minimum_time as T
+    make, opts, xf, U0, dt, dt_mt, _ = T.pendulum_case(tog)
+    p = make(U0, dt_mt, tf="min")
+    pmt = tog.minimum_time_problem(p, opts.R_minimum_time, opts.dt_max, opts.dt_min)
+    o = oracle.OracleSolver(pmt, opts.opts_al)
+    with pytest.raises(NotImplementedError):
+        o.solve_pn(tog.ProjectedNewtonSolverOptions(solve_type="optimal"))
 
 
 def test_car_batch_problem(tog, oracle):
@@ -205,3 +254,35 @@ def test_gpu_pn_quad_maze(tog, oracle, gpu):
     prob, opts = tog.Problems.config_quad_maze(B=2, N=41)
     pn = tog.ProjectedNewtonSolverOptions(feasibility_tolerance=1e-8, n_steps=2)
     _pn_compare(tog, oracle, prob, opts, pn)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ft,n_steps", [(1e-10, 1), (1e-6, 1), (0.0, 3)])
+def test_gpu_pn_optimal_parity(tog, oracle, gpu, ft, n_steps):
+    """solve_type :optimal on the device (k_pn_kkt, k_pn_ls_begin / k_pn_ls_proj / k_pn_ls_end, tog_pn.hpp)
+    against the oracle from the same AL iterates, 4 perturbed car starts: X, U and every statistic to 1e-13
+    (one newton step; three steps that restart from solver.V)."""
+    prob = car_batch(tog, 4)
+    pn = tog.ProjectedNewtonSolverOptions(feasibility_tolerance=ft, n_steps=n_steps, solve_type="optimal")
+    gp, st = _pn_compare(tog, oracle, prob, car_al_opts(tog), pn)
+    assert np.all(np.isfinite(gp._X)) and np.all(np.isfinite(gp._U))
+
+
+@pytest.mark.gpu
+def test_gpu_altro_pn_optimal(tog, oracle, gpu):
+    """ALTRO with opts_pn.solve_type = :optimal end to end (altro_methods.jl:31-39): the AL phase to 1e-2 and
+    the KKT polish on the device against the oracle's two phases."""
+    prob = car_batch(tog, 3, seed=11)
+    opts = tog.ALTROSolverOptions(opts_al=car_al_opts(tog, tol=1e-3), projected_newton=True,
+                                  projected_newton_tolerance=1e-2)
+    opts.opts_pn.feasibility_tolerance = 1e-8
+    opts.opts_pn.solve_type = "optimal"
+    gp = prob.copy()
+    solver = tog.solve_b(gp, opts)
+    for b in range(prob.B):
+        o = oracle.OracleSolver(prob, opts.opts_al, b=b)
+        o.solve()
+        out = o.solve_pn(opts.opts_pn)
+        assert rel(gp._X[b], o.get("X")) < TOL_STEP and rel(gp._U[b], o.get("U")) < TOL_STEP, b
+        assert solver.stats_pn["iterations"][b] == out[tog.abi.PN_STEPS]
+        assert abs(solver.stats_pn["c_max"][b] - out[tog.abi.PN_C_MAX]) <= 1e-13

@@ -3254,7 +3254,8 @@ struct ModelOps {
   void (*cost)(const DevProblem*, const DevBuffers&, long long B, int al, int use_bar, double* J, hipStream_t);
   void (*rollout)(const DevProblem*, const DevBuffers&, long long B, int integ, double alpha, int* ok, hipStream_t);
   void (*update_constraints)(const DevProblem*, const DevBuffers&, long long B, hipStream_t);
-  // projected Newton (tog_pn.hpp): phase 0 = k_pn_begin, 1 = k_pn_project, 2 = k_pn_finish; null for
+  // projected Newton (tog_pn.hpp): phase 0 = k_pn_begin, 1 = k_pn_project, 2 = k_pn_finish, :optimal's
+  // 3 = k_pn_kkt, 4 = k_pn_ls_begin, 5 = k_pn_ls_proj, 6 = k_pn_ls_end; null for
   // the infeasible (slack) models
   void (*pn)(const DevProblem*, const DevBuffers&, const PNBuffers&, long long B, int integ, int phase, hipStream_t);
   bool implicit;                   // TOG_RK3_IMPLICIT / TOG_MIDPOINT_IMPLICIT instantiated
@@ -3603,8 +3604,18 @@ struct ModelLaunch {
       hipLaunchKernelGGL((k_pn_begin<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
     else if (phase == 1)
       hipLaunchKernelGGL((k_pn_project<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
-    else
+    else if (phase == 2)
       hipLaunchKernelGGL((k_pn_finish<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+    else if constexpr (!ModelTraits<M>::min_time) {  // solve_type :optimal (not built for minimum time)
+      if (phase == 3)
+        hipLaunchKernelGGL((k_pn_kkt<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+      else if (phase == 4)
+        hipLaunchKernelGGL((k_pn_ls_begin<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+      else if (phase == 5)
+        hipLaunchKernelGGL((k_pn_ls_proj<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+      else
+        hipLaunchKernelGGL((k_pn_ls_end<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+    }
   }
   static void pn(const DevProblem* P, const DevBuffers& Bf, const PNBuffers& W, long long B, int integ, int phase,
                  hipStream_t st) {

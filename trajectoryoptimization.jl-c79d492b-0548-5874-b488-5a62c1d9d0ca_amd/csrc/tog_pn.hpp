@@ -27,6 +27,11 @@ struct PNState {
   int error;     // TOG_TRAJ_PN_ERROR path
   int steps, projections, linesearches, refinements;
   int active0;   // the solver's own active flag, restored by k_pn_finish (k_jacobian gates on it)
+  // solve_type :optimal
+  int has_S;     // a _projection_solve! has set solver.stats[:S] (its factor in Ld, Lo, block sizes in szS)
+  int ls;        // line search stage: 0 none, 1 begin pending, 2 projecting the trial, 3 trial projected
+  int ls_count, pcount;  // line search trials, projection! iterations of the current trial
+  double alpha, res0;
 };
 
 struct PNBuffers {
@@ -37,6 +42,15 @@ struct PNBuffers {
   int *act, *na, *sz;               // (B, N, pmax) active rows, (B, N) counts, (B, nb) block sizes
   PNState* st;                      // (B)
   double* wt;                       // (B, N n + (N-1) m) H⁻¹ diagonal of a minimum-time problem, per newton step
+  // solve_type :optimal (allocated by the first such call)
+  double *Ld2, *Lo2;                // (B, nb, SM, SM) factor of Y Yᵀ / of S without regularization
+  double *lb, *tb;                  // (B, nb, SM) active duals in block order, scratch
+  double *g, *rz, *dz;              // (B, N (n+m)) cost gradient, g + Yᵀλ, δz (knot j at j (n+m))
+  double *nu, *dnu, *nut;           // (B, N, n) dynamics-row duals of solver.V, of δV, of the trial V_
+  double *lc, *dlc, *lct;           // (B, N, pmax) constraint-row duals (every row, active or not)
+  double *Xv, *Uv;                  // solver.V's primals while the line search moves X, U
+  int* szS;                         // (B, nb) block sizes of the factor in Ld, Lo
+  int optimal;                      // this call's solve_type is :optimal
   int SM, nb;
   double atol, eps;                 // active_set_tolerance, feasibility_tolerance
 };
@@ -44,7 +58,8 @@ struct PNBuffers {
 // per-trajectory views of the workspace
 struct PNView {
   double *Sd, *So, *Ld, *Lo, *yv, *xv, *rv, *wv, *dv, *yd, *Xs, *wt;
-  int *act, *na, *sz;
+  double *Ld2, *Lo2, *lb, *tb, *g, *rz, *dz, *nu, *dnu, *nut, *lc, *dlc, *lct, *Xv, *Uv;
+  int *act, *na, *sz, *szS;
   int SM;
   __device__ double* M(double* A, int b) const { return A + (size_t)b * SM * SM; }
   __device__ double* V(double* v, int b) const { return v + (size_t)b * SM; }
@@ -69,6 +84,25 @@ __device__ __forceinline__ PNView pn_view(const PNBuffers& W, const DevProblem* 
   v.na = W.na + (size_t)b * P->N;
   v.sz = W.sz + (size_t)b * W.nb;
   v.SM = W.SM;
+  if (W.optimal) {
+    const size_t nz = (size_t)P->N * (P->n + P->m), nx = (size_t)P->N * P->n, nc = (size_t)P->N * (P->pmax > 0 ? P->pmax : 1);
+    v.Ld2 = W.Ld2 + b * blk;
+    v.Lo2 = W.Lo2 + b * blk;
+    v.lb = W.lb + b * vec;
+    v.tb = W.tb + b * vec;
+    v.g = W.g + b * nz;
+    v.rz = W.rz + b * nz;
+    v.dz = W.dz + b * nz;
+    v.nu = W.nu + b * nx;
+    v.dnu = W.dnu + b * nx;
+    v.nut = W.nut + b * nx;
+    v.lc = W.lc + b * nc;
+    v.dlc = W.dlc + b * nc;
+    v.lct = W.lct + b * nc;
+    v.Xv = W.Xv + b * nx;
+    v.Uv = W.Uv + b * (size_t)(P->N - 1) * P->m;
+    v.szS = W.szS + (size_t)b * W.nb;
+  }
   return v;
 }
 
@@ -213,15 +247,17 @@ __device__ void pn_block_rows(const DevProblem* P, const DevBuffers& Bf, long lo
   pn_sync();
 }
 
-// S = Y H⁻¹ Yᵀ by blocks (projected_newton.jl:233-234; structure of _buildShurCompliment!, :728-757)
-template <class M>
+// S = Y H⁻¹ Yᵀ by blocks (projected_newton.jl:233-234; structure of _buildShurCompliment!, :728-757);
+// UNIT: Y Yᵀ (multiplier_projection!)
+template <class M, bool UNIT = false>
 __device__ void pn_build_S(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
                            double* Yz, int nb, int lane) {
   constexpr int n = M::n, m = M::m;
   const int N = P->N, SM = w.SM;
   {
     double* S0 = w.M(w.Sd, 0);
-    for (int e = lane; e < SM * SM; e += WAVE) S0[e] = ((e % SM) == (e / SM) && (e % SM) < n) ? pn_wx<M>(P, w, 0, e % SM) : 0.0;
+    for (int e = lane; e < SM * SM; e += WAVE)
+      S0[e] = ((e % SM) == (e / SM) && (e % SM) < n) ? (UNIT ? 1.0 : pn_wx<M>(P, w, 0, e % SM)) : 0.0;
   }
   for (int bb = 1; bb < nb; bb++) {
     const int j = bb - 1, sb = w.sz[bb], sp = w.sz[bb - 1], nv = (bb < N) ? n + m : n;
@@ -231,17 +267,17 @@ __device__ void pn_build_S(const DevProblem* P, const DevBuffers& Bf, long long 
       const int i = e % sb, l = e / sb;
       double acc = 0.0;
       for (int v = 0; v < nv; v++) {
-        const double wv = v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
+        const double wv = UNIT ? 1.0 : v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
         acc = fma(Yz[i + SM * v], wv * Yz[l + SM * v], acc);
       }
-      if (bb < N && i < n && i == l) acc = acc + pn_wx<M>(P, w, j + 1, i);
+      if (bb < N && i < n && i == l) acc = acc + (UNIT ? 1.0 : pn_wx<M>(P, w, j + 1, i));
       Sd[i + SM * l] = acc;
     }
     const double sg = (bb - 1 == 0) ? 1.0 : -1.0;
     double* So = w.M(w.So, bb);
     for (int e = lane; e < sb * sp; e += WAVE) {
       const int i = e % sb, c = e / sb;
-      So[i + SM * c] = (c < n) ? Yz[i + SM * c] * (sg * pn_wx<M>(P, w, j, c)) : 0.0;
+      So[i + SM * c] = (c < n) ? Yz[i + SM * c] * (sg * (UNIT ? 1.0 : pn_wx<M>(P, w, j, c))) : 0.0;
     }
     pn_sync();
   }
@@ -449,17 +485,26 @@ __global__ void __launch_bounds__(64) k_pn_begin(const DevProblem* __restrict__ 
   if (s.finished) return;
   const PNView w = pn_view(W, P, b);
   const int N = P->N;
+  if (W.optimal && s.steps > 0) {  // :optimal: every newton step starts from solver.V, not from the returned V_
+    for (int e = lane; e < N * M::n; e += WAVE) Bf.X[(size_t)b * N * M::n + e] = w.Xv[e];
+    for (int e = lane; e < (N - 1) * M::m; e += WAVE) Bf.U[(size_t)b * (N - 1) * M::m + e] = w.Uv[e];
+    pn_sync();
+  }
   if constexpr (ModelTraits<M>::min_time)
     pn_weights_min_time<M>(P, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
   pn_eval<M, INTEG>(P, Bf, b, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
   pn_active_set(P, Bf, b, w, W.atol, W.nb, lane);
   const double viol = pn_gather_y(P, Bf, b, w, W.nb, lane);
+  if (W.optimal) {  // update!'s Jacobians at V: the first k_jacobian of the projection loop, for every trajectory
+    for (int e = lane; e < N * M::n; e += WAVE) w.Xs[e] = Bf.X[(size_t)b * N * M::n + e];
+    pn_sync();
+  }
   if (lane == 0) {
     s.viol = viol;
     s.count = 0;
     // k_jacobian runs only for active trajectories: a converged AL solve left them inactive
     s.active0 = Bf.st[b].active;
-    Bf.st[b].active = (viol > W.eps) ? 1 : 0;
+    Bf.st[b].active = (W.optimal || viol > W.eps) ? 1 : 0;
   }
 }
 
@@ -470,7 +515,10 @@ __global__ void __launch_bounds__(64) k_pn_project(const DevProblem* __restrict_
   const int lane = threadIdx.x;
   __shared__ PNLds sh;
   PNState s = W.st[b];
-  if (s.finished || s.error || s.count >= 10 || !(s.viol > W.eps)) return;  // while count < 10 && viol > eps
+  if (s.finished || s.error || s.count >= 10 || !(s.viol > W.eps)) {  // while count < 10 && viol > eps
+    if (W.optimal && lane == 0 && !s.finished) Bf.st[b].active = 0;     // (:optimal: Jacobians at V are kept)
+    return;
+  }
   constexpr int n = M::n, m = M::m;
   const int N = P->N, nb = W.nb;
   const PNView w = pn_view(W, P, b);
@@ -487,6 +535,10 @@ __global__ void __launch_bounds__(64) k_pn_project(const DevProblem* __restrict_
   if (pn_factor(w, nb, 1e-2, sh.A, sh.Bm, sh.Cm, lane)) {
     s.error = 1;  // PosDefException in cholesky
   } else {
+    s.has_S = 1;  // solver.stats[:S] = Sreg
+    if (W.optimal && lane < nb) {
+      for (int bb = lane; bb < nb; bb += WAVE) w.szS[bb] = w.sz[bb];
+    }
     double viol_prev = viol0;
     for (int count = 0; count < 10; count++) {
       // _projection_linesearch!: y at the current point (last evaluation), δλ, trial, y at the trial
@@ -545,6 +597,385 @@ __global__ void __launch_bounds__(64) k_pn_finish(const DevProblem* __restrict__
   if (s.error || s.c_max <= W.eps) s.finished = 1;
   if (s.error) Bf.st[b].flags |= TOG_TRAJ_PN_ERROR;
   W.st[b] = s;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// solve_type :optimal: newton_step! after the projection (projected_newton.jl:522-546). The oracle's
+// pn_grad / pn_form_r / pn_multiplier_projection / pn_kkt / pn_line_search (oracle/tog_oracle_pn.c) with the
+// same operations in the same order. Kernels: k_pn_kkt (cost_expansion!, multiplier_projection!,
+// solveKKT_Shur at solver.V), k_pn_ls_begin (line_search's update! and res0, first trial),
+// k_pn_ls_proj (one projection! iteration at the trial, after k_jacobian there), k_pn_ls_end
+// (multiplier_projection! at the projected trial, the acceptance test, the next trial).
+// ---------------------------------------------------------------------------------------------------------
+
+// the plain objective's gradient (cost_expansion!'s gradient!, :139-148) at X, U into w.g; a lane per knot
+template <class M>
+__device__ void pn_grad(const DevProblem* P, const PNView& w, const double* X, const double* U, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  for (int k = lane; k < N; k += WAVE) {
+    const double* x = X + (size_t)k * n;
+    double* q = w.g + (size_t)k * (n + m);
+    if (k < N - 1) {
+      const double* u = U + (size_t)k * m;
+      const CostView C_ = cost_at<n, m>(P, k);
+      const double dt = P->dt;
+      for (int i = 0; i < n; i++) {
+        double a = 0.0, c = 0.0;
+        for (int j = 0; j < n; j++) a = fma(C_.Q[i + n * j], x[j], a);
+        for (int j = 0; j < m; j++) c = fma(C_.H[j + m * i], u[j], c);
+        q[i] = ((a + C_.q[i]) + c) * dt;
+      }
+      for (int i = 0; i < m; i++) {
+        double a = 0.0, c = 0.0;
+        for (int j = 0; j < m; j++) a = fma(C_.R[i + m * j], u[j], a);
+        for (int j = 0; j < n; j++) c = fma(C_.H[i + m * j], x[j], c);
+        q[n + i] = ((a + C_.r[i]) + c) * dt;
+      }
+    } else {
+      for (int i = 0; i < n; i++) {
+        double a = 0.0;
+        for (int j = 0; j < n; j++) a = fma(P->Qf[i + n * j], x[j], a);
+        q[i] = a + P->qf[i];
+      }
+    }
+  }
+  pn_sync();
+}
+
+// duals (full layout) <-> the active duals in block order; a lane per block
+__device__ void pn_gather_duals(const DevProblem* P, const PNView& w, const double* nu, const double* lc, double* lb,
+                                int nb, int lane) {
+  const int N = P->N, pmax = P->pmax, n = P->n;
+  for (int bb = lane; bb < nb; bb += WAVE) {
+    double* l = lb + (size_t)bb * w.SM;
+    int r = 0;
+    if (bb < N)
+      for (int i = 0; i < n; i++) l[r++] = nu[(size_t)bb * n + i];
+    if (bb >= 1)
+      for (int q = 0; q < w.na[bb - 1]; q++) l[r++] = lc[(size_t)(bb - 1) * pmax + w.act[(bb - 1) * pmax + q]];
+  }
+  pn_sync();
+}
+__device__ void pn_scatter_duals(const DevProblem* P, const PNView& w, const double* lb, double* nu, double* lc,
+                                 int nb, int lane) {
+  const int N = P->N, pmax = P->pmax, n = P->n;
+  for (int bb = lane; bb < nb; bb += WAVE) {
+    const double* l = lb + (size_t)bb * w.SM;
+    int r = 0;
+    if (bb < N)
+      for (int i = 0; i < n; i++) nu[(size_t)bb * n + i] = l[r++];
+    if (bb >= 1)
+      for (int q = 0; q < w.na[bb - 1]; q++) lc[(size_t)(bb - 1) * pmax + w.act[(bb - 1) * pmax + q]] = l[r++];
+  }
+  pn_sync();
+}
+
+// out = Yᵀ l: column z_j gets ±l_j (+I initial condition, -I dynamics of block j), then block j+1's rows
+template <class M>
+__device__ void pn_yt(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
+                      const double* l, double* out, double* Yz, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, SM = w.SM;
+  for (int j = 0; j < N; j++) {
+    const int bb = j + 1, nv = (j < N - 1) ? n + m : n;
+    pn_block_rows<M>(P, Bf, b, w, bb, X, Yz, lane);
+    if (lane < nv) {
+      const int v = lane;
+      double t = (v < n) ? ((j == 0) ? l[v] : -l[(size_t)j * SM + v]) : 0.0;
+      const double* lbb = l + (size_t)bb * SM;
+      for (int i = 0; i < w.sz[bb]; i++) t = fma(Yz[i + SM * v], lbb[i], t);
+      out[(size_t)j * (n + m) + v] = t;
+    }
+    pn_sync();
+  }
+}
+
+// out = Y z (block order): row i of block bb from its ±I term, then block bb's own variables z_{bb-1}
+template <class M>
+__device__ void pn_ymul(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
+                        const double* z, double* out, double* Yz, int nb, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, SM = w.SM;
+  for (int bb = 0; bb < nb; bb++) {
+    const int j = bb - 1, nv = (j < N - 1) ? n + m : n;
+    if (bb >= 1) pn_block_rows<M>(P, Bf, b, w, bb, X, Yz, lane);
+    if (lane < w.sz[bb]) {
+      const int i = lane;
+      double t = (bb < N && i < n) ? ((bb == 0) ? z[i] : -z[(size_t)bb * (n + m) + i]) : 0.0;
+      if (bb >= 1)
+        for (int v = 0; v < nv; v++) t = fma(Yz[i + SM * v], z[(size_t)j * (n + m) + v], t);
+      out[(size_t)bb * SM + i] = t;
+    }
+    pn_sync();
+  }
+}
+
+// |[g + Yᵀλ; y]|₂ with rz = g + Yᵀλ formed: the oracle's sequential sum of squares (lane 0)
+__device__ double pn_res_norm(const DevProblem* P, const PNView& w, int nb, int lane) {
+  double ss = 0.0;
+  if (lane == 0) {
+    const int n = P->n, m = P->m, N = P->N;
+    for (int j = 0; j < N; j++)
+      for (int v = 0; v < ((j < N - 1) ? n + m : n); v++) {
+        const double r = w.rz[(size_t)j * (n + m) + v];
+        ss = fma(r, r, ss);
+      }
+    for (int bb = 0; bb < nb; bb++)
+      for (int i = 0; i < w.sz[bb]; i++) {
+        const double y = w.yv[(size_t)bb * w.SM + i];
+        ss = fma(y, y, ss);
+      }
+  }
+  return sqrt(__shfl(ss, 0, WAVE));
+}
+
+// rz = g + Yᵀλ, λ the active rows of (nu, lc)
+template <class M>
+__device__ void pn_form_r(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
+                          const double* nu, const double* lc, double* Yz, int nb, int lane) {
+  constexpr int n = M::n, m = M::m;
+  pn_gather_duals(P, w, nu, lc, w.lb, nb, lane);
+  pn_yt<M>(P, Bf, b, w, X, w.lb, w.rz, Yz, lane);
+  for (int e = lane; e < P->N * (n + m); e += WAVE) w.rz[e] = w.g[e] + w.rz[e];
+  pn_sync();
+}
+
+// multiplier_projection! (:407-420): λ += -(Y Yᵀ) \ (Y (g + Yᵀλ)); returns the residual norm after it
+template <class M>
+__device__ double pn_multiplier_projection(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w,
+                                           const double* X, double* nu, double* lc, PNLds& sh, int nb, int lane,
+                                           int& err) {
+  pn_form_r<M>(P, Bf, b, w, X, nu, lc, sh.Yz, nb, lane);
+  pn_ymul<M>(P, Bf, b, w, X, w.rz, w.tb, sh.Yz, nb, lane);
+  pn_build_S<M, true>(P, Bf, b, w, X, sh.Yz, nb, lane);
+  PNView w2 = w;
+  w2.Ld = w.Ld2;
+  w2.Lo = w.Lo2;
+  if (pn_factor(w2, nb, 0.0, sh.A, sh.Bm, sh.Cm, lane)) {
+    err = 1;  // Y Yᵀ not positive definite
+    return NAN;
+  }
+  pn_fsolve(w2, nb, w.tb, w.xv, sh.A, sh.Bm, sh.vec, lane);
+  for (int bb = 0; bb < nb; bb++)
+    if (lane < w.sz[bb]) w.lb[(size_t)bb * w.SM + lane] = w.lb[(size_t)bb * w.SM + lane] + -w.xv[(size_t)bb * w.SM + lane];
+  pn_sync();
+  pn_scatter_duals(P, w, w.lb, nu, lc, nb, lane);
+  pn_form_r<M>(P, Bf, b, w, X, nu, lc, sh.Yz, nb, lane);
+  return pn_res_norm(P, w, nb, lane);
+}
+
+// solveKKT_Shur (:436-452): δλ = L \ (y - Y H⁻¹ r) with stats[:S]'s factor, δz = -H⁻¹ (r + Yᵀδλ)
+template <class M>
+__device__ void pn_kkt(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, const double* X,
+                       PNLds& sh, int nb, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N;
+  for (int e = lane; e < N * (n + m); e += WAVE) {
+    const int j = e / (n + m), v = e % (n + m);
+    if (j == N - 1 && v >= n) continue;
+    const double wv = v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
+    w.dz[e] = wv * w.rz[e];
+  }
+  pn_sync();
+  pn_ymul<M>(P, Bf, b, w, X, w.dz, w.tb, sh.Yz, nb, lane);
+  for (int bb = 0; bb < nb; bb++)
+    if (lane < w.sz[bb]) w.tb[(size_t)bb * w.SM + lane] = w.yv[(size_t)bb * w.SM + lane] - w.tb[(size_t)bb * w.SM + lane];
+  pn_sync();
+  pn_fsolve(w, nb, w.tb, w.xv, sh.A, sh.Bm, sh.vec, lane);
+  pn_yt<M>(P, Bf, b, w, X, w.xv, w.dz, sh.Yz, lane);
+  for (int e = lane; e < N * (n + m); e += WAVE) {
+    const int j = e / (n + m), v = e % (n + m);
+    if (j == N - 1 && v >= n) continue;
+    const double wv = v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
+    w.dz[e] = -(wv * (w.rz[e] + w.dz[e]));
+  }
+  for (int e = lane; e < N * n; e += WAVE) w.dnu[e] = 0.0;
+  for (int e = lane; e < N * P->pmax; e += WAVE) w.dlc[e] = 0.0;
+  pn_sync();
+  pn_scatter_duals(P, w, w.xv, w.dnu, w.dlc, nb, lane);
+}
+
+// V_ = solver.V + α δV into X, U and the trial duals
+template <class M>
+__device__ void pn_ls_trial(const DevProblem* P, const PNView& w, double* X, double* U, double alpha, int lane) {
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, pm = P->pmax;
+  for (int e = lane; e < N * n; e += WAVE) X[e] = w.Xv[e] + alpha * w.dz[(size_t)(e / n) * (n + m) + e % n];
+  for (int e = lane; e < (N - 1) * m; e += WAVE) U[e] = w.Uv[e] + alpha * w.dz[(size_t)(e / m) * (n + m) + n + e % m];
+  for (int e = lane; e < N * n; e += WAVE) w.nut[e] = w.nu[e] + alpha * w.dnu[e];
+  for (int e = lane; e < N * pm; e += WAVE) w.lct[e] = w.lc[e] + alpha * w.dlc[e];
+  pn_sync();
+}
+
+// line_search's failure: return solver.V
+template <class M>
+__device__ void pn_ls_restore(const DevProblem* P, const PNView& w, double* X, double* U, int lane) {
+  const int N = P->N;
+  for (int e = lane; e < N * M::n; e += WAVE) X[e] = w.Xv[e];
+  for (int e = lane; e < (N - 1) * M::m; e += WAVE) U[e] = w.Uv[e];
+  pn_sync();
+}
+
+// after projection_solve! (k_jacobian left Jacobians at w.Xs in AB): cost_expansion!, multiplier_projection!,
+// solveKKT_Shur at solver.V
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_kkt(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ PNLds sh;
+  PNState s = W.st[b];
+  if (!W.optimal || s.finished || s.error) return;
+  const int N = P->N, nb = W.nb;
+  const PNView w = pn_view(W, P, b);
+  // stats[:S] must exist (KeyError) and, when this step did not project, match the active set's blocks
+  int mismatch = 0;
+  if (s.has_S && s.count == 0)
+    for (int bb = lane; bb < nb; bb += WAVE) mismatch |= (w.szS[bb] != w.sz[bb]);
+  mismatch = __syncthreads_or(mismatch);
+  int err = (!s.has_S || mismatch) ? 1 : 0;
+  if (!err) {
+    pn_grad<M>(P, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
+    pn_multiplier_projection<M>(P, Bf, b, w, w.Xs, w.nu, w.lc, sh, nb, lane, err);
+  }
+  if (!err) pn_kkt<M>(P, Bf, b, w, w.Xs, sh, nb, lane);
+  if (lane == 0) {
+    if (err) {
+      s.error = 1;
+    } else {
+      s.ls = 1;
+      Bf.st[b].active = 1;  // line_search's update!: Jacobians at solver.V
+    }
+    W.st[b] = s;
+  }
+}
+
+// line_search (:463-472): update! at solver.V, res0, the first trial V_ = V + δV
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_ls_begin(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ PNLds sh;
+  PNState s = W.st[b];
+  if (!W.optimal || s.finished || s.error || s.ls != 1) return;
+  const int N = P->N, nb = W.nb;
+  const PNView w = pn_view(W, P, b);
+  double* X = Bf.X + (size_t)b * N * M::n;
+  double* U = Bf.U + (size_t)b * (N - 1) * M::m;
+  for (int e = lane; e < N * M::n; e += WAVE) w.Xv[e] = X[e];
+  for (int e = lane; e < (N - 1) * M::m; e += WAVE) w.Uv[e] = U[e];
+  pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
+  pn_active_set(P, Bf, b, w, W.atol, nb, lane);
+  pn_gather_y(P, Bf, b, w, nb, lane);
+  pn_grad<M>(P, w, X, U, lane);
+  pn_form_r<M>(P, Bf, b, w, X, w.nu, w.lc, sh.Yz, nb, lane);
+  const double res0 = pn_res_norm(P, w, nb, lane);
+  pn_ls_trial<M>(P, w, X, U, 1.0, lane);
+  if (lane == 0) {
+    s.res0 = res0;
+    s.alpha = 1.0;
+    s.ls_count = 0;
+    s.pcount = 0;
+    s.ls = 2;
+    W.st[b] = s;  // k_jacobian stays on: the trial's Jacobians
+  }
+}
+
+// one pass of projection! (:328-357) at the trial (Jacobians from k_jacobian there): stop on viol < eps or
+// after 11 Newton steps, else δZ = -H⁻¹Yᵀ (Y H⁻¹ Yᵀ) \ y
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_ls_proj(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ PNLds sh;
+  PNState s = W.st[b];
+  if (!W.optimal || s.finished || s.error || s.ls != 2) return;
+  constexpr int n = M::n, m = M::m;
+  const int N = P->N, nb = W.nb;
+  const PNView w = pn_view(W, P, b);
+  double* X = Bf.X + (size_t)b * N * n;
+  double* U = Bf.U + (size_t)b * (N - 1) * m;
+  pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
+  pn_active_set(P, Bf, b, w, W.atol, nb, lane);
+  const double viol = pn_gather_y(P, Bf, b, w, nb, lane);
+  if (viol < W.eps || s.pcount > 10) {
+    if (lane == 0) {
+      s.ls = 3;
+      Bf.st[b].active = 0;  // AB keeps the Jacobians at the projected trial
+      W.st[b] = s;
+    }
+    return;
+  }
+  pn_build_S<M>(P, Bf, b, w, X, sh.Yz, nb, lane);
+  PNView w2 = w;
+  w2.Ld = w.Ld2;
+  w2.Lo = w.Lo2;
+  if (pn_factor(w2, nb, 0.0, sh.A, sh.Bm, sh.Cm, lane)) {
+    if (lane == 0) {  // the trial is rejected (oracle pn_line_search: more active rows than free variables)
+      s.ls = 4;
+      Bf.st[b].active = 0;
+      W.st[b] = s;
+    }
+    return;
+  }
+  pn_fsolve(w2, nb, w.yv, w.xv, sh.A, sh.Bm, sh.vec, lane);
+  pn_yt<M>(P, Bf, b, w, X, w.xv, w.rz, sh.Yz, lane);
+  for (int e = lane; e < N * (n + m); e += WAVE) {
+    const int j = e / (n + m), v = e % (n + m);
+    if (j == N - 1 && v >= n) continue;
+    const double wv = v < n ? pn_wx<M>(P, w, j, v) : pn_wu<M>(P, w, j, v - n);
+    const double dz = -(wv * w.rz[e]);
+    if (v < n)
+      X[(size_t)j * n + v] = X[(size_t)j * n + v] + dz;
+    else
+      U[(size_t)j * m + (v - n)] = U[(size_t)j * m + (v - n)] + dz;
+  }
+  if (lane == 0) {
+    s.pcount++;
+    W.st[b] = s;
+  }
+}
+
+// line_search (:478-494) after projection!: cost_expansion! and multiplier_projection! at V_, the test
+// res < (1 - 0.01 α) res0, else α /= 2 and the next trial; after 10 trials solver.V. A trial whose
+// Y H⁻¹ Yᵀ or Y Yᵀ does not factor is rejected (the oracle's pn_line_search).
+template <class M, int INTEG>
+__global__ void __launch_bounds__(64) k_pn_ls_end(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
+  const long long b = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ PNLds sh;
+  PNState s = W.st[b];
+  if (!W.optimal || s.finished || s.error || (s.ls != 3 && s.ls != 4)) return;
+  const int N = P->N, nb = W.nb;
+  const PNView w = pn_view(W, P, b);
+  double* X = Bf.X + (size_t)b * N * M::n;
+  double* U = Bf.U + (size_t)b * (N - 1) * M::m;
+  int rejected = s.ls == 4;  // projection!'s Y H⁻¹ Yᵀ did not factor
+  double res = NAN;
+  if (!rejected) {
+    pn_grad<M>(P, w, X, U, lane);
+    res = pn_multiplier_projection<M>(P, Bf, b, w, X, w.nut, w.lct, sh, nb, lane, rejected);
+  }
+  int next = 0;
+  if (!rejected && res < (1.0 - s.alpha * 0.01) * s.res0) {
+    s.ls = 0;  // V_ accepted: prob = V_
+  } else {
+    s.alpha /= 2.0;
+    s.ls_count++;
+    if (s.ls_count >= 10) {
+      pn_ls_restore<M>(P, w, X, U, lane);
+      s.ls = 0;
+    } else {
+      pn_ls_trial<M>(P, w, X, U, s.alpha, lane);
+      s.pcount = 0;
+      s.ls = 2;
+      next = 1;
+    }
+  }
+  if (lane == 0) {
+    if (next) Bf.st[b].active = 1;
+    W.st[b] = s;
+  }
 }
 
 }  // namespace tog

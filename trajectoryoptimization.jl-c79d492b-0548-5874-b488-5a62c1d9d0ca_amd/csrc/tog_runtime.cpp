@@ -125,7 +125,7 @@ struct tog_handle {
   StreamPair sp = {nullptr, nullptr, nullptr};
   // projected Newton workspace, allocated by the first tog_solve_pn (tog_pn.hpp)
   PNBuffers pn = {};
-  bool pn_alloc = false;
+  bool pn_alloc = false, pn_opt_alloc = false;
   // solver_pn.stats histories of the last tog_solve_pn: (2, n_steps, B) [cost, c_max], records per trajectory
   std::vector<double> pn_hist;
   std::vector<int32_t> pn_hist_rec;
@@ -1636,7 +1636,10 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     return each_part(h, [&](tog_handle* p, size_t o) {
       return tog_solve_pn(p, opts, out ? out + o * TOG_PN_NSTATS : nullptr);
     });
-  if (opts->solve_type != 0) return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal is not built");
+  if (opts->solve_type != 0 && opts->solve_type != 1) return fail(TOG_ERR_ARG, "solve_type must be 0 (:feasible) or 1 (:optimal)");
+  const bool optimal = opts->solve_type == 1;
+  if (optimal && h->ops->min_time)
+    return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal on a minimum-time problem is not built");
   if (opts->n_steps < 0) return fail(TOG_ERR_ARG, "n_steps must be >= 0");
   if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than n + m = 24 are not built");
   const int SM = h->n + h->pmax;
@@ -1678,6 +1681,36 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     }
     h->pn_alloc = true;
   }
+  if (optimal && !h->pn_opt_alloc) {  // :optimal's workspace: two more block factors, the duals and the KKT vectors
+    const size_t blk = (size_t)B * W.nb * SM * SM, vec = (size_t)B * W.nb * SM;
+    const size_t nz = (size_t)B * h->N * (h->n + h->m), nx = (size_t)B * h->N * h->n;
+    const size_t nc = (size_t)B * h->N * (h->pmax > 0 ? h->pmax : 1), nu = (size_t)B * (h->N - 1) * h->m;
+    const size_t need = sizeof(double) * (2 * blk + 2 * vec + 3 * nz + 4 * nx + 3 * nc + nu) + sizeof(int) * (size_t)B * W.nb;
+    size_t fr = 0, tot = 0;
+    HIPCHECK(hipMemGetInfo(&fr, &tot));
+    if (need > fr)
+      return fail(TOG_ERR_NOMEM, "projected Newton :optimal workspace (" + std::to_string(need >> 20) +
+                                     " MiB) exceeds free device memory (" + std::to_string(fr >> 20) + " MiB)");
+    const size_t mark = h->allocs.size();
+    int rc;
+    if ((rc = dalloc(h, &W.Ld2, blk)) || (rc = dalloc(h, &W.Lo2, blk)) || (rc = dalloc(h, &W.lb, vec)) ||
+        (rc = dalloc(h, &W.tb, vec)) || (rc = dalloc(h, &W.g, nz)) || (rc = dalloc(h, &W.rz, nz)) ||
+        (rc = dalloc(h, &W.dz, nz)) || (rc = dalloc(h, &W.nu, nx)) || (rc = dalloc(h, &W.dnu, nx)) ||
+        (rc = dalloc(h, &W.nut, nx)) || (rc = dalloc(h, &W.Xv, nx)) || (rc = dalloc(h, &W.lc, nc)) ||
+        (rc = dalloc(h, &W.dlc, nc)) || (rc = dalloc(h, &W.lct, nc)) || (rc = dalloc(h, &W.Uv, nu)) ||
+        (rc = dalloc(h, &W.szS, (size_t)B * W.nb))) {
+      for (size_t i = mark; i < h->allocs.size(); i++) (void)hipFree(h->allocs[i]);
+      h->allocs.resize(mark);
+      (void)hipGetLastError();
+      return rc;
+    }
+    h->pn_opt_alloc = true;
+  }
+  W.optimal = optimal ? 1 : 0;
+  if (optimal) {  // PrimalDual(prob): zero duals
+    HIPCHECK(hipMemsetAsync(W.nu, 0, sizeof(double) * (size_t)B * h->N * h->n, h->stream));
+    HIPCHECK(hipMemsetAsync(W.lc, 0, sizeof(double) * (size_t)B * h->N * (h->pmax > 0 ? h->pmax : 1), h->stream));
+  }
   W.atol = opts->active_set_tolerance;
   W.eps = opts->feasibility_tolerance;
   HIPCHECK(hipMemsetAsync(W.st, 0, sizeof(PNState) * B, h->stream));
@@ -1691,6 +1724,18 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     for (int it = 0; it < 10; it++) {
       h->ops->jacobian(h->dP, h->buf, B, h->N, h->integ, h->stream);
       h->ops->pn(h->dP, h->buf, W, B, h->integ, 1, h->stream);
+    }
+    if (optimal) {  // the KKT step and its line search: 10 trials of at most 12 projection! passes
+      h->ops->pn(h->dP, h->buf, W, B, h->integ, 3, h->stream);
+      h->ops->jacobian(h->dP, h->buf, B, h->N, h->integ, h->stream);
+      h->ops->pn(h->dP, h->buf, W, B, h->integ, 4, h->stream);
+      for (int ls = 0; ls < 10; ls++) {
+        for (int it = 0; it < 12; it++) {
+          h->ops->jacobian(h->dP, h->buf, B, h->N, h->integ, h->stream);
+          h->ops->pn(h->dP, h->buf, W, B, h->integ, 5, h->stream);
+        }
+        h->ops->pn(h->dP, h->buf, W, B, h->integ, 6, h->stream);
+      }
     }
     h->ops->pn(h->dP, h->buf, W, B, h->integ, 2, h->stream);
     HIPCHECK(hipGetLastError());

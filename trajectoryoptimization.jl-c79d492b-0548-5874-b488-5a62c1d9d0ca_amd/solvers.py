@@ -130,11 +130,9 @@ class ProjectedNewtonSolverOptions:
 def to_tog_pn_options(opts: ProjectedNewtonSolverOptions) -> abi.tog_pn_options:
     if opts.solve_type not in ("feasible", "optimal"):
         raise ValueError("solve_type must be :feasible or :optimal")
-    if opts.solve_type == "optimal":
-        raise NotImplementedError("projected Newton solve_type :optimal is not built")
     o = abi.tog_pn_options()
     o.n_steps = int(opts.n_steps)
-    o.solve_type = 0
+    o.solve_type = 1 if opts.solve_type == "optimal" else 0
     o.active_set_tolerance = float(opts.active_set_tolerance)
     o.feasibility_tolerance = float(opts.feasibility_tolerance)
     return o
