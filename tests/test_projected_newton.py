@@ -257,13 +257,15 @@ def test_gpu_pn_quad_maze(tog, oracle, gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ft,n_steps", [(1e-10, 1), (1e-6, 1), (0.0, 3)])
-def test_gpu_pn_optimal_parity(tog, oracle, gpu, ft, n_steps):
+@pytest.mark.parametrize("ft,at,n_steps", [(1e-10, 1e-3, 1), (1e-6, 1e-3, 1), (1e-8, 1e-5, 3), (1e-8, 0.0, 1)])
+def test_gpu_pn_optimal_parity(tog, oracle, gpu, ft, at, n_steps):
     """solve_type :optimal on the device (k_pn_kkt, k_pn_ls_begin / k_pn_ls_proj / k_pn_ls_end, tog_pn.hpp)
-    against the oracle from the same AL iterates, 4 perturbed car starts: X, U and every statistic to 1e-13
-    (one newton step; three steps that restart from solver.V)."""
+    against the oracle from the same AL iterates, 4 perturbed car starts: X, U and every statistic to 1e-13.
+    The small active-set tolerances make the full KKT step violate rows outside the active set, so the line
+    search's projection! grows the active set past the free variables and rejects trials (the reject path)."""
     prob = car_batch(tog, 4)
-    pn = tog.ProjectedNewtonSolverOptions(feasibility_tolerance=ft, n_steps=n_steps, solve_type="optimal")
+    pn = tog.ProjectedNewtonSolverOptions(feasibility_tolerance=ft, active_set_tolerance=at, n_steps=n_steps,
+                                          solve_type="optimal")
     gp, st = _pn_compare(tog, oracle, prob, car_al_opts(tog), pn)
     assert np.all(np.isfinite(gp._X)) and np.all(np.isfinite(gp._U))
 
