@@ -1252,42 +1252,79 @@ attempt:
     }
     // ---- regularisation (backward_pass.jl:38-48 / :120-126) and the restart test
     if (!SQRT) {
-      if (lane == 0) {
-        double* G = sh.G;
-        for (int e = 0; e < m * m; e++) G[e] = sh.Quu[e];
+      // Quu_reg = Q.uu + ρI (or + ρB'B), isposdef(Hermitian(Quu_reg)) and its LU factor, wave-parallel (round
+      // 5; these ran on lane 0 and were most of a knot for m = 17, the infeasible quadrotor): every entry
+      // gets the serial restatement's operations in its order -- the Cholesky test's row j entries are
+      // independent given rows < j, the LU's right-looking update is one fma per entry and step, and the
+      // pivot search and the diagonal recurrence run redundantly (uniformly) in every lane
+      double* G = sh.G;
+      for (int e = lane; e < m * m; e += WAVE) {
+        double g = sh.Quu[e];
         if (!state_reg) {
-          for (int i = 0; i < m; i++) G[i + m * i] += s.rho;
+          if (e % m == e / m) g += s.rho;
         } else {
-          for (int j = 0; j < m; j++)
-            for (int i = 0; i < m; i++) {
-              double t = 0.0;
-              for (int l = 0; l < n; l++) t = fma(Bm[l + n * i], Bm[l + n * j], t);
-              G[i + m * j] += s.rho * t;
+          const int i = e % m, j = e / m;
+          double t = 0.0;
+          for (int l = 0; l < n; l++) t = fma(Bm[l + n * i], Bm[l + n * j], t);
+          g += s.rho * t;
+        }
+        G[e] = g;
+      }
+      wsync();
+      // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle, row j of U by lanes c > j
+      double* U = sh.Uc;
+      bool pd = true;
+      for (int j = 0; j < m; j++) {
+        double d0 = G[j + m * j];
+        for (int l = 0; l < j; l++) d0 -= U[l + m * j] * U[l + m * j];
+        if (!(d0 > 0.0)) {
+          pd = false;
+          break;
+        }
+        const double ujj = sqrt(d0);
+        if (lane == j) U[j + m * j] = ujj;
+        if (lane > j && lane < m) {
+          const int c = lane;
+          double t = G[j + m * c];
+          for (int l = 0; l < j; l++) t -= U[l + m * j] * U[l + m * c];
+          U[j + m * c] = t / ujj;
+        }
+        wsync();
+      }
+      if (lane == 0) sh.flag = pd ? 1 : 0;
+      if (pd) {  // lu_factor (partial pivoting), in G
+        for (int k = 0; k < m; k++) {
+          int p = k;
+          double amax = fabs(G[k + m * k]);
+          for (int i = k + 1; i < m; i++)
+            if (fabs(G[i + m * k]) > amax) {
+              amax = fabs(G[i + m * k]);
+              p = i;
             }
-        }
-        // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle
-        double* U = sh.Uc;
-        bool pd = true;
-        for (int j = 0; j < m && pd; j++) {
-          double d0 = G[j + m * j];
-          for (int l = 0; l < j; l++) d0 -= U[l + m * j] * U[l + m * j];
-          if (!(d0 > 0.0)) {
-            pd = false;
-            break;
+          if (lane == 0) sh.piv[k] = p;
+          wsync();
+          if (p != k) {
+            if (lane < m) {
+              const double t = G[k + m * lane];
+              G[k + m * lane] = G[p + m * lane];
+              G[p + m * lane] = t;
+            }
+            wsync();
           }
-          const double ujj = sqrt(d0);
-          U[j + m * j] = ujj;
-          for (int c = j + 1; c < m; c++) {
-            double t = G[j + m * c];
-            for (int l = 0; l < j; l++) t -= U[l + m * j] * U[l + m * c];
-            U[j + m * c] = t / ujj;
+          const double akk = G[k + m * k];
+          if (akk != 0.0) {
+            const double r = 1.0 / akk;
+            if (lane > k && lane < m) G[lane + m * k] *= r;
+            wsync();
           }
+          const int t = m - k - 1;
+          for (int e = lane; e < t * t; e += WAVE) {
+            const int i = k + 1 + e % t, j = k + 1 + e / t;
+            G[i + m * j] = fma(-G[i + m * k], G[k + m * j], G[i + m * j]);
+          }
+          wsync();
         }
-        sh.flag = pd ? 1 : 0;
-        if (pd) {
-          lu_factor<m>(G, sh.piv);
-          for (int e = 0; e < m * m; e++) sh.F[e] = G[e];
-        }
+        for (int e = lane; e < m * m; e += WAVE) sh.F[e] = G[e];
       }
     } else {
       if (lane == 0) {
@@ -1436,14 +1473,17 @@ attempt:
         const int i = e % n, j = e / n;
         sh.S[e] = 0.5 * (sh.T1[i + n * j] + sh.T1[j + n * i]);
       }
+      // ΔV terms: t_j = Σ_i 0.5 d_i Quu[i, j] by lane j, then lane 0's chains over them in order
+      if (lane < m) {
+        double t = 0.0;
+        for (int i = 0; i < m; i++) t = fma(0.5 * sh.dd[i], sh.Quu[i + m * lane], t);
+        sh.red[lane] = t;
+      }
+      wsync();
       if (lane == 0) {
         double a = 0.0, bb = 0.0;
         for (int i = 0; i < m; i++) a = fma(sh.dd[i], sh.Qu[i], a);
-        for (int j = 0; j < m; j++) {
-          double t = 0.0;
-          for (int i = 0; i < m; i++) t = fma(0.5 * sh.dd[i], sh.Quu[i + m * j], t);
-          bb = fma(t, sh.dd[j], bb);
-        }
+        for (int j = 0; j < m; j++) bb = fma(sh.red[j], sh.dd[j], bb);
         dV0 += a;
         dV1 += bb;
       }
