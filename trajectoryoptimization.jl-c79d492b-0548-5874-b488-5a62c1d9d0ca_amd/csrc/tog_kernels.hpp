@@ -811,6 +811,8 @@ struct BwdLds {
   double cval[PC], wv[PC], wsv[PC], gv[PC];
   double cx[PC * n];
   double cu[PC * m];
+  static constexpr int RW = (PC + 63) / 64;
+  unsigned long long rmask[(n + m) * RW];  // per variable: the rows whose gradient entry is nonzero
   double red[WAVE];
   // lane-0 serial scratch (kept in LDS: private arrays with runtime indexing spill to scratch memory)
   double G[m * m];
@@ -931,25 +933,46 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
   }
   wsync();
   if (!SQRT) {
-    // Q.xx .+= cx'Iμ*cx ; Q.uu .+= cu'Iμ*cu ; Q.ux .+= cu'Iμ*cx
+    // Q.xx .+= cx'Iμ*cx ; Q.uu .+= cu'Iμ*cu ; Q.ux .+= cu'Iμ*cx. Entry (i, j) is the chain over the rows r
+    // ascending; a row with a zero gradient entry in column i or j adds an exact zero (fma(0, ., t) = t: t
+    // starts at +0 and never becomes -0), so the chain runs over the rows both columns touch (the AND of
+    // their row masks) and gives the dense chain's value bit for bit (round 5: the infeasible quadrotor's
+    // 69 rows touch 1-3 columns each)
+    constexpr int RW = BwdLds<M, SQRT>::RW;
+    for (int v = lane; v < n + m; v += WAVE) {
+      const double* col = v < n ? sh.cx + p * v : sh.cu + p * (v - n);
+      for (int w = 0; w < RW; w++) {
+        unsigned long long mk = 0ull;
+        for (int r = 64 * w; r < p && r < 64 * (w + 1); r++)
+          if (col[r] != 0.0) mk |= 1ull << (r - 64 * w);
+        sh.rmask[v * RW + w] = mk;
+      }
+    }
+    wsync();
+    auto chain = [&](const double* ci, const double* cj, int vi, int vj) {
+      double t = 0.0;
+      for (int w = 0; w < RW; w++) {
+        unsigned long long mk = sh.rmask[vi * RW + w] & sh.rmask[vj * RW + w];
+        while (mk) {
+          const int r = 64 * w + __builtin_ctzll(mk);
+          mk &= mk - 1;
+          t = fma(ci[r] * sh.wv[r], cj[r], t);
+        }
+      }
+      return t;
+    };
     for (int e = lane; e < n * n; e += WAVE) {
       const int i = e % n, j = e / n;
-      double t = 0.0;
-      for (int r = 0; r < p; r++) t = fma(sh.cx[r + p * i] * sh.wv[r], sh.cx[r + p * j], t);
-      sh.Qxx[e] += t;
+      sh.Qxx[e] += chain(sh.cx + p * i, sh.cx + p * j, i, j);
     }
     if (!term) {
       for (int e = lane; e < m * m; e += WAVE) {
         const int i = e % m, j = e / m;
-        double t = 0.0;
-        for (int r = 0; r < p; r++) t = fma(sh.cu[r + p * i] * sh.wv[r], sh.cu[r + p * j], t);
-        sh.Quu[e] += t;
+        sh.Quu[e] += chain(sh.cu + p * i, sh.cu + p * j, n + i, n + j);
       }
       for (int e = lane; e < m * n; e += WAVE) {
         const int i = e % m, j = e / m;
-        double t = 0.0;
-        for (int r = 0; r < p; r++) t = fma(sh.cu[r + p * i] * sh.wv[r], sh.cx[r + p * j], t);
-        sh.Qux[e] += t;
+        sh.Qux[e] += chain(sh.cu + p * i, sh.cx + p * j, n + i, j);
       }
     }
   } else {
