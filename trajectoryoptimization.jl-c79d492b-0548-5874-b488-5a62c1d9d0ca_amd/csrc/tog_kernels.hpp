@@ -1228,12 +1228,48 @@ attempt:
     if (!SQRT) {
       // T1 = [A B]' S (L x n), then Qxx += (A'S)A ; Quu += (B'S)B ; Qux += (B'S)A  (A.16 association,
       // backward_pass.jl:32-36)
-      wmm<L, n, n, true, false, false>(sh.T1, sh.AB, n, sh.S, n);
-      wsync();
-      wmm<n, n, n, false, false, true>(sh.Qxx, sh.T1, L, A, n);
-      wmm<m, n, m, false, false, true>(sh.Quu, sh.T1 + n, L, Bm, n);
-      wmm<m, n, n, false, false, true>(sh.Qux, sh.T1 + n, L, A, n);
-      wsync();
+      if constexpr (ModelTraits<M>::slack > 0 && !ModelTraits<M>::min_time) {
+        // infeasible model, B = [B_m I] (the slack columns' identity, src/model.jl:771-774): the identity's
+        // products are copies -- T1's slack rows are S's rows, Quu's slack columns T1's -- each "+ 0.0", which
+        // is the dense chain's value bit for bit (its other terms add exact zeros to a +0 start; barring
+        // inf/NaN in S). Round 5: 390 of the 900 length-13 chains of the infeasible quadrotor.
+        constexpr int ns = ModelTraits<M>::slack, mb = m - ns;
+        for (int e = lane; e < L * n; e += WAVE) {
+          const int r = e % L, j = e / L;
+          double t;
+          if (r < n + mb) {
+            t = 0.0;
+#pragma unroll
+            for (int l = 0; l < n; l++) t = fma(sh.AB[l + n * r], sh.S[l + n * j], t);
+          } else {
+            t = sh.S[(r - n - mb) + n * j] + 0.0;
+          }
+          sh.T1[e] = t;
+        }
+        wsync();
+        wmm<n, n, n, false, false, true>(sh.Qxx, sh.T1, L, A, n);
+        for (int e = lane; e < m * m; e += WAVE) {
+          const int i = e % m, j = e / m;
+          double t;
+          if (j < mb) {
+            t = 0.0;
+#pragma unroll
+            for (int l = 0; l < n; l++) t = fma(sh.T1[(n + i) + L * l], Bm[l + n * j], t);
+          } else {
+            t = sh.T1[(n + i) + L * (j - mb)] + 0.0;
+          }
+          sh.Quu[e] = sh.Quu[e] + t;
+        }
+        wmm<m, n, n, false, false, true>(sh.Qux, sh.T1 + n, L, A, n);
+        wsync();
+      } else {
+        wmm<L, n, n, true, false, false>(sh.T1, sh.AB, n, sh.S, n);
+        wsync();
+        wmm<n, n, n, false, false, true>(sh.Qxx, sh.T1, L, A, n);
+        wmm<m, n, m, false, false, true>(sh.Quu, sh.T1 + n, L, Bm, n);
+        wmm<m, n, n, false, false, true>(sh.Qux, sh.T1 + n, L, A, n);
+        wsync();
+      }
     } else {
       // tmp_x = S*A, tmp_u = S*B ; Q.xx ← qr([Q.xx; tmp_x]).R ; Q.uu ← qr([Q.uu; tmp_u]).R ;
       // Q.ux += tmp_u'tmp_x   (backward_pass.jl:112-118)
