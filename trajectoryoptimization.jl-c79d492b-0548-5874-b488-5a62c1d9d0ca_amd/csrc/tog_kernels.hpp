@@ -1333,9 +1333,20 @@ attempt:
       // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle, row j of U by lanes c > j
       double* U = sh.Uc;
       bool pd = true;
+      // (each step's operands are loaded as a batch over the compile-time extent m -- rows l >= j select an
+      // unused 0.0 -- so the LDS reads are in flight together; the chains are the serial ones, in order)
       for (int j = 0; j < m; j++) {
+        double uj[m], uc[m];
+        const int c = (lane > j && lane < m) ? lane : j;
+#pragma unroll
+        for (int l = 0; l < m; l++) {
+          uj[l] = (l < j) ? U[l + m * j] : 0.0;
+          uc[l] = (l < j) ? U[l + m * c] : 0.0;
+        }
         double d0 = G[j + m * j];
-        for (int l = 0; l < j; l++) d0 -= U[l + m * j] * U[l + m * j];
+#pragma unroll
+        for (int l = 0; l < m; l++)
+          if (l < j) d0 -= uj[l] * uj[l];
         if (!(d0 > 0.0)) {
           pd = false;
           break;
@@ -1343,9 +1354,10 @@ attempt:
         const double ujj = sqrt(d0);
         if (lane == j) U[j + m * j] = ujj;
         if (lane > j && lane < m) {
-          const int c = lane;
           double t = G[j + m * c];
-          for (int l = 0; l < j; l++) t -= U[l + m * j] * U[l + m * c];
+#pragma unroll
+          for (int l = 0; l < m; l++)
+            if (l < j) t -= uj[l] * uc[l];
           U[j + m * c] = t / ujj;
         }
         wsync();
@@ -1353,13 +1365,20 @@ attempt:
       if (lane == 0) sh.flag = pd ? 1 : 0;
       if (pd) {  // lu_factor (partial pivoting), in G
         for (int k = 0; k < m; k++) {
+          double ck[m];
+#pragma unroll
+          for (int i = 0; i < m; i++) ck[i] = G[i + m * k];
           int p = k;
-          double amax = fabs(G[k + m * k]);
-          for (int i = k + 1; i < m; i++)
-            if (fabs(G[i + m * k]) > amax) {
-              amax = fabs(G[i + m * k]);
+          double amax = 0.0;
+#pragma unroll
+          for (int i = 0; i < m; i++) {  // amax = |G[k, k]|, then the strict-greater scan over i > k, in order
+            if (i == k) {
+              amax = fabs(ck[i]);
+            } else if (i > k && fabs(ck[i]) > amax) {
+              amax = fabs(ck[i]);
               p = i;
             }
+          }
           if (lane == 0) sh.piv[k] = p;
           wsync();
           if (p != k) {
