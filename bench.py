@@ -91,10 +91,23 @@ def bwd_flops(n, m, N, p_x, p_u, sqrt=True):
     return per_knot * (N - 1)
 
 
+def lib_sha16():
+    """First 16 hex digits of sha256(libtog.so): the build a PMC summary belongs to."""
+    import hashlib
+
+    p = os.path.join(ROOT, "trajectoryoptimization.jl-c79d492b-0548-5874-b488-5a62c1d9d0ca_amd", "csrc", "libtog.so")
+    try:
+        with open(p, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def measured_traffic(kernel, workload="quadrotor"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_traffic.json,
-    written by tools/rocpd_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
-    this same bench command, FETCH_SIZE x2 per the gfx950 correction). None if absent."""
+    """HBM bytes per launch of `kernel` from the committed PMC summary of THIS build (profiles/*_traffic.json,
+    written by tools/rocpd_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    same bench command, FETCH_SIZE x2 per the gfx950 correction, stamped with the sha256 of the libtog.so
+    they measured). A summary of another build is never used: (None, reason) then."""
     import glob
 
     # the headline workload's summaries are <round>_traffic.json; <round>_<workload>_traffic.json
@@ -105,14 +118,22 @@ def measured_traffic(kernel, workload="quadrotor"):
             return b.count("_") == 1
         return b.endswith(f"_{workload}_traffic.json") and b.split("_", 1)[1] == f"{workload}_traffic.json"
 
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")) if ours(f))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        t = json.load(f)["per_launch"].get(kernel)
-    if not t:
-        return None, None
-    return round(t["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+    sha = lib_sha16()
+    match = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        if not ours(f):
+            continue
+        with open(f) as fh:
+            t = json.load(fh)
+        if sha is not None and t.get("libtog_sha16") == sha:
+            match.append((f, t))
+    if not match:
+        return None, f"no committed PMC summary of this build (libtog.so sha256[:16] {sha})"
+    f, t = match[-1]
+    per = t["per_launch"].get(kernel)
+    if not per:
+        return None, f"{os.path.relpath(f, ROOT)} has no {kernel} entry"
+    return round(per["traffic_bytes"]), os.path.relpath(f, ROOT)
 
 
 def host_cpu_info():
@@ -206,6 +227,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-solve-leg", action="store_true", help="skip the full-solve timing leg")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--solve-sets", type=int, default=None,
+                    help="whole solves on this many disjoint start sets (offsets 0, B, 2B per GPU slice); value is "
+                         "set 0's, the others are reported beside it (default: 3 for the headline, else 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,8 +353,9 @@ def main():
     flop_rate = flops / (bwd_avg_ms * 1e-3) / 1e12
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "traffic_source": (f"{tsrc} (committed PMC passes of this command; not measured in this run)"
-                                   if tsrc else None),
+                "traffic_source": (f"{tsrc} (committed PMC passes of this command on this build; not measured "
+                                   "in this run)" if traffic is not None else tsrc),
+                "libtog_sha16": lib_sha16(),
                 "algorithmic_bytes_per_launch": round(alg_bytes), "kernel": names[dom],
                 "kernel_ms": {nm_: round(float(ms[i] / max(1, launches[i])), 4) for i, nm_ in enumerate(names)},
                 "step_achieved": round(step_gbs, 2),
@@ -344,8 +369,21 @@ def main():
 
     # ---------------------------------------------------------------- leg 2: the whole solve
     solve_leg = None
+    solve_sets = None
     if not args.no_solve_leg:
         solve_leg = time_solve(h, abi, mode, prob, dist, allreduce_stats, barrier_sync, local_rank, pkg)
+        nsets = args.solve_sets if args.solve_sets is not None else (3 if args.workload == "quadrotor" else 1)
+        if nsets > 1:
+            # the whole-solve rate depends on each set's slowest trajectories: disjoint start sets of the same
+            # size (set s: the job's trajectories s*B*world .. (s+1)*B*world - 1, this rank's contiguous slice)
+            solve_sets = [{"offset": 0, "value": solve_leg["value"], "wall_s": solve_leg["wall_s"],
+                           "steps": solve_leg["steps"], "max_traj_iterations": solve_leg["traj_iterations"]["max"]}]
+            for sidx in range(1, nsets):
+                off = sidx * B * world + offset
+                prob_s, _ = getattr(pkg.Problems, cfg_fn)(B=count, offset=off)
+                r = time_solve(h, abi, mode, prob_s, dist, allreduce_stats, barrier_sync, local_rank, pkg)
+                solve_sets.append({"offset": sidx * B * world, "value": r["value"], "wall_s": r["wall_s"],
+                                   "steps": r["steps"], "max_traj_iterations": r["traj_iterations"]["max"]})
     # value: SURVEY.md §8(d)'s metric, the whole solve (tog_solve_init until no trajectory is active);
     # the full-batch step window is reported beside it as window_rate
     value = solve_leg["value"] if solve_leg is not None else window_rate
@@ -377,6 +415,12 @@ def main():
                                                 "is solve_rate, the whole solve"}},
             "window_rate": round(window_rate, 2),
             "solve_rate": solve_leg,
+            "solve_rate_sets": (None if solve_sets is None else {
+                "sets": solve_sets,
+                "mean": round(float(np.mean([x["value"] for x in solve_sets])), 2),
+                "min": round(float(np.min([x["value"] for x in solve_sets])), 2),
+                "max": round(float(np.max([x["value"] for x in solve_sets])), 2),
+                "note": "the whole solve on disjoint start sets of the same size; value is the first set's (offset 0)"}),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

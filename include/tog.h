@@ -469,6 +469,10 @@ enum tog_pn_stat {
    when its first trial does not reduce the violation (projected_newton.jl:273-277): such a
    trajectory stops with this flag and keeps the last accepted iterate. */
 #define TOG_TRAJ_PN_ERROR (1 << 11)
+/* The device's projected Newton blocks hold at most 64 rows (n + the rows active at a knot, a row per lane of
+   a wave; the stride is min(n + pmax, 64)): a trajectory whose active set outgrows them stops with
+   TOG_TRAJ_PN_ERROR | TOG_TRAJ_PN_BLOCK and keeps its last iterate. A device limit, not the reference's. */
+#define TOG_TRAJ_PN_BLOCK (1 << 12)
 
 /* solve!(prob, ProjectedNewtonSolver(prob, opts)) (projected_newton.jl:6-20) on every trajectory's
    current X, U (in place): n_steps newton steps of the feasible projection, each

@@ -1366,7 +1366,8 @@ static void hist_push(double** buf, int* n, int* cap, int w, const double* rec) 
 /* mb: the controls a bound row may constrain (m less the slack controls of an infeasible-start problem:
    its BoundConstraint keeps the model's m, update_constraint_set_jacobians constraint_sets.jl:135-150) */
 /* mb: the controls of the model inside add_slack_controls / add_min_time_controls; slack: the slack count.
-   A trim=false bound keeps one row per model control (the slack and time-step controls get none); a trimmed
+   A trim=false bound keeps one row per model control and one for the time step h (the slack controls get none;
+   BoundConstraint(n̄, m̄, trim=false) keeps every u row of the problem it was built for); a trimmed
    bound has rows for its finite entries over all m (an infeasible problem's slack entries are infinite;
    the infeasible minimum-time problem's combined bound reaches u[1:m+1], minimum_time.jl:125-141) */
 static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb, int slack) {
@@ -1390,8 +1391,10 @@ static void con_init(oc_con* oc, const tog_constraint* tc, int n, int m, int mb,
       for (int i = 0; i < m; i++) {
         oc->u_max[i] = D[2 * n + i];
         oc->u_min[i] = D[2 * n + m + i];
-        oc->au_max[i] = (keep ? i < mb : 1) && (keep || isfinite(D[2 * n + i]));
-        oc->au_min[i] = (keep ? i < mb : 1) && (keep || isfinite(D[2 * n + m + i]));
+        /* trim=false keeps the model's controls and the time step h (the last control when m - mb - slack = 1) */
+        const int ku = i < mb || (i == m - 1 && m - mb - slack > 0);
+        oc->au_max[i] = (keep ? ku : 1) && (keep || isfinite(D[2 * n + i]));
+        oc->au_min[i] = (keep ? ku : 1) && (keep || isfinite(D[2 * n + m + i]));
         cu += oc->au_max[i];
         cun += oc->au_min[i];
       }

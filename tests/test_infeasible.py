@@ -409,3 +409,43 @@ def test_gpu_infeasible_projected_newton(tog, oracle, gpu, resolve):
     tol = TOL_SOLVE if resolve else TOL_STEP
     assert rel(prob.X, Xo) < tol and rel(prob.U, Uo) < tol
     assert int(solver.stats_pn["iterations"][0]) >= 1
+
+
+def _pendulum_line_bound(tog, trim):
+    """pendulum_line's constrained variant with a finite state bound as well, trimmed or not."""
+    prob = tog.Problems.pendulum()
+    n, m, N = 2, 1, prob.N
+    bnd = tog.BoundConstraint(n, m, x_min=[-20.0, -20.0], x_max=[20.0, 20.0], u_min=-3.0, u_max=3.0, trim=trim)
+    cons = tog.Constraints([bnd], N)
+    cons[N - 1] = cons[N - 1] + tog.goal_constraint(prob.xf)
+    prob = tog.Problem(prob.model, prob.obj, prob.U, constraints=cons, x0=prob.x0[0], xf=prob.xf, N=N, dt=prob.dt)
+    prob.X = tog.line_trajectory(prob.x0[0], prob.xf, prob.N)
+    return prob
+
+
+def test_oracle_infeasible_untrimmed_bound(tog, oracle):
+    """BoundConstraint(trim=false) on an infeasible-start problem (built since round 6): the bound keeps the
+    model's m (update_constraint_set_jacobians, constraint_sets.jl:135-150), so with every entry finite the
+    untrimmed solve equals the trimmed one bit for bit."""
+    opts = pendulum_opts(tog, False)
+    out = []
+    for trim in (True, False):
+        prob = _pendulum_line_bound(tog, trim)
+        pinf = tog.infeasible_problem(prob, opts.R_inf)
+        assert pinf.constraints[0][0].to_abi(pinf.model.m)[1] == (0 if trim else 1)
+        X, U, si, _ = oracle.solve_altro_infeasible(prob, opts, 0)
+        out.append((X, U, si.history()[1]))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.gpu
+def test_gpu_infeasible_untrimmed_bound(tog, oracle, gpu):
+    """The untrimmed infeasible-start case on the device equals the oracle (X, U to 1e-6, AL records)."""
+    opts = pendulum_opts(tog, True)
+    prob = _pendulum_line_bound(tog, False)
+    gp = prob.copy()
+    solver = tog.solve_b(gp, opts)
+    X, U, si, sf = oracle.solve_altro_infeasible(prob, opts, 0)
+    assert rel(gp._X[0], X) < TOL_SOLVE and rel(gp._U[0], U) < TOL_SOLVE
+    assert solver.solver_al.traj_stats(0)["iterations"] == len(si.history()[1])

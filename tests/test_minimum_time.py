@@ -279,3 +279,62 @@ def test_gpu_min_time_projected_newton(tog, oracle, gpu, infeasible):
     assert np.max(np.abs(p._U[0] - Uo)) <= tol * scale(Uo)
     assert np.max(np.abs(p.h[0] - ho)) <= tol
     assert int(solver.stats_pn["iterations"][0]) >= 1
+
+
+def _untrimmed_mt_problem(tog):
+    """A minimum-time pendulum built by hand with an untrimmed bound on [x; τ] and [u; h]
+    (BoundConstraint(n̄, m̄, trim=false), constraints.jl:155-188): every u row is kept, the time step h's
+    √dt bounds included."""
+    make, opts, *_ = pendulum_case(tog)
+    p = make(np.ones((30, 1)), 0.15)
+    pmt = tog.minimum_time_problem(p, 15.0, 0.15, 1e-3)
+    n, m, N = pmt.model.n, pmt.model.m, pmt.N
+    bnd = tog.BoundConstraint(n, m, x_min=[-10.0, -10.0, -1.0], x_max=[10.0, 10.0, 1.0],
+                              u_min=[-5.0, math.sqrt(1e-3)], u_max=[5.0, math.sqrt(0.15)], trim=False)
+    cons = tog.Constraints(N)
+    for k in range(N):
+        cons[k] += bnd
+        if 0 < k < N - 1:
+            cons[k] += tog.MinTimeEquality()
+    q = tog.Problem(pmt.model, pmt.obj, pmt._U[0], constraints=cons, x0=pmt.x0[0], xf=pmt.xf, N=N, dt=pmt.dt)
+    q._X[0] = pmt._X[0]
+    return q, bnd, opts
+
+
+def test_oracle_untrimmed_min_time_bound_keeps_h_rows(tog, oracle):
+    """An untrimmed bound on a minimum-time problem keeps the rows of h, the last control (advisor r5: they
+    were dropped with the slack controls'): the oracle's constraint values equal the host BoundConstraint's."""
+    q, bnd, opts = _untrimmed_mt_problem(tog)
+    o = oracle.OracleSolver(q, opts.opts_al, 0)
+    o.rollout_open_loop()
+    o.update_constraints()
+    C = o.get("C")
+    X, U = o.get("X"), o.get("U")
+    assert bnd.length("stage") == 10
+    for k in (0, 5, q.N - 2):
+        assert np.array_equal(C[k, :10], bnd.evaluate(X[k], U[k])), k
+    assert np.array_equal(C[q.N - 1, :6], bnd.evaluate(X[q.N - 1]))
+
+
+@pytest.mark.gpu
+def test_gpu_untrimmed_min_time_bound_rows(tog, oracle, gpu):
+    """The device's rows of the untrimmed minimum-time bound (tog_update_constraints) equal the oracle's,
+    and an AL solve on it matches the oracle's iteration count and X, U within 1e-6."""
+    q, bnd, opts = _untrimmed_mt_problem(tog)
+    o = oracle.OracleSolver(q, opts.opts_al, 0)
+    o.rollout_open_loop()
+    o.update_constraints()
+    solver = tog.AugmentedLagrangianSolver(q, opts.opts_al)
+    q2 = q.copy()
+    q2._X[0] = o.get("X")
+    solver.handle.upload_state(q2)
+    tog.update_constraints_b(q2, solver)
+    C = solver.handle.get(tog.abi.FIELD_C)[0]
+    assert np.array_equal(C[:, :11], o.get("C")[:, :11])
+    o2 = oracle.OracleSolver(q, opts.opts_al, 0)
+    steps = o2.solve()
+    gp = q.copy()
+    s = tog.solve_b(gp, opts.opts_al)
+    assert int(s.stats["iterations_total"][0]) == steps
+    scale = max(1.0, float(np.max(np.abs(o2.get("X")))))
+    assert np.max(np.abs(gp._X[0] - o2.get("X"))) <= 1e-6 * scale

@@ -78,21 +78,18 @@ def test_altro_pn_tolerances(tog):
     assert opts.opts_al.constraint_tolerance == tol0
 
 
-def test_pn_accepts_infeasible_start(tog):
-    """Round 5: phase 2 on the infeasible-start problem is built (tests/test_infeasible.py
-    test_gpu_infeasible_projected_newton); the host check lets it through."""
-    prob = tog.Problems.pendulum()
-    prob.X = tog.line_trajectory(prob.x0[0], prob.xf, prob.N)
-    tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
-
-
-def test_pn_accepts_min_time(tog):
-    """Round 5: phase 2 on a minimum-time problem (altro_methods.jl:98-124) is built (its H from MinTimeCost's
-    hessian!, tests/test_minimum_time.py test_gpu_min_time_projected_newton); the host check lets it through."""
-    prob = tog.Problems.pendulum()
-    prob.tf = 0.0
-    tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=True))
-    tog.solvers._altro_check(prob, tog.ALTROSolverOptions(projected_newton=False))
+def test_iros_maze_options(tog):
+    """The IROS 2019 quadrotor maze demo's options (examples/IROS_2019/quadrotor_maze.jl:8-34), and
+    altro_methods.jl:5-13's AL tolerance once projected Newton is on."""
+    opts = tog.Problems.quadrotor_maze_iros_options()
+    assert opts.projected_newton and not opts.resolve_feasible_problem and opts.R_inf == 1e-8
+    assert opts.opts_pn.feasibility_tolerance == 1e-8 and opts.opts_pn.solve_type == "feasible"
+    assert opts.opts_pn.n_steps == 1 and opts.opts_pn.active_set_tolerance == 1e-3
+    al = opts.opts_al
+    assert (al.iterations, al.cost_tolerance, al.cost_tolerance_intermediate, al.penalty_scaling,
+            al.penalty_initial, al.opts_uncon.iterations) == (40, 1e-5, 1e-4, 10.0, 1.0, 300)
+    tog.solvers._altro_pn_tolerances(opts)
+    assert opts.opts_al.constraint_tolerance == 1e-4
 
 
 @pytest.mark.parametrize("ft,at", [(1e-6, 1e-3), (1e-10, 1e-3), (1e-10, 1e-4)])
@@ -288,3 +285,57 @@ def test_gpu_altro_pn_optimal(tog, oracle, gpu):
         assert rel(gp._X[b], o.get("X")) < TOL_STEP and rel(gp._U[b], o.get("U")) < TOL_STEP, b
         assert solver.stats_pn["iterations"][b] == out[tog.abi.PN_STEPS]
         assert abs(solver.stats_pn["c_max"][b] - out[tog.abi.PN_C_MAX]) <= 1e-13
+
+
+def _oracle_iros(args):
+    oracle, prob, opts, b = args
+    X, U, si, _ = oracle.solve_altro_infeasible(prob, opts, b)
+    _, hout, hpn = si.history()
+    return X, U, len(hout), hpn, int(si.get("stats")[oracle._pkg.abi.STAT_FLAGS])
+
+
+@pytest.mark.gpu
+def test_gpu_iros_quadrotor_maze_altro_pn(tog, oracle, gpu):
+    """The reference's IROS 2019 demo, solve(Problems.quadrotor_maze, opts_altro) with projected Newton
+    (examples/IROS_2019/quadrotor_maze.jl:23-48): the infeasible-start AL phase (n = 13, m = 4 + 13, 69 rows a
+    knot) to 1e-4, then the feasible projection on the infeasible problem (blocks of n + active rows, up to
+    n + m = 30 variables a knot) to 1e-8. Trajectory 0 starts from the reference's own guess
+    (problems/quadrotor_maze.jl:104-113), 1-3 from jittered way-points. Device == oracle within the north star's
+    1e-6 (relative, fp64), equal AL outer iterations, newton steps and flags. Starts 1 and 2 hit the reference's
+    own exception in _projection_linesearch! (projected_newton.jl:273-277) on both sides; the reference's start
+    ends feasible to 1e-8, as the notebook's 9.63e-9 (examples/quadrotor/Quadrotor Maze.ipynb, cell 3)."""
+    from concurrent.futures import ThreadPoolExecutor
+    B = 4
+    prob = tog.Problems.quadrotor_maze_batch(B)
+    prob._X[0] = tog.Problems.quadrotor_maze_batch(1, jitter=0.0)._X[0]
+    opts = tog.Problems.quadrotor_maze_iros_options()
+    gp = prob.copy()
+    try:
+        solver = tog.solve_b(gp, opts)
+        raised = []
+    except tog.ProjectedNewtonError as e:  # the reference raises for such a start; the batch's results stand
+        solver, raised = e.solver, e.trajectories
+    assert solver.stats["time_pn"] > 0.0
+    o_opts = tog.Problems.quadrotor_maze_iros_options()
+    tog.solvers._altro_pn_tolerances(o_opts)
+    with ThreadPoolExecutor(B) as ex:  # the oracle's C calls release the GIL
+        refs = list(ex.map(_oracle_iros, [(oracle, prob, o_opts, b) for b in range(B)]))
+    print(f"\nIROS maze ALTRO+PN on the device: {B} starts in {solver.stats['time']:.2f} s "
+          f"(AL {solver.stats['time_al']:.2f} s, PN {solver.stats['time_pn']:.3f} s); "
+          f"the reference publishes 85.8 s for one start (context only)")
+    flags = solver.stats_pn["flags"]
+    err_o = []
+    for b, (X, U, n_out, hpn, fo) in enumerate(refs):
+        assert rel(gp._X[b], X) < 1e-6 and rel(gp._U[b], U) < 1e-6, b
+        assert solver.solver_al.traj_stats(b)["iterations"] == n_out, b
+        assert solver.stats_pn["iterations"][b] == len(hpn), b
+        assert bool(flags[b] & tog.abi.TRAJ_PN_ERROR) == bool(fo & tog.abi.TRAJ_PN_ERROR), b
+        if fo & tog.abi.TRAJ_PN_ERROR:
+            err_o.append(b)
+        c = solver.stats_pn["c_max"][b]
+        assert abs(c - hpn[-1, 1]) <= 1e-9 * max(1.0, hpn[-1, 1]), (b, c, hpn[-1, 1])
+        print(f"  start {b}: AL outer {n_out}, c_max after PN {c:.3e} (oracle {hpn[-1, 1]:.3e})"
+              + (" [the reference's _projection_linesearch! exception]" if fo & tog.abi.TRAJ_PN_ERROR else ""))
+    assert list(raised) == err_o
+    assert solver.stats_pn["c_max"][0] <= 1e-8 and not flags[0] & tog.abi.TRAJ_PN_ERROR
+    assert not np.any(flags & tog.abi.TRAJ_PN_BLOCK)

@@ -88,7 +88,12 @@ if __name__ == "__main__":
     src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_r1"
     t = main(src)
     if len(sys.argv) > 2 and t:
-        pathlib.Path(sys.argv[2]).write_text(json.dumps({"source": src, "per_launch": t}, indent=1) + "\n")
+        import hashlib
+
+        # stamped with the build the passes measured: bench.py uses a summary only for the same libtog.so
+        lib = pathlib.Path(__file__).resolve().parent.parent / "trajectoryoptimization.jl-c79d492b-0548-5874-b488-5a62c1d9d0ca_amd" / "csrc" / "libtog.so"
+        sha = hashlib.sha256(lib.read_bytes()).hexdigest()[:16]
+        pathlib.Path(sys.argv[2]).write_text(json.dumps({"source": src, "libtog_sha16": sha, "per_launch": t}, indent=1) + "\n")
 
 
 def sq_summary(d):

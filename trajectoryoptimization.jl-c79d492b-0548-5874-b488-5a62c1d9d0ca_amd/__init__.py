@@ -20,7 +20,7 @@ from .problem import (BoundConstraint, CircleConstraints, Constraints, Constrain
                       minimum_time_problem, mintime_constraints, total_time, MinTimeEquality, GenericCost, generic_cost)
 from .solvers import (Expansion, AbstractSolver, AbstractSolverFor, ALTROSolver, ALTROSolverOptions, AugmentedLagrangianSolver,
                       AugmentedLagrangianSolverOptions, iLQRSolver, iLQRSolverOptions, ProjectedNewtonSolver,
-                      ProjectedNewtonSolverOptions, PosDefException, solve, solve_b, solver_name, to_tog_options,
+                      ProjectedNewtonSolverOptions, PosDefException, ProjectedNewtonError, solve, solve_b, solver_name, to_tog_options,
                       to_tog_pn_options)
 from .steps import backwardpass_b, cost, cost_expansion_b, forwardpass_b, jacobian_b, rollout_b, update_constraints_b
 from . import problems as Problems
@@ -36,5 +36,5 @@ __all__ = [
     "to_tog_options", "Expansion", "backwardpass_b", "cost", "cost_expansion_b", "update_constraints_b", "forwardpass_b", "jacobian_b", "rollout_b",
     "Problems", "add_slack_controls", "InfeasibleConstraint", "infeasible_constraints", "infeasible_problem",
     "line_trajectory", "ProjectedNewtonSolver", "ProjectedNewtonSolverOptions", "to_tog_pn_options",
-    "GenericCost", "generic_cost", "PosDefException",
+    "GenericCost", "generic_cost", "PosDefException", "ProjectedNewtonError",
 ]

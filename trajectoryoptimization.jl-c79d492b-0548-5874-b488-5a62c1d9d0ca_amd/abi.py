@@ -53,6 +53,7 @@ TRAJ_AL_MAX_ITERS = 1 << 8
 TRAJ_SINGULAR = 1 << 9
 TRAJ_BP_ABORTED = 1 << 10
 TRAJ_PN_ERROR = 1 << 11
+TRAJ_PN_BLOCK = 1 << 12  # a projected Newton block outgrew the device's 64 rows (TOG_TRAJ_PN_BLOCK)
 
 # projected Newton statistics row (tog_pn_stat)
 PN_VIOL, PN_C_MAX, PN_J, PN_PROJECTIONS, PN_LINESEARCHES, PN_REFINEMENTS, PN_STEPS = range(7)

@@ -813,6 +813,8 @@ struct BwdLds {
   double cu[PC * m];
   static constexpr int RW = (PC + 63) / 64;
   unsigned long long rmask[(n + m) * RW];  // per variable: the rows whose gradient entry is nonzero
+  unsigned long long rnf[(n + m) * RW];    // per variable: the rows whose gradient entry is not finite
+  unsigned long long rbad[RW];             // rows with a non-finite gradient entry or weight: always chained
   double red[WAVE];
   // lane-0 serial scratch (kept in LDS: private arrays with runtime indexing spill to scratch memory)
   double G[m * m];
@@ -937,22 +939,34 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
     // ascending; a row with a zero gradient entry in column i or j adds an exact zero (fma(0, ., t) = t: t
     // starts at +0 and never becomes -0), so the chain runs over the rows both columns touch (the AND of
     // their row masks) and gives the dense chain's value bit for bit (round 5: the infeasible quadrotor's
-    // 69 rows touch 1-3 columns each)
+    // 69 rows touch 1-3 columns each). A row with a non-finite gradient entry or weight anywhere is chained
+    // in every entry (rbad), so a diverging trajectory's Inf/NaN reaches Q exactly as the dense chain's does.
     constexpr int RW = BwdLds<M, SQRT>::RW;
     for (int v = lane; v < n + m; v += WAVE) {
       const double* col = v < n ? sh.cx + p * v : sh.cu + p * (v - n);
       for (int w = 0; w < RW; w++) {
-        unsigned long long mk = 0ull;
-        for (int r = 64 * w; r < p && r < 64 * (w + 1); r++)
+        unsigned long long mk = 0ull, nf = 0ull;
+        for (int r = 64 * w; r < p && r < 64 * (w + 1); r++) {
           if (col[r] != 0.0) mk |= 1ull << (r - 64 * w);
+          if (!isfinite(col[r])) nf |= 1ull << (r - 64 * w);
+        }
         sh.rmask[v * RW + w] = mk;
+        sh.rnf[v * RW + w] = nf;
       }
+    }
+    wsync();
+    if (lane < RW) {
+      unsigned long long bad = 0ull;
+      for (int v = 0; v < n + m; v++) bad |= sh.rnf[v * RW + lane];
+      for (int r = 64 * lane; r < p && r < 64 * (lane + 1); r++)
+        if (!isfinite(sh.wv[r])) bad |= 1ull << (r - 64 * lane);
+      sh.rbad[lane] = bad;
     }
     wsync();
     auto chain = [&](const double* ci, const double* cj, int vi, int vj) {
       double t = 0.0;
       for (int w = 0; w < RW; w++) {
-        unsigned long long mk = sh.rmask[vi * RW + w] & sh.rmask[vj * RW + w];
+        unsigned long long mk = (sh.rmask[vi * RW + w] & sh.rmask[vj * RW + w]) | sh.rbad[w];
         while (mk) {
           const int r = 64 * w + __builtin_ctzll(mk);
           mk &= mk - 1;
@@ -1158,6 +1172,8 @@ template <class M, int SQRTI, int ALI>
 __global__ void __launch_bounds__(64) k_backward(const DevProblem* __restrict__ P, DevBuffers Bf, int flags) {
   constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
   constexpr int n = M::n, m = M::m, L = n + m, NQ = nq_of<M>();
+  // the wave-parallel Quu factorization, the LU's pivot swap and the ΔV terms give lane j column j
+  static_assert(m <= WAVE, "k_backward: more controls than lanes in a wave");
   __shared__ BwdLds<M, SQRT> sh;
   const long long b = traj_of_slot(Bf, blockIdx.x, P->B);
   const int lane = threadIdx.x;
@@ -3718,21 +3734,30 @@ struct ModelLaunch {
   template <int INTEG>
   static void pn_phase(const DevProblem* P, const DevBuffers& Bf, const PNBuffers& W, long long B, int phase,
                        hipStream_t st) {
+    // the factoring kernels' LDS is sized by the block stride (pn_lds_bytes; up to 113 KB at SM = 64)
+    const size_t lds = pn_lds_bytes(W.SM, M::n + M::m);
+    auto big = [&](auto kern) {  // allow dynamic LDS above 64 KB (gfx950: 160 KB per workgroup)
+      if (lds > 65536) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipGetLastError();
+      }
+      hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(64), lds, st, P, Bf, W);
+    };
     if (phase == 0)
       hipLaunchKernelGGL((k_pn_begin<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
     else if (phase == 1)
-      hipLaunchKernelGGL((k_pn_project<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+      big(k_pn_project<M, INTEG>);
     else if (phase == 2)
       hipLaunchKernelGGL((k_pn_finish<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
     else if constexpr (!ModelTraits<M>::min_time) {  // solve_type :optimal (not built for minimum time)
       if (phase == 3)
-        hipLaunchKernelGGL((k_pn_kkt<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+        big(k_pn_kkt<M, INTEG>);
       else if (phase == 4)
-        hipLaunchKernelGGL((k_pn_ls_begin<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+        big(k_pn_ls_begin<M, INTEG>);
       else if (phase == 5)
-        hipLaunchKernelGGL((k_pn_ls_proj<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+        big(k_pn_ls_proj<M, INTEG>);
       else
-        hipLaunchKernelGGL((k_pn_ls_end<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
+        big(k_pn_ls_end<M, INTEG>);
     }
   }
   static void pn(const DevProblem* P, const DevBuffers& Bf, const PNBuffers& W, long long B, int integ, int phase,
@@ -3760,9 +3785,8 @@ struct ModelLaunch {
     o.cost = cost;
     o.rollout = rollout;
     o.update_constraints = update_constraints;
-    // projected Newton: plain models; the infeasible-start and minimum-time models whose [x; u] fits the PN
-    // kernels' blocks (n + m <= 24; tog_solve_pn refuses larger ones)
-    if constexpr ((ModelTraits<M>::slack == 0 && !ModelTraits<M>::min_time) || M::n + M::m <= 24)
+    // projected Newton: every model whose [x; u] fits a wave (a lane per variable of a knot)
+    if constexpr (M::n + M::m <= PN_SM_MAX)
       o.pn = pn;
     else
       o.pn = nullptr;

@@ -8,7 +8,11 @@
 //
 // Mapping (MI355X): one wave (64-thread block) per trajectory. The dual vector is ordered as the
 // reference's (direct_solvers.jl:80-105): G_0 = x_1 - x0, G_b = [f(x_b,u_b) - x_{b+1}; active C_b],
-// G_N = active C_N. S = Y H⁻¹ Yᵀ is then block tridiagonal with blocks of n + p_active ≤ 32 rows.
+// G_N = active C_N. S = Y H⁻¹ Yᵀ is then block tridiagonal with blocks of n + p_active rows: the
+// blocks are sized by the rows *active* at a knot, not by every row it carries (the quadrotor maze's
+// infeasible problem has 69 rows a knot, of which 13-16 are active), with a stride of
+// SM = min(n + pmax, PN_SM_MAX) rows. A block larger than the stride (more than 64 - n active rows)
+// stops that trajectory with TOG_TRAJ_PN_ERROR | TOG_TRAJ_PN_BLOCK; nothing is written past it.
 // The blocks are built in parallel over their entries (a lane per entry), the block Cholesky of
 // S + 1e-2 I sweeps the knots with the current and previous factor staged in LDS (a lane per row
 // for the off-diagonal solves, a lane per entry for the Schur updates), and the substitutions run a
@@ -18,7 +22,7 @@
 
 namespace tog {
 
-constexpr int PN_SM_MAX = 32;  // largest block (n + pmax) of the wave kernels
+constexpr int PN_SM_MAX = 64;  // largest block (n + active rows): a row per lane of the wave
 
 struct PNState {
   double viol, c_max, J;
@@ -27,6 +31,7 @@ struct PNState {
   int error;     // TOG_TRAJ_PN_ERROR path
   int steps, projections, linesearches, refinements;
   int active0;   // the solver's own active flag, restored by k_pn_finish (k_jacobian gates on it)
+  int over;      // a block outgrew the stride SM (TOG_TRAJ_PN_BLOCK)
   // solve_type :optimal
   int has_S;     // a _projection_solve! has set solver.stats[:S] (its factor in Ld, Lo, block sizes in szS)
   int ls;        // line search stage: 0 none, 1 begin pending, 2 projecting the trial, 3 trial projected
@@ -185,8 +190,9 @@ __device__ void pn_eval(const DevProblem* P, const DevBuffers& Bf, long long b, 
 }
 
 // active_set! (projected_newton.jl:75-93) and the block sizes. A lane per knot.
-__device__ void pn_active_set(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, double tol,
-                              int nb, int lane) {
+// Returns (to every lane) whether a block outgrew the stride SM; the caller then stops the trajectory.
+__device__ int pn_active_set(const DevProblem* P, const DevBuffers& Bf, long long b, const PNView& w, double tol,
+                             int nb, int lane) {
   const int N = P->N, pmax = P->pmax, n = P->n;
   const double* C = Bf.C + (size_t)b * N * pmax;
   for (int k = lane; k < N; k += WAVE) {
@@ -197,8 +203,12 @@ __device__ void pn_active_set(const DevProblem* P, const DevBuffers& Bf, long lo
     w.na[k] = c;
   }
   pn_sync();
-  for (int bb = lane; bb < nb; bb += WAVE) w.sz[bb] = (bb < N ? n : 0) + (bb >= 1 ? w.na[bb - 1] : 0);
-  pn_sync();
+  int over = 0;
+  for (int bb = lane; bb < nb; bb += WAVE) {
+    w.sz[bb] = (bb < N ? n : 0) + (bb >= 1 ? w.na[bb - 1] : 0);
+    over |= w.sz[bb] > w.SM;
+  }
+  return __syncthreads_or(over);
 }
 
 // y[a] into yv (block order) and its Inf norm (NaN propagates); every lane returns it
@@ -426,11 +436,25 @@ __device__ double pn_residual(const PNView& w, int nb, const double* y, const do
   return sqrt(__shfl(ss, 0, WAVE));
 }
 
-struct PNLds {  // LDS of k_pn_project (SM <= PN_SM_MAX)
-  double A[PN_SM_MAX * PN_SM_MAX], Bm[PN_SM_MAX * PN_SM_MAX], Cm[PN_SM_MAX * PN_SM_MAX];
-  double Yz[PN_SM_MAX * 24];
-  double vec[PN_SM_MAX], vec2[PN_SM_MAX];
+// LDS of the kernels that factor and solve (dynamic, sized by the stride SM and L = n + m): three SM x SM
+// blocks, the rows of one block on its knot's variables (SM x L), two vectors. 113 KB at SM = 64, L = 30.
+struct PNLds {
+  double *A, *Bm, *Cm, *Yz, *vec, *vec2;
 };
+__host__ __device__ constexpr size_t pn_lds_bytes(int SM, int L) {
+  return sizeof(double) * ((size_t)3 * SM * SM + (size_t)SM * L + 2 * (size_t)SM);
+}
+__device__ __forceinline__ PNLds pn_lds(int SM, int L) {
+  extern __shared__ double pn_smem[];
+  PNLds s;
+  s.A = pn_smem;
+  s.Bm = s.A + SM * SM;
+  s.Cm = s.Bm + SM * SM;
+  s.Yz = s.Cm + SM * SM;
+  s.vec = s.Yz + SM * L;
+  s.vec2 = s.vec + SM;
+  return s;
+}
 
 // reg_solve(S, y, Sreg, 1e-8, 25) into xv (projected_newton.jl:286-303)
 __device__ void pn_reg_solve(const PNView& w, int nb, PNLds& sh, PNState& s, int lane) {
@@ -493,7 +517,15 @@ __global__ void __launch_bounds__(64) k_pn_begin(const DevProblem* __restrict__ 
   if constexpr (ModelTraits<M>::min_time)
     pn_weights_min_time<M>(P, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
   pn_eval<M, INTEG>(P, Bf, b, w, Bf.X + (size_t)b * N * M::n, Bf.U + (size_t)b * (N - 1) * M::m, lane);
-  pn_active_set(P, Bf, b, w, W.atol, W.nb, lane);
+  if (pn_active_set(P, Bf, b, w, W.atol, W.nb, lane)) {
+    if (lane == 0) {
+      s.active0 = Bf.st[b].active;
+      s.error = s.over = 1;
+      s.viol = NAN;
+      Bf.st[b].active = 0;
+    }
+    return;
+  }
   const double viol = pn_gather_y(P, Bf, b, w, W.nb, lane);
   if (W.optimal) {  // update!'s Jacobians at V: the first k_jacobian of the projection loop, for every trajectory
     for (int e = lane; e < N * M::n; e += WAVE) w.Xs[e] = Bf.X[(size_t)b * N * M::n + e];
@@ -508,12 +540,21 @@ __global__ void __launch_bounds__(64) k_pn_begin(const DevProblem* __restrict__ 
   }
 }
 
+// a block outgrew the stride: stop the trajectory (k_pn_finish flags it)
+__device__ __forceinline__ void pn_stop_over(PNState& s, PNState* dst, TrajState& ts, int lane) {
+  if (lane == 0) {
+    s.error = s.over = 1;
+    *dst = s;
+    ts.active = 0;
+  }
+}
+
 // one pass of projection_solve!'s loop: _projection_solve! (Jacobians from k_jacobian at X, U)
 template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_pn_project(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
-  __shared__ PNLds sh;
+  PNLds sh = pn_lds(W.SM, M::n + M::m);
   PNState s = W.st[b];
   if (s.finished || s.error || s.count >= 10 || !(s.viol > W.eps)) {  // while count < 10 && viol > eps
     if (W.optimal && lane == 0 && !s.finished) Bf.st[b].active = 0;     // (:optimal: Jacobians at V are kept)
@@ -528,7 +569,7 @@ __global__ void __launch_bounds__(64) k_pn_project(const DevProblem* __restrict_
   s.projections++;
   for (int e = lane; e < N * n; e += WAVE) w.Xs[e] = X[e];
   pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
-  pn_active_set(P, Bf, b, w, W.atol, nb, lane);
+  if (pn_active_set(P, Bf, b, w, W.atol, nb, lane)) return pn_stop_over(s, &W.st[b], Bf.st[b], lane);
   const double viol0 = pn_gather_y(P, Bf, b, w, nb, lane);
   pn_build_S<M>(P, Bf, b, w, X, sh.Yz, nb, lane);
   double viol = viol0;
@@ -595,7 +636,7 @@ __global__ void __launch_bounds__(64) k_pn_finish(const DevProblem* __restrict__
   s.c_max = traj_max_violation(P, Bf, b);
   s.J = traj_cost<M>(P, Bf, b, X, U, false, nullptr);
   if (s.error || s.c_max <= W.eps) s.finished = 1;
-  if (s.error) Bf.st[b].flags |= TOG_TRAJ_PN_ERROR;
+  if (s.error) Bf.st[b].flags |= TOG_TRAJ_PN_ERROR | (s.over ? TOG_TRAJ_PN_BLOCK : 0);
   W.st[b] = s;
 }
 
@@ -823,7 +864,7 @@ template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_pn_kkt(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
-  __shared__ PNLds sh;
+  PNLds sh = pn_lds(W.SM, M::n + M::m);
   PNState s = W.st[b];
   if (!W.optimal || s.finished || s.error) return;
   const int N = P->N, nb = W.nb;
@@ -855,7 +896,7 @@ template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_pn_ls_begin(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
-  __shared__ PNLds sh;
+  PNLds sh = pn_lds(W.SM, M::n + M::m);
   PNState s = W.st[b];
   if (!W.optimal || s.finished || s.error || s.ls != 1) return;
   const int N = P->N, nb = W.nb;
@@ -865,7 +906,7 @@ __global__ void __launch_bounds__(64) k_pn_ls_begin(const DevProblem* __restrict
   for (int e = lane; e < N * M::n; e += WAVE) w.Xv[e] = X[e];
   for (int e = lane; e < (N - 1) * M::m; e += WAVE) w.Uv[e] = U[e];
   pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
-  pn_active_set(P, Bf, b, w, W.atol, nb, lane);
+  if (pn_active_set(P, Bf, b, w, W.atol, nb, lane)) return pn_stop_over(s, &W.st[b], Bf.st[b], lane);
   pn_gather_y(P, Bf, b, w, nb, lane);
   pn_grad<M>(P, w, X, U, lane);
   pn_form_r<M>(P, Bf, b, w, X, w.nu, w.lc, sh.Yz, nb, lane);
@@ -887,7 +928,7 @@ template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_pn_ls_proj(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
-  __shared__ PNLds sh;
+  PNLds sh = pn_lds(W.SM, M::n + M::m);
   PNState s = W.st[b];
   if (!W.optimal || s.finished || s.error || s.ls != 2) return;
   constexpr int n = M::n, m = M::m;
@@ -896,7 +937,7 @@ __global__ void __launch_bounds__(64) k_pn_ls_proj(const DevProblem* __restrict_
   double* X = Bf.X + (size_t)b * N * n;
   double* U = Bf.U + (size_t)b * (N - 1) * m;
   pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
-  pn_active_set(P, Bf, b, w, W.atol, nb, lane);
+  if (pn_active_set(P, Bf, b, w, W.atol, nb, lane)) return pn_stop_over(s, &W.st[b], Bf.st[b], lane);
   const double viol = pn_gather_y(P, Bf, b, w, nb, lane);
   if (viol < W.eps || s.pcount > 10) {
     if (lane == 0) {
@@ -943,7 +984,7 @@ template <class M, int INTEG>
 __global__ void __launch_bounds__(64) k_pn_ls_end(const DevProblem* __restrict__ P, DevBuffers Bf, PNBuffers W) {
   const long long b = blockIdx.x;
   const int lane = threadIdx.x;
-  __shared__ PNLds sh;
+  PNLds sh = pn_lds(W.SM, M::n + M::m);
   PNState s = W.st[b];
   if (!W.optimal || s.finished || s.error || (s.ls != 3 && s.ls != 4)) return;
   const int N = P->N, nb = W.nb;

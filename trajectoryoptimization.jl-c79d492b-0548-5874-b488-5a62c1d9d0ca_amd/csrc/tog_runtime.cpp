@@ -134,6 +134,9 @@ struct tog_handle {
   double* h_stats = nullptr;
   hipEvent_t stats_ev = nullptr;
   bool stats_pending = false;
+  // tog_history_enable's allocations (DevBuffers::hist_in / hist_out point into them while recording is on)
+  double *hist_in_alloc = nullptr, *hist_out_alloc = nullptr;
+  int hist_cap_alloc = 0, hist_ocap_alloc = 0;
   hipEvent_t sync_ev = nullptr;  // tog_synchronize's watchdog wait
 };
 
@@ -267,18 +270,20 @@ static int build_rows(const tog_problem_desc* d, int slack, int pcap, int has_co
           // m (update_constraint_set_jacobians, constraint_sets.jl:135-150)
           // (trimmed bounds: rows for the finite entries over all m; the infeasible minimum-time problem's
           // combined bound reaches u[1:m+1], mintime_constraints, minimum_time.jl:125-141)
+          // (trim=false: the model's controls and, on a minimum-time problem, the time step h = u[m-1])
           const bool keep = (con.count == 1);
           const int mb = keep ? m - slack - mt : m;
+          auto u_row = [&](int i) { return i < mb || (keep && mt && i == m - 1); };
           for (int i = 0; i < n; i++)
             if (keep || isfinite(D[i])) rows.push_back({ROW_XMAX, i, D[i], 0, 0, 0});
           if (!term)
-            for (int i = 0; i < mb; i++)
-              if (keep || isfinite(D[2 * n + i])) rows.push_back({ROW_UMAX, i, D[2 * n + i], 0, 0, 0});
+            for (int i = 0; i < m; i++)
+              if (u_row(i) && (keep || isfinite(D[2 * n + i]))) rows.push_back({ROW_UMAX, i, D[2 * n + i], 0, 0, 0});
           for (int i = 0; i < n; i++)
             if (keep || isfinite(D[n + i])) rows.push_back({ROW_XMIN, i, D[n + i], 0, 0, 0});
           if (!term)
-            for (int i = 0; i < mb; i++)
-              if (keep || isfinite(D[2 * n + m + i])) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
+            for (int i = 0; i < m; i++)
+              if (u_row(i) && (keep || isfinite(D[2 * n + m + i]))) rows.push_back({ROW_UMIN, i, D[2 * n + m + i], 0, 0, 0});
           break;
         }
         case TOG_CON_GOAL: {  // count: rows x[1:count] - xf (the goal's inds); 0 = n
@@ -344,6 +349,16 @@ static int dalloc(tog_handle* h, T** p, size_t count) {
   h->allocs.push_back(v);
   *p = (T*)v;
   return TOG_OK;
+}
+// release one dalloc'ed buffer before the handle is destroyed (null: nothing)
+static void dfree(tog_handle* h, void* v) {
+  if (!v) return;
+  for (size_t i = 0; i < h->allocs.size(); i++)
+    if (h->allocs[i] == v) {
+      (void)hipFree(v);
+      h->allocs.erase(h->allocs.begin() + (long)i);
+      return;
+    }
 }
 
 // =============================================================================================
@@ -1074,13 +1089,22 @@ int32_t tog_history_enable(tog_handle* h, int32_t capacity) {
     b.hcap = b.ocap = 0;
     return TOG_OK;
   }
-  if (capacity != b.hcap || !b.hist_in) {
+  if (capacity > h->hist_cap_alloc || ocap > h->hist_ocap_alloc || !h->hist_in_alloc) {  // grow (old ones released)
     int rc;
-    if ((rc = dalloc(h, &b.hist_in, (size_t)h->B * 3 * capacity)) || (rc = dalloc(h, &b.hist_out, (size_t)h->B * 4 * ocap)))
+    dfree(h, h->hist_in_alloc);
+    dfree(h, h->hist_out_alloc);
+    h->hist_in_alloc = h->hist_out_alloc = nullptr;
+    h->hist_cap_alloc = h->hist_ocap_alloc = 0;
+    if ((rc = dalloc(h, &h->hist_in_alloc, (size_t)h->B * 3 * capacity)) ||
+        (rc = dalloc(h, &h->hist_out_alloc, (size_t)h->B * 4 * ocap)))
       return rc;
-    b.hcap = capacity;
-    b.ocap = ocap;
+    h->hist_cap_alloc = capacity;
+    h->hist_ocap_alloc = ocap;
   }
+  b.hist_in = h->hist_in_alloc;  // a smaller capacity reuses the allocation (records are strided by hcap)
+  b.hist_out = h->hist_out_alloc;
+  b.hcap = capacity;
+  b.ocap = ocap;
   return TOG_OK;
 }
 
@@ -1424,6 +1448,7 @@ int32_t tog_solve_init(tog_handle* h, int32_t mode) {
   HIPCHECK(hipSetDevice(h->device));
   h->mode = mode;
   h->last_active = -1.0;
+  h->stats_pending = false;  // a check left open by a failed solve is abandoned (its readback is never read)
   h->ops->init(h->dP, h->buf, h->B, h->integ, mode, h->stream);
   HIPCHECK(hipGetLastError());
   return TOG_OK;
@@ -1557,6 +1582,13 @@ int32_t tog_total_steps(tog_handle* h, int64_t* out) {
 // statistics, so the device never idles on the host round trip. The last chunk after the batch finished
 // runs on inactive trajectories only (every kernel returns at once for them); the arithmetic of the
 // solve does not depend on when the host learns the active count (it only picks launch widths).
+// after a failure between tog_batch_stats_begin and _end: no check stays pending on any part, so that the
+// handle's next tog_batch_stats / tog_solve does not fail with "the previous check was not ended"
+static void abandon_stats(tog_handle* h) {
+  h->stats_pending = false;
+  for (tog_handle* p : h->parts) abandon_stats(p);
+}
+
 int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps) {
   int rc = tog_solve_init(h, mode);
   if (rc) return rc;
@@ -1564,10 +1596,10 @@ int32_t tog_solve(tog_handle* h, int32_t mode, int32_t max_steps) {
   const int chunk = 4;
   double stats[3];
   int done = chunk < max_steps ? chunk : max_steps;
-  if ((rc = tog_solve_step(h, done)) || (rc = tog_batch_stats_begin(h))) return rc;
+  if ((rc = tog_solve_step(h, done)) || (rc = tog_batch_stats_begin(h))) return abandon_stats(h), rc;
   while (true) {
     const int next = chunk < max_steps - done ? chunk : max_steps - done;
-    if (next > 0 && (rc = tog_solve_step(h, next))) return rc;
+    if (next > 0 && (rc = tog_solve_step(h, next))) return abandon_stats(h), rc;
     done += next;
     if ((rc = tog_batch_stats_end(h, stats))) return rc;  // the chunk before `next`
     if (stats[0] == 0.0 || next == 0) break;
@@ -1641,13 +1673,15 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
   if (optimal && h->ops->min_time)
     return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal on a minimum-time problem is not built");
   if (opts->n_steps < 0) return fail(TOG_ERR_ARG, "n_steps must be >= 0");
-  if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than n + m = 24 are not built");
-  const int SM = h->n + h->pmax;
-  if (SM > PN_SM_MAX || h->n + h->m > 24)
-    return fail(TOG_ERR_UNSUPPORTED, "projected Newton blocks larger than 32 rows (n + pmax) are not built");
+  if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton needs n + m <= 64 (a lane per variable of a knot)");
+  // block stride: n + every row of a knot, capped at a wave's 64 rows; blocks are sized by the *active* rows
+  // (k_pn_* flag TOG_TRAJ_PN_BLOCK on a trajectory whose active set outgrows the stride)
+  const int SM = std::min(h->n + h->pmax, PN_SM_MAX);
+  if (SM < h->n) return fail(TOG_ERR_UNSUPPORTED, "projected Newton needs n <= 64");
   HIPCHECK(hipSetDevice(h->device));
   PNBuffers& W = h->pn;
   const long long B = h->B;
+  if (h->pn_alloc && W.SM != SM) return fail(TOG_ERR_ARG, "projected Newton workspace stride changed");
   if (!h->pn_alloc) {
     W.SM = SM;
     W.nb = h->N + 1;

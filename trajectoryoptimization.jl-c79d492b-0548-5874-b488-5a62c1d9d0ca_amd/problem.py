@@ -577,11 +577,10 @@ class BoundConstraint(_Constraint):
         return jac[sel]
 
     def to_abi(self, m=None):
-        # an infeasible problem's controls are [u; slack]: the slack entries are unbounded
-        # (trimmed), so the rows are those of the model controls (constraint_sets.jl:135-150)
+        # an infeasible problem's controls are [u; slack]: the bound keeps the model's m
+        # (update_constraint_set_jacobians, constraint_sets.jl:135-150), so the rows are those of the model
+        # controls, trimmed or not (the device's build_rows and the oracle's con_init skip the slack entries)
         pad = np.full(0 if m is None else m - self.m, np.inf)
-        if pad.size and not self.trim:
-            raise NotImplementedError("trim=false bounds on an infeasible-start problem are not built")
         data = np.concatenate([self.x_max, self.x_min, self.u_max, pad, self.u_min, -pad])
         return (abi.CON_BOUND, 0 if self.trim else 1, data)
 

@@ -449,18 +449,42 @@ def maze_altro_options():
     return ALTROSolverOptions(resolve_feasible_problem=False, opts_al=al, R_inf=0.001)
 
 
+def quadrotor_maze_iros_options():
+    """The ALTRO options of the reference's IROS 2019 quadrotor maze demo
+    (examples/IROS_2019/quadrotor_maze.jl:8-34): AL to 1e-4 (projected_newton_tolerance), then projected
+    Newton's feasible projection to 1e-8, R_inf = 1e-8, no resolve. The reference publishes 85.8 s and a final
+    violation of 9.63e-9 for one solve (examples/quadrotor/Quadrotor Maze.ipynb, cell 3)."""
+    il = iLQRSolverOptions(iterations=300)
+    al = AugmentedLagrangianSolverOptions(opts_uncon=il, iterations=40, cost_tolerance=1e-5,
+                                          cost_tolerance_intermediate=1e-4, constraint_tolerance=1e-8,
+                                          penalty_scaling=10.0, penalty_initial=1.0)
+    opts = ALTROSolverOptions(opts_al=al, R_inf=1e-8, resolve_feasible_problem=False,
+                              projected_newton=True, projected_newton_tolerance=1e-4)
+    opts.opts_pn.feasibility_tolerance = 1e-8
+    opts.opts_pn.solve_type = "feasible"
+    return opts
+
+
+def quadrotor_maze_batch(B, offset=0, jitter=0.5):
+    """B copies of ``quadrotor_maze()`` whose state guesses are the five interior way-points of
+    problems/quadrotor_maze.jl:104-113 jittered by N(0, jitter^2) per coordinate (seed 5000+offset+b; jitter 0
+    gives the reference's own guess), hover controls."""
+    p0 = quadrotor_maze()
+    N = p0.N
+    Xs = _per_traj_rng(5000 + offset, B, lambda r: _maze_guess(
+        N, 5.0, p0.x0[0], p0.xf, _MAZE_WAYPOINTS + jitter * r.standard_normal(_MAZE_WAYPOINTS.shape)).ravel())
+    p0b = Problem(p0.model, p0.obj, np.broadcast_to(p0.U, (B, N - 1, 4)).copy(), constraints=p0.constraints,
+                  x0=np.tile(p0.x0[0], (B, 1)), xf=p0.xf, N=N, dt=p0.dt)
+    p0b.X = Xs.reshape(B, N, 13)
+    return p0b
+
+
 def config_quadrotor_maze_infeasible(B=1024, offset=0):
     """The quadrotor_maze infeasible-start AL phase (ALTRO with a state guess) as a batch: the five
     interior way-points of problems/quadrotor_maze.jl jittered by N(0, 0.5^2) per coordinate (seed
     5000+b), hover controls; returns the *infeasible* problem (slack controls still to be filled
     by ``slack_controls``) and the ALTRO options."""
-    p0 = quadrotor_maze()
-    N = p0.N
-    Xs = _per_traj_rng(5000 + offset, B, lambda r: _maze_guess(
-        N, 5.0, p0.x0[0], p0.xf, _MAZE_WAYPOINTS + 0.5 * r.standard_normal(_MAZE_WAYPOINTS.shape)).ravel())
-    p0b = Problem(p0.model, p0.obj, np.broadcast_to(p0.U, (B, N - 1, 4)).copy(), constraints=p0.constraints,
-                  x0=np.tile(p0.x0[0], (B, 1)), xf=p0.xf, N=N, dt=p0.dt)
-    p0b.X = Xs.reshape(B, N, 13)
+    p0b = quadrotor_maze_batch(B, offset)
     opts = maze_altro_options()
     return infeasible_problem(p0b, opts.R_inf), opts
 

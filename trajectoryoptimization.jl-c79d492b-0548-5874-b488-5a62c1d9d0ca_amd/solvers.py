@@ -404,10 +404,31 @@ def _solve_pn(prob, solver: ProjectedNewtonSolver):
     flags = h.status()
     solver.stats = _pn_stats(out, flags)
     solver.pn_history = h.pn_history(solver.opts.n_steps)
-    if np.any(flags & abi.TRAJ_PN_ERROR):
-        raise RuntimeError("projected Newton: line search did not reduce the violation "
-                           "(the reference's _projection_linesearch! raises here)")
+    _raise_pn_errors(flags, solver)
     return solver
+
+
+class ProjectedNewtonError(RuntimeError):
+    """The reference's exception in ``_projection_linesearch!`` (``count += a``, a MethodError, when the first
+    trial does not reduce the violation; projected_newton.jl:273-277), raised after the batch.
+    ``trajectories`` lists the flagged ones (TRAJ_PN_ERROR; they keep their last accepted iterate) and
+    ``solver`` is the finished solve (its statistics and the other trajectories' results stand)."""
+
+    def __init__(self, msg, trajectories, solver):
+        super().__init__(msg)
+        self.trajectories = list(trajectories)
+        self.solver = solver
+
+
+def _raise_pn_errors(flags, solver):
+    flags = np.asarray(flags)
+    if np.any(flags & abi.TRAJ_PN_BLOCK):
+        raise ProjectedNewtonError("projected Newton: a block of n + active rows exceeded the device's 64 rows "
+                                   "(TOG_TRAJ_PN_BLOCK)", np.flatnonzero(flags & abi.TRAJ_PN_BLOCK), solver)
+    if np.any(flags & abi.TRAJ_PN_ERROR):
+        bad = np.flatnonzero(flags & abi.TRAJ_PN_ERROR)
+        raise ProjectedNewtonError("projected Newton: line search did not reduce the violation for trajectories "
+                                   f"{bad.tolist()} (the reference's _projection_linesearch! raises here)", bad, solver)
 
 
 def AbstractSolverFor(prob, opts, **kw):
@@ -415,7 +436,6 @@ def AbstractSolverFor(prob, opts, **kw):
     if isinstance(opts, iLQRSolverOptions):
         return iLQRSolver(prob, opts, **kw)
     if isinstance(opts, ALTROSolverOptions):
-        _altro_check(prob, opts)
         _altro_pn_tolerances(opts)
         return ALTROSolver(prob, opts, **kw)
     if isinstance(opts, ProjectedNewtonSolverOptions):
@@ -423,12 +443,6 @@ def AbstractSolverFor(prob, opts, **kw):
     if isinstance(opts, AugmentedLagrangianSolverOptions):
         return AugmentedLagrangianSolver(prob, opts, **kw)
     raise ValueError("Can't create an Abstract Solver without knowing the type of the Solver Options")
-
-
-def _altro_check(prob, opts):
-    # projected Newton on the infeasible-start and minimum-time problems: the device builds it for models whose
-    # [x; u] has n + m <= 24 (tog_solve_pn refuses larger blocks with TOG_ERR_UNSUPPORTED)
-    return None
 
 
 def _altro_pn_tolerances(opts):
@@ -538,9 +552,7 @@ def _solve_altro(prob, opts: ALTROSolverOptions, device: int, max_steps=None, hi
     _raise_trajectory_errors(flags)
     if opts.projected_newton:
         solver.stats_pn = pnv.stats
-        if np.any(solver.stats["flags"] & abi.TRAJ_PN_ERROR):
-            raise RuntimeError("projected Newton: line search did not reduce the violation "
-                               "(the reference's _projection_linesearch! raises here)")
+        _raise_pn_errors(solver.stats["flags"], solver)
     return solver
 
 
@@ -561,7 +573,6 @@ def solve_b(prob, solver_or_opts, *, max_steps: int | None = None, device: int =
         if isinstance(opts, ProjectedNewtonSolverOptions):
             return _solve_pn(prob, ProjectedNewtonSolver(prob, opts, device=device))
         if isinstance(opts, ALTROSolverOptions):
-            _altro_check(prob, opts)
             _altro_pn_tolerances(opts)  # (mutates opts.opts_al, as the reference does)
             return _solve_altro(prob, opts, device, max_steps=max_steps, history=history)
         if isinstance(opts, AugmentedLagrangianSolverOptions) and not prob.is_constrained():
