@@ -36,6 +36,10 @@ WORKLOADS = {
     "quadrotor": ("config_quadrotor", 8192, True,
                   "quadrotor point-to-point, AL-iLQR, u in [0,15] + goal, sqrt backward pass (BASELINE.json configs[2])",
                   "synthetic (seeded random starts: x0[1:3]+N(0,1), U0 = hover + 0.1 N(0,1))"),
+    "quadrotor_tv": ("config_quadrotor_tv", 8192, True,
+                     "config 3 with a time-varying Objective: 100 stage costs LQRCost(Q w_k, R v_k) + terminal "
+                     "(per-knot cost table; the team backward's TV variant)",
+                     "synthetic (config 3's seeded starts)"),
     "cartpole": ("config_cartpole", 1024, False,
                  "cartpole swing-up, unconstrained iLQR (BASELINE.json configs[1])",
                  "synthetic (seeded U0 = 0.01 + 0.5 N(0,1), x0 = 0)"),
@@ -134,6 +138,27 @@ def measured_traffic(kernel, workload="quadrotor"):
     if not per:
         return None, f"{os.path.relpath(f, ROOT)} has no {kernel} entry"
     return round(per["traffic_bytes"]), os.path.relpath(f, ROOT)
+
+
+def measured_mfma(workload):
+    """The matrix-core utilisation of this build's MFMA kernels from a committed PMC summary
+    (profiles/*_<workload>_mfma.json, tools/mfma_prof.sh + tools/mfma_summary.py), or None."""
+    import glob
+
+    sha = lib_sha16()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_mfma.json")), reverse=True):
+        with open(f) as fh:
+            t = json.load(fh)
+        if sha is not None and t.get("libtog_sha16") == sha:
+            out = {"source": os.path.relpath(f, ROOT) + " (committed rocprofv3 passes of this build)",
+                   **t["per_kernel"]}
+            if "tog::k_kuka_chain<tog::Kuka>" in out or any("k_kuka_chain" in k for k in out):
+                # kj_chain_product (csrc/tog_kuka_jac.hpp): J (7 x 14) times T (14 x 21) as two 16x16 output
+                # tiles of v_mfma_f64_16x16x4_f64, 4 k-steps each: 7 of 16 rows, 21 of 32 columns, 14 of 16 k
+                out["tile_occupancy"] = {"output_rows": "7/16", "output_cols": "21/32", "k": "14/16",
+                                         "useful_mac_fraction": round(7 * 21 * 14 / (2 * 16 * 16 * 16), 4)}
+            return out
+    return None
 
 
 def host_cpu_info():
@@ -422,6 +447,7 @@ def main():
                 "max": round(float(np.max([x["value"] for x in solve_sets])), 2),
                 "note": "the whole solve on disjoint start sets of the same size; value is the first set's (offset 0)"}),
             "roofline": roofline,
+            "mfma": (measured_mfma(args.workload) if args.workload == "kuka" else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

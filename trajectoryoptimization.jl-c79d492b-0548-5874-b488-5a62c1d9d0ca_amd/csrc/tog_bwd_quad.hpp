@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
   using Cfg = TeamCfg<M>;
   using D = QuadLayout<M>;
-  constexpr bool SQRT = true, AL = ALI != 0;
+  constexpr bool SQRT = true, AL = (ALI & 1) != 0, TV = (ALI & 2) != 0;  // TV: a time-varying Objective
   constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, NQ = nq_of<M>(), NE = ne_of<M>();
   static_assert(TEAM == 16 && m <= n && n + 1 <= 16, "quad kernel: 16-lane DPP rows");
   __shared__ double lds[D::TOTAL];
@@ -169,9 +169,10 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
       const double* ek = Eg + (size_t)kk * NE;
 #pragma unroll
       for (int i = 0; i < n; i++) Qx[i] = ek[n + m + m * m + i + n * c];
-    } else {  // (the shared cost: a time-varying Objective takes the LDS kernel)
+    } else {  // the stage cost's square-root factor (a time-varying Objective's knot kk)
+      const double* cQ = TV ? cost_at<n, m>(P, kk).cQ : P->cQ;
 #pragma unroll
-      for (int i = 0; i < n; i++) Qx[i] = P->cQ[i + n * c];
+      for (int i = 0; i < n; i++) Qx[i] = cQ[i + n * c];
     }
   };
   // wave B: knot kk's Q.x entry, Q.u and Q.uu column (the replayed ones in faithful mode), a knot ahead
@@ -525,8 +526,14 @@ k_bwd_quad(const DevProblem* P, DevBuffers Bf, int flags) {
       } else if (wv == 2) {
         // ---------------------------------------------------------------- C: Q.ux, tmp1
         double Quxc[m];
+        if constexpr (TV) {  // knot k's H dt
+          const double* Hk = cost_at<n, m>(P, k).H;
 #pragma unroll
-        for (int i = 0; i < m; i++) Quxc[i] = replay ? Cqr[i] : Hdt[i];  // sqrt AL adds no Q.ux term (A.5)
+          for (int i = 0; i < m; i++) Quxc[i] = replay ? Cqr[i] : Hk[i + m * c] * dt;
+        } else {
+#pragma unroll
+          for (int i = 0; i < m; i++) Quxc[i] = replay ? Cqr[i] : Hdt[i];  // sqrt AL adds no Q.ux term (A.5)
+        }
         // Q.ux += tmp_u' tmp_x (backward_pass.jl:118), the sum wave B formed from S_{k+1}'s rows
 #pragma unroll
         for (int i = 0; i < m; i++) Quxc[i] += QXT[i + m * c];

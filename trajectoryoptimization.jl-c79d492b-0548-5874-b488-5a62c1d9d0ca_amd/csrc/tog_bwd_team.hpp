@@ -893,7 +893,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // (P is deliberately not __restrict__: that would let LICM hoist ~100 loop-invariant problem
   // constants out of the knot loop and keep them in registers for the whole kernel)
   using Cfg = TeamCfg<M>;
-  constexpr bool SQRT = SQRTI != 0, AL = ALI != 0;
+  // ALI: bit 0 the AL expansion, bit 1 a time-varying Objective (TV: knot k's cost through cost_at, a table
+  // every trajectory shares, so it stays in L2; a variant of its own so that the shared-cost kernels keep
+  // their schedule)
+  constexpr bool SQRT = SQRTI != 0, AL = (ALI & 1) != 0, TV = (ALI & 2) != 0;
   constexpr int n = M::n, m = M::m, L = n + m, TEAM = Cfg::TEAM, NQ = nq_of<M>(), NE = ne_of<M>();
   static_assert(m <= n && n + 1 <= TEAM, "team layout");
   extern __shared__ double team_lds[];
@@ -953,9 +956,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   int pk = -1;  // knot whose inputs the p* registers hold
   BPROF_DECL
 
-  // (the team kernels run the shared stage cost only: a time-varying Objective takes the LDS kernel. Every
-  // alternative form of this lambda measured -- a branch on the per-knot table, strided cost pointers, packed
-  // Q.xx records read back here -- made the std AL backward 20-30 % slower on config 4, profiles/r5s_*)
+  // (the shared-cost variants read P's cost: every alternative form of this lambda measured -- a branch on the
+  // per-knot table, strided cost pointers, packed Q.xx records read back here -- made the std AL backward
+  // 20-30 % slower on config 4, profiles/r5s_*; so the per-knot cost is a template variant, TV)
   // Q blocks of knot k (terminal when TERM) from its expansion record (k_expand_team, ne_of):
   // this lane's columns of Q.xx, Q.uu, Q.ux, its Q.x entry and the whole Q.u
   auto expand = [&](const int k, auto term_c, double& Qxs, double(&Qu)[m], double(&Qxc)[n], double(&Quuc)[m],
@@ -969,6 +972,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     if (knot_dense<SQRT, AL>(k, N, cnt, AL ? knx[k] : 0)) {
 #pragma unroll
       for (int i = 0; i < n; i++) Qxc[i] = e[n + m + m * m + i + n * c];
+    } else if constexpr (TV) {
+      const CostView C_ = cost_at<n, m>(P, k);
+#pragma unroll
+      for (int i = 0; i < n; i++) Qxc[i] = SQRT ? C_.cQ[i + n * c] : C_.Q[i + n * c] * dt;
     } else {
 #pragma unroll
       for (int i = 0; i < n; i++) Qxc[i] = SQRT ? P->cQ[i + n * c] : P->Q[i + n * c] * dt;
@@ -979,9 +986,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int i = 0; i < m; i++) Quuc[i] = e[n + m + i + m * cu];
       const bool zterm = !SQRT && AL && cnt > 0;  // the std AL expansion's "+= cu'Iμcx" (an exact zero)
+      const double* Hk = TV ? cost_at<n, m>(P, k).H : P->H;
 #pragma unroll
       for (int i = 0; i < m; i++) {
-        const double h = P->H[i + m * c] * dt;
+        const double h = Hk[i + m * c] * dt;
         Quxc[i] = zterm ? h + 0.0 : h;
       }
     } else {

@@ -184,6 +184,7 @@ struct DevBuffers {
   int spec_tail_shmem; // LDS bytes of k_ls_spec_tail's chunk image (0: the tail uses k_ls_spec)
   int spec_tail2_shmem; // LDS bytes of k_ls_spec_tail2 (two staging images + the ring; 0: not admissible)
   int cost_diag;       // DevProblem::diag_cost (host copy: kernel variants that inline the diagonal cost)
+  int tv;              // a time-varying Objective (DevProblem::kc): the team backward kernels' per-knot-cost variants
   int rows_lds;        // LDS bytes of a block's copy of the row tables (bulk k_ls_spec; 0: global tables)
   int ls_first;       // width of the first speculative round (>= nc: one round)
   int nknots;         // N (host-side launch geometry)

@@ -3494,14 +3494,25 @@ struct ModelLaunch {
       Bl.bwd_stride = Bf.bwd_stride2[sq ? 1 : 0];
       Bl.bwd_shmem = Bf.bwd_shmem2[sq ? 1 : 0];
       const unsigned sm = (unsigned)Bl.bwd_shmem;
+      // (ALI bit 1: the time-varying-Objective variants, Bf.tv)
       auto launch = [&](auto wpe_c) {
         constexpr int W = decltype(wpe_c)::value;
         if (sq) {
-          if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1, W>), g, blk, sm, st, P, Bl, flags);
-          else hipLaunchKernelGGL((k_bwd_team<M, 1, 0, W>), g, blk, sm, st, P, Bl, flags);
+          if (Bf.tv) {
+            if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 3, W>), g, blk, sm, st, P, Bl, flags);
+            else hipLaunchKernelGGL((k_bwd_team<M, 1, 2, W>), g, blk, sm, st, P, Bl, flags);
+          } else {
+            if (al) hipLaunchKernelGGL((k_bwd_team<M, 1, 1, W>), g, blk, sm, st, P, Bl, flags);
+            else hipLaunchKernelGGL((k_bwd_team<M, 1, 0, W>), g, blk, sm, st, P, Bl, flags);
+          }
         } else {
-          if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1, W>), g, blk, sm, st, P, Bl, flags);
-          else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
+          if (Bf.tv) {
+            if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 3, W>), g, blk, sm, st, P, Bl, flags);
+            else hipLaunchKernelGGL((k_bwd_team<M, 0, 2, W>), g, blk, sm, st, P, Bl, flags);
+          } else {
+            if (al) hipLaunchKernelGGL((k_bwd_team<M, 0, 1, W>), g, blk, sm, st, P, Bl, flags);
+            else hipLaunchKernelGGL((k_bwd_team<M, 0, 0, W>), g, blk, sm, st, P, Bl, flags);
+          }
         }
       };
       // TOG_BWD_TAIL: "quad" (default) or "team" (the one-wave team kernel), for A/B checks (read per
@@ -3513,8 +3524,13 @@ struct ModelLaunch {
         // and the downdate on four waves (tog_bwd_quad.hpp)
         if constexpr (TeamCfg<M>::TEAM == 16) {
           const dim3 gd((unsigned)B);
-          if (al) hipLaunchKernelGGL((k_bwd_quad<M, 1>), gd, dim3(256), 0, st, P, Bf, flags);
-          else hipLaunchKernelGGL((k_bwd_quad<M, 0>), gd, dim3(256), 0, st, P, Bf, flags);
+          if (Bf.tv) {
+            if (al) hipLaunchKernelGGL((k_bwd_quad<M, 3>), gd, dim3(256), 0, st, P, Bf, flags);
+            else hipLaunchKernelGGL((k_bwd_quad<M, 2>), gd, dim3(256), 0, st, P, Bf, flags);
+          } else {
+            if (al) hipLaunchKernelGGL((k_bwd_quad<M, 1>), gd, dim3(256), 0, st, P, Bf, flags);
+            else hipLaunchKernelGGL((k_bwd_quad<M, 0>), gd, dim3(256), 0, st, P, Bf, flags);
+          }
         }
       } else if (Bf.tail) {
         launch(std::integral_constant<int, 1>{});

@@ -856,9 +856,8 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
     // TOG_BWD=lds forces the one-wave-per-trajectory LDS backward kernel (A/B checks)
     const char* ev = getenv("TOG_BWD");
     const bool force_lds = ev && strcmp(ev, "lds") == 0;
-    // (a time-varying Objective takes the LDS kernel too: the team kernels run the shared stage cost on
-    // their serial chain, where every per-knot cost read measured 20-30 % slower)
-    h->bwd_team = (!force_lds && !ops->min_time && !d->stage_costs &&
+    // (a time-varying Objective runs the team kernels' TV variants, which read knot k's cost from the table)
+    h->bwd_team = (!force_lds && !ops->min_time &&
                    team_rows_fit(off.data(), cnt.data(), rows.data(), N, n, m, (int)rows.size()))
                       ? 1 : 0;
     for (int sq = 0; sq < 2; sq++) {
@@ -887,6 +886,7 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   HIPCHECK(hipMemcpy(h->dP, &P, sizeof(P), hipMemcpyHostToDevice));
 
   DevBuffers& b = h->buf;
+  b.tv = d->stage_costs ? 1 : 0;
   b.dense_stage_knots = 0;  // a stage knot with a state row (its square-root expansion changes Q.xx)
   for (int k = 0; k + 1 < N; k++)
     if (nxk[k] > 0) b.dense_stage_knots = 1;

@@ -7,8 +7,8 @@ import math
 
 import numpy as np
 
-from .problem import (BoundConstraint, CircleConstraints, Constraints, Dynamics, LQRObjective, Problem,
-                      discretize_model, infeasible_problem,
+from .problem import (BoundConstraint, CircleConstraints, Constraints, Dynamics, LQRCost, LQRCostTerminal,
+                      LQRObjective, Objective, Problem, discretize_model, infeasible_problem,
                       SphereConstraints, goal_constraint, rk3, rk4)
 from .solvers import ALTROSolverOptions, AugmentedLagrangianSolverOptions, iLQRSolverOptions
 
@@ -316,6 +316,24 @@ def config_quadrotor(B=8192, offset=0):
     opts_al = AugmentedLagrangianSolverOptions(opts_uncon=opts_ilqr, constraint_tolerance=1e-3,
                                                cost_tolerance=1e-5, cost_tolerance_intermediate=1e-4)
     return prob, opts_al
+
+
+def config_quadrotor_tv(B=8192, offset=0):
+    """Config 3 with a time-varying Objective (src/objective.jl:15-29): knot k's stage cost is
+    LQRCost(Q w_k, R v_k, xf), w_k rising 0.5 -> 2.0 and v_k falling 2.0 -> 1.0 along the horizon (100 stage
+    costs and the terminal one); the starts and options are config 3's. The bench's per-knot-cost line."""
+    prob, opts = config_quadrotor(B=B, offset=offset)
+    st, term = prob.obj.stage, prob.obj.terminal
+    N = prob.N
+    costs = []
+    for k in range(N - 1):
+        w = 0.5 + 1.5 * k / (N - 2)
+        v = 2.0 - 1.0 * k / (N - 2)
+        costs.append(LQRCost(w * st.Q, v * st.R, prob.xf))
+    obj = Objective(costs + [LQRCostTerminal(term.Q, prob.xf)])
+    p = Problem(prob.model, obj, prob._U.copy(), constraints=prob.constraints, x0=prob.x0.copy(), xf=prob.xf,
+                N=N, dt=prob.dt)
+    return p, opts
 
 
 def config_quad_maze(B=8192, offset=0, N=201):
