@@ -226,7 +226,7 @@ class OracleSolver:
         out = np.zeros(abi.PN_NSTATS)
         rc = self.L.oc_solve_pn(self.s, C.byref(_pkg.to_tog_pn_options(pn_opts)), _dp(out))
         if rc != 0:
-            raise NotImplementedError("projected Newton solve_type :optimal on a minimum-time problem is not built")
+            raise ValueError(f"oc_solve_pn: unknown solve_type ({rc})")
         return out
 
     def history(self):

@@ -492,6 +492,8 @@ static double pn_update(oc_solver* s, pn_ws* ws, double atol) {
   return pn_gather_y(s, ws);
 }
 
+static void pn_weights_min_time(const oc_solver* s, pn_ws* ws);
+
 /* line_search (:463-496) from solver.V (s->X, s->U, ws->nu, ws->lc) along (δz, δλ); leaves the returned
    V_ (or solver.V) in s->X, s->U and solver.V in ws->Xv, ws->Uv. A trial whose Y H⁻¹ Yᵀ or Y Yᵀ does not
    factor (a KKT step so long that the active rows outnumber the free variables: the reference's sparse
@@ -502,6 +504,9 @@ static void pn_line_search(oc_solver* s, pn_ws* ws, double atol, double eps) {
   memcpy(ws->Xv, s->X, sizeof(double) * nx);
   memcpy(ws->Uv, s->U, sizeof(double) * nu_);
   pn_update(s, ws, atol);
+  /* update!'s cost_expansion! at solver.V: a minimum-time problem's H (MinTimeCost's hessian!) moves with V, and
+     projection! of the first trial uses it (H = Diagonal(solver.H), :328-333) */
+  if (s->mt) pn_weights_min_time(s, ws);
   pn_grad(s, ws, s->X, s->U);
   pn_form_r(s, ws, s->X, s->U, ws->nu, ws->lc);
   const double res0 = pn_res_norm(s, ws);
@@ -533,6 +538,7 @@ static void pn_line_search(oc_solver* s, pn_ws* ws, double atol, double eps) {
         }
     }
     pn_grad(s, ws, s->X, s->U);
+    if (s->mt) pn_weights_min_time(s, ws); /* cost_expansion!(prob, solver, V_): the next trial's projection! H */
     int fail = 0;
     double res = pn_multiplier_projection(s, ws, s->X, s->U, ws->nut, ws->lct, &fail);
     if (!fail && res < (1.0 - alpha * 0.01) * res0) return;
@@ -571,11 +577,14 @@ static void pn_weights_min_time(const oc_solver* s, pn_ws* ws) {
   ws->wx[(size_t)(N - 1) * n + n - 1] = 1.0 / s->R_mt;
 }
 
-/* solve!(prob, ProjectedNewtonSolver) (projected_newton.jl:6-20); out: TOG_PN_NSTATS doubles.
-   Returns 0, or -4 for solve_type :optimal on a minimum-time problem (not built: its H moves with V). */
+/* solve!(prob, ProjectedNewtonSolver) (projected_newton.jl:6-20); out: TOG_PN_NSTATS doubles. Returns 0, or
+   -4 for an unknown solve_type. A minimum-time problem's H (MinTimeCost's hessian!, its diagonal) is formed at
+   each newton step's V (update!) and, under :optimal, again wherever the reference calls cost_expansion!: at
+   solver.V when the line search starts and at each projected trial V_ (pn_line_search); solveKKT_Shur keeps the
+   newton step's Hinv (:501-547). */
 OC_EXPORT int oc_solve_pn(oc_solver* s, const tog_pn_options* o, double* out) {
   const int optimal = o->solve_type == 1;
-  if (o->solve_type != 0 && !(optimal && !s->mt)) return -4;
+  if (o->solve_type != 0 && !optimal) return -4;
   int n = s->n, m = s->m, N = s->N, P = s->pmax > 0 ? s->pmax : 1;
   pn_ws W, *ws = &W;
   memset(ws, 0, sizeof(W));

@@ -255,24 +255,31 @@ def test_oracle_min_time_projected_newton(tog, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("infeasible", [False, True])
-def test_gpu_min_time_projected_newton(tog, oracle, gpu, infeasible):
+@pytest.mark.parametrize("infeasible,solve_type", [(False, "feasible"), (True, "feasible"), (False, "optimal"),
+                                                   (True, "optimal")])
+def test_gpu_min_time_projected_newton(tog, oracle, gpu, infeasible, solve_type):
     """solve_b with tf = :min and projected_newton (and an initial state trajectory): the device's projected
-    Newton on MinTime<Pendulum> / MinTime<Infeasible<Pendulum>> (per-knot H from the newton step's X, U)
-    against the oracle's same flow: X, U, h within 1e-6, as the minimum-time AL phase before it."""
+    Newton on MinTime<Pendulum> / MinTime<Infeasible<Pendulum>> (per-knot H from X, U: at the newton step's
+    point, and under :optimal again at the line search's start and at each projected trial) against the
+    oracle's same flow: X, U, h within 1e-6, as the minimum-time AL phase before it."""
     if infeasible:
         p, opts, _ = _inf_mt_case(tog, resolve=False)
     else:
         make, opts, xf, U0, dt, dt_mt, _ = pendulum_case(tog)
         p = make(U0, dt_mt, tf="min")
     opts = _pn_mt_opts(opts)
+    opts.opts_pn.solve_type = solve_type
     ref = p.copy()
-    solver = tog.solve_b(p, opts)
+    try:
+        solver, raised = tog.solve_b(p, opts), False
+    except tog.ProjectedNewtonError as e:  # the reference raises in _projection_linesearch! for this start
+        solver, raised = e.solver, True
     assert solver.stats["time_pn"] > 0.0
     if infeasible:
         Xo, Uo, ho, si, _ = oracle.solve_altro_infeasible_min_time(ref, opts, 0)
     else:
         Xo, Uo, ho, si = oracle.solve_altro_min_time(ref, opts, 0)
+    assert raised == bool(int(si.get("stats")[tog.abi.STAT_FLAGS]) & tog.abi.TRAJ_PN_ERROR)
     tol = 1e-6
     scale = lambda a: max(1.0, float(np.max(np.abs(a))))  # noqa: E731
     assert np.max(np.abs(p._X[0] - Xo)) <= tol * scale(Xo)
@@ -338,3 +345,69 @@ def test_gpu_untrimmed_min_time_bound_rows(tog, oracle, gpu):
     assert int(s.stats["iterations_total"][0]) == steps
     scale = max(1.0, float(np.max(np.abs(o2.get("X")))))
     assert np.max(np.abs(gp._X[0] - o2.get("X"))) <= 1e-6 * scale
+
+
+def _inf_mt_model_case(tog, name):
+    """minimum_time_problem(infeasible_problem(prob)) for the quadrotor and the Kuka arm (round 6; the state guess
+    a straight line x0 -> xf, short horizons): MinTime<Infeasible<M>> on the LDS backward kernel."""
+    if name == "quadrotor":
+        n, m, N = 13, 4, 21
+        q0 = np.array([1.0, 0.0, 0.0, 0.0])
+        x0, xf = np.zeros(n), np.zeros(n)
+        x0[3:7] = q0
+        xf[0:3] = [0.0, 4.0, 0.0]
+        xf[3:7] = q0
+        obj = tog.LQRObjective(1e-2 * np.eye(n), 1e-2 * np.eye(m), 100.0 * np.eye(n), xf, N)
+        cons = tog.Constraints(N)
+        bnd = tog.BoundConstraint(n, m, u_min=0.0, u_max=15.0)
+        for k in range(N - 1):
+            cons[k] += bnd
+        cons[N - 1] += tog.goal_constraint(xf)
+        U0 = tog.Problems.HOVER * np.ones((N - 1, m))
+        p = tog.Problem(tog.rk4(tog.Dynamics.quadrotor), obj, U0, constraints=cons, x0=x0, xf=xf, N=N, dt=0.1,
+                        tf="min")
+        dt_max = 0.15
+    else:
+        n, m, N = 14, 7, 11
+        base = tog.Problems.kuka(N=N, tf=0.5)
+        cons = tog.Constraints(N)
+        bnd = tog.BoundConstraint(n, m, u_min=-80.0, u_max=80.0)
+        for k in range(N - 1):
+            cons[k] += bnd
+        cons[N - 1] += tog.goal_constraint(base.xf)
+        x0, xf = base.x0[0], base.xf
+        p = tog.Problem(base.model, base.obj, base._U[0], constraints=cons, x0=x0, xf=xf, N=N, dt=base.dt, tf="min")
+        dt_max = 0.1
+    p.X = np.stack([x0 + (xf - x0) * k / (N - 1) for k in range(N)])
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(iterations=40), iterations=4,
+                                              penalty_scaling=10.0)
+    opts = tog.ALTROSolverOptions(opts_al=al, R_minimum_time=1.0, dt_max=dt_max, dt_min=1e-3, R_inf=1.0,
+                                  resolve_feasible_problem=False)
+    return p, opts
+
+
+@pytest.mark.parametrize("name", ["quadrotor", "kuka"])
+def test_oracle_infeasible_min_time_models(tog, oracle, name):
+    """The oracle's infeasible minimum-time flow runs for the quadrotor and the Kuka arm (finite iterates) with
+    the composite model's shapes. (h may go negative: mintime_constraints' quirk leaves it unbounded, dt = h².)"""
+    p, opts = _inf_mt_model_case(tog, name)
+    X, U, h, si, _ = oracle.solve_altro_infeasible_min_time(p, opts, 0)
+    n, m = p.model.n, p.model.m
+    assert X.shape == (p.N, n) and U.shape == (p.N - 1, m) and si.m == m + n + 1
+    assert np.all(np.isfinite(X)) and np.all(np.isfinite(U)) and np.all(np.isfinite(h))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["quadrotor", "kuka"])
+def test_gpu_infeasible_min_time_models(tog, oracle, gpu, name):
+    """MinTime<Infeasible<Quadrotor>> and MinTime<Infeasible<Kuka>> (round 6) on the device against the
+    oracle's flow: X, U, h within 1e-6 and equal AL iteration counts."""
+    p, opts = _inf_mt_model_case(tog, name)
+    ref = p.copy()
+    solver = tog.solve_b(p, opts)
+    Xo, Uo, ho, si, _ = oracle.solve_altro_infeasible_min_time(ref, opts, 0)
+    scale = lambda a: max(1.0, float(np.max(np.abs(a))))  # noqa: E731
+    assert np.max(np.abs(p._X[0] - Xo)) <= 1e-6 * scale(Xo)
+    assert np.max(np.abs(p._U[0] - Uo)) <= 1e-6 * scale(Uo)
+    assert np.max(np.abs(p.h[0] - ho)) <= 1e-6
+    assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])

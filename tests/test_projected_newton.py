@@ -164,16 +164,29 @@ def test_oracle_optimal_steps_restart_from_solver_v(tog, oracle):
         assert np.array_equal(one[0].get("U"), three[0].get("U"))
 
 
-def test_oracle_optimal_refused_on_min_time(tog, oracle):
-    """The minimum-time problem's H moves with V inside the line search: :optimal there is not built, on the
-    oracle as on the device (TOG_ERR_UNSUPPORTED)."""
+def test_oracle_optimal_on_min_time(tog, oracle):
+    """solve_type :optimal on a minimum-time problem (round 6): the minimum-time problem's H (MinTimeCost's
+    hessian! diagonal) and g (its gradient!) move with V, so they are re-formed wherever newton_step! and
+    line_search call cost_expansion! (projected_newton.jl:463-547). The step reaches the feasibility tolerance
+    and costs no more than the :feasible projection of the same AL iterate, or is flagged as the reference
+    would raise."""
     import test_minimum_time as T
     make, opts, xf, U0, dt, dt_mt, _ = T.pendulum_case(tog)
     p = make(U0, dt_mt, tf="min")
     pmt = tog.minimum_time_problem(p, opts.R_minimum_time, opts.dt_max, opts.dt_min)
-    o = oracle.OracleSolver(pmt, opts.opts_al)
-    with pytest.raises(NotImplementedError):
-        o.solve_pn(tog.ProjectedNewtonSolverOptions(solve_type="optimal"))
+    al = opts.opts_al
+    al.constraint_tolerance = 1e-3
+    res = {}
+    for st in ("feasible", "optimal"):
+        o = oracle.OracleSolver(pmt, al)
+        o.solve()
+        out = o.solve_pn(tog.ProjectedNewtonSolverOptions(feasibility_tolerance=1e-8, n_steps=2, solve_type=st))
+        res[st] = (o, out, int(o.get("stats")[tog.abi.STAT_FLAGS]))
+    (of, outf, ff), (oo, outo, fo) = res["feasible"], res["optimal"]
+    assert np.isfinite(oo.get("X")).all() and np.isfinite(oo.get("U")).all()
+    if not fo & tog.abi.TRAJ_PN_ERROR:
+        assert outo[tog.abi.PN_C_MAX] <= 1e-8
+        assert outo[tog.abi.PN_J] <= outf[tog.abi.PN_J] * (1 + 1e-9)
 
 
 def test_car_batch_problem(tog, oracle):

@@ -206,3 +206,44 @@ def test_user_pendulum_min_time_equals_builtin(tog, gpu):
     for key in ("iterations_total", "flags", "cost", "c_max"):
         assert np.array_equal(su.stats[key], sb.stats[key]), key
     assert 0.0 < tog.total_time(pu) < math.inf
+
+
+@pytest.mark.gpu
+def test_user_constraint_min_time_equals_builtin_and_oracle(tog, oracle, gpu):
+    """Minimum time with user constraint rows (round 6; mintime_constraints keeps every constraint over the base
+    model's x, u, minimum_time.jl:125-141): tf = :min on the user pendulum with its circle as a user function
+    (MinTime<M>::con) equals the built-in pendulum with CircleConstraints bit for bit, and that one equals the
+    oracle's minimum-time flow within 1e-6."""
+    import math
+
+    user = tog.Model.from_plugin(PLUG / "user_pendulum.so")
+    n, m, N = 2, 1, 31
+    Q, R = 1e-3 * np.eye(n), 1e-3 * np.eye(m)
+    xf, x0 = np.array([math.pi, 0.0]), np.zeros(n)
+
+    def make(model, con):
+        cons = tog.Constraints(N)
+        bnd = tog.BoundConstraint(n, m, u_min=-5.0, u_max=5.0)
+        for k in range(N - 1):
+            cons[k] += bnd
+            cons[k] += con
+        cons[N - 1] += tog.goal_constraint(xf)
+        U0 = np.ones((N - 1, m)) + 0.1 * np.sin(np.arange(N - 1))[:, None]
+        return tog.Problem(tog.rk3(model), tog.LQRObjective(Q, R, Q, xf, N), U0, constraints=cons, dt=0.075,
+                           x0=x0, N=N, tf="min")
+
+    al = tog.AugmentedLagrangianSolverOptions(opts_uncon=tog.iLQRSolverOptions(), iterations=30, penalty_scaling=10.0)
+    opts = tog.ALTROSolverOptions(opts_al=al, R_minimum_time=15.0, dt_max=0.15, dt_min=1.0e-3)
+    circ = tog.CircleConstraints(2, 1, [[1.2, 2.5, 0.6]])
+    pu = make(user, tog.UserConstraint(2, 1, 1, fid=0))
+    pb = make(tog.Dynamics.pendulum, circ)
+    ref = pb.copy()
+    su = tog.solve_b(pu, opts.copy())
+    sb = tog.solve_b(pb, opts.copy())
+    assert np.array_equal(pu._X, pb._X) and np.array_equal(pu._U, pb._U) and np.array_equal(pu.h, pb.h)
+    for key in ("iterations_total", "flags", "cost", "c_max"):
+        assert np.array_equal(su.stats[key], sb.stats[key]), key
+    Xo, Uo, ho, so = oracle.solve_altro_min_time(ref, opts.copy(), 0)
+    assert np.max(np.abs(pb._X[0] - Xo)) <= 1e-6 * max(1.0, np.max(np.abs(Xo)))
+    assert np.max(np.abs(pb._U[0] - Uo)) <= 1e-6 * max(1.0, np.max(np.abs(Uo)))
+    assert np.max(np.abs(pb.h[0] - ho)) <= 1e-6

@@ -247,8 +247,9 @@ inline int min_time_desc(const tog_problem_desc* s, double R_min_time, double dt
             if (!bnd) bnd = &con;
             continue;
           }
-          if (con.type == TOG_CON_USER || con.type == TOG_CON_INFEASIBLE)
-            return tog__fail(TOG_ERR_UNSUPPORTED, "minimum time with user or slack constraint rows");
+          // (user rows keep their function over the base model's x, u: MinTime<M>::con)
+          if (con.type == TOG_CON_INFEASIBLE)
+            return tog__fail(TOG_ERR_UNSUPPORTED, "minimum time of a problem that already has slack constraint rows");
           tog_constraint cc = con;
           if (cc.type == TOG_CON_GOAL && cc.count == 0) cc.count = n;  // the goal stays on x[1:n]
           cs.push_back(cc);

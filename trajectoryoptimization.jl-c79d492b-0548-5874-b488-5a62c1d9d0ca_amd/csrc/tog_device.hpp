@@ -946,6 +946,13 @@ template <class Mb>
 struct MinTime {
   using Base = Mb;
   static constexpr int n = Mb::n + 1, m = Mb::m + 1, id = Mb::id;
+  // user constraint functions see the base model's x[1:n], u[1:m] (mintime_constraints'
+  // update_constraint_set_jacobians(PC[k], n, n+1, m), minimum_time.jl:125-141): τ and h get zero gradients
+  static constexpr bool has_con = HasCon<Mb>::value;
+  template <class T>
+  __host__ __device__ __forceinline__ static void con(int fid, T* c, const T* x, const T* u) {
+    if constexpr (HasCon<Mb>::value) Mb::con(fid, c, x, u);
+  }
 };
 
 template <class M>

@@ -3765,7 +3765,7 @@ struct ModelLaunch {
       big(k_pn_project<M, INTEG>);
     else if (phase == 2)
       hipLaunchKernelGGL((k_pn_finish<M, INTEG>), dim3((unsigned)B), dim3(64), 0, st, P, Bf, W);
-    else if constexpr (!ModelTraits<M>::min_time) {  // solve_type :optimal (not built for minimum time)
+    else {  // solve_type :optimal
       if (phase == 3)
         big(k_pn_kkt<M, INTEG>);
       else if (phase == 4)

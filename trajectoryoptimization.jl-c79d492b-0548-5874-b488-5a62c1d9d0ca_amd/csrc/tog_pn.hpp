@@ -649,10 +649,13 @@ __global__ void __launch_bounds__(64) k_pn_finish(const DevProblem* __restrict__
 // (multiplier_projection! at the projected trial, the acceptance test, the next trial).
 // ---------------------------------------------------------------------------------------------------------
 
-// the plain objective's gradient (cost_expansion!'s gradient!, :139-148) at X, U into w.g; a lane per knot
+// the objective's gradient (cost_expansion!'s gradient!, :139-148) at X, U into w.g; a lane per knot. A
+// minimum-time problem's is MinTimeCost's gradient! (minimum_time.jl:201-237): the padded quadratic cost's at
+// dt = h², R_min_time τ for τ, τ (2 ℓ(x, u) + R_min_time) for h, terminal Qf x + qf and R_min_time τ
 template <class M>
 __device__ void pn_grad(const DevProblem* P, const PNView& w, const double* X, const double* U, int lane) {
   constexpr int n = M::n, m = M::m;
+  constexpr bool MT = ModelTraits<M>::min_time;
   const int N = P->N;
   for (int k = lane; k < N; k += WAVE) {
     const double* x = X + (size_t)k * n;
@@ -660,7 +663,7 @@ __device__ void pn_grad(const DevProblem* P, const PNView& w, const double* X, c
     if (k < N - 1) {
       const double* u = U + (size_t)k * m;
       const CostView C_ = cost_at<n, m>(P, k);
-      const double dt = P->dt;
+      const double dt = MT ? u[m - 1] * u[m - 1] : P->dt;
       for (int i = 0; i < n; i++) {
         double a = 0.0, c = 0.0;
         for (int j = 0; j < n; j++) a = fma(C_.Q[i + n * j], x[j], a);
@@ -673,12 +676,18 @@ __device__ void pn_grad(const DevProblem* P, const PNView& w, const double* X, c
         for (int j = 0; j < n; j++) c = fma(C_.H[i + m * j], x[j], c);
         q[n + i] = ((a + C_.r[i]) + c) * dt;
       }
+      if constexpr (MT) {
+        const double l1 = stage_cost_dt<n, m>(P, k, x, u, 1.0);
+        q[n + m - 1] = u[m - 1] * (2.0 * l1 + P->R_min_time);
+        q[n - 1] = P->R_min_time * x[n - 1];
+      }
     } else {
       for (int i = 0; i < n; i++) {
         double a = 0.0;
         for (int j = 0; j < n; j++) a = fma(P->Qf[i + n * j], x[j], a);
         q[i] = a + P->qf[i];
       }
+      if constexpr (MT) q[n - 1] = P->R_min_time * x[n - 1];
     }
   }
   pn_sync();
@@ -905,6 +914,8 @@ __global__ void __launch_bounds__(64) k_pn_ls_begin(const DevProblem* __restrict
   double* U = Bf.U + (size_t)b * (N - 1) * M::m;
   for (int e = lane; e < N * M::n; e += WAVE) w.Xv[e] = X[e];
   for (int e = lane; e < (N - 1) * M::m; e += WAVE) w.Uv[e] = U[e];
+  // update!'s cost_expansion! at solver.V: a minimum-time problem's H for the first trial's projection!
+  if constexpr (ModelTraits<M>::min_time) pn_weights_min_time<M>(P, w, X, U, lane);
   pn_eval<M, INTEG>(P, Bf, b, w, X, U, lane);
   if (pn_active_set(P, Bf, b, w, W.atol, nb, lane)) return pn_stop_over(s, &W.st[b], Bf.st[b], lane);
   pn_gather_y(P, Bf, b, w, nb, lane);
@@ -995,6 +1006,8 @@ __global__ void __launch_bounds__(64) k_pn_ls_end(const DevProblem* __restrict__
   double res = NAN;
   if (!rejected) {
     pn_grad<M>(P, w, X, U, lane);
+    // cost_expansion!(prob, solver, V_): a minimum-time problem's H at the trial, the next trial's projection!'s
+    if constexpr (ModelTraits<M>::min_time) pn_weights_min_time<M>(P, w, X, U, lane);
     res = pn_multiplier_projection<M>(P, Bf, b, w, X, w.nut, w.lct, sh, nb, lane, rejected);
   }
   int next = 0;

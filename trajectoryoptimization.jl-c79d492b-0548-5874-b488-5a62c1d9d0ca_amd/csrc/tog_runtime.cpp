@@ -41,6 +41,8 @@ const ModelOps* ops_mtinf_pendulum();
 const ModelOps* ops_mtinf_car();
 const ModelOps* ops_mtinf_double_integrator();
 const ModelOps* ops_mtinf_cartpole();
+const ModelOps* ops_mtinf_quadrotor();
+const ModelOps* ops_mtinf_kuka();
 const ModelOps* ops_mt_car();
 const ModelOps* ops_mt_double_integrator();
 const ModelOps* ops_mt_quadrotor();
@@ -183,12 +185,14 @@ struct tog_model {
 static const ModelOps* ops_for(int model, bool infeasible, bool min_time, const tog_model* user, int integ) {
   if (model == TOG_MODEL_KUKA && !infeasible && !min_time && (integ == TOG_RK3_IMPLICIT || integ == TOG_MIDPOINT_IMPLICIT))
     return ops_kuka_implicit();
-  if (min_time && infeasible) {  // minimum_time_problem(infeasible_problem(prob)): the small models
+  if (min_time && infeasible) {  // minimum_time_problem(infeasible_problem(prob))
     switch (model) {
       case TOG_MODEL_PENDULUM: return ops_mtinf_pendulum();
       case TOG_MODEL_CAR: return ops_mtinf_car();
       case TOG_MODEL_DOUBLE_INTEGRATOR: return ops_mtinf_double_integrator();
       case TOG_MODEL_CARTPOLE: return ops_mtinf_cartpole();
+      case TOG_MODEL_QUADROTOR: return ops_mtinf_quadrotor();
+      case TOG_MODEL_KUKA: return ops_mtinf_kuka();
     }
     return nullptr;
   }
@@ -1670,8 +1674,6 @@ int32_t tog_solve_pn(tog_handle* h, const tog_pn_options* opts, double* out) {
     });
   if (opts->solve_type != 0 && opts->solve_type != 1) return fail(TOG_ERR_ARG, "solve_type must be 0 (:feasible) or 1 (:optimal)");
   const bool optimal = opts->solve_type == 1;
-  if (optimal && h->ops->min_time)
-    return fail(TOG_ERR_UNSUPPORTED, "projected Newton solve_type :optimal on a minimum-time problem is not built");
   if (opts->n_steps < 0) return fail(TOG_ERR_ARG, "n_steps must be >= 0");
   if (!h->ops->pn) return fail(TOG_ERR_UNSUPPORTED, "projected Newton needs n + m <= 64 (a lane per variable of a knot)");
   // block stride: n + every row of a knot, capped at a wave's 64 rows; blocks are sized by the *active* rows
