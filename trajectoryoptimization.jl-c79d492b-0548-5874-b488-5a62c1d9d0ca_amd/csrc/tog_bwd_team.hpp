@@ -24,15 +24,6 @@ namespace tog {
 // loads) ahead of their FMAs, which would need ~2x the registers of the logical working set.
 #define TEAM_FENCE() asm volatile("" ::: "memory")
 
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
 constexpr int PX = 20;  // rows with a state gradient per knot kept in registers (sqrt AL expansion)
 
 template <class M>

@@ -813,7 +813,6 @@ struct BwdLds {
   double cu[PC * m];
   static constexpr int RW = (PC + 63) / 64;
   unsigned long long rmask[(n + m) * RW];  // per variable: the rows whose gradient entry is nonzero
-  unsigned long long rnf[(n + m) * RW];    // per variable: the rows whose gradient entry is not finite
   unsigned long long rbad[RW];             // rows with a non-finite gradient entry or weight: always chained
   double red[WAVE];
   // lane-0 serial scratch (kept in LDS: private arrays with runtime indexing spill to scratch memory)
@@ -913,6 +912,11 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
   const double* mu = Bf.mu + ((size_t)b * N + k) * pmax;
   for (int e = lane; e < p * n; e += WAVE) sh.cx[e] = 0.0;
   for (int e = lane; e < p * m; e += WAVE) sh.cu[e] = 0.0;
+  if constexpr (!SQRT) {  // the row masks of the std AL chains below, set as the rows are evaluated
+    constexpr int RW = BwdLds<M, SQRT>::RW;
+    for (int e = lane; e < (n + m) * RW; e += WAVE) sh.rmask[e] = 0ull;
+    if (lane < RW) sh.rbad[lane] = 0ull;
+  }
   wsync();
   for (int r = lane; r < p; r += WAVE) {  // p may exceed the wave (PCAP > 64)
     const double c = row_value_m<M>(rows[r], sh.xk, term ? nullptr : sh.uk);
@@ -932,6 +936,17 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
       else
         sh.cu[r + p * (idx[z] - n)] = v[z];
     }
+    if constexpr (!SQRT) {  // row r's bit in the masks of the columns its gradient touches (LDS atomics)
+      constexpr int RW = BwdLds<M, SQRT>::RW;
+      const int wd = r >> 6;
+      const unsigned long long bit = 1ull << (r & 63);
+      bool bad = !isfinite(w);
+      for (int z = 0; z < nz; z++) {
+        if (v[z] != 0.0) atomicOr(&sh.rmask[idx[z] * RW + wd], bit);
+        bad = bad || !isfinite(v[z]);
+      }
+      if (bad) atomicOr(&sh.rbad[wd], bit);
+    }
   }
   wsync();
   if (!SQRT) {
@@ -941,28 +956,9 @@ __device__ void bwd_expand(const DevProblem* __restrict__ P, const DevBuffers& B
     // their row masks) and gives the dense chain's value bit for bit (round 5: the infeasible quadrotor's
     // 69 rows touch 1-3 columns each). A row with a non-finite gradient entry or weight anywhere is chained
     // in every entry (rbad), so a diverging trajectory's Inf/NaN reaches Q exactly as the dense chain's does.
+    // (the masks: rmask[v] has row r's bit when the row's gradient entry in column v is nonzero, rbad the rows
+    // with a non-finite gradient entry or weight; both set by the row evaluation above)
     constexpr int RW = BwdLds<M, SQRT>::RW;
-    for (int v = lane; v < n + m; v += WAVE) {
-      const double* col = v < n ? sh.cx + p * v : sh.cu + p * (v - n);
-      for (int w = 0; w < RW; w++) {
-        unsigned long long mk = 0ull, nf = 0ull;
-        for (int r = 64 * w; r < p && r < 64 * (w + 1); r++) {
-          if (col[r] != 0.0) mk |= 1ull << (r - 64 * w);
-          if (!isfinite(col[r])) nf |= 1ull << (r - 64 * w);
-        }
-        sh.rmask[v * RW + w] = mk;
-        sh.rnf[v * RW + w] = nf;
-      }
-    }
-    wsync();
-    if (lane < RW) {
-      unsigned long long bad = 0ull;
-      for (int v = 0; v < n + m; v++) bad |= sh.rnf[v * RW + lane];
-      for (int r = 64 * lane; r < p && r < 64 * (lane + 1); r++)
-        if (!isfinite(sh.wv[r])) bad |= 1ull << (r - 64 * lane);
-      sh.rbad[lane] = bad;
-    }
-    wsync();
     auto chain = [&](const double* ci, const double* cj, int vi, int vj) {
       double t = 0.0;
       for (int w = 0; w < RW; w++) {
@@ -1056,6 +1052,24 @@ __device__ __forceinline__ void bwd_load_q(const double* q, BwdLds<M, SQRT>& sh)
   }
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// lane L's value of v in every lane (two v_readlane_b32; L a compile-time constant)
+template <int L>
+__device__ __forceinline__ double lane_read(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), L);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), L);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // LU with partial pivoting of the m x m matrix F in place (dgetrf; Julia `\`), lane 0 only.
 template <int m>
 __device__ __forceinline__ void lu_factor(double* F, int* piv) {
@@ -1107,6 +1121,33 @@ __device__ __forceinline__ void lu_solve_col(const double* F, const int* piv, do
 #pragma unroll
     for (int i = 0; i < j; i++) bcol[i] = fma(-F[i + m * j], bcol[j], bcol[i]);
   }
+}
+// lu_solve_col with the factor in registers: lane c holds column c of F (gcol); F[i][j] reaches every lane by
+// v_readlane from lane j. The same operations in the same order as lu_solve_col. Call in uniform control flow.
+template <int m>
+__device__ __forceinline__ void lu_solve_col_reg(const double (&gcol)[m], const int* piv, double* bcol) {
+#pragma unroll
+  for (int k = 0; k < m; k++) {
+    const int p = piv[k];
+#pragma unroll
+    for (int i = k + 1; i < m; i++)
+      if (i == p) {
+        const double t = bcol[k];
+        bcol[k] = bcol[i];
+        bcol[i] = t;
+      }
+  }
+  static_for<0, m>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+#pragma unroll
+    for (int i = j + 1; i < m; i++) bcol[i] = fma(-lane_read<j>(gcol[i]), bcol[j], bcol[i]);
+  });
+  static_for<0, m>([&](auto jr) {
+    constexpr int j = m - 1 - decltype(jr)::value;
+    bcol[j] /= lane_read<j>(gcol[j]);
+#pragma unroll
+    for (int i = 0; i < j; i++) bcol[i] = fma(-lane_read<j>(gcol[i]), bcol[j], bcol[i]);
+  });
 }
 
 // 2-norm condition number test cond(R) > 1e8 for an upper-triangular m x m R (backward_pass.jl:129).
@@ -1326,6 +1367,7 @@ attempt:
       kmin = k < kmin ? k : kmin;
     }
     // ---- regularisation (backward_pass.jl:38-48 / :120-126) and the restart test
+    double gcol[m];  // (std pass) lane c: column c of Quu_reg's LU factor, kept in registers for the gains
     if (!SQRT) {
       // Quu_reg = Q.uu + ρI (or + ρB'B), isposdef(Hermitian(Quu_reg)) and its LU factor, wave-parallel (round
       // 5; these ran on lane 0 and were most of a knot for m = 17, the infeasible quadrotor): every entry
@@ -1346,79 +1388,91 @@ attempt:
         G[e] = g;
       }
       wsync();
-      // isposdef(Hermitian(Quu_reg)): Cholesky of the upper triangle, row j of U by lanes c > j
-      double* U = sh.Uc;
+      // isposdef(Hermitian(Quu_reg)) and the LU, register-resident (round 6): lane c holds column c of G and of
+      // the Cholesky test's U in registers; step j's operands from other columns arrive by v_readlane (the step
+      // index is a compile-time constant after unrolling), so the 2m steps run without LDS round trips or
+      // barriers. Every value keeps the operations and order of the LDS form (and of the oracle): the test's
+      // d0 and the LU's pivot scan, reciprocal and scaled column are formed redundantly (uniformly) in every
+      // lane from the broadcast column.
+      const int cl = lane < m ? lane : 0;
+      double ucol[m];
+#pragma unroll
+      for (int i = 0; i < m; i++) {
+        gcol[i] = G[i + m * cl];
+        ucol[i] = 0.0;
+      }
       bool pd = true;
-      // (each step's operands are loaded as a batch over the compile-time extent m -- rows l >= j select an
-      // unused 0.0 -- so the LDS reads are in flight together; the chains are the serial ones, in order)
-      for (int j = 0; j < m; j++) {
-        double uj[m], uc[m];
-        const int c = (lane > j && lane < m) ? lane : j;
+      static_for<0, m>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if (!pd) return;
+        double uj[j > 0 ? j : 1];
 #pragma unroll
-        for (int l = 0; l < m; l++) {
-          uj[l] = (l < j) ? U[l + m * j] : 0.0;
-          uc[l] = (l < j) ? U[l + m * c] : 0.0;
-        }
-        double d0 = G[j + m * j];
+        for (int l = 0; l < j; l++) uj[l] = lane_read<j>(ucol[l]);
+        double d0 = lane_read<j>(gcol[j]);
 #pragma unroll
-        for (int l = 0; l < m; l++)
-          if (l < j) d0 -= uj[l] * uj[l];
+        for (int l = 0; l < j; l++) d0 -= uj[l] * uj[l];
         if (!(d0 > 0.0)) {
           pd = false;
-          break;
+          return;
         }
         const double ujj = sqrt(d0);
-        if (lane == j) U[j + m * j] = ujj;
+        if (lane == j) ucol[j] = ujj;
         if (lane > j && lane < m) {
-          double t = G[j + m * c];
+          double t = gcol[j];
 #pragma unroll
-          for (int l = 0; l < m; l++)
-            if (l < j) t -= uj[l] * uc[l];
-          U[j + m * c] = t / ujj;
+          for (int l = 0; l < j; l++) t -= uj[l] * ucol[l];
+          ucol[j] = t / ujj;
         }
-        wsync();
-      }
+      });
       if (lane == 0) sh.flag = pd ? 1 : 0;
-      if (pd) {  // lu_factor (partial pivoting), in G
-        for (int k = 0; k < m; k++) {
+      if (pd) {  // lu_factor (partial pivoting)
+        static_for<0, m>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
           double ck[m];
 #pragma unroll
-          for (int i = 0; i < m; i++) ck[i] = G[i + m * k];
+          for (int i = 0; i < m; i++) ck[i] = lane_read<k>(gcol[i]);
           int p = k;
-          double amax = 0.0;
+          double amax = fabs(ck[k]);
 #pragma unroll
-          for (int i = 0; i < m; i++) {  // amax = |G[k, k]|, then the strict-greater scan over i > k, in order
-            if (i == k) {
-              amax = fabs(ck[i]);
-            } else if (i > k && fabs(ck[i]) > amax) {
+          for (int i = k + 1; i < m; i++) {  // the strict-greater scan over i > k, in order
+            if (fabs(ck[i]) > amax) {
               amax = fabs(ck[i]);
               p = i;
             }
           }
           if (lane == 0) sh.piv[k] = p;
-          wsync();
-          if (p != k) {
-            if (lane < m) {
-              const double t = G[k + m * lane];
-              G[k + m * lane] = G[p + m * lane];
-              G[p + m * lane] = t;
+          if (p != k) {  // rows k and p of every column (p uniform: a select per candidate row)
+#pragma unroll
+            for (int i = k + 1; i < m; i++) {
+              if (i == p) {
+                const double t = gcol[k];
+                gcol[k] = gcol[i];
+                gcol[i] = t;
+                const double tc = ck[k];
+                ck[k] = ck[i];
+                ck[i] = tc;
+              }
             }
-            wsync();
           }
-          const double akk = G[k + m * k];
+          const double akk = ck[k];
           if (akk != 0.0) {
             const double r = 1.0 / akk;
-            if (lane > k && lane < m) G[lane + m * k] *= r;
-            wsync();
+#pragma unroll
+            for (int i = k + 1; i < m; i++) ck[i] *= r;  // column k below the diagonal, as lane k scales it
+            if (lane == k) {
+#pragma unroll
+              for (int i = k + 1; i < m; i++) gcol[i] = ck[i];
+            }
           }
-          const int t = m - k - 1;
-          for (int e = lane; e < t * t; e += WAVE) {
-            const int i = k + 1 + e % t, j = k + 1 + e / t;
-            G[i + m * j] = fma(-G[i + m * k], G[k + m * j], G[i + m * j]);
+          if (lane > k && lane < m) {
+#pragma unroll
+            for (int i = k + 1; i < m; i++) gcol[i] = fma(-ck[i], gcol[k], gcol[i]);
           }
-          wsync();
+        });
+        if (lane < m) {
+#pragma unroll
+          for (int i = 0; i < m; i++) sh.F[i + m * lane] = gcol[i];
         }
-        for (int e = lane; e < m * m; e += WAVE) sh.F[e] = G[e];
       }
     } else {
       if (lane == 0) {
@@ -1482,7 +1536,9 @@ attempt:
       goto attempt;
     }
     // ---- gains: K = -(Quu_reg \ Qux_reg), d = -(Quu_reg \ Q.u)
-    if (lane <= n) {
+    // (std pass: every lane runs the substitutions -- lanes past n on a zero column -- so that the LU factor's
+    // entries can come from the owning lanes' registers by v_readlane in uniform control flow)
+    if (!SQRT || lane <= n) {
       double col[m];
       if (lane < n) {
 #pragma unroll
@@ -1496,12 +1552,15 @@ attempt:
           }
           col[i] = v;
         }
-      } else {
+      } else if (lane == n) {
 #pragma unroll
         for (int i = 0; i < m; i++) col[i] = sh.Qu[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < m; i++) col[i] = 0.0;
       }
       if (!SQRT) {
-        lu_solve_col<m>(sh.F, sh.piv, col);
+        lu_solve_col_reg<m>(gcol, sh.piv, col);
       } else {
         // Quu_reg' \ col (forward substitution), then Quu_reg \ (back substitution); contract v2:
         // multiply by the diagonal reciprocals
@@ -1526,7 +1585,7 @@ attempt:
       if (lane < n) {
 #pragma unroll
         for (int i = 0; i < m; i++) sh.Kt[i + m * lane] = -1.0 * col[i];
-      } else {
+      } else if (lane == n) {
 #pragma unroll
         for (int i = 0; i < m; i++) sh.dd[i] = -1.0 * col[i];
       }
