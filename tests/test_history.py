@@ -183,3 +183,37 @@ def test_history_off_by_default_on_handles(tog, gpu):
     with pytest.raises(RuntimeError):
         out = np.empty((2, 1, 3))
         tog.abi.check(s.handle.lib, s.handle.lib.tog_get(s.handle.h, tog.abi.FIELD_HIST_INNER, tog.abi.as_dp(out)))
+
+
+@pytest.mark.gpu
+def test_history_reenable_reuses_buffers(tog, gpu):
+    """tog_history_enable on one long-lived handle with shrinking and growing capacities (advisor round 5: each
+    change used to allocate new buffers and keep the old ones until tog_destroy): a smaller capacity reuses the
+    allocation, a larger one replaces it, off (0) and on again works, and every solve's records equal those of
+    a fresh handle with the same capacity."""
+    prob, opts = tog.Problems.config_quadrotor(B=2)
+    solver = tog.AbstractSolverFor(prob, opts)
+    for cap in (4000, 30, 0, 2500, 6000):
+        gp = prob.copy()
+        s = tog.solve_b(gp, solver, history=cap if cap else False)
+        if cap == 0:
+            assert s.history is None
+            continue
+        fresh = tog.solve_b(prob.copy(), tog.AbstractSolverFor(prob, opts), history=cap)
+        for a, b_ in zip(s.history, fresh.history):
+            assert a.shape == b_.shape, cap
+            if a.ndim == 3 and a.shape[-1] == 3:  # inner records: compare the written ones
+                cnt = s.history[2][:, 0]
+                for b in range(prob.B):
+                    # (record 0's gradient is calculate_gradient at the start with the solver's current d: the
+                    # previous solve's on a reused solver, as in the reference; zero on the fresh one)
+                    k = min(int(cnt[b]), cap)
+                    assert np.array_equal(a[b, 0, :2], b_[b, 0, :2]), (cap, b)
+                    assert np.array_equal(a[b, 1:k], b_[b, 1:k], equal_nan=True), (cap, b)
+            elif a.ndim == 3:  # outer records: the written ones (unwritten slots hold whatever memory held)
+                cnt = s.history[2][:, 1]
+                for b in range(prob.B):
+                    k = min(int(cnt[b]), a.shape[1])
+                    assert np.array_equal(a[b, :k], b_[b, :k], equal_nan=True), (cap, b)
+            else:
+                assert np.array_equal(a, b_), cap
