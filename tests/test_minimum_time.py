@@ -411,3 +411,46 @@ def test_gpu_infeasible_min_time_models(tog, oracle, gpu, name):
     assert np.max(np.abs(p._U[0] - Uo)) <= 1e-6 * scale(Uo)
     assert np.max(np.abs(p.h[0] - ho)) <= 1e-6
     assert int(solver.stats["iterations_total"][0]) == int(si.get("stats")[tog.abi.STAT_TOTAL_STEPS])
+
+
+@pytest.mark.gpu
+def test_gpu_min_time_kuka_divergent_trials_rejected(tog, oracle, gpu):
+    """Regression for round 4's MinTime<Kuka> rollout fault (profiles/r4j_mt_kuka_trials_split_f.txt: written
+    through the chol()/solve() helpers, the speculative rollouts accepted trials whose states had passed
+    max_state_value; rollout.jl:18-20 rejects them). Replays that case: the line search of step 20 of the
+    minimum-time Kuka solve, whose first trials (α = 1 .. 1/32) diverge. Every trial's verdict equals the
+    oracle's rollout from the same state, and the accepted trials' costs equal the oracle's bit for bit
+    (tog__debug_ls dumps the device's trials)."""
+    import ctypes as C
+    abi = tog.abi
+    prob, opts = _mt_model_case(tog, "kuka")
+    s = tog.AbstractSolverFor(prob.copy(), opts)
+    h = s.handle
+    h.solve_init(abi.MODE_AL)
+    for _ in range(19):
+        h.solve_step(1)
+    st0 = {f: h.get(f, raw=True) for f in (abi.FIELD_X, abi.FIELD_U, abi.FIELD_LAMBDA, abi.FIELD_MU, abi.FIELD_RHO)}
+    h.solve_step(1)
+    nc = C.c_int32()
+    J = np.zeros(64)
+    ok = np.zeros(64, dtype=np.int32)
+    abi.check(h.lib, h.lib.tog__debug_ls(h.h, J.ctypes.data_as(C.POINTER(C.c_double)),
+                                         ok.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(nc)))
+    o = oracle.OracleSolver(prob, opts, b=0)
+    for f, nm in ((abi.FIELD_X, "X"), (abi.FIELD_U, "U"), (abi.FIELD_LAMBDA, "lambda"), (abi.FIELD_MU, "mu"),
+                  (abi.FIELD_RHO, "rho")):
+        o.set(nm, st0[f][0])
+    o.update_constraints()
+    o.jacobians()
+    assert o.cost_expansion(False, True) == 0
+    o.backward(False)
+    diverged = 0
+    assert nc.value >= 8
+    for j in range(nc.value):
+        oko = o.rollout(2.0 ** -j)
+        assert bool(ok[j]) == bool(oko), (j, ok[j], oko)
+        if oko:
+            assert J[j] == o.cost_bar(True), j
+        else:
+            diverged += 1
+    assert diverged >= 1  # the case still exercises the divergence test

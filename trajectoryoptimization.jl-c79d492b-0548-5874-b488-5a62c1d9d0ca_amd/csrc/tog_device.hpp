@@ -880,6 +880,14 @@ struct Kuka {
     T tau[7], cq[7], sq[7], L[7][7], y[7];
     bias<T, T, LIT>(tau, cq, sq, q, qd);
     mass<T, LIT>(L, cq, sq);
+#ifdef TOG_KUKA_HELPER_F  // round 4's helper form (tools/kuka_helper_build.py: the miscompile investigation only)
+    chol(L);
+    solve(xd + 7, L, u, tau);
+#pragma unroll
+    for (int i = 0; i < 7; i++) xd[i] = qd[i];
+    (void)y;
+    return;
+#endif
     // Cholesky M = L Lᵀ in place (entry (i,j) of M is read once, before L[i][j] replaces it)
 #pragma unroll
     for (int j = 0; j < 7; j++) {
