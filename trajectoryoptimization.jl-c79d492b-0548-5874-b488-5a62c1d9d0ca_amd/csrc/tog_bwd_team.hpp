@@ -926,6 +926,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const bool colu = tl < m;  // this lane owns a control column
   const int c = colx ? tl : 0;
   const int cu = colu ? tl : 0;
+  // this lane's slot (base + tl * mul) of a team LDS array, formed at the use from an opaque copy of tl:
+  // formed once, such addresses stay live across the knot loop and spill, and every spill reload waits
+  // on vmcnt(0), which also drains the K/d stores and the loads in flight
+  auto lane_at = [&](double* base, int mul) { return base + opaque(tl) * mul; };
   RegState s;
   s.rho = live ? Bf.st[b].rho : 0.0;
   s.drho = live ? Bf.st[b].drho : 0.0;
@@ -1275,8 +1279,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     // ---------------------------------------------------------------- regularise, test, gains
     // (backward_pass.jl:38-48 / :120-126). Every lane needs the full Q.uu: all-gather its columns.
     if (colu) {
+      double* qc = lane_at(QU, m);
 #pragma unroll
-      for (int i = 0; i < m; i++) QU[i + m * tl] = Quuc[i];
+      for (int i = 0; i < m; i++) qc[i] = Quuc[i];
       if (state_reg) {  // (:state regularisation only; reloaded to keep [A|B] out of registers)
         const double* bk = ABg + (size_t)k * n * L + n * (n + tl);
 #pragma unroll
@@ -1683,8 +1688,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       // all-gather tmp1 (row-major at bus[TB + r*m + j]) and s
       constexpr int TB = 32;
       if (colx) {
+        double* tr = lane_at(bus + TB, m);
 #pragma unroll
-        for (int i = 0; i < m; i++) bus[TB + tl * m + i] = t1[i];
+        for (int i = 0; i < m; i++) tr[i] = t1[i];
       }
       team_sync();
       // tmp2 = chol_minus(Q.uu, tmp1): lowrankdowndate! by each row of tmp1 (backward_pass.jl:186-192).
@@ -1698,9 +1704,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       bool pd_abort = false;
       {
         double u[m], w[m], wn[m];
+        const double* qd = lane_at(QU, m + 1);  // (Q.uu's diagonal entry of row tl)
 #pragma unroll
         for (int k = 0; k < m; k++) {
-          u[k] = (colu && tl + k < m) ? QU[tl + m * (tl + k)] : 0.0;
+          u[k] = (colu && tl + k < m) ? qd[m * k] : 0.0;
           w[k] = 0.0;
           wn[k] = bus[TB + k];  // lane 0: row 0 of tmp1 (the other lanes ignore wn)
         }
@@ -1783,12 +1790,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         const unsigned long long tmask = (TEAM >= 64 ? ~0ull : ((1ull << TEAM) - 1ull)) << (team * TEAM);
         const bool fail = (__ballot(!okd) & tmask) != 0ull;
         if (colu) {
-#pragma unroll
-          for (int jj = 0; jj < m; jj++)
-            if (jj < tl) bus2[2 * m * m + tl + m * jj] = 0.0;
-#pragma unroll
-          for (int k = 0; k < m; k++)
-            if (tl + k < m) bus2[2 * m * m + tl + m * (tl + k)] = u[k];
+          // row tl of tmp2 (column-major): entry (tl, jj) is u[jj - tl] from the diagonal on, 0 below it;
+          // written branch-free, every column of the row
+          double* tr = lane_at(bus2 + 2 * m * m, 1);
+          const int tq = opaque(tl);
+          static_for<0, m>([&](auto jc) {
+            constexpr int jj = decltype(jc)::value;
+            double v = 0.0;
+            static_for<0, jj + 1>([&](auto kc) {
+              constexpr int k = decltype(kc)::value;
+              v = (tq + k == jj) ? u[k] : v;
+            });
+            tr[m * jj] = v;
+          });
         }
         team_sync();
         U2p = bus2 + 2 * m * m;
@@ -1831,7 +1845,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         if (colx) {
 #pragma unroll
           for (int i = 0; i < n; i++) Sreg[i + n * tl] = (i <= tl) ? a[i] : 0.0;
-          Sreg[SOFF + tl] = sown;
+          *lane_at(Sreg + SOFF, 1) = sown;
         }
         team_sync();
       }
