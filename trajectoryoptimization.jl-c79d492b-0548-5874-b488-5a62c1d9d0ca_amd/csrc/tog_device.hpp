@@ -192,6 +192,7 @@ struct DevBuffers {
   double* cand;       // (NCP, n+m, N, B) every trial's rollout (candidate-copy line search), or null
   int ncp;            // candidate slots per element (nc rounded up to 8)
   int tail;           // few trajectories active (last host readback): latency-sized backward kernels
+  int simds;          // SIMDs of the device (CUs x 4): a team backward of at most this many waves runs WPE = 1
   int* ls_win;        // (B) accepted trial of the current forward pass (k_ls_decide)
   double* ls_Jw;      // (B) its cost
   double* gk;         // (N, B) per-knot todorov gradient terms of the accepted Ū

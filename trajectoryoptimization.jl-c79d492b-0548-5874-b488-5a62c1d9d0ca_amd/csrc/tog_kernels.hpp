@@ -3591,7 +3591,9 @@ struct ModelLaunch {
             else hipLaunchKernelGGL((k_bwd_quad<M, 0>), gd, dim3(256), 0, st, P, Bf, flags);
           }
         }
-      } else if (Bf.tail) {
+      } else if (Bf.tail || (B + TPW - 1) / TPW <= Bf.simds) {
+        // (a batch that gives at most one wave per SIMD, e.g. config 5's 4,096 Kuka trajectories in 1,024
+        // waves, gains nothing from the 2-wave register budget and would spill under it)
         launch(std::integral_constant<int, 1>{});
       } else {
         launch(std::integral_constant<int, TOG_BWD_WAVES>{});

@@ -933,6 +933,11 @@ static int32_t create_single(tog_handle* h, const tog_problem_desc* d, const tog
   }
   b.ncp = (b.nc + 7) & ~7;
   b.tail = 0;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) cus = 0;
+    b.simds = getenv("TOG_BWD_W2") ? 0 : 4 * cus;  // (TOG_BWD_W2: the 2-wave variant at every batch size, A/B)
+  }
   b.ls_pend_ok = getenv("TOG_LS_NOPEND") ? 0 : 1;
   b.ls_first = LS_FIRST;
   b.cand = nullptr;
